@@ -1,0 +1,938 @@
+// frhip engine: C-ABI handle, weight-blob loader, static per-arch forward plans and the
+// gallery/match entry points.  See include/frhip.h for the boundary contract and
+// DESIGN.md for the data layout.
+//
+// The forward plans restate the reference backbones as a list of fused ops:
+//   FR_ARCH_RESNET50_ARCFACE  models/arcface/arcface_model.py:118-132 + head :192-196
+//   FR_ARCH_IRESNET100        insightface iresnet100 (IBasicBlock; README.md:72)
+//   FR_ARCH_IRV1_FACENET      facenet_pytorch InceptionResnetV1 (facenet_model.py:12-16)
+// BN is folded into the conv weights/bias by the Python importer
+// (facerecognition_amd/weights.py); this file only knows tensor names.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/frhip.h"
+#include "kernels.h"
+
+namespace fr {
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+}  // namespace fr
+
+using namespace fr;
+
+namespace {
+
+struct HostT {
+    std::vector<int64_t> dims;
+    std::vector<float> v;
+};
+
+struct DevConvW {
+    bf16_t* w = nullptr;
+    float* bias = nullptr;
+    float* slope = nullptr;
+    float* aff_s = nullptr;
+    float* aff_b = nullptr;
+    int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0;
+};
+
+struct TensorDesc {
+    int H, W, C;
+    bf16_t* dev = nullptr;
+    std::string name;  // oracle module whose output this tensor equals ("" = internal)
+};
+
+enum OpKind { OP_PRE, OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD };
+
+struct Op {
+    OpKind kind;
+    int in = -1, in_off = 0, cin = 0;
+    int out = -1, out_off = 0;
+    int res = -1, res_off = 0;
+    int out2 = -1;
+    int kh = 1, kw = 1, sh = 1, sw = 1, ph = 0, pw = 0;
+    int act = 0;
+    int wi = -1;
+    int pk = 0, ps = 0, pp = 0;
+};
+
+int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct fr_handle {
+    int device = 0, arch = 0, dtype = 0;
+    std::mutex mu;
+    bool loaded = false;
+    int in_size = 112, embed_dim = 512;
+    std::vector<TensorDesc> tensors;
+    std::vector<Op> ops;
+    std::vector<DevConvW> convw;
+    std::vector<void*> weight_allocs;
+    int max_batch = 0;
+    std::vector<void*> act_allocs;
+    float* partial = nullptr;
+    size_t partial_floats = 0;
+    // gallery
+    float* gallery = nullptr;
+    int64_t g_rows = 0;
+    int g_dim = 0;
+    int64_t g_base = 0;
+    float* cand_s = nullptr;
+    int32_t* cand_i = nullptr;
+    size_t cand_cap = 0;
+};
+
+namespace {
+
+// ------------------------------------------------------------------ device memory helpers
+int dev_alloc(void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? FR_ERR_OOM : FR_ERR_HIP;
+    }
+    return FR_OK;
+}
+
+template <class T>
+int upload(fr_handle* h, T** dst, const std::vector<T>& src) {
+    void* p = nullptr;
+    int rc = dev_alloc(&p, src.size() * sizeof(T));
+    if (rc) return rc;
+    h->weight_allocs.push_back(p);
+    FR_HIP_CHECK(hipMemcpy(p, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    *dst = (T*)p;
+    return FR_OK;
+}
+
+void free_acts(fr_handle* h) {
+    for (void* p : h->act_allocs) (void)hipFree(p);
+    h->act_allocs.clear();
+    for (auto& t : h->tensors) t.dev = nullptr;
+    h->partial = nullptr;
+    h->partial_floats = 0;
+    h->max_batch = 0;
+}
+
+void free_weights(fr_handle* h) {
+    for (void* p : h->weight_allocs) (void)hipFree(p);
+    h->weight_allocs.clear();
+    h->convw.clear();
+}
+
+// ------------------------------------------------------------------ weight blob
+// FRW1 := "FRW1" u32 count { u32 name_len, name, u32 ndim, i64 dims[ndim], f32 data[prod] }*
+int parse_blob(const void* blob, size_t n, std::unordered_map<std::string, HostT>& out) {
+    const uint8_t* p = (const uint8_t*)blob;
+    const uint8_t* end = p + n;
+    auto need = [&](size_t k) { return (size_t)(end - p) >= k; };
+    if (!need(8) || std::memcmp(p, "FRW1", 4) != 0) {
+        set_error("weight blob: bad magic (expected FRW1)");
+        return FR_ERR_WEIGHTS;
+    }
+    p += 4;
+    uint32_t count;
+    std::memcpy(&count, p, 4);
+    p += 4;
+    for (uint32_t i = 0; i < count; ++i) {
+        uint32_t nl, nd;
+        if (!need(4)) goto trunc;
+        std::memcpy(&nl, p, 4);
+        p += 4;
+        if (!need(nl + 4)) goto trunc;
+        {
+            std::string name((const char*)p, nl);
+            p += nl;
+            std::memcpy(&nd, p, 4);
+            p += 4;
+            if (nd > 8 || !need(8ull * nd)) goto trunc;
+            HostT t;
+            t.dims.resize(nd);
+            std::memcpy(t.dims.data(), p, 8ull * nd);
+            p += 8ull * nd;
+            size_t cnt = 1;
+            for (auto d : t.dims) cnt *= (size_t)d;
+            if (!need(4 * cnt)) goto trunc;
+            t.v.resize(cnt);
+            std::memcpy(t.v.data(), p, 4 * cnt);
+            p += 4 * cnt;
+            out[name] = std::move(t);
+        }
+    }
+    return FR_OK;
+trunc:
+    set_error("weight blob: truncated");
+    return FR_ERR_WEIGHTS;
+}
+
+// ------------------------------------------------------------------ plan builder
+struct Builder {
+    fr_handle* h;
+    std::unordered_map<std::string, HostT>& W;
+    int rc = FR_OK;
+
+    int tensor(int H, int Wd, int C, const std::string& name = "") {
+        h->tensors.push_back({H, Wd, C, nullptr, name});
+        return (int)h->tensors.size() - 1;
+    }
+
+    const HostT* find(const std::string& n) {
+        auto it = W.find(n);
+        return it == W.end() ? nullptr : &it->second;
+    }
+
+    bool stem = false;  // next conv is the network stem: fold 1/255 + hi/lo split (see launch_preprocess)
+
+    float round16(float v) const {
+        return h->dtype == FR_DTYPE_F16 ? host_h2f(host_f2h(v)) : host_bf2f(host_f2bf(v));
+    }
+
+    // Build one (possibly N-concatenated) conv weight: names[i].w is [Cout_i, kh, kw, Cin_w] f32.
+    int make_convw(const std::vector<std::string>& names, int kh, int kw, int cin, int act, const std::string& aff) {
+        const bool stem_split = stem;
+        stem = false;
+        DevConvW cw;
+        cw.Kh = kh;
+        cw.Kw = kw;
+        cw.Cin = cin;
+        cw.K = kh * kw * cin;
+        std::vector<float> wrows, bias, slope;
+        int cout = 0;
+        for (const auto& nm : names) {
+            const HostT* w = find(nm + ".w");
+            if (!w || w->dims.size() != 4 || w->dims[1] != kh || w->dims[2] != kw || w->dims[3] > cin) {
+                set_error("weights: missing or mis-shaped tensor " + nm + ".w");
+                rc = FR_ERR_WEIGHTS;
+                return -1;
+            }
+            const int co = (int)w->dims[0], ci = (int)w->dims[3];
+            if (stem_split && (ci != 3 || cin != 8)) {
+                set_error("plan: stem conv " + nm + " must have 3 input channels");
+                rc = FR_ERR_WEIGHTS;
+                return -1;
+            }
+            for (int o = 0; o < co; ++o)
+                for (int r = 0; r < kh; ++r)
+                    for (int s = 0; s < kw; ++s)
+                        for (int c = 0; c < cin; ++c) {
+                            if (stem_split) {
+                                // input channels are [q, q, 0, 0], q = 255*x: weights [hi, lo, 0, 0] of w/255
+                                const float wv = w->v[(((size_t)o * kh + r) * kw + s) * ci + (c % 3)] / 255.0f;
+                                const float hi = round16(wv);
+                                wrows.push_back(c < 3 ? hi : (c < 6 ? wv - hi : 0.f));
+                            } else {
+                                wrows.push_back(c < ci ? w->v[(((size_t)o * kh + r) * kw + s) * ci + c] : 0.f);
+                            }
+                        }
+            const HostT* b = find(nm + ".b");
+            for (int o = 0; o < co; ++o) bias.push_back(b ? b->v[o] : 0.f);
+            if (act == 2) {
+                const HostT* sl = find(nm + ".slope");
+                if (!sl) {
+                    set_error("weights: missing " + nm + ".slope");
+                    rc = FR_ERR_WEIGHTS;
+                    return -1;
+                }
+                for (int o = 0; o < co; ++o) slope.push_back(sl->v[o]);
+            }
+            cout += co;
+        }
+        cw.Cout = cout;
+        cw.Npad = round_up(cout, 128);
+        cw.Kpad = round_up(cw.K, 64);
+        std::vector<bf16_t> packed((size_t)cw.Npad * cw.Kpad, 0);
+        const bool f16 = h->dtype == FR_DTYPE_F16;
+        for (int o = 0; o < cout; ++o)
+            for (int k = 0; k < cw.K; ++k) {
+                const float v = wrows[(size_t)o * cw.K + k];
+                packed[(size_t)o * cw.Kpad + k] = f16 ? host_f2h(v) : host_f2bf(v);
+            }
+        bias.resize(cw.Npad, 0.f);
+        if ((rc = upload(h, &cw.w, packed))) return -1;
+        if ((rc = upload(h, &cw.bias, bias))) return -1;
+        if (act == 2) {
+            slope.resize(cw.Npad, 0.f);
+            if ((rc = upload(h, &cw.slope, slope))) return -1;
+        }
+        if (!aff.empty()) {
+            const HostT* s = find(aff + ".s");
+            const HostT* t = find(aff + ".t");
+            if (!s || !t || (int)s->v.size() != cout || (int)t->v.size() != cout) {
+                set_error("weights: missing or mis-sized affine " + aff + ".s/.t");
+                rc = FR_ERR_WEIGHTS;
+                return -1;
+            }
+            std::vector<float> sv = s->v, tv = t->v;
+            sv.resize(cw.Npad, 0.f);
+            tv.resize(cw.Npad, 0.f);
+            if ((rc = upload(h, &cw.aff_s, sv))) return -1;
+            if ((rc = upload(h, &cw.aff_b, tv))) return -1;
+        }
+        h->convw.push_back(cw);
+        return (int)h->convw.size() - 1;
+    }
+
+    // conv op; returns output spatial size through the out tensor (must already exist).
+    void conv(const std::vector<std::string>& names, int in, int in_off, int cin, int out, int out_off, int kh, int kw,
+              int sh, int sw, int ph, int pw, int act, int res = -1, int res_off = 0, int out2 = -1,
+              const std::string& aff = "") {
+        if (rc) return;
+        Op op;
+        op.kind = OP_CONV;
+        op.in = in; op.in_off = in_off; op.cin = cin;
+        op.out = out; op.out_off = out_off;
+        op.res = res; op.res_off = res_off; op.out2 = out2;
+        op.kh = kh; op.kw = kw; op.sh = sh; op.sw = sw; op.ph = ph; op.pw = pw; op.act = act;
+        op.wi = make_convw(names, kh, kw, cin, act, aff);
+        if (op.wi < 0) return;
+        const auto& ti = h->tensors[in];
+        const auto& to = h->tensors[out];
+        const int Ho = (ti.H + 2 * ph - kh) / sh + 1, Wo = (ti.W + 2 * pw - kw) / sw + 1;
+        const int cout = h->convw[op.wi].Cout;
+        if (Ho != to.H || Wo != to.W || out_off + cout > to.C || in_off + cin > ti.C ||
+            (res >= 0 && (h->tensors[res].H != Ho || res_off + cout > h->tensors[res].C))) {
+            set_error("plan: shape mismatch at conv " + names[0]);
+            rc = FR_ERR_ARG;
+            return;
+        }
+        h->ops.push_back(op);
+    }
+    void maxpool(int in, int out, int out_off, int k, int s, int p) {
+        Op op;
+        op.kind = OP_MAXPOOL;
+        op.in = in; op.out = out; op.out_off = out_off; op.pk = k; op.ps = s; op.pp = p;
+        op.cin = h->tensors[in].C;
+        h->ops.push_back(op);
+    }
+    void avgpool(int in, int out) {
+        Op op;
+        op.kind = OP_AVGPOOL;
+        op.in = in; op.out = out;
+        h->ops.push_back(op);
+    }
+    void head(int in) {
+        if (rc) return;
+        const HostT* w = find("head.w");
+        const auto& t = h->tensors[in];
+        const int K = t.H * t.W * t.C;
+        if (!w || w->dims.size() != 2 || w->dims[1] != K) {
+            set_error("weights: missing or mis-shaped head.w (expected [N, " + std::to_string(K) + "])");
+            rc = FR_ERR_WEIGHTS;
+            return;
+        }
+        W["head.__as_conv.w"] = HostT{{w->dims[0], 1, 1, K}, w->v};
+        if (find("head.b")) W["head.__as_conv.b"] = *find("head.b");
+        Op op;
+        op.kind = OP_HEAD;
+        op.in = in;
+        op.wi = make_convw({"head.__as_conv"}, 1, 1, K, 0, "");
+        if (op.wi < 0) return;
+        h->embed_dim = h->convw[op.wi].Cout;
+        h->ops.push_back(op);
+    }
+};
+
+std::string L(int l, int i) { return "layer" + std::to_string(l) + "." + std::to_string(i); }
+
+void build_iresnet100(Builder& b) {
+    fr_handle* h = b.h;
+    h->in_size = 112;
+    const int in = b.tensor(112, 112, 8);
+    h->ops.push_back(Op{OP_PRE, -1, 0, 0, in});
+    int x = b.tensor(112, 112, 64, "prelu"), xb = b.tensor(112, 112, 64, L(1, 0) + ".bn1");
+    b.stem = true;
+    b.conv({"conv1"}, in, 0, 8, x, 0, 3, 3, 1, 1, 1, 1, 2, -1, 0, xb, L(1, 0) + ".bn1");
+    const int planes[4] = {64, 128, 256, 512}, nblk[4] = {3, 13, 30, 3};
+    int H = 112, C = 64;
+    for (int l = 0; l < 4; ++l) {
+        const int P = planes[l], Ho = H / 2;
+        for (int i = 0; i < nblk[l]; ++i) {
+            const std::string pre = L(l + 1, i);
+            const int Hin = i == 0 ? H : Ho, st = i == 0 ? 2 : 1;
+            const int hmid = b.tensor(Hin, Hin, P, pre + ".prelu");
+            b.conv({pre + ".conv1"}, xb, 0, C, hmid, 0, 3, 3, 1, 1, 1, 1, 2);
+            int res = x;
+            if (i == 0) {
+                res = b.tensor(Ho, Ho, P, pre + ".downsample");
+                b.conv({pre + ".downsample"}, x, 0, C, res, 0, 1, 1, 2, 2, 0, 0, 0);
+            }
+            std::string next;
+            if (i + 1 < nblk[l]) next = L(l + 1, i + 1) + ".bn1";
+            else if (l + 1 < 4) next = L(l + 2, 0) + ".bn1";
+            const int y = b.tensor(Ho, Ho, P, pre);
+            const int yb = next.empty() ? -1 : b.tensor(Ho, Ho, P, next);
+            b.conv({pre + ".conv2"}, hmid, 0, P, y, 0, 3, 3, st, st, 1, 1, 0, res, 0, yb, next);
+            x = y;
+            xb = yb;
+            C = P;
+        }
+        H = Ho;
+    }
+    b.head(x);
+}
+
+void build_resnet50(Builder& b) {
+    fr_handle* h = b.h;
+    h->in_size = 112;
+    const int in = b.tensor(112, 112, 8);
+    h->ops.push_back(Op{OP_PRE, -1, 0, 0, in});
+    const int c1 = b.tensor(56, 56, 64, "backbone.relu");
+    b.stem = true;
+    b.conv({"backbone.conv1"}, in, 0, 8, c1, 0, 7, 7, 2, 2, 3, 3, 1);
+    int x = b.tensor(28, 28, 64, "backbone.maxpool");
+    b.maxpool(c1, x, 0, 3, 2, 1);
+    const int planes[4] = {64, 128, 256, 512}, nblk[4] = {3, 4, 6, 3}, strd[4] = {1, 2, 2, 2};
+    int H = 28, C = 64;
+    for (int l = 0; l < 4; ++l) {
+        const int P = planes[l];
+        for (int i = 0; i < nblk[l]; ++i) {
+            const std::string pre = "backbone." + L(l + 1, i);
+            const int s = i == 0 ? strd[l] : 1;
+            const int Ho = (H + 2 - 3) / s + 1;
+            const int h1 = b.tensor(H, H, P);
+            b.conv({pre + ".conv1"}, x, 0, C, h1, 0, 1, 1, 1, 1, 0, 0, 1);
+            const int h2 = b.tensor(Ho, Ho, P);
+            b.conv({pre + ".conv2"}, h1, 0, P, h2, 0, 3, 3, s, s, 1, 1, 1);
+            int id = x;
+            if (i == 0) {
+                id = b.tensor(Ho, Ho, 4 * P, pre + ".downsample");
+                b.conv({pre + ".downsample"}, x, 0, C, id, 0, 1, 1, s, s, 0, 0, 0);
+            }
+            const int y = b.tensor(Ho, Ho, 4 * P, pre);
+            b.conv({pre + ".conv3"}, h2, 0, P, y, 0, 1, 1, 1, 1, 0, 0, 1, id, 0);
+            x = y;
+            C = 4 * P;
+            H = Ho;
+        }
+    }
+    const int pool = b.tensor(1, 1, C, "backbone.avgpool");
+    b.avgpool(x, pool);
+    b.head(pool);
+}
+
+void build_irv1(Builder& b) {
+    fr_handle* h = b.h;
+    h->in_size = 160;
+    const std::string m = "model.";
+    const int in = b.tensor(160, 160, 8);
+    h->ops.push_back(Op{OP_PRE, -1, 0, 0, in});
+    const int a = b.tensor(79, 79, 32, m + "conv2d_1a");
+    b.stem = true;
+    b.conv({m + "conv2d_1a"}, in, 0, 8, a, 0, 3, 3, 2, 2, 0, 0, 1);
+    const int bb = b.tensor(77, 77, 32, m + "conv2d_2a");
+    b.conv({m + "conv2d_2a"}, a, 0, 32, bb, 0, 3, 3, 1, 1, 0, 0, 1);
+    const int c = b.tensor(77, 77, 64, m + "conv2d_2b");
+    b.conv({m + "conv2d_2b"}, bb, 0, 32, c, 0, 3, 3, 1, 1, 1, 1, 1);
+    const int d = b.tensor(38, 38, 64, m + "maxpool_3a");
+    b.maxpool(c, d, 0, 3, 2, 0);
+    const int e = b.tensor(38, 38, 80, m + "conv2d_3b");
+    b.conv({m + "conv2d_3b"}, d, 0, 64, e, 0, 1, 1, 1, 1, 0, 0, 1);
+    const int f = b.tensor(36, 36, 192, m + "conv2d_4a");
+    b.conv({m + "conv2d_4a"}, e, 0, 80, f, 0, 3, 3, 1, 1, 0, 0, 1);
+    int x = b.tensor(17, 17, 256, m + "conv2d_4b");
+    b.conv({m + "conv2d_4b"}, f, 0, 192, x, 0, 3, 3, 2, 2, 0, 0, 1);
+    // repeat_1: Block35 x5 @17x17. cat layout [t1 | t2 | b0 | b1 | b2]; conv2d reads [64:160].
+    for (int i = 0; i < 5; ++i) {
+        const std::string p = m + "repeat_1." + std::to_string(i) + ".";
+        const int cat = b.tensor(17, 17, 160);
+        b.conv({p + "branch1.0", p + "branch2.0", p + "branch0"}, x, 0, 256, cat, 0, 1, 1, 1, 1, 0, 0, 1);
+        b.conv({p + "branch1.1"}, cat, 0, 32, cat, 96, 3, 3, 1, 1, 1, 1, 1);
+        const int t = b.tensor(17, 17, 32);
+        b.conv({p + "branch2.1"}, cat, 32, 32, t, 0, 3, 3, 1, 1, 1, 1, 1);
+        b.conv({p + "branch2.2"}, t, 0, 32, cat, 128, 3, 3, 1, 1, 1, 1, 1);
+        const int y = b.tensor(17, 17, 256, m + "repeat_1." + std::to_string(i));
+        b.conv({p + "conv2d"}, cat, 64, 96, y, 0, 1, 1, 1, 1, 0, 0, 1, x, 0);
+        x = y;
+    }
+    {  // mixed_6a
+        const std::string p = m + "mixed_6a.";
+        const int cat = b.tensor(8, 8, 896, m + "mixed_6a");
+        b.conv({p + "branch0"}, x, 0, 256, cat, 0, 3, 3, 2, 2, 0, 0, 1);
+        const int u = b.tensor(17, 17, 192), v = b.tensor(17, 17, 192);
+        b.conv({p + "branch1.0"}, x, 0, 256, u, 0, 1, 1, 1, 1, 0, 0, 1);
+        b.conv({p + "branch1.1"}, u, 0, 192, v, 0, 3, 3, 1, 1, 1, 1, 1);
+        b.conv({p + "branch1.2"}, v, 0, 192, cat, 384, 3, 3, 2, 2, 0, 0, 1);
+        b.maxpool(x, cat, 640, 3, 2, 0);
+        x = cat;
+    }
+    // repeat_2: Block17 x10 @8x8. cat layout [t1 | b0 | b1]; conv2d reads [128:384].
+    for (int i = 0; i < 10; ++i) {
+        const std::string p = m + "repeat_2." + std::to_string(i) + ".";
+        const int cat = b.tensor(8, 8, 384);
+        b.conv({p + "branch1.0", p + "branch0"}, x, 0, 896, cat, 0, 1, 1, 1, 1, 0, 0, 1);
+        const int t = b.tensor(8, 8, 128);
+        b.conv({p + "branch1.1"}, cat, 0, 128, t, 0, 1, 7, 1, 1, 0, 3, 1);
+        b.conv({p + "branch1.2"}, t, 0, 128, cat, 256, 7, 1, 1, 1, 3, 0, 1);
+        const int y = b.tensor(8, 8, 896, m + "repeat_2." + std::to_string(i));
+        b.conv({p + "conv2d"}, cat, 128, 256, y, 0, 1, 1, 1, 1, 0, 0, 1, x, 0);
+        x = y;
+    }
+    {  // mixed_7a
+        const std::string p = m + "mixed_7a.";
+        const int cat = b.tensor(3, 3, 1792, m + "mixed_7a");
+        const int u = b.tensor(8, 8, 768);
+        b.conv({p + "branch0.0", p + "branch1.0", p + "branch2.0"}, x, 0, 896, u, 0, 1, 1, 1, 1, 0, 0, 1);
+        b.conv({p + "branch0.1"}, u, 0, 256, cat, 0, 3, 3, 2, 2, 0, 0, 1);
+        b.conv({p + "branch1.1"}, u, 256, 256, cat, 384, 3, 3, 2, 2, 0, 0, 1);
+        const int v = b.tensor(8, 8, 256);
+        b.conv({p + "branch2.1"}, u, 512, 256, v, 0, 3, 3, 1, 1, 1, 1, 1);
+        b.conv({p + "branch2.2"}, v, 0, 256, cat, 640, 3, 3, 2, 2, 0, 0, 1);
+        b.maxpool(x, cat, 896, 3, 2, 0);
+        x = cat;
+    }
+    // repeat_3: Block8 x5 + final block8 (noReLU) @3x3. cat layout [t1 | b0 | b1]; conv2d reads [192:576].
+    for (int i = 0; i < 6; ++i) {
+        const std::string p = i < 5 ? m + "repeat_3." + std::to_string(i) + "." : m + "block8.";
+        const int cat = b.tensor(3, 3, 576);
+        b.conv({p + "branch1.0", p + "branch0"}, x, 0, 1792, cat, 0, 1, 1, 1, 1, 0, 0, 1);
+        const int t = b.tensor(3, 3, 192);
+        b.conv({p + "branch1.1"}, cat, 0, 192, t, 0, 1, 3, 1, 1, 0, 1, 1);
+        b.conv({p + "branch1.2"}, t, 0, 192, cat, 384, 3, 1, 1, 1, 1, 0, 1);
+        const int y = b.tensor(3, 3, 1792, i < 5 ? m + "repeat_3." + std::to_string(i) : m + "block8");
+        b.conv({p + "conv2d"}, cat, 192, 384, y, 0, 1, 1, 1, 1, 0, 0, i < 5 ? 1 : 0, x, 0);
+        x = y;
+    }
+    const int pool = b.tensor(1, 1, 1792, m + "avgpool_1a");
+    b.avgpool(x, pool);
+    b.head(pool);
+}
+
+// ------------------------------------------------------------------ execution
+int choose_split(int tiles, int nkt) {
+    if (tiles >= 192 || nkt < 8) return 1;
+    int s = (512 + tiles - 1) / tiles;
+    s = std::min(s, nkt / 4);
+    return std::max(1, s);
+}
+
+int conv_tiles(int M, int Cout) {
+    const int BM = Cout <= 64 ? 256 : 128, BN = Cout <= 64 ? 64 : 128;
+    return ((M + BM - 1) / BM) * ((Cout + BN - 1) / BN);
+}
+
+size_t partial_need(fr_handle* h, int B) {
+    size_t need = 0;
+    for (const auto& op : h->ops) {
+        if (op.kind != OP_CONV && op.kind != OP_HEAD) continue;
+        const auto& cw = h->convw[op.wi];
+        int M;
+        if (op.kind == OP_HEAD) {
+            M = B;
+        } else {
+            const auto& to = h->tensors[op.out];
+            M = B * to.H * to.W;
+        }
+        int sp = choose_split(conv_tiles(M, cw.Cout), cw.Kpad / 64);
+        if (op.kind == OP_HEAD) sp = std::max(sp, 1);
+        if (sp > 1 || op.kind == OP_HEAD) need = std::max(need, (size_t)sp * M * cw.Npad);
+    }
+    return need;
+}
+
+int reserve(fr_handle* h, int maxB) {
+    if (maxB <= h->max_batch) return FR_OK;
+    free_acts(h);
+    for (auto& t : h->tensors) {
+        void* p = nullptr;
+        int rc = dev_alloc(&p, (size_t)maxB * t.H * t.W * t.C * sizeof(bf16_t));
+        if (rc) { free_acts(h); return rc; }
+        h->act_allocs.push_back(p);
+        t.dev = (bf16_t*)p;
+    }
+    size_t need = partial_need(h, maxB);
+    for (int b = 1; b < maxB; b *= 2) need = std::max(need, partial_need(h, b));
+    void* p = nullptr;
+    int rc = dev_alloc(&p, need * sizeof(float));
+    if (rc) { free_acts(h); return rc; }
+    h->act_allocs.push_back(p);
+    h->partial = (float*)p;
+    h->partial_floats = need;
+    h->max_batch = maxB;
+    return FR_OK;
+}
+
+int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
+    const int tiles = conv_tiles(a.M, a.Cout);
+    int split = a.partial ? std::max(1, a.split_k) : choose_split(tiles, a.Kpad / 64);
+    if (split > 1 && !a.partial) {
+        while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) --split;
+        if (split > 1) a.partial = h->partial;
+    }
+    a.split_k = split;
+    FR_HIP_CHECK(launch_conv(a, s));
+    if (split > 1 && a.y) FR_HIP_CHECK(launch_splitk_epilogue(a, s));
+    return FR_OK;
+}
+
+int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
+    const int f16 = h->dtype == FR_DTYPE_F16;
+    for (const auto& op : h->ops) {
+        switch (op.kind) {
+            case OP_PRE: {
+                const auto& t = h->tensors[op.out];
+                FR_HIP_CHECK(launch_preprocess(in, in_fmt, B, t.H, t.W, t.dev, f16, s));
+                break;
+            }
+            case OP_CONV: {
+                const auto& cw = h->convw[op.wi];
+                const auto& ti = h->tensors[op.in];
+                const auto& to = h->tensors[op.out];
+                ConvArgs a{};
+                a.f16 = f16;
+                a.x = ti.dev; a.B = B; a.H = ti.H; a.W = ti.W; a.Cx = ti.C; a.x_off = op.in_off; a.Cin = op.cin;
+                a.w = cw.w; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
+                a.K = cw.K; a.Kpad = cw.Kpad;
+                a.Ho = to.H; a.Wo = to.W; a.M = B * to.H * to.W; a.Cout = cw.Cout; a.Npad = cw.Npad;
+                a.bias = cw.bias; a.slope = cw.slope; a.act = op.act;
+                if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
+                a.y = to.dev; a.Cy = to.C; a.y_off = op.out_off;
+                if (op.out2 >= 0) {
+                    a.y2 = h->tensors[op.out2].dev; a.Cy2 = h->tensors[op.out2].C; a.y2_off = 0;
+                    a.aff_s = cw.aff_s; a.aff_b = cw.aff_b;
+                }
+                int rc = run_conv_args(h, a, s);
+                if (rc) return rc;
+                break;
+            }
+            case OP_MAXPOOL: {
+                const auto& ti = h->tensors[op.in];
+                const auto& to = h->tensors[op.out];
+                FR_HIP_CHECK(launch_maxpool(ti.dev, B, ti.H, ti.W, ti.C, 0, ti.C, op.pk, op.ps, op.pp, to.dev, to.C,
+                                            op.out_off, to.H, to.W, f16, s));
+                break;
+            }
+            case OP_AVGPOOL: {
+                const auto& ti = h->tensors[op.in];
+                FR_HIP_CHECK(launch_avgpool(ti.dev, B, ti.H, ti.W, ti.C, h->tensors[op.out].dev, f16, s));
+                break;
+            }
+            case OP_HEAD: {
+                const auto& cw = h->convw[op.wi];
+                const auto& ti = h->tensors[op.in];
+                ConvArgs a{};
+                a.f16 = f16;
+                a.x = ti.dev; a.B = B; a.H = 1; a.W = 1; a.Cx = cw.K; a.x_off = 0; a.Cin = cw.K;
+                a.w = cw.w; a.Kh = 1; a.Kw = 1; a.sh = 1; a.sw = 1; a.K = cw.K; a.Kpad = cw.Kpad;
+                a.Ho = 1; a.Wo = 1; a.M = B; a.Cout = cw.Cout; a.Npad = cw.Npad;
+                int split = choose_split(conv_tiles(B, cw.Cout), cw.Kpad / 64);
+                while (split > 1 && (size_t)split * B * cw.Npad > h->partial_floats) --split;
+                a.split_k = split;
+                a.partial = h->partial;
+                FR_HIP_CHECK(launch_conv(a, s));
+                FR_HIP_CHECK(launch_head_finalize(h->partial, split, B, cw.Cout, cw.Npad, cw.bias,
+                                                  (flags & FR_EMBED_RAW) ? 0 : 1, out, s));
+                break;
+            }
+        }
+    }
+    return FR_OK;
+}
+
+bool valid_arch(int a) { return a == FR_ARCH_RESNET50_ARCFACE || a == FR_ARCH_IRESNET100 || a == FR_ARCH_IRV1_FACENET; }
+
+}  // namespace
+
+// ==================================================================== C ABI
+extern "C" {
+
+const char* fr_last_error(void) { return g_err.c_str(); }
+int fr_abi_version(void) { return FR_ABI_VERSION; }
+
+int fr_create(fr_handle** out, int device, int arch, int dtype) {
+    if (!out || !valid_arch(arch) || (dtype != FR_DTYPE_BF16 && dtype != FR_DTYPE_F16)) {
+        set_error("fr_create: bad argument (arch/dtype)");
+        return FR_ERR_ARG;
+    }
+    int n = 0;
+    FR_HIP_CHECK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) {
+        set_error("fr_create: device " + std::to_string(device) + " out of range (" + std::to_string(n) + ")");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(hipSetDevice(device));
+    auto* h = new fr_handle();
+    h->device = device;
+    h->arch = arch;
+    h->dtype = dtype;
+    h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
+    *out = h;
+    return FR_OK;
+}
+
+void fr_destroy(fr_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    free_acts(h);
+    free_weights(h);
+    if (h->gallery) (void)hipFree(h->gallery);
+    if (h->cand_s) (void)hipFree(h->cand_s);
+    if (h->cand_i) (void)hipFree(h->cand_i);
+    delete h;
+}
+
+int fr_load_weights(fr_handle* h, const void* blob, size_t nbytes) {
+    if (!h || !blob) { set_error("fr_load_weights: null argument"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    std::unordered_map<std::string, HostT> W;
+    int rc = parse_blob(blob, nbytes, W);
+    if (rc) return rc;
+    const int keep_batch = h->max_batch;
+    free_acts(h);
+    free_weights(h);
+    h->tensors.clear();
+    h->ops.clear();
+    h->loaded = false;
+    Builder b{h, W};
+    if (h->arch == FR_ARCH_IRESNET100) build_iresnet100(b);
+    else if (h->arch == FR_ARCH_RESNET50_ARCFACE) build_resnet50(b);
+    else build_irv1(b);
+    if (b.rc) {
+        free_weights(h);
+        h->tensors.clear();
+        h->ops.clear();
+        return b.rc;
+    }
+    h->loaded = true;
+    if (keep_batch > 0) return reserve(h, keep_batch);
+    return FR_OK;
+}
+
+int fr_reserve(fr_handle* h, int max_batch) {
+    if (!h || max_batch <= 0) { set_error("fr_reserve: bad argument"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->loaded) { set_error("fr_reserve: weights not loaded"); return FR_ERR_STATE; }
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    return reserve(h, max_batch);
+}
+
+int fr_embed_dim(const fr_handle* h) { return h ? h->embed_dim : 0; }
+int fr_input_size(const fr_handle* h) { return h ? h->in_size : 0; }
+
+static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, float* out, int flags,
+                        void* stream) {
+    if (!h->loaded) { set_error("fr_embed: weights not loaded"); return FR_ERR_STATE; }
+    if (!in || !out || B <= 0) { set_error("fr_embed: bad argument"); return FR_ERR_ARG; }
+    if (H != h->in_size || W != h->in_size) {
+        set_error("fr_embed: input must be " + std::to_string(h->in_size) + "x" + std::to_string(h->in_size) +
+                  " (got " + std::to_string(H) + "x" + std::to_string(W) + ")");
+        return FR_ERR_ARG;
+    }
+    if (in_fmt != FR_IN_U8_NHWC && in_fmt != FR_IN_F32_NCHW) { set_error("fr_embed: bad in_fmt"); return FR_ERR_ARG; }
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    if (B > h->max_batch) {
+        int rc = reserve(h, B);
+        if (rc) return rc;
+    }
+    return forward(h, in, in_fmt, B, out, flags, (hipStream_t)stream);
+}
+
+int fr_embed(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, float* out, int flags, void* stream) {
+    if (!h) { set_error("fr_embed: null handle"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    return embed_locked(h, in, in_fmt, B, H, W, out, flags, stream);
+}
+
+int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index_base, int g_on_device) {
+    if (!h || (!G && N > 0) || N < 0 || D <= 0 || D % 4 != 0 || N + index_base > INT32_MAX) {
+        set_error("fr_gallery_set: bad argument (D must be a multiple of 4, indices must fit int32)");
+        return FR_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    if (h->gallery) { (void)hipFree(h->gallery); h->gallery = nullptr; }
+    h->g_rows = 0;
+    if (N > 0) {
+        void* p = nullptr;
+        int rc = dev_alloc(&p, (size_t)N * D * sizeof(float));
+        if (rc) return rc;
+        h->gallery = (float*)p;
+        FR_HIP_CHECK(hipMemcpy(p, G, (size_t)N * D * sizeof(float),
+                               g_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+        FR_HIP_CHECK(launch_gallery_prepare(h->gallery, N, D, nullptr));
+        FR_HIP_CHECK(hipDeviceSynchronize());
+    }
+    h->g_rows = N;
+    h->g_dim = D;
+    h->g_base = index_base;
+    return FR_OK;
+}
+
+int64_t fr_gallery_rows(const fr_handle* h) { return h ? h->g_rows : 0; }
+
+static int match_locked(fr_handle* h, const float* P, int B, int k, float* scores, int32_t* idx, void* stream) {
+    if (!P || !scores || !idx || B <= 0 || k <= 0 || k > 16) {
+        set_error("fr_match_topk: bad argument (1 <= k <= 16)");
+        return FR_ERR_ARG;
+    }
+    if (!h->gallery || h->g_rows <= 0) { set_error("fr_match_topk: no gallery"); return FR_ERR_STATE; }
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    int n_split;
+    int64_t rps;
+    match_split_plan(B, h->g_rows, &n_split, &rps);
+    const size_t need = (size_t)B * n_split * k;
+    if (need > h->cand_cap) {
+        if (h->cand_s) (void)hipFree(h->cand_s);
+        if (h->cand_i) (void)hipFree(h->cand_i);
+        h->cand_s = nullptr;
+        h->cand_i = nullptr;
+        h->cand_cap = 0;
+        int rc = dev_alloc((void**)&h->cand_s, need * sizeof(float));
+        if (rc) return rc;
+        rc = dev_alloc((void**)&h->cand_i, need * sizeof(int32_t));
+        if (rc) return rc;
+        h->cand_cap = need;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    FR_HIP_CHECK(launch_match_topk(P, B, h->gallery, h->g_rows, h->g_dim, k, h->g_base, h->cand_s, h->cand_i,
+                                   n_split, rps, s));
+    FR_HIP_CHECK(launch_topk_merge(h->cand_s, h->cand_i, B, n_split, k, scores, idx, s));
+    return FR_OK;
+}
+
+int fr_match_topk(fr_handle* h, const float* P, int B, int k, float* scores, int32_t* idx, void* stream) {
+    if (!h) { set_error("fr_match_topk: null handle"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    return match_locked(h, P, B, k, scores, idx, stream);
+}
+
+int fr_topk_merge(const float* cand_s, const int32_t* cand_i, int B, int n_lists, int k, float* scores,
+                  int32_t* idx, void* stream) {
+    if (!cand_s || !cand_i || !scores || !idx || B <= 0 || n_lists <= 0 || k <= 0 || k > 16) {
+        set_error("fr_topk_merge: bad argument");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_topk_merge(cand_s, cand_i, B, n_lists, k, scores, idx, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_embed_match(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, int k, float* emb_out,
+                   float* scores, int32_t* idx, void* stream) {
+    if (!h) { set_error("fr_embed_match: null handle"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = embed_locked(h, in, in_fmt, B, H, W, emb_out, 0, stream);
+    if (rc) return rc;
+    return match_locked(h, emb_out, B, k, scores, idx, stream);
+}
+
+int fr_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, int n_seg, float* out, void* stream) {
+    if (!E || !seg_start || !out || D <= 0 || n_seg <= 0) { set_error("fr_segment_mean_normalize: bad argument"); return FR_ERR_ARG; }
+    FR_HIP_CHECK(launch_segment_mean_normalize(E, D, seg_start, n_seg, out, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_debug_tensor_count(const fr_handle* h) { return h ? (int)h->tensors.size() : 0; }
+
+const char* fr_debug_tensor_name(const fr_handle* h, int t) {
+    if (!h || t < 0 || t >= (int)h->tensors.size()) return "";
+    return h->tensors[t].name.c_str();
+}
+
+int fr_debug_tensor_shape(const fr_handle* h, int t, int* H, int* W, int* C) {
+    if (!h || t < 0 || t >= (int)h->tensors.size() || !H || !W || !C) { set_error("fr_debug_tensor_shape: bad argument"); return FR_ERR_ARG; }
+    *H = h->tensors[t].H; *W = h->tensors[t].W; *C = h->tensors[t].C;
+    return FR_OK;
+}
+
+int fr_debug_copy_tensor(fr_handle* h, int t, int B, void* dst, void* stream) {
+    if (!h || t < 0 || t >= (int)h->tensors.size() || !dst || B <= 0 || B > h->max_batch || !h->tensors[t].dev) {
+        set_error("fr_debug_copy_tensor: bad argument (tensor id / batch / not reserved)");
+        return FR_ERR_ARG;
+    }
+    const auto& d = h->tensors[t];
+    FR_HIP_CHECK(hipMemcpyAsync(dst, d.dev, (size_t)B * d.H * d.W * d.C * sizeof(bf16_t), hipMemcpyDeviceToDevice,
+                                (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
+    if (!d || !d->x || !d->w || !d->y || d->B <= 0 || d->Cin <= 0 || d->Cin % 8 || d->Cx % 8 || d->x_off % 8 ||
+        d->Cout <= 0 || d->Cout % 8 || d->Cy % 8 || d->y_off % 8 || d->Npad % 128 || d->Kpad % 64 ||
+        d->Npad < d->Cout || d->Kpad < d->Kh * d->Kw * d->Cin || d->x_off + d->Cin > d->Cx ||
+        d->y_off + d->Cout > d->Cy || (d->act == 2 && !d->slope) || (d->res && (d->Cres % 8 || d->res_off % 8)) ||
+        (d->y2 && (!d->aff_s || !d->aff_b || d->Cy2 % 8 || d->y2_off % 8)) || d->stride_h <= 0 || d->stride_w <= 0) {
+        set_error("fr_op_conv2d: bad descriptor (see alignment rules in frhip.h)");
+        return FR_ERR_ARG;
+    }
+    ConvArgs a{};
+    a.x = (const bf16_t*)d->x; a.B = d->B; a.H = d->H; a.W = d->W; a.Cx = d->Cx; a.x_off = d->x_off; a.Cin = d->Cin;
+    a.w = (const bf16_t*)d->w; a.Kh = d->Kh; a.Kw = d->Kw; a.sh = d->stride_h; a.sw = d->stride_w;
+    a.ph = d->pad_h; a.pw = d->pad_w; a.K = d->Kh * d->Kw * d->Cin; a.Kpad = d->Kpad;
+    a.Ho = d->Ho ? d->Ho : (d->H + 2 * d->pad_h - d->Kh) / d->stride_h + 1;
+    a.Wo = d->Wo ? d->Wo : (d->W + 2 * d->pad_w - d->Kw) / d->stride_w + 1;
+    a.M = d->B * a.Ho * a.Wo; a.Cout = d->Cout; a.Npad = d->Npad;
+    a.bias = d->bias; a.slope = d->slope; a.act = d->act;
+    a.res = (const bf16_t*)d->res; a.Cres = d->Cres; a.res_off = d->res_off;
+    a.y = (bf16_t*)d->y; a.Cy = d->Cy; a.y_off = d->y_off;
+    a.y2 = (bf16_t*)d->y2; a.Cy2 = d->Cy2; a.y2_off = d->y2_off; a.aff_s = d->aff_s; a.aff_b = d->aff_b;
+    a.f16 = d->dtype == FR_DTYPE_F16;
+    if (d->split_k > 1) {
+        if (!d->partial) { set_error("fr_op_conv2d: split_k > 1 needs partial workspace"); return FR_ERR_ARG; }
+        a.split_k = d->split_k;
+        a.partial = d->partial;
+        FR_HIP_CHECK(launch_conv(a, (hipStream_t)stream));
+        FR_HIP_CHECK(launch_splitk_epilogue(a, (hipStream_t)stream));
+    } else {
+        a.split_k = 1;
+        FR_HIP_CHECK(launch_conv(a, (hipStream_t)stream));
+    }
+    return FR_OK;
+}
+
+int fr_op_preprocess(const void* in, int in_fmt, int B, int H, int W, void* out, int dtype, void* stream) {
+    if (!in || !out || B <= 0 || H <= 0 || W <= 0 || (in_fmt != FR_IN_U8_NHWC && in_fmt != FR_IN_F32_NCHW)) {
+        set_error("fr_op_preprocess: bad argument");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_preprocess(in, in_fmt, B, H, W, (bf16_t*)out, dtype == FR_DTYPE_F16, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_op_maxpool(const void* x, int B, int H, int W, int Cx, int x_off, int C, int k, int stride, int pad, void* y,
+                  int Cy, int y_off, int Ho, int Wo, int dtype, void* stream) {
+    if (!x || !y || C % 8 || Cx % 8 || x_off % 8 || Cy % 8 || y_off % 8 || k <= 0 || stride <= 0 || pad < 0 ||
+        pad >= k) {
+        set_error("fr_op_maxpool: bad argument");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_maxpool((const bf16_t*)x, B, H, W, Cx, x_off, C, k, stride, pad, (bf16_t*)y, Cy, y_off, Ho,
+                                Wo, dtype == FR_DTYPE_F16, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_op_avgpool(const void* x, int B, int H, int W, int C, void* y, int dtype, void* stream) {
+    if (!x || !y || C % 8) { set_error("fr_op_avgpool: bad argument"); return FR_ERR_ARG; }
+    FR_HIP_CHECK(launch_avgpool((const bf16_t*)x, B, H, W, C, (bf16_t*)y, dtype == FR_DTYPE_F16, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, int Kpad, const float* bias,
+                 int normalize, float* out, int split_k, float* partial, int dtype, void* stream) {
+    if (!x || !w || !out || !partial || B <= 0 || K <= 0 || K % 8 || N <= 0 || N % 8 || Npad % 128 || Kpad % 64 ||
+        Npad < N || Kpad < K || split_k <= 0) {
+        set_error("fr_op_linear: bad argument");
+        return FR_ERR_ARG;
+    }
+    ConvArgs a{};
+    a.x = (const bf16_t*)x; a.B = B; a.H = 1; a.W = 1; a.Cx = K; a.x_off = 0; a.Cin = K;
+    a.w = (const bf16_t*)w; a.Kh = 1; a.Kw = 1; a.sh = 1; a.sw = 1; a.K = K; a.Kpad = Kpad;
+    a.Ho = 1; a.Wo = 1; a.M = B; a.Cout = N; a.Npad = Npad;
+    a.split_k = split_k;
+    a.partial = partial;
+    a.f16 = dtype == FR_DTYPE_F16;
+    FR_HIP_CHECK(launch_conv(a, (hipStream_t)stream));
+    FR_HIP_CHECK(launch_head_finalize(partial, split_k, B, N, Npad, bias, normalize, out, (hipStream_t)stream));
+    return FR_OK;
+}
+
+}  // extern "C"

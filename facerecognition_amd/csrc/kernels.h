@@ -1,0 +1,55 @@
+// Internal launcher interface between the C-ABI/graph runner (engine.cpp) and the
+// HIP kernels (conv_igemm.hip, misc.hip, match.hip).  Not part of the public ABI.
+#pragma once
+#include "common.h"
+
+namespace fr {
+
+// Implicit-GEMM convolution, NHWC bf16 in/out, f32 accumulate, fused epilogue.
+// GEMM view: M = B*Ho*Wo output pixels, N = Cout, K = Kh*Kw*Cin (c fastest).
+struct ConvArgs {
+    const bf16_t* x; int B, H, W, Cx, x_off, Cin;
+    const bf16_t* w; int Kh, Kw, sh, sw, ph, pw, K, Kpad;
+    int Ho, Wo, M, Cout, Npad;
+    const float* bias; const float* slope; int act;  // act: 0 none, 1 relu, 2 prelu
+    const bf16_t* res; int Cres, res_off;
+    bf16_t* y; int Cy, y_off;
+    bf16_t* y2; int Cy2, y2_off; const float* aff_s; const float* aff_b;
+    float* partial; int split_k;  // partial != null: raw f32 partials [split][M][Npad], no epilogue
+    int f16;                      // 0: bf16 storage + bf16 MFMA; 1: f16 storage + f16 MFMA
+};
+
+// Chooses a tile variant (and honours a.split_k); returns hipError_t.
+hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
+// Split-K reduction + the same fused epilogue as the conv kernel.
+hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
+// Number of K-tiles of 64 (for split-k planning).
+inline int conv_k_tiles(int Kpad) { return Kpad / 64; }
+
+// Input prep: channels [q0,q1,q2,q0,q1,q2,0,0] with q = 2u-255 (u8: exact in bf16/f16) or
+// q = 255*x (normalized f32).  The stem conv folds 1/255 and a hi/lo weight split into the
+// duplicated channels, so x = (u/255-0.5)/0.5 enters the first conv without rounding.
+hipError_t launch_preprocess(const void* in, int in_fmt, int B, int H, int W, bf16_t* out, int f16, hipStream_t s);
+hipError_t launch_maxpool(const bf16_t* x, int B, int H, int W, int Cx, int x_off, int C, int k, int stride,
+                          int pad, bf16_t* y, int Cy, int y_off, int Ho, int Wo, int f16, hipStream_t s);
+hipError_t launch_avgpool(const bf16_t* x, int B, int H, int W, int C, bf16_t* y, int f16, hipStream_t s);
+// Sum split-K partials [split][B][Npad] + bias, optional L2 normalize → out [B][N] f32.
+hipError_t launch_head_finalize(const float* partial, int split, int B, int N, int Npad, const float* bias,
+                                int normalize, float* out, hipStream_t s);
+// Row-wise L2 normalize in place (F.normalize, eps 1e-12).
+hipError_t launch_l2norm_rows(float* x, int B, int D, hipStream_t s);
+
+// Gallery match.
+hipError_t launch_match_topk(const float* P, int B, const float* G, int64_t N, int D, int k,
+                             int64_t index_base, float* cand_s, int32_t* cand_i, int n_split,
+                             int64_t rows_per_split, hipStream_t s);
+hipError_t launch_topk_merge(const float* cs, const int32_t* ci, int B, int n_lists, int k, float* out_s,
+                             int32_t* out_i, hipStream_t s);
+// Choose n_split / rows_per_split for a (B, N) match.
+void match_split_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split);
+hipError_t launch_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, int n_seg,
+                                         float* out, hipStream_t s);
+// Gallery preparation: rows with |‖g‖-1| >= 1e-3 divided by ‖g‖ (cosine_similarity semantics).
+hipError_t launch_gallery_prepare(float* G, int64_t N, int D, hipStream_t s);
+
+}  // namespace fr

@@ -1,0 +1,106 @@
+"""Device-resident gallery with exact inner-product top-k (libfrhip match kernel).
+
+Drop-in for the reference's three match paths:
+  * ``RecognitionEngine.recognize_with_db`` — per-row ``cosine_similarity`` loop + stable
+    ``sort(reverse=True)`` (inference/recognition_engine.py:267-289, :41-63);
+  * FAISS ``IndexFlatIP`` (``build_faiss_index`` extract_embeddings.py:595-645, searched in
+    recognition_engine.py:291-326) — ``DeviceGallery`` exposes the same ``add``/``search``/
+    ``ntotal`` surface, ``search`` returning (scores, ids) with ids int64 and -1 padding;
+  * the notebook's batched ``np.dot(emb, P.T)`` + ``argmax``/``argsort[:, -5:]``.
+Order is (score desc, index asc) everywhere, i.e. ``np.argmax``'s first-max rule and the
+stable sort's insertion order on ties.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _native as N
+
+
+class DeviceGallery:
+    def __init__(self, rows=None, dim: int = 512, device: int = 0, index_base: int = 0, handle=None):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("DeviceGallery needs a ROCm GPU; there is deliberately no CPU fallback")
+        self.device = torch.device("cuda", device)
+        self.d = dim
+        self.index_base = int(index_base)
+        self._own = handle is None
+        if handle is None:
+            h = ctypes.c_void_p()
+            N.check(N.lib().fr_create(ctypes.byref(h), device, 0, N.FR_DTYPE_BF16), "fr_create")
+            handle = h
+        self._h = handle
+        self._rows = torch.empty((0, dim), dtype=torch.float32)
+        if rows is not None:
+            self.add(rows)
+
+    @property
+    def ntotal(self) -> int:
+        return int(self._rows.shape[0])
+
+    def reset(self) -> None:
+        import torch
+        self._rows = torch.empty((0, self.d), dtype=torch.float32)
+        N.check(N.lib().fr_gallery_set(self._h, None, 0, self.d, self.index_base, 0), "fr_gallery_set")
+
+    def add(self, rows) -> None:
+        """Append rows (IndexFlatIP.add); re-uploads the whole matrix (gallery builds are rare)."""
+        import torch
+
+        r = torch.as_tensor(np.asarray(rows, dtype=np.float32) if not torch.is_tensor(rows) else rows)
+        r = r.detach().float().cpu().reshape(-1, self.d)
+        self._rows = torch.cat([self._rows, r], 0).contiguous()
+        self._upload()
+
+    def set_device_rows(self, rows_dev) -> None:
+        """Install rows already resident on the GPU (no host round trip)."""
+        rows_dev = rows_dev.float().contiguous()
+        self._rows = rows_dev.detach().cpu()
+        N.check(N.lib().fr_gallery_set(self._h, N.ptr(rows_dev), int(rows_dev.shape[0]), self.d, self.index_base, 1),
+                "fr_gallery_set")
+
+    def _upload(self) -> None:
+        N.check(N.lib().fr_gallery_set(self._h, N.ptr(self._rows), self.ntotal, self.d, self.index_base, 0),
+                "fr_gallery_set")
+
+    def search_device(self, probes_dev, k: int):
+        """probes_dev: cuda f32 [B, D] → (scores [B,k] f32, idx [B,k] int32) on the device."""
+        import torch
+
+        p = probes_dev.float().contiguous()
+        B = int(p.shape[0])
+        s = torch.empty((B, k), dtype=torch.float32, device=self.device)
+        i = torch.empty((B, k), dtype=torch.int32, device=self.device)
+        N.check(N.lib().fr_match_topk(self._h, N.ptr(p), B, k, N.ptr(s), N.ptr(i), N.stream_ptr(self.device)),
+                "fr_match_topk")
+        return s, i
+
+    def search(self, probes, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        """IndexFlatIP.search: (scores [B,k] f32, ids [B,k] int64, -1 where fewer than k rows)."""
+        import torch
+
+        p = torch.as_tensor(np.asarray(probes, dtype=np.float32) if not torch.is_tensor(probes) else probes)
+        p = p.reshape(-1, self.d).to(self.device)
+        if p.shape[0] == 0:
+            return np.zeros((0, k), np.float32), np.zeros((0, k), np.int64)
+        if self.ntotal == 0:
+            B = p.shape[0]
+            return np.full((B, k), -np.inf, np.float32), np.full((B, k), -1, np.int64)
+        s, i = self.search_device(p, k)
+        return s.cpu().numpy(), i.cpu().numpy().astype(np.int64)
+
+    def close(self) -> None:
+        if self._own and getattr(self, "_h", None):
+            N.lib().fr_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,174 @@
+/*
+ * frhip.h — C ABI of the MI355X-native face-embedding + gallery-match path.
+ *
+ * This is the drop-in boundary for the hot path of sin0235/FaceRecognition
+ * (SURVEY.md §8a/§8b).  The reference has no FFI layer: its boundary is the
+ * Python call `model(x, labels=None)` / `model(x)` plus the match loops.
+ * Each entry point below names the reference interface it replaces
+ * (paths relative to the reference root).  Plain C types only: device
+ * buffers are passed as raw pointers (e.g. torch `tensor.data_ptr()`),
+ * streams as `void*` (a hipStream_t, e.g. torch `current_stream().cuda_stream`),
+ * and every function returns FR_OK (0) or a negative FR_ERR_* code with a
+ * thread-local message in fr_last_error().
+ */
+#ifndef FRHIP_H
+#define FRHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FR_ABI_VERSION 1
+
+/* ---- status codes (reference error convention: SURVEY.md §8b row "Error convention") ---- */
+#define FR_OK 0
+#define FR_ERR_ARG (-1)     /* bad argument / unsupported shape              */
+#define FR_ERR_HIP (-2)     /* a HIP runtime call failed                      */
+#define FR_ERR_WEIGHTS (-3) /* weight blob malformed or tensor missing        */
+#define FR_ERR_STATE (-4)   /* call order violated (no weights, no gallery)   */
+#define FR_ERR_OOM (-5)     /* device allocation failed                       */
+
+/* ---- backbone architectures ---- */
+#define FR_ARCH_RESNET50_ARCFACE 0 /* models/arcface/arcface_model.py:65-202 (ArcFaceModel, ResNet-50 trunk) */
+#define FR_ARCH_IRESNET100 1       /* insightface iresnet100 (README.md:72 only; no reference code)         */
+#define FR_ARCH_IRV1_FACENET 2     /* models/facenet/facenet_model.py:7-36 (facenet_pytorch InceptionResnetV1) */
+
+/* ---- compute dtypes ---- */
+#define FR_DTYPE_BF16 0 /* bf16 activations/weights, f32 accumulate (v_mfma_f32_16x16x32_bf16) */
+#define FR_DTYPE_F16 1  /* f16 activations/weights, f32 accumulate (v_mfma_f32_16x16x32_f16): same MFMA
+                           rate, 3 more mantissa bits; stores saturate at +-65504 */
+
+/* ---- input formats accepted by fr_embed ---- */
+#define FR_IN_U8_NHWC 0  /* aligned crops, u8 [B,H,W,3] RGB; ToTensor+Normalize(0.5,0.5) fused (extract_embeddings.py:170-185) */
+#define FR_IN_F32_NCHW 1 /* already-normalized f32 [B,3,H,W], i.e. the output of get_transform()                             */
+
+/* ---- fr_embed flags ---- */
+#define FR_EMBED_RAW 1 /* return the un-normalized head output (= model(x, labels=None)); default is F.normalize'd */
+
+typedef struct fr_handle fr_handle;
+
+/* Thread-local message describing the last failure on this thread ("" if none). */
+const char* fr_last_error(void);
+int fr_abi_version(void);
+
+/* Create a handle bound to HIP device `device`.
+ * Replaces: ArcFaceModel(...)/FaceNetModel(...) construction in
+ * load_arcface_model (inference/extract_embeddings.py:80-123) and
+ * load_facenet_model (:126-167). */
+int fr_create(fr_handle** out, int device, int arch, int dtype);
+void fr_destroy(fr_handle* h);
+
+/* Load BN-folded weights (FRW1 blob written by facerecognition_amd/weights.py).
+ * Replaces: model.load_state_dict(checkpoint['model_state_dict'])
+ * (inference/extract_embeddings.py:104-106, :150-153). */
+int fr_load_weights(fr_handle* h, const void* blob, size_t nbytes);
+
+/* Pre-allocate activation workspace for batches up to max_batch (no allocation
+ * happens inside fr_embed once reserved, so it can be stream-captured). */
+int fr_reserve(fr_handle* h, int max_batch);
+
+/* Embedding dimension (512) and the square input side the arch expects (112/160). */
+int fr_embed_dim(const fr_handle* h);
+int fr_input_size(const fr_handle* h);
+
+/* Forward pass: `in` (device) → `out` (device f32 [B, embed_dim]).
+ * Replaces: `model(x, labels=None)` + `F.normalize(p=2, dim=1)` in
+ * extract_embedding_single (inference/extract_embeddings.py:377-382) and
+ * extract_embeddings_batch (:430-435); FaceNetModel.forward (facenet_model.py:28-36). */
+int fr_embed(fr_handle* h, const void* in, int in_fmt, int B, int H, int W,
+             float* out, int flags, void* stream);
+
+/* ---- gallery + match (replaces RecognitionEngine.recognize_with_db's loop,
+ *      recognition_engine.py:267-289, the notebook np.dot+argmax/argsort,
+ *      evaluate_arcface_kaggle.ipynb cells 15-16, and faiss IndexFlatIP.search,
+ *      recognition_engine.py:291-326) ---- */
+
+/* Install gallery rows G [N, D] f32 (host or device memory).  Rows whose L2
+ * norm differs from 1 by >= 1e-3 are divided by their norm so that the stored
+ * dot product equals cosine_similarity (recognition_engine.py:41-63); zero rows
+ * stay zero (score 0.0).  `index_base` is added to every returned index (gallery
+ * sharding: rank r passes the global row of its first shard row). */
+int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index_base, int g_on_device);
+int64_t fr_gallery_rows(const fr_handle* h);
+
+/* Top-k of P [B, D] (device f32, L2-normalized probes) against the gallery.
+ * Results (device): scores [B, k] f32 descending, idx [B, k] int32; ties are
+ * broken by lower index (stable sort(reverse=True) / np.argmax semantics).
+ * Rows past the gallery end come back as score -inf, idx -1.  k <= 16. */
+int fr_match_topk(fr_handle* h, const float* P, int B, int k, float* scores, int32_t* idx, void* stream);
+
+/* Merge n_lists candidate lists per probe: cand_s/cand_i [B, n_lists, k] → [B, k]
+ * with the same (score desc, index asc) order.  Used after the RCCL all-gather of
+ * per-shard candidates. */
+int fr_topk_merge(const float* cand_s, const int32_t* cand_i, int B, int n_lists, int k,
+                  float* scores, int32_t* idx, void* stream);
+
+/* Fused convenience: fr_embed (normalized) then fr_match_topk on the same stream. */
+int fr_embed_match(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, int k,
+                   float* emb_out, float* scores, int32_t* idx, void* stream);
+
+/* Segmented mean + renormalize (gallery construction: extract_embedding_for_folder
+ * inference/extract_embeddings.py:755-760, compute_prototypes :555-592,
+ * RecognitionEngine.add_to_db recognition_engine.py:411-413):
+ * out[s] = m / (||m|| + 1e-8), m = mean of E[seg_start[s] .. seg_start[s+1]) (device). */
+int fr_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, int n_seg,
+                              float* out, void* stream);
+
+/* ---- op-level entry points (kernel parity tests and custom graphs) ---- */
+
+/* Implicit-GEMM convolution on NHWC bf16 with fused epilogue:
+ *   y = act( conv(x, w) + bias + res )   written to y[..., y_off : y_off+Cout]
+ *   y2 = y * aff_s + aff_b                (optional second output, bf16)
+ * Weights: bf16 [Npad][Kpad], row n = output channel, K ordered (r, s, c) with
+ * c fastest (KRSC), zero padded; Npad % 128 == 0, Kpad % 64 == 0.
+ * Requirements: Cin % 8 == 0, Cx/x_off/Cy/y_off/Cres/res_off % 8 == 0, Cout % 8 == 0. */
+typedef struct fr_conv_desc {
+    const void* x; int B, H, W, Cx, x_off, Cin;  /* input tensor [B,H,W,Cx], channels [x_off, x_off+Cin) */
+    const void* w; int Cout, Kh, Kw, stride_h, stride_w, pad_h, pad_w, Npad, Kpad;
+    const float* bias;   /* [Cout] or NULL */
+    int act;             /* 0 none, 1 relu, 2 prelu (slope) */
+    const float* slope;  /* [Cout] for prelu */
+    const void* res; int Cres, res_off; /* residual [B,Ho,Wo,Cres] bf16 or NULL */
+    void* y; int Cy, y_off;             /* output [B,Ho,Wo,Cy] bf16 */
+    void* y2; int Cy2, y2_off; const float* aff_s; const float* aff_b; /* optional */
+    int Ho, Wo;          /* filled by fr_conv_out_shape if 0 */
+    int split_k;         /* 0/1 = fused epilogue; >1 = f32 partials into `partial` then reduce */
+    float* partial;      /* workspace [split_k, B*Ho*Wo, Npad] f32 when split_k > 1 */
+    int dtype;           /* FR_DTYPE_BF16 / FR_DTYPE_F16: element type of x, w, res, y, y2 */
+} fr_conv_desc;
+
+int fr_op_conv2d(const fr_conv_desc* d, void* stream);
+
+/* u8 NHWC [B,H,W,3] or f32 NCHW [B,3,H,W] → 16-bit NHWC [B,H,W,8] = [q0,q1,q2,q0,q1,q2,0,0] with
+ * q = 2u-255 (u8; exact) or q = 255*x (normalized f32), i.e. q = 255 * ((u/255-0.5)/0.5).  The stem
+ * conv weights carry 1/255 as a hi/lo pair on the duplicated channels (exact first layer). */
+int fr_op_preprocess(const void* in, int in_fmt, int B, int H, int W, void* out, int dtype, void* stream);
+
+/* Max pool NHWC bf16 (padding never wins, as torch MaxPool2d). */
+int fr_op_maxpool(const void* x, int B, int H, int W, int Cx, int x_off, int C,
+                  int k, int stride, int pad, void* y, int Cy, int y_off, int Ho, int Wo, int dtype, void* stream);
+
+/* Global average pool NHWC bf16 [B,H,W,C] → bf16 [B,C]. */
+int fr_op_avgpool(const void* x, int B, int H, int W, int C, void* y, int dtype, void* stream);
+
+/* Linear head: out[B,N] = x[B,K] (bf16) · w[Npad,Kpad]ᵀ (bf16) + bias, f32 out, optional L2
+ * normalize (F.normalize eps 1e-12).  `partial` must hold split_k*B*Npad floats. */
+int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, int Kpad,
+                 const float* bias, int normalize, float* out, int split_k, float* partial, int dtype, void* stream);
+
+/* ---- debug: named intermediate tensors of the forward plan (per-layer drift tests) ----
+ * Tensor names are the reference/oracle module whose output the tensor equals
+ * (e.g. "backbone.layer2.0", "layer3.7.prelu", "model.repeat_1.2"); "" for internal buffers. */
+int fr_debug_tensor_count(const fr_handle* h);
+const char* fr_debug_tensor_name(const fr_handle* h, int t);
+int fr_debug_tensor_shape(const fr_handle* h, int t, int* H, int* W, int* C);
+/* Copy the first B samples of tensor t (bf16 NHWC) to dst (device) after an fr_embed. */
+int fr_debug_copy_tensor(fr_handle* h, int t, int B, void* dst, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRHIP_H */

@@ -1,0 +1,124 @@
+"""End-to-end parity: libfrhip forward (bf16 MFMA) vs the CPU oracle (fp32) per backbone.
+
+Bar (BASELINE.json north_star): embeddings within 1e-3 cosine of the reference PyTorch-CPU
+embeddings (1 - cos <= 1e-3 per face), identical top-1 identity indices on a planted gallery.
+ResNet-50 ArcFace is additionally pinned to the reference's own code through the golden
+fixture (tests/test_golden.py checks the oracle against it on CPU).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+COS_TOL = 1e-3
+
+
+def _probes(arch, n, seed=0):
+    from facerecognition_amd.synthetic import synthetic_crops
+    from facerecognition_amd.weights import INPUT_SIZE
+    return synthetic_crops(n, INPUT_SIZE[arch], seed=seed)
+
+
+_cache = {}
+
+
+def _oracle_embed(arch, u8):
+    from facerecognition_amd.weights import synth_state_dict
+    from oracle import models as M
+    key = (arch, u8.shape, int(u8.sum()))
+    if key not in _cache:
+        torch.set_num_threads(16)
+        m = M.build_model(arch, synth_state_dict(arch))
+        _cache[key] = M.embed(m, arch, u8)
+    return _cache[key]
+
+
+# (arch, dtype): every backbone at the 1e-3 bar in its default dtype, plus f16 for all.
+# bf16 InceptionResnetV1 is measured (test_irv1_bf16_drift_report) — DESIGN.md §5.
+CASES = [("iresnet100", "bf16"), ("resnet50_arcface", "bf16"), ("irv1_facenet", "f16"),
+         ("iresnet100", "f16"), ("resnet50_arcface", "f16")]
+
+
+@pytest.fixture(scope="module", params=CASES, ids=[f"{a}-{d}" for a, d in CASES])
+def arch_model(request, gpu):
+    from facerecognition_amd.model import FRModel
+    arch, dtype = request.param
+    m = FRModel.synthetic(arch, dtype=dtype)
+    yield arch, m
+    m.close()
+
+
+def test_embedding_cosine(arch_model):
+    arch, m = arch_model
+    u8 = _probes(arch, 6)
+    ref = _oracle_embed(arch, u8)
+    got = m.embed(torch.from_numpy(u8)).cpu().numpy()
+    assert got.shape == ref.shape
+    cos = np.sum(got * ref, axis=1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(ref, axis=1))
+    assert np.all(1 - cos <= COS_TOL), f"{arch}: 1-cos = {1 - cos}"
+    assert np.allclose(np.linalg.norm(got, axis=1), 1, atol=1e-5)
+
+
+def test_f32_nchw_input_matches_u8(arch_model):
+    arch, m = arch_model
+    u8 = _probes(arch, 3, seed=1)
+    from oracle.models import preprocess_u8_nhwc
+    a = m.embed(torch.from_numpy(u8)).cpu()
+    b = m.embed(preprocess_u8_nhwc(u8)).cpu()
+    assert torch.allclose(a, b, atol=1e-6)
+
+
+def test_raw_vs_normalized(arch_model):
+    arch, m = arch_model
+    u8 = torch.from_numpy(_probes(arch, 2, seed=2))
+    raw = m.embed(u8, normalize=False)
+    nrm = m.embed(u8, normalize=True)
+    assert torch.allclose(torch.nn.functional.normalize(raw, dim=1), nrm, atol=1e-6)
+
+
+def test_batch_independence(arch_model):
+    """A face's embedding must not depend on its batch neighbours; the batch size only changes
+    the split-K decomposition (f32 summation order), so agreement is at the parity tolerance."""
+    arch, m = arch_model
+    u8 = torch.from_numpy(_probes(arch, 5, seed=3))
+    full = m.embed(u8).cpu()
+    again = m.embed(u8).cpu()
+    assert torch.equal(full, again), "forward is not deterministic"
+    one = m.embed(u8[2:3]).cpu()
+    cos = float((full[2] * one[0]).sum())
+    assert 1 - cos <= COS_TOL, 1 - cos
+
+
+def test_top1_planted_gallery(arch_model):
+    """Identical top-1 vs the oracle on a 10k gallery whose first rows are planted matches."""
+    from facerecognition_amd.gallery import DeviceGallery
+    from oracle.match import topk_dot
+    arch, m = arch_model
+    u8 = _probes(arch, 6)
+    ref = _oracle_embed(arch, u8)
+    rng = np.random.default_rng(1)
+    G = rng.standard_normal((10000, 512)).astype(np.float32)
+    G[:6] = ref + 0.05 * rng.standard_normal((6, 512))
+    G /= np.linalg.norm(G, axis=1, keepdims=True)
+    gal = DeviceGallery(G)
+    e = m.embed(torch.from_numpy(u8))
+    s, i = gal.search_device(e, 5)
+    _, ri = topk_dot(ref, G, 5)
+    assert np.array_equal(i[:, 0].cpu().numpy(), ri[:, 0])
+    assert np.array_equal(ri[:, 0], np.arange(6))
+
+
+def test_irv1_bf16_drift_report(gpu):
+    """bf16 InceptionResnetV1 on the synthetic weights: the stem's rounding is amplified by the
+    random network to ~2e-3 cosine (CPU bf16 emulation of the oracle gives the same number), so
+    its bar here is 5e-3; the f16 path meets 1e-3 (CASES above)."""
+    from facerecognition_amd.model import FRModel
+    m = FRModel.synthetic("irv1_facenet", dtype="bf16")
+    u8 = _probes("irv1_facenet", 6)
+    ref = _oracle_embed("irv1_facenet", u8)
+    got = m.embed(torch.from_numpy(u8)).cpu().numpy()
+    cos = np.sum(got * ref, axis=1)
+    print("irv1 bf16 1-cos", 1 - cos)
+    assert np.all(1 - cos <= 5e-3)
+    m.close()

@@ -1,0 +1,250 @@
+"""Kernel-level parity: every libfrhip op vs a torch fp32 / numpy reference of the same op.
+
+Tolerances: conv/linear operands are bf16-exact in both paths and both accumulate in f32,
+so the only differences are summation order and the final bf16 rounding of the output
+(relative 2^-8): |got - ref| <= 1e-2 * (|ref| + max|ref|/8).  Pool / preprocess are exact.
+The match kernel is exact f32 (fmaf chain): scores within 1e-5, indices identical wherever the
+reference's top-k gap exceeds 1e-5, and identical on constructed ties.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from facerecognition_amd import _native as N
+from tests.helpers import TORCH_DT, bf16_round, conv_op, conv_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, tol=1e-2):
+    got = got.float().cpu()
+    ref = ref.float().cpu()
+    scale = ref.abs().max().item() + 1e-6
+    err = (got - ref).abs()
+    bound = tol * (ref.abs() + scale / 8)
+    bad = (err > bound).sum().item()
+    assert bad == 0, f"{bad} / {err.numel()} elements out of tolerance; max err {err.max().item():.4g} (scale {scale:.4g})"
+
+
+CONV_CASES = [
+    # B, H, W, Cin, Cout, kh, kw, stride, pad
+    (2, 14, 14, 256, 256, 3, 3, (1, 1), (1, 1)),   # IResNet100 layer3 conv
+    (2, 28, 28, 128, 128, 3, 3, (2, 2), (1, 1)),   # stride-2 block conv
+    (2, 56, 56, 64, 64, 3, 3, (1, 1), (1, 1)),     # layer1 (BN=64 tile)
+    (3, 7, 7, 512, 512, 3, 3, (1, 1), (1, 1)),     # layer4
+    (2, 16, 16, 64, 256, 1, 1, (1, 1), (0, 0)),    # bottleneck expand
+    (2, 16, 16, 256, 128, 1, 1, (2, 2), (0, 0)),   # 1x1 stride-2 downsample
+    (2, 30, 30, 8, 64, 7, 7, (2, 2), (3, 3)),      # ResNet-50 stem (Cin padded to 8)
+    (2, 20, 20, 8, 64, 3, 3, (1, 1), (1, 1)),      # IResNet stem
+    (2, 21, 21, 8, 32, 3, 3, (2, 2), (0, 0)),      # IRV1 conv2d_1a
+    (2, 19, 19, 80, 192, 3, 3, (1, 1), (0, 0)),    # IRV1 conv2d_4a (Cin=80, K not /64)
+    (2, 8, 8, 128, 128, 1, 7, (1, 1), (0, 3)),     # Block17 1x7
+    (2, 8, 8, 128, 128, 7, 1, (1, 1), (3, 0)),     # Block17 7x1
+    (2, 5, 5, 192, 192, 1, 3, (1, 1), (0, 1)),     # Block8 1x3
+    (2, 9, 9, 32, 32, 3, 3, (1, 1), (1, 1)),       # Block35 3x3 (Cin=32)
+    (1, 3, 3, 1792, 384, 1, 1, (1, 1), (0, 0)),    # Block8 fused 1x1 (tiny M)
+]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_parity(gpu, case, dtype):
+    B, H, W, Cin, Cout, kh, kw, stride, pad = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(B, H, W, Cin, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    w = torch.randn(Cout, Cin, kh, kw, generator=g) / np.sqrt(Cin * kh * kw)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    y = conv_op(x, w, stride=stride, pad=pad, bias=bias, act=1, dtype=dtype)
+    ref = conv_ref(x, w, stride=stride, pad=pad, bias=bias, act=1, dtype=dtype)
+    _close(y, ref, tol=1e-2 if dtype == "bf16" else 2e-3)
+
+
+def test_conv_residual_prelu_dual_output(gpu):
+    g = torch.Generator().manual_seed(5)
+    B, H, Cin, Cout = 2, 14, 128, 128
+    x = torch.randn(B, H, H, Cin, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    slope = torch.rand(Cout, generator=g) * 0.5
+    res = torch.randn(B, 7, 7, Cout, generator=g).to(torch.bfloat16).to(gpu)
+    s = torch.rand(Cout, generator=g) + 0.5
+    t = torch.randn(Cout, generator=g) * 0.1
+    y2 = torch.zeros(B, 7, 7, Cout, dtype=torch.bfloat16, device=gpu)
+    y = conv_op(x, w, stride=(2, 2), pad=(1, 1), bias=bias, act=2, slope=slope, res=res, y2=y2, aff_s=s, aff_b=t)
+    ref = conv_ref(x, w, stride=(2, 2), pad=(1, 1), bias=bias, act=2, slope=slope, res=res)
+    _close(y, ref)
+    _close(y2, y.float().cpu() * s + t)
+
+
+def test_conv_channel_slices(gpu):
+    """Concat-free Inception wiring: read channels [32:64) of a 160-ch buffer, write [96:128)."""
+    g = torch.Generator().manual_seed(9)
+    B, H = 2, 17
+    buf = torch.randn(B, H, H, 160, generator=g).to(torch.bfloat16).to(gpu)
+    before = buf.clone()
+    w = torch.randn(32, 32, 3, 3, generator=g) / 17
+    conv_op(buf.clone(), w, pad=(1, 1), x_off=32, cin=32, act=1, y=buf, y_off=96)
+    ref = conv_ref(before, w, pad=(1, 1), x_off=32, cin=32, act=1)
+    _close(buf[..., 96:128], ref)
+    assert torch.equal(buf[..., :96], before[..., :96]) and torch.equal(buf[..., 128:], before[..., 128:])
+
+
+@pytest.mark.parametrize("split", [2, 5])
+def test_conv_split_k(gpu, split):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 7, 7, 512, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(512, 512, 3, 3, generator=g) / 68
+    res = torch.randn(2, 7, 7, 512, generator=g).to(torch.bfloat16).to(gpu)
+    y = conv_op(x, w, pad=(1, 1), res=res, act=1, split_k=split)
+    _close(y, conv_ref(x, w, pad=(1, 1), res=res, act=1))
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_preprocess_u8_and_f32(gpu, dtype):
+    """q = 255 * Normalize(ToTensor(u)) = 2u - 255, exact, duplicated into channels 3..5."""
+    rng = np.random.default_rng(0)
+    u8 = rng.integers(0, 256, (3, 9, 11, 3), dtype=np.uint8)
+    xin = torch.from_numpy(u8).to(gpu)
+    dt = N.FR_DTYPE[dtype]
+    out = torch.empty(3, 9, 11, 8, dtype=TORCH_DT[dtype], device=gpu)
+    N.check(N.lib().fr_op_preprocess(xin.data_ptr(), N.FR_IN_U8_NHWC, 3, 9, 11, out.data_ptr(), dt, N.stream_ptr()))
+    torch.cuda.synchronize()
+    q = 2 * torch.from_numpy(u8).float() - 255
+    assert torch.equal(out[..., :3].float().cpu(), q) and torch.equal(out[..., 3:6].float().cpu(), q)
+    assert torch.count_nonzero(out[..., 6:]) == 0
+    ref = (torch.from_numpy(u8).float().div(255) - 0.5) / 0.5  # ToTensor + Normalize(0.5, 0.5)
+    f = ref.permute(0, 3, 1, 2).contiguous().to(gpu)
+    out2 = torch.empty_like(out)
+    N.check(N.lib().fr_op_preprocess(f.data_ptr(), N.FR_IN_F32_NCHW, 3, 9, 11, out2.data_ptr(), dt, N.stream_ptr()))
+    torch.cuda.synchronize()
+    assert torch.allclose(out2.float(), out.float(), atol=0.5)
+
+
+@pytest.mark.parametrize("k,s,p,H", [(3, 2, 1, 56), (3, 2, 0, 77), (3, 2, 0, 17)])
+def test_maxpool(gpu, k, s, p, H):
+    x = torch.randn(2, H, H, 64).to(torch.bfloat16).to(gpu)
+    Ho = (H + 2 * p - k) // s + 1
+    y = torch.zeros(2, Ho, Ho, 128, dtype=torch.bfloat16, device=gpu)
+    N.check(N.lib().fr_op_maxpool(x.data_ptr(), 2, H, H, 64, 0, 64, k, s, p, y.data_ptr(), 128, 64, Ho, Ho,
+                                  0, N.stream_ptr()))
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.max_pool2d(x.float().cpu().permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1)
+    assert torch.equal(y[..., 64:].float().cpu(), ref)
+    assert torch.count_nonzero(y[..., :64]) == 0
+
+
+def test_avgpool(gpu):
+    x = torch.randn(3, 4, 4, 2048).to(torch.bfloat16).to(gpu)
+    y = torch.empty(3, 2048, dtype=torch.bfloat16, device=gpu)
+    N.check(N.lib().fr_op_avgpool(x.data_ptr(), 3, 4, 4, 2048, y.data_ptr(), 0, N.stream_ptr()))
+    torch.cuda.synchronize()
+    _close(y, x.float().cpu().mean(dim=(1, 2)), tol=8e-3)
+
+
+@pytest.mark.parametrize("B,K,split,norm", [(5, 2048, 4, 1), (256, 25088, 32, 1), (7, 1792, 1, 0)])
+def test_linear_head(gpu, B, K, split, norm):
+    from tests.helpers import pack_weight
+    g = torch.Generator().manual_seed(B)
+    x = torch.randn(B, K, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(512, K, generator=g) / np.sqrt(K)
+    b = torch.randn(512, generator=g) * 0.1
+    wp, npad, kpad = pack_weight(w.view(512, K, 1, 1), gpu)
+    bd = b.to(gpu)
+    out = torch.empty(B, 512, device=gpu)
+    part = torch.empty(split * B * npad, device=gpu)
+    N.check(N.lib().fr_op_linear(x.data_ptr(), B, K, wp.data_ptr(), 512, npad, kpad, bd.data_ptr(), norm,
+                                 out.data_ptr(), split, part.data_ptr(), 0, N.stream_ptr()))
+    torch.cuda.synchronize()
+    ref = x.float().cpu() @ bf16_round(w).t() + b
+    if norm:
+        ref = torch.nn.functional.normalize(ref, dim=1)
+    assert torch.allclose(out.cpu(), ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
+
+
+# ------------------------------------------------------------------------------ match
+def _np_topk(P, G, k):
+    """oracle: notebook np.dot + stable (score desc, index asc) order."""
+    from oracle.match import topk_dot
+    return topk_dot(P, G, k)
+
+
+def _norm(a):
+    return (a / np.linalg.norm(a, axis=1, keepdims=True)).astype(np.float32)
+
+
+@pytest.mark.parametrize("B,Ng,k", [(256, 10000, 5), (3, 1000, 1), (70, 130, 16), (1, 64, 8), (65, 4097, 5)])
+def test_match_topk(gpu, B, Ng, k):
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(B + Ng)
+    G = _norm(rng.standard_normal((Ng, 512)))
+    P = _norm(rng.standard_normal((B, 512)))
+    P[: min(B, Ng)] = _norm(G[: min(B, Ng)] + 0.05 * rng.standard_normal((min(B, Ng), 512)))  # planted
+    gal = DeviceGallery(G)
+    s, i = gal.search(P, k)
+    rs, ri = _np_topk(P, G, k)
+    assert np.allclose(s, rs, atol=1e-5)
+    kk = min(k, Ng)
+    gap_ok = np.ones_like(ri, dtype=bool)
+    gap_ok[:, :-1] = (rs[:, :-1] - rs[:, 1:]) > 1e-5  # only compare positions separated by a real gap
+    assert np.array_equal(i[:, :kk][gap_ok[:, :kk]], ri[:, :kk][gap_ok[:, :kk]])
+    assert np.array_equal(i[:, 0], ri[:, 0])
+
+
+def test_match_ties_lowest_index(gpu):
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(3)
+    base = _norm(rng.standard_normal((50, 512)))
+    G = np.concatenate([base, base, base], 0)  # every row present 3x: exact score ties
+    gal = DeviceGallery(G)
+    s, i = gal.search(base[:10], 3)
+    for r in range(10):
+        assert list(i[r]) == [r, r + 50, r + 100], i[r]
+        assert s[r, 0] == s[r, 1] == s[r, 2]
+
+
+def test_match_unnormalized_rows_cosine(gpu):
+    """cosine_similarity semantics: non-unit rows are divided by their norm, zero rows score 0."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(4)
+    G = rng.standard_normal((20, 512)).astype(np.float32) * 3.0
+    G[7] = 0
+    P = _norm(rng.standard_normal((2, 512)))
+    gal = DeviceGallery(G)
+    s, i = gal.search(P, 16)
+    ref = P @ _norm(np.where(np.linalg.norm(G, axis=1, keepdims=True) == 0, 1, G)).T
+    ref[:, 7] = 0
+    for r in range(2):
+        assert np.allclose(s[r], np.sort(ref[r])[::-1][:16], atol=1e-5)
+
+
+def test_topk_merge(gpu):
+    rng = np.random.default_rng(8)
+    B, L, k = 9, 6, 5
+    cs = np.sort(rng.standard_normal((B, L, k)).astype(np.float32), axis=2)[:, :, ::-1].copy()
+    ci = rng.permutation(B * L * k).reshape(B, L, k).astype(np.int32)
+    cs[0, 1, 0] = cs[0, 0, 0] = 9.0  # tie across lists → lower index first
+    tcs, tci = torch.from_numpy(cs).to(gpu), torch.from_numpy(ci).to(gpu)
+    os_, oi = torch.empty(B, k, device=gpu), torch.empty(B, k, dtype=torch.int32, device=gpu)
+    N.check(N.lib().fr_topk_merge(tcs.data_ptr(), tci.data_ptr(), B, L, k, os_.data_ptr(), oi.data_ptr(),
+                                  N.stream_ptr()))
+    torch.cuda.synchronize()
+    for b in range(B):
+        cand = sorted(zip(cs[b].ravel().tolist(), ci[b].ravel().tolist()), key=lambda t: (-t[0], t[1]))[:k]
+        assert oi[b].cpu().tolist() == [c[1] for c in cand]
+        assert np.allclose(os_[b].cpu().numpy(), [c[0] for c in cand])
+
+
+def test_segment_mean_normalize(gpu):
+    rng = np.random.default_rng(2)
+    E = _norm(rng.standard_normal((10, 512)))
+    seg = np.array([0, 3, 4, 10], np.int32)
+    te, ts = torch.from_numpy(E).to(gpu), torch.from_numpy(seg).to(gpu)
+    out = torch.empty(3, 512, device=gpu)
+    N.check(N.lib().fr_segment_mean_normalize(te.data_ptr(), 512, ts.data_ptr(), 3, out.data_ptr(), N.stream_ptr()))
+    torch.cuda.synchronize()
+    from oracle.match import folder_mean
+    for s in range(3):
+        ref = folder_mean(E[seg[s]:seg[s + 1]])
+        assert np.allclose(out[s].cpu().numpy(), ref, atol=1e-6)
