@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Headline benchmark: aligned faces/sec, embed + match, IResNet100 @112, bs=256 per GPU.
+
+BASELINE.json metric "aligned faces/sec (embed+match) ArcFace@112 bs=256, 1/2/4/8 MI355X",
+workload = configs[1] (IResNet100 bf16 bs=256 on one MI355X, 10k x 512 gallery, top-k match).
+
+One step = one pass of the hot path over one batch of HBM-resident synthetic u8 crops:
+  fr_embed (preprocess → IResNet100 forward → folded head → L2 norm)  [libfrhip.so]
+  N > 1: RCCL all-gather of the normalized embeddings
+  fr_match_topk of all gathered probes against this rank's gallery shard (global indices)
+  N > 1: RCCL all-gather of the per-shard top-k candidates + fr_topk_merge
+Weak scaling: every rank embeds 256 faces; the gallery is row-sharded across ranks.
+value = faces embedded by all ranks / max-over-ranks wall time of the timed steps.
+
+Launch: python bench.py --gpus N --steps K --warmup W   (N > 1 under torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "aligned faces/sec (embed+match) ArcFace@112 bs=256, 1/2/4/8 MI355X"
+IRESNET100_GFLOP_PER_FACE = 24.179  # 2 * (conv + fc MACs)
+BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--gallery-rows", type=int, default=10000)
+    ap.add_argument("--k", type=int, default=5)
+    ap.add_argument("--arch", default="iresnet100")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(arch, seconds):
+    """The oracle (PyTorch fp32 CPU restatement of the path; IResNet100 has no reference code, so
+    kind='port') on a bounded sample: batches of 8 synthetic crops through embed + F.normalize, then
+    the reference's batched np.dot+argmax match against a 1k-row gallery (BASELINE configs[0])."""
+    from facerecognition_amd.synthetic import synthetic_crops
+    from facerecognition_amd.weights import INPUT_SIZE, synth_state_dict
+    from oracle import models as M
+    from oracle.match import topk_dot
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    model = M.build_model(arch, synth_state_dict(arch))
+    s = INPUT_SIZE[arch]
+    gal = np.random.default_rng(1).standard_normal((1000, 512)).astype(np.float32)
+    gal /= np.linalg.norm(gal, axis=1, keepdims=True)
+    bs, done = 8, 0
+    u8 = synthetic_crops(bs, s, seed=11)
+    M.embed(model, arch, u8[:2])  # warm the allocator / kernels
+    t0 = time.perf_counter()
+    while True:
+        e = M.embed(model, arch, u8)
+        topk_dot(e, gal, 5)
+        done += bs
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 3), "unit": "faces/s", "cores": threads, "kind": "port",
+            "sample": f"{done} synthetic 112x112 crops in batches of {bs}: {arch} fp32 forward + F.normalize "
+                      f"+ np.dot top-5 vs 1000x512 gallery, torch {threads} threads, {dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from facerecognition_amd.gallery import DeviceGallery
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    from facerecognition_amd import _native as N
+
+    B, K = args.batch, args.k
+    model = FRModel.synthetic(args.arch, device=local, max_batch=B, dtype=args.dtype)
+    size = model.input_size
+    u8 = torch.from_numpy(synthetic_crops(B, size, seed=100 + rank)).to(dev)  # HBM-resident input
+    # gallery: rows [r*rows/N, (r+1)*rows/N) on rank r; global indices via index_base
+    rows = args.gallery_rows
+    lo, hi = rank * rows // world, (rank + 1) * rows // world
+    g = np.random.default_rng(1).standard_normal((rows, 512)).astype(np.float32)[lo:hi]
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    gallery = DeviceGallery(g, device=local, index_base=lo)
+    emb = torch.empty((B, 512), dtype=torch.float32, device=dev)
+    all_emb = torch.empty((world * B, 512), dtype=torch.float32, device=dev)
+    cand_s = torch.empty((world, world * B, K), dtype=torch.float32, device=dev)
+    cand_i = torch.empty((world, world * B, K), dtype=torch.int32, device=dev)
+    fin_s = torch.empty((world * B, K), dtype=torch.float32, device=dev)
+    fin_i = torch.empty((world * B, K), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        model.embed(u8, out=emb)
+        if i is not None:
+            ev[i][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(all_emb, emb)
+            probes = all_emb
+        else:
+            probes = emb
+        s, idx = gallery.search_device(probes, K)
+        if world > 1:
+            dist.all_gather_into_tensor(cand_s.view(-1), s.contiguous().view(-1))
+            dist.all_gather_into_tensor(cand_i.view(-1), idx.contiguous().view(-1))
+            # candidates [rank][probe][k] -> [probe][rank][k] for the merge
+            cs = cand_s.permute(1, 0, 2).contiguous()
+            ci = cand_i.permute(1, 0, 2).contiguous()
+            N.check(N.lib().fr_topk_merge(cs.data_ptr(), ci.data_ptr(), world * B, world, K, fin_s.data_ptr(),
+                                          fin_i.data_ptr(), N.stream_ptr(dev)), "fr_topk_merge")
+            return fin_s, fin_i
+        return s, idx
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out_s, out_i = step(i)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    embed_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))  # forward duration on its stream
+    if dist:
+        t = torch.tensor([elapsed, embed_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, embed_ms = float(t[0]), float(t[1])
+    # sanity: top-1 indices are valid global gallery rows
+    assert int(out_i[:, 0].min()) >= 0 and int(out_i[:, 0].max()) < rows
+
+    faces = world * B * args.steps
+    value = faces / elapsed
+    flop_fwd = IRESNET100_GFLOP_PER_FACE * 1e9 * B if args.arch == "iresnet100" else None
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "faces/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic u8 112x112x3 aligned crops (HBM-resident), random-init BN-calibrated weights, "
+                "random unit-norm gallery",
+        "config": {"workload": f"{args.arch} {args.dtype} embed bs={B}/GPU + top-{K} match vs "
+                               f"{rows}x512 f32 gallery (row-sharded over {world} GPU(s))",
+                   "batch_per_gpu": B, "global_batch": world * B, "gallery_rows": rows, "k": K,
+                   "parallelism": f"dp{world}"},
+    }
+    if flop_fwd:
+        achieved = flop_fwd / (embed_ms * 1e-3) / 1e12
+        result["roofline"] = {"bound": "mfma", "kernel": "fr_embed forward (conv_igemm MFMA launches + "
+                              "preprocess/split-K/head), HIP events on the embed stream",
+                              "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": None,
+                              "embed_ms": round(embed_ms, 4)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.arch, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -36,7 +36,7 @@ class FrConvDesc(ctypes.Structure):
         ("y", c_void_p), ("Cy", c_int), ("y_off", c_int),
         ("y2", c_void_p), ("Cy2", c_int), ("y2_off", c_int), ("aff_s", c_void_p), ("aff_b", c_void_p),
         ("Ho", c_int), ("Wo", c_int),
-        ("split_k", c_int), ("partial", c_void_p), ("dtype", c_int),
+        ("split_k", c_int), ("partial", c_void_p), ("dtype", c_int), ("tile", c_int),
     ]
 
 

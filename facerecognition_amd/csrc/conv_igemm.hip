@@ -1,21 +1,23 @@
-// Implicit-GEMM convolution for CDNA4 (gfx950), NHWC bf16 activations, KRSC bf16
-// weights, f32 accumulation on v_mfma_f32_16x16x32_bf16, fused epilogue.
+// Implicit-GEMM convolution for CDNA4 (gfx950): NHWC 16-bit activations, KRSC 16-bit weights,
+// f32 accumulation on v_mfma_f32_16x16x32_{bf16,f16}, fused epilogue.
 //
 // Replaces the torch conv+BN+ReLU/PReLU+residual chains of the reference backbones:
 //   ResNetBackbone.forward            models/arcface/arcface_model.py:118-132 (torchvision Bottleneck)
 //   FaceNet InceptionResnetV1 trunk   models/facenet/facenet_model.py:12-16 (BasicConv2d/Block35/17/8)
 //   insightface IBasicBlock (IResNet100, README.md:72; no reference code)
 //
-// GEMM view: C[n][m] = sum_k W[n][k] * X[m][k]; m = output pixel (b, oh, ow), n = output
-// channel, k = (r, s, c) with c fastest.  MFMA operand A = weight rows (n), operand B =
-// gathered activation rows (m), so each lane's 4 accumulator registers are 4 consecutive
-// output channels of one pixel (a ds_write_b128 into the epilogue tile).
+// GEMM view: C[n][m] = sum_k W[n][k] * X[m][k]; m = output pixel (b, oh, ow), n = output channel,
+// k = (r, s, c) with c fastest.  MFMA operand A = weight rows (n), operand B = gathered activation
+// rows (m): each lane's 4 accumulator registers are 4 consecutive channels of one pixel.
 //
-// Tile: BM pixels x BN channels x BK=64, 4 waves (WM x WN), LDS double buffered with
-// register staging (loads for tile t+1 are issued before the MFMAs of tile t and written
-// to LDS after them; one barrier per K-step).  LDS rows are 128 B (64 bf16); the 16-B
-// chunk index is XOR-swizzled with (row>>1)&7, which makes both the ds_write_b128 stores
-// and the MFMA-fragment ds_read_b128 loads bank-conflict free.
+// Staging: both operand tiles go global → LDS by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per
+// wave instruction = 8 tile rows of 128 B), two LDS stages, one barrier per 64-deep K-step: the DMA
+// for step t+1 is issued before the MFMAs of step t.  The im2col gather is the per-lane source
+// offset; a padding tap or a row past M gets an out-of-range offset and the buffer unit returns
+// zeros (no select, no zero page).  LDS rows are 128 B; the 16-B chunk index is XOR-swizzled with
+// (row>>1)&7 by permuting the per-lane SOURCE chunk (the DMA destination is lane-linear), which
+// makes the MFMA-fragment ds_read_b128 loads bank-conflict free.
+// FASTK (Cin % 64 == 0): a K-step is one (r, s) tap and 64 channels, tracked in scalars.
 #include "kernels.h"
 
 namespace fr {
@@ -23,8 +25,15 @@ namespace fr {
 namespace {
 
 constexpr int BK = 64;
+constexpr uint32_t OOB = 0x80000000u;  // buffer offset past num_records → the DMA writes zeros
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
+}
 
 // Shared fused epilogue for 8 consecutive channels n..n+7 of output pixel m.
 template <bool F16>
@@ -61,25 +70,24 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, float* v, int m, in
     }
 }
 
-template <bool F16, int BM, int BN, int WM, int WN>
+template <bool F16, int BM, int BN, int WM, int WN, bool FASTK>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
+    static_assert(WM * WN == 4, "4 waves");
     typedef Num<F16> T;
     typedef typename T::frag frag;
-    static_assert(WM * WN == 4, "4 waves");
     constexpr int TWM = BM / WM, TWN = BN / WN;  // wave tile (pixels, channels)
     constexpr int FM = TWM / 16, FN = TWN / 16;  // MFMA tiles per wave
-    constexpr int A_CH = BM * 8 / 256;           // 16-B activation chunks per thread per K-step
-    constexpr int W_CH = BN * 8 / 256;           // 16-B weight chunks per thread per K-step
-    constexpr int STAGE = (BM + BN) * BK;        // bf16 elements per LDS stage
-    constexpr int EPI_LD = BN + 4;               // f32 epilogue tile leading dim
-    constexpr int LDS_A = 2 * STAGE * 2, LDS_E = BM * EPI_LD * 4;
+    constexpr int NA = BM / 32, NB = BN / 32;    // DMA instructions per wave per K-step
+    constexpr int STAGE_A = BM * BK * 2, STAGE = (BM + BN) * BK * 2;  // bytes
+    constexpr int EPI_LD = BN + 4;
+    constexpr int LDS_A = 2 * STAGE, LDS_E = BM * EPI_LD * 4;
     constexpr int LDS_BYTES = LDS_A > LDS_E ? LDS_A : LDS_E;
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];  // the ONLY LDS object (guide §5 trap 4a)
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave % WM, wn = wave / WM;
-    const int nwg = gridDim.x;
-    const int lid = xcd_remap(blockIdx.x, nwg);
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
     const int tm = lid / tiles_n, tn = lid - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int split = blockIdx.y;
@@ -87,71 +95,79 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
     const int kt0 = split * kt_per_split;
     const int kt1 = min(nkt, kt0 + kt_per_split);
 
-    const int col8 = tid & 7, row_base = tid >> 3;
-    const int HoWo = p.Ho * p.Wo;
+    // Lane's DMA slot: rows 8*(wave + 4i) + (lane>>3); the logical chunk it fetches is the same for
+    // every i (the swizzle term (row>>1)&7 = (4*wave + (lane>>4)) & 7 does not depend on i).
+    const int lrow = lane >> 3;
+    const int cl = (lane & 7) ^ ((4 * wave + (lane >> 4)) & 7);
 
-    // Per-thread activation rows: input pixel base and top-left input coordinate.
-    int a_pix[A_CH], a_ih[A_CH], a_iw[A_CH];
+    const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * p.H * p.W * p.Cx * 2);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
+    const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
+
+    const int HoWo = p.Ho * p.Wo;
+    int a_ih[NA], a_iw[NA];
+    uint32_t a_base[NA];  // byte offset of (b, ih0, iw0, x_off [+ 8*cl]) — wraps if ih0/iw0 < 0, only used when valid
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-        const int m = m0 + row_base + 32 * i;
+    for (int i = 0; i < NA; ++i) {
+        const int m = m0 + 8 * (wave + 4 * i) + lrow;
         if (m < p.M) {
             const int b = m / HoWo, r = m - b * HoWo;
             const int oh = r / p.Wo, ow = r - oh * p.Wo;
-            a_pix[i] = b * p.H * p.W;
             a_ih[i] = oh * p.sh - p.ph;
             a_iw[i] = ow * p.sw - p.pw;
+            // FASTK: c_cur is the K-step's channel base, the lane adds its chunk here;
+            // generic: c_cur already is the lane's own channel.
+            a_base[i] = (uint32_t)((((b * p.H + a_ih[i]) * p.W + a_iw[i]) * p.Cx + p.x_off + (FASTK ? 8 * cl : 0)) * 2);
         } else {
-            a_pix[i] = 0;
             a_ih[i] = -(1 << 28);
             a_iw[i] = 0;
+            a_base[i] = 0;
         }
     }
-    // (r, s, c) of this thread's k-chunk at the first K-step.
-    int kc = kt0 * BK + col8 * 8;
-    int c_cur, s_cur, r_cur;
+    uint32_t b_base[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) b_base[j] = (uint32_t)(((n0 + 8 * (wave + 4 * j) + lrow) * p.Kpad + 8 * cl) * 2);
+
+    // K-step position: FASTK → wave-uniform (r, s, c0); generic → per-lane (r, s, c) of k = kt*64 + 8*cl.
+    int r_cur, s_cur, c_cur;
     {
-        const int rs = kc / p.Cin;
-        c_cur = kc - rs * p.Cin;
+        const int k = kt0 * BK + (FASTK ? 0 : 8 * cl);
+        const int rs = k / p.Cin;
+        c_cur = k - rs * p.Cin;
         r_cur = rs / p.Kw;
         s_cur = rs - r_cur * p.Kw;
     }
-    const bf16_t* xb = p.x + p.x_off;
-    const bf16_t* wb = p.w + (size_t)(n0 + row_base) * p.Kpad + col8 * 8;
+    int k_cur = kt0 * BK + 8 * cl;
 
-    uint4 ra[A_CH], rw[W_CH];
-    auto gload = [&](int kt) {
-        const bool kval = kc < p.K;
+    auto issue = [&](int kt, int buf) {
+        const char* sA = smem + buf * STAGE;
+        const char* sB = sA + STAGE_A;
+        const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
 #pragma unroll
-        for (int i = 0; i < A_CH; ++i) {
+        for (int i = 0; i < NA; ++i) {
             const int ih = a_ih[i] + r_cur, iw = a_iw[i] + s_cur;
-            const bool ok = kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (ok) v = *(const uint4*)(xb + (size_t)(a_pix[i] + ih * p.W + iw) * p.Cx + c_cur);
-            ra[i] = v;
+            bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            if (!FASTK) ok = ok && k_cur < p.K;
+            const uint32_t off = ok ? a_base[i] + (uint32_t)soff : OOB;
+            dma16(xr, sA + (wave + 4 * i) * 1024, off);
         }
 #pragma unroll
-        for (int j = 0; j < W_CH; ++j) rw[j] = *(const uint4*)(wb + (size_t)(32 * j) * p.Kpad + kt * BK);
-        // advance this thread's k-chunk by one K-step
-        kc += BK;
-        c_cur += BK;
-        while (c_cur >= p.Cin) {
-            c_cur -= p.Cin;
-            if (++s_cur == p.Kw) { s_cur = 0; ++r_cur; }
-        }
-    };
-    auto sstore = [&](int buf) {
-        bf16_t* sA = (bf16_t*)smem + buf * STAGE;
-        bf16_t* sW = sA + BM * BK;
-#pragma unroll
-        for (int i = 0; i < A_CH; ++i) {
-            const int row = row_base + 32 * i;
-            *(uint4*)(sA + row * BK + swz(row, col8) * 8) = ra[i];
-        }
-#pragma unroll
-        for (int j = 0; j < W_CH; ++j) {
-            const int row = row_base + 32 * j;
-            *(uint4*)(sW + row * BK + swz(row, col8) * 8) = rw[j];
+        for (int j = 0; j < NB; ++j) dma16(wr, sB + (wave + 4 * j) * 1024, b_base[j] + (uint32_t)(kt * BK * 2));
+        // advance one K-step
+        if (FASTK) {
+            c_cur += BK;
+            if (c_cur == p.Cin) {
+                c_cur = 0;
+                if (++s_cur == p.Kw) { s_cur = 0; ++r_cur; }
+            }
+        } else {
+            k_cur += BK;
+            c_cur += BK;
+            while (c_cur >= p.Cin) {
+                c_cur -= p.Cin;
+                if (++s_cur == p.Kw) { s_cur = 0; ++r_cur; }
+            }
         }
     };
 
@@ -162,16 +178,15 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
         for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
     if (kt0 < kt1) {
-        gload(kt0);
-        sstore(0);
+        issue(kt0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     int buf = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
-        const bool more = kt + 1 < kt1;
-        if (more) gload(kt + 1);
-        const bf16_t* sA = (const bf16_t*)smem + buf * STAGE;
-        const bf16_t* sW = sA + BM * BK;
+        if (kt + 1 < kt1) issue(kt + 1, buf ^ 1);
+        const bf16_t* sA = (const bf16_t*)(smem + buf * STAGE);
+        const bf16_t* sW = (const bf16_t*)(smem + buf * STAGE + STAGE_A);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             frag af[FN], bfr[FM];
@@ -189,11 +204,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
-                for (int j = 0; j < FM; ++j)
-                    acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
+                for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
         }
-        if (more) sstore(buf ^ 1);
-        __syncthreads();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next stage landed (this wave's DMA)
+        __syncthreads();                     // ... and every other wave's; stage `buf` free again
         buf ^= 1;
     }
 
@@ -215,12 +229,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
         if (m >= p.M || n >= p.Cout) continue;
         const float4 v0 = *(const float4*)(sE + ml * EPI_LD + g * 8);
         const float4 v1 = *(const float4*)(sE + ml * EPI_LD + g * 8 + 4);
-        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
         if (p.partial) {
             float* dst = p.partial + ((size_t)split * p.M + m) * p.Npad + n;
             *(float4*)dst = v0;
             *(float4*)(dst + 4) = v1;
         } else {
+            float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
             epilogue8<F16>(p, v, m, n);
         }
     }
@@ -250,21 +264,55 @@ hipError_t launch_variant(const ConvArgs& a, hipStream_t s) {
     const int split = a.split_k > 1 ? a.split_k : 1;
     const int per = (nkt + split - 1) / split;
     dim3 grid(tiles_m * tiles_n, split);
-    hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN>), grid, dim3(256), 0, s, a, tiles_n, per);
+    if (a.Cin % 64 == 0)
+        hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN, true>), grid, dim3(256), 0, s, a, tiles_n, per);
+    else
+        hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN, false>), grid, dim3(256), 0, s, a, tiles_n, per);
     return hipGetLastError();
+}
+
+template <bool F16>
+hipError_t launch_dtype(const ConvArgs& a, hipStream_t s) {
+    switch (a.tile) {
+        case TILE_256x64: return launch_variant<F16, 256, 64, 4, 1>(a, s);
+        case TILE_128x64: return launch_variant<F16, 128, 64, 2, 2>(a, s);
+        case TILE_64x128: return launch_variant<F16, 64, 128, 2, 2>(a, s);
+        default: return launch_variant<F16, 128, 128, 2, 2>(a, s);
+    }
 }
 
 }  // namespace
 
-hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
-    // Tile choice: 64-channel layers (IResNet layer1, ResNet-50 layer1 bottleneck mids,
-    // small IRV1 branches) use a tall 256x64 tile; everything else 128x128.
-    if (a.f16) {
-        if (a.Cout <= 64) return launch_variant<true, 256, 64, 4, 1>(a, s);
-        return launch_variant<true, 128, 128, 2, 2>(a, s);
+int conv_tile_bm(int tile) { return tile == TILE_256x64 ? 256 : tile == TILE_64x128 ? 64 : 128; }
+int conv_tile_bn(int tile) { return (tile == TILE_256x64 || tile == TILE_128x64) ? 64 : 128; }
+
+// Tile + split-K choice: minimise (rounds of resident blocks) x (tile area / tile efficiency),
+// where a round is 2 blocks per CU on 256 CUs.  Small-M layers get split-K to fill the chip.
+void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
+    static const int tiles[4] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128};
+    static const double eff[4] = {1.0, 0.95, 0.8, 0.8};
+    const int nkt = Kpad / BK;
+    double best = 1e30;
+    int bt = TILE_128x128, bs = 1;
+    for (int v = 0; v < 4; ++v) {
+        const int BM = conv_tile_bm(tiles[v]), BN = conv_tile_bn(tiles[v]);
+        if (BN == 128 && Cout <= 64) continue;
+        const long nt = (long)((M + BM - 1) / BM) * ((Cout + BN - 1) / BN);
+        for (int sk = 1; sk <= 16; sk *= 2) {
+            if (sk > 1 && nkt / sk < 4) break;
+            const long blocks = nt * sk;
+            const double rounds = (double)((blocks + 511) / 512);
+            const double per_block = (double)BM * BN * ((nkt + sk - 1) / sk) / eff[v];
+            const double cost = rounds * per_block + (sk > 1 ? 0.02 * nt * BM * BN / 512.0 : 0.0);
+            if (cost < best * 0.999) { best = cost; bt = tiles[v]; bs = sk; }
+        }
     }
-    if (a.Cout <= 64) return launch_variant<false, 256, 64, 4, 1>(a, s);
-    return launch_variant<false, 128, 128, 2, 2>(a, s);
+    *tile = bt;
+    *split = bs;
+}
+
+hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
+    return a.f16 ? launch_dtype<true>(a, s) : launch_dtype<false>(a, s);
 }
 
 hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s) {

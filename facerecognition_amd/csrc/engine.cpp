@@ -507,32 +507,14 @@ void build_irv1(Builder& b) {
 }
 
 // ------------------------------------------------------------------ execution
-int choose_split(int tiles, int nkt) {
-    if (tiles >= 192 || nkt < 8) return 1;
-    int s = (512 + tiles - 1) / tiles;
-    s = std::min(s, nkt / 4);
-    return std::max(1, s);
-}
-
-int conv_tiles(int M, int Cout) {
-    const int BM = Cout <= 64 ? 256 : 128, BN = Cout <= 64 ? 64 : 128;
-    return ((M + BM - 1) / BM) * ((Cout + BN - 1) / BN);
-}
-
 size_t partial_need(fr_handle* h, int B) {
     size_t need = 0;
     for (const auto& op : h->ops) {
         if (op.kind != OP_CONV && op.kind != OP_HEAD) continue;
         const auto& cw = h->convw[op.wi];
-        int M;
-        if (op.kind == OP_HEAD) {
-            M = B;
-        } else {
-            const auto& to = h->tensors[op.out];
-            M = B * to.H * to.W;
-        }
-        int sp = choose_split(conv_tiles(M, cw.Cout), cw.Kpad / 64);
-        if (op.kind == OP_HEAD) sp = std::max(sp, 1);
+        const int M = op.kind == OP_HEAD ? B : B * h->tensors[op.out].H * h->tensors[op.out].W;
+        int tile, sp;
+        conv_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
         if (sp > 1 || op.kind == OP_HEAD) need = std::max(need, (size_t)sp * M * cw.Npad);
     }
     return need;
@@ -561,12 +543,11 @@ int reserve(fr_handle* h, int maxB) {
 }
 
 int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
-    const int tiles = conv_tiles(a.M, a.Cout);
-    int split = a.partial ? std::max(1, a.split_k) : choose_split(tiles, a.Kpad / 64);
-    if (split > 1 && !a.partial) {
-        while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) --split;
-        if (split > 1) a.partial = h->partial;
-    }
+    int tile, split;
+    conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
+    a.tile = tile;
+    while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) split /= 2;
+    if (split > 1) a.partial = h->partial;
     a.split_k = split;
     FR_HIP_CHECK(launch_conv(a, s));
     if (split > 1 && a.y) FR_HIP_CHECK(launch_splitk_epilogue(a, s));
@@ -623,8 +604,10 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.x = ti.dev; a.B = B; a.H = 1; a.W = 1; a.Cx = cw.K; a.x_off = 0; a.Cin = cw.K;
                 a.w = cw.w; a.Kh = 1; a.Kw = 1; a.sh = 1; a.sw = 1; a.K = cw.K; a.Kpad = cw.Kpad;
                 a.Ho = 1; a.Wo = 1; a.M = B; a.Cout = cw.Cout; a.Npad = cw.Npad;
-                int split = choose_split(conv_tiles(B, cw.Cout), cw.Kpad / 64);
-                while (split > 1 && (size_t)split * B * cw.Npad > h->partial_floats) --split;
+                int tile, split;
+                conv_plan(B, cw.Cout, cw.Kpad, &tile, &split);
+                while (split > 1 && (size_t)split * B * cw.Npad > h->partial_floats) split /= 2;
+                a.tile = tile;
                 a.split_k = split;
                 a.partial = h->partial;
                 FR_HIP_CHECK(launch_conv(a, s));
@@ -876,6 +859,14 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
     a.y = (bf16_t*)d->y; a.Cy = d->Cy; a.y_off = d->y_off;
     a.y2 = (bf16_t*)d->y2; a.Cy2 = d->Cy2; a.y2_off = d->y2_off; a.aff_s = d->aff_s; a.aff_b = d->aff_b;
     a.f16 = d->dtype == FR_DTYPE_F16;
+    if (d->tile > 0) {
+        if (d->tile > 4) { set_error("fr_op_conv2d: bad tile"); return FR_ERR_ARG; }
+        a.tile = d->tile - 1;
+    } else {
+        int tile, sp;
+        conv_plan(a.M, a.Cout, a.Kpad, &tile, &sp);
+        a.tile = tile;
+    }
     if (d->split_k > 1) {
         if (!d->partial) { set_error("fr_op_conv2d: split_k > 1 needs partial workspace"); return FR_ERR_ARG; }
         a.split_k = d->split_k;
@@ -930,6 +921,11 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
     a.split_k = split_k;
     a.partial = partial;
     a.f16 = dtype == FR_DTYPE_F16;
+    {
+        int tile, sp;
+        conv_plan(a.M, a.Cout, a.Kpad, &tile, &sp);
+        a.tile = tile;
+    }
     FR_HIP_CHECK(launch_conv(a, (hipStream_t)stream));
     FR_HIP_CHECK(launch_head_finalize(partial, split_k, B, N, Npad, bias, normalize, out, (hipStream_t)stream));
     return FR_OK;

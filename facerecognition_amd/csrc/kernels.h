@@ -5,6 +5,9 @@
 
 namespace fr {
 
+// Conv tile variants (BM pixels x BN channels, 4 waves each).
+enum { TILE_128x128 = 0, TILE_256x64 = 1, TILE_128x64 = 2, TILE_64x128 = 3 };
+
 // Implicit-GEMM convolution, NHWC bf16 in/out, f32 accumulate, fused epilogue.
 // GEMM view: M = B*Ho*Wo output pixels, N = Cout, K = Kh*Kw*Cin (c fastest).
 struct ConvArgs {
@@ -17,9 +20,15 @@ struct ConvArgs {
     bf16_t* y2; int Cy2, y2_off; const float* aff_s; const float* aff_b;
     float* partial; int split_k;  // partial != null: raw f32 partials [split][M][Npad], no epilogue
     int f16;                      // 0: bf16 storage + bf16 MFMA; 1: f16 storage + f16 MFMA
+    int tile;                     // TILE_* variant (conv_plan)
 };
 
-// Chooses a tile variant (and honours a.split_k); returns hipError_t.
+// Choose tile variant and split-K factor for a GEMM of M x Cout x Kpad.
+void conv_plan(int M, int Cout, int Kpad, int* tile, int* split);
+int conv_tile_bm(int tile);
+int conv_tile_bn(int tile);
+
+// Launches a.tile with a.split_k; returns hipError_t.
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
 // Split-K reduction + the same fused epilogue as the conv kernel.
 hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);

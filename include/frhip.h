@@ -138,7 +138,14 @@ typedef struct fr_conv_desc {
     int split_k;         /* 0/1 = fused epilogue; >1 = f32 partials into `partial` then reduce */
     float* partial;      /* workspace [split_k, B*Ho*Wo, Npad] f32 when split_k > 1 */
     int dtype;           /* FR_DTYPE_BF16 / FR_DTYPE_F16: element type of x, w, res, y, y2 */
+    int tile;            /* 0 = automatic (cost model); 1 + FR_TILE_* forces a tile variant */
 } fr_conv_desc;
+
+/* conv tile variants (pixels x channels per 256-thread block) */
+#define FR_TILE_128x128 0
+#define FR_TILE_256x64 1
+#define FR_TILE_128x64 2
+#define FR_TILE_64x128 3
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 

@@ -33,7 +33,8 @@ def pack_weight(w: torch.Tensor, device, dtype: str = "bf16") -> tuple:
 
 
 def conv_op(x_nhwc, w, *, stride=(1, 1), pad=(0, 0), bias=None, act=0, slope=None, res=None, res_off=0,
-            x_off=0, cin=None, y=None, y_off=0, y2=None, aff_s=None, aff_b=None, split_k=1, dtype="bf16"):
+            x_off=0, cin=None, y=None, y_off=0, y2=None, aff_s=None, aff_b=None, split_k=1, dtype="bf16",
+            tile=None):
     """Run fr_op_conv2d. x_nhwc: cuda 16-bit [B,H,W,Cx] of `dtype`; w: cpu f32 [Cout,Cin,kh,kw]."""
     dev = x_nhwc.device
     assert x_nhwc.dtype == TORCH_DT[dtype]
@@ -69,6 +70,7 @@ def conv_op(x_nhwc, w, *, stride=(1, 1), pad=(0, 0), bias=None, act=0, slope=Non
         d.aff_s, d.aff_b = dptr(aff_s), dptr(aff_b)
     d.Ho, d.Wo = Ho, Wo
     d.dtype = 1 if dtype == "f16" else 0
+    d.tile = 0 if tile is None else tile + 1
     part = None
     if split_k > 1:
         part = torch.empty(split_k * B * Ho * Wo * npad, dtype=torch.float32, device=dev)

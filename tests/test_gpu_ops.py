@@ -61,6 +61,18 @@ def test_conv_parity(gpu, case, dtype):
     _close(y, ref, tol=1e-2 if dtype == "bf16" else 2e-3)
 
 
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("case", [(2, 14, 14, 256, 256, 3, 3, (1, 1), (1, 1)), (2, 19, 19, 80, 192, 3, 3, (1, 1), (0, 0)),
+                                  (3, 9, 9, 64, 64, 1, 1, (2, 2), (0, 0))])
+def test_conv_every_tile(gpu, case, tile):
+    B, H, W, Cin, Cout, kh, kw, stride, pad = case
+    g = torch.Generator().manual_seed(tile)
+    x = torch.randn(B, H, W, Cin, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(Cout, Cin, kh, kw, generator=g) / np.sqrt(Cin * kh * kw)
+    y = conv_op(x, w, stride=stride, pad=pad, act=1, tile=tile)
+    _close(y, conv_ref(x, w, stride=stride, pad=pad, act=1))
+
+
 def test_conv_residual_prelu_dual_output(gpu):
     g = torch.Generator().manual_seed(5)
     B, H, Cin, Cout = 2, 14, 128, 128
