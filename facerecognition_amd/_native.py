@@ -22,6 +22,7 @@ FR_DTYPE = {"bf16": FR_DTYPE_BF16, "f16": FR_DTYPE_F16}
 FR_IN_U8_NHWC = 0
 FR_IN_F32_NCHW = 1
 FR_EMBED_RAW = 1
+FR_TILE_BAND = 7
 
 c_int, c_int64, c_size_t, c_void_p, c_float_p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p
 
@@ -58,6 +59,7 @@ _SIGS = {
                                c_void_p, c_void_p]),
     "fr_segment_mean_normalize": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "fr_debug_tensor_count": (c_int, [c_void_p]),
+    "fr_debug_plan": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t]),
     "fr_debug_tensor_name": (ctypes.c_char_p, [c_void_p, c_int]),
     "fr_debug_tensor_shape": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                       ctypes.POINTER(c_int)]),

@@ -1,0 +1,334 @@
+// Row-band direct 3x3 convolution (stride 1, pad 1) for CDNA4 (gfx950).
+//
+// The dominant IResNet100 layers (3x3 s1 256->256 @14x14 = 55.5 % of FLOPs,
+// 128->128 @28x28 = 22.9 %, 64->64 @56/@112 = 7.6 %) are 3x3 / stride 1 / pad 1.  An implicit GEMM
+// re-gathers every input pixel for all 9 taps (9x the activation bytes through L2 -> LDS) and, at
+// bs=256, its 128x128 tiles quantize badly on 256 CUs.  This kernel instead gives each block TH full
+// output rows of ONE image (TH*W ~ 200 pixels: one whole 14x14 image, 7 rows of 28, 4 of 56, 2 of 112)
+// x BN output channels, so the tile count is always a multiple of the batch (256 images -> whole
+// rounds of 256 CUs), and:
+//   * the (TH+2) x (W+2) input patch (zero halo) of one 64-channel chunk is DMA'd into LDS once and
+//     read by all 9 taps at shifted positions;
+//   * per (chunk, tap) K-step only the [BN][64] weight slice streams in (double buffered);
+//   * the next chunk's patch DMA overlaps the current chunk's 9 K-steps (double buffered).
+// MFMA: v_mfma_f32_16x16x32_{bf16,f16}; operand A = weight rows (n), operand B = patch rows (pixels),
+// so each lane ends with 4 consecutive channels of one pixel and the fused epilogue (bias, residual,
+// ReLU/PReLU, second affine output) stores 8-byte groups straight from registers.
+// LDS rows are 128 B (64 channels); chunk index XOR (row>>1)&7, applied to the per-lane DMA source.
+#include "kernels.h"
+
+namespace fr {
+namespace {
+
+constexpr uint32_t OOB = 0x80000000u;
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int swzb(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+constexpr int MAXPW = 8;  // max patch DMA instructions per wave per chunk
+
+// Patch LDS image, chunk-major: [8 chunks of 8 channels][P64 positions][16 B].  A tap shift is then a
+// pure position offset, i.e. an immediate on ds_read_b128, and 16 lanes reading 16 consecutive
+// positions of one chunk hit 16 distinct 16-B slots (planes are whole 1-KiB DMA blocks, so aligned).
+// Weight slices stay row-major [BN][64] with the (row>>1)&7 chunk XOR; their read addresses are
+// step-invariant and precomputed.
+template <bool F16, int W, int TH, int WM, int WN, int FM, int FN, int WS>
+__global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_band_kernel(ConvArgs p, int ntn) {
+    constexpr int NW = WM * WN;
+    constexpr int BN = 16 * FN * WN;
+    constexpr int Wp = W + 2;
+    constexpr int P = (TH + 2) * Wp;
+    constexpr int P64 = (P + 63) / 64 * 64;     // a DMA instruction fills 64 positions (1 KiB)
+    constexpr int PLANE = P64 * 16;             // bytes of one chunk plane
+    constexpr int PATCH = 8 * PLANE;            // bytes of one patch buffer
+    constexpr int NPB = P64 / 64;               // 64-position DMA blocks per chunk plane
+    constexpr int PI = 8 * NPB;                 // patch DMA instructions
+    constexpr int NPW = (PI + NW - 1) / NW;     // patch DMA instructions per wave (upper bound)
+    static_assert(NPW <= MAXPW, "patch too large");
+    constexpr int WSL = BN * 128;
+    constexpr int NWI = BN / 8 / NW;
+    static_assert(NWI * 8 * NW == BN, "weight slice rows must split evenly over waves");
+    // MFMA row m <-> patch position m (tap (0,0) of output pixel (m / Wp, m % Wp)): columns W, W+1 of
+    // each row are computed and discarded.  Consecutive m are consecutive LDS slots (conflict-free
+    // ds_read_b128) and a tap is a constant position shift.
+    constexpr int Mv = TH * Wp - 2;
+    static_assert(16 * FM * WM >= Mv, "MFMA rows must cover the band");
+    typedef Num<F16> T;
+    typedef typename T::frag frag;
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [patch0][patch1][wsl0..wsl{WS-1}]
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int H = p.H;
+    const int bands = H / TH;
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tn = lid % ntn;
+    const int rest = lid / ntn;
+    const int band = rest % bands, b = rest / bands;
+    const int oh0 = band * TH, n0 = tn * BN;
+
+    const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * H * W * p.Cx * 2);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
+    const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
+
+    // Patch DMA: instruction q -> chunk plane c = q / NPB, positions 64*(q % NPB) + lane.  The
+    // source offsets are recomputed per chunk (Wp is a compile-time constant) to save registers.
+    auto patch_src = [&](int u) -> uint32_t {
+        const int q = wave + NW * u;
+        const int c = q / NPB, pos = 64 * (q - c * NPB) + lane;
+        const int ih = oh0 - 1 + pos / Wp, iw = pos % Wp - 1;
+        const bool ok = q < PI && pos < P && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        return ok ? (uint32_t)((((b * H + ih) * W + iw) * p.Cx + p.x_off + 8 * c) * 2) : OOB;
+    };
+    // Weight slice DMA (row-major, swizzled source chunk).
+    uint32_t woff[NWI];
+#pragma unroll
+    for (int u = 0; u < NWI; ++u) {
+        const int row = 8 * (wave + NW * u) + (lane >> 3);
+        const int cl = (lane & 7) ^ ((row >> 1) & 7);
+        woff[u] = (uint32_t)(((n0 + row) * p.Kpad + 8 * cl) * 2);
+    }
+    // Fragment read offsets (bytes within a buffer) for kk = 0; kk = 1 is +4 chunk planes for the
+    // patch and an XOR of byte bit 6 for the swizzled weight rows ((4+x)^k == (x^k)^4 for x < 4).
+    int aoff[FM];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+        const int m = 16 * (wm * FM + j) + (lane & 15);
+        aoff[j] = (lane >> 4) * PLANE + (m < Mv ? m : 0) * 16;
+    }
+    int boff[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+        const int row = wn * 16 * FN + 16 * i + (lane & 15);
+        boff[i] = row * 128 + swzb(row, lane >> 4) * 16;
+    }
+
+    const int npw = __builtin_amdgcn_readfirstlane((PI - wave + NW - 1) / NW);  // this wave's patch instrs
+    const int dbg = p.dbg;
+    auto issue_patch = [&](int chunk, int pb) {
+        if ((dbg & 2) && chunk > 0) return;
+        const uint32_t cadd = (uint32_t)(chunk * 64 * 2);
+        char* dst = smem + pb * PATCH;
+#pragma unroll
+        for (int u = 0; u < NPW; ++u)
+            if (u < npw) {
+                const uint32_t src = patch_src(u);
+                dma16(xr, dst + (wave + NW * u) * 1024, src == OOB ? OOB : src + cadd);
+            }
+    };
+    auto issue_w = [&](int step, int wb) {
+        if ((dbg & 1) && step >= WS) return;
+        const int chunk = step / 9, tap = step - chunk * 9;
+        const uint32_t kadd = (uint32_t)((tap * p.Cin + chunk * 64) * 2);
+        char* dst = smem + 2 * PATCH + wb * WSL;
+#pragma unroll
+        for (int u = 0; u < NWI; ++u) dma16(wr, dst + (wave + NW * u) * 1024, woff[u] + kadd);
+    };
+
+    f32x4_t acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+    auto mma_tap = [&](const char* pa, const char* wa, int shift_bytes) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            frag af[FN], bfr[FM];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) af[i] = *(const frag*)(wa + (boff[i] ^ (kk * 64)));
+#pragma unroll
+            for (int j = 0; j < FM; ++j) bfr[j] = *(const frag*)(pa + aoff[j] + kk * 4 * PLANE + shift_bytes);
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
+        }
+    };
+
+    const int nchunk = p.Cin / 64;
+    const int nsteps = nchunk * 9;
+    // Prologue: patch 0 and the first WS-1 weight slices.
+    issue_patch(0, 0);
+    for (int s = 0; s < WS - 1 && s < nsteps; ++s) issue_w(s, s);
+    // Warm this XCD's L2 with the block's whole [BN][K] weight panel while the prologue DMA is in
+    // flight: every CU would otherwise miss on the same cold 32-KiB slice in lockstep at each K-step.
+    // Blocks b, b+8, ... share an XCD (round-robin dispatch; a speed assumption only); the 32 blocks of
+    // an XCD each touch one 4-byte word per 128-B line of a 1/32 share of the panel.
+    {
+        const uint32_t panel = (uint32_t)BN * p.Kpad * 2;
+        const uint32_t share = (panel + 31) / 32;
+        const uint32_t base = (uint32_t)n0 * p.Kpad * 2 + (uint32_t)((blockIdx.x / 8) % 32) * share;
+        const uint32_t stride = (uint32_t)NW * 64 * 128;
+        unsigned dummy;
+        for (uint32_t o = (uint32_t)(wave * 64 + lane) * 128; o < share; o += stride) {
+            asm volatile("buffer_load_dword %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
+                         : "=&v"(dummy) : "v"(base + o), "s"(wr) : "memory");
+        }
+    }
+    wait_vm<0>();
+    __syncthreads();
+    int step = 0;
+    for (int chunk = 0; chunk < nchunk; ++chunk) {
+        const char* pa = smem + (chunk & 1) * PATCH;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap, ++step) {
+            const int ahead = step + WS - 1;  // slice to prefetch now
+            if (ahead < nsteps) issue_w(ahead, ahead % WS);
+            const bool np = tap == 0 && chunk + 1 < nchunk;
+            if (np) issue_patch(chunk + 1, (chunk + 1) & 1);
+            mma_tap(pa, smem + 2 * PATCH + (step % WS) * WSL, ((tap / 3) * Wp + (tap % 3)) * 16);
+            // Retire slice step+1 (and, at the chunk's last tap, the next patch).  Younger groups
+            // allowed in flight: the slices step+2..step+WS-1 (WS=3: one) and a patch issued this step.
+            const int younger_w = (WS == 3 && step + 2 < nsteps && ahead >= step + 2) ? NWI : 0;
+            if (tap == 8) {
+                wait_vm<0>();
+            } else if (np) {
+                // order of issue this step: slice `ahead`, then patch -> both may stay outstanding
+                if (NWI + NPW <= 8 && younger_w + npw <= 8) {
+                    if (younger_w + npw == 8) wait_vm<8>(); else if (younger_w + npw == 7) wait_vm<7>();
+                    else if (younger_w + npw == 6) wait_vm<6>(); else if (younger_w + npw == 5) wait_vm<5>();
+                    else if (younger_w + npw == 4) wait_vm<4>(); else if (younger_w + npw == 3) wait_vm<3>();
+                    else if (younger_w + npw == 2) wait_vm<2>(); else if (younger_w + npw == 1) wait_vm<1>();
+                    else wait_vm<0>();
+                } else {
+                    wait_vm<0>();
+                }
+            } else {
+                if (younger_w == 4) wait_vm<4>(); else if (younger_w == 2) wait_vm<2>();
+                else if (younger_w == 1) wait_vm<1>(); else wait_vm<0>();
+            }
+            __syncthreads();
+        }
+    }
+
+    // Fused epilogue straight from registers: lane = 4 consecutive channels of one pixel.
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+        const int m = 16 * (wm * FM + j) + (lane & 15);
+        const int r = m / Wp, c = m - r * Wp;
+        if (m >= Mv || c >= W) continue;
+        const size_t pix = (size_t)(b * H + oh0 + r) * W + c;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+            const int n = n0 + wn * 16 * FN + 16 * i + 4 * (lane >> 4);
+            if (n >= p.Cout) continue;
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if (p.bias) {
+                const float4 bb = *(const float4*)(p.bias + n);
+                v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+            }
+            if (p.res) {
+                const uint2 r = *(const uint2*)(p.res + pix * p.Cres + p.res_off + n);
+                float f[8];
+                T::unpack8(make_uint4(r.x, r.y, 0, 0), f);
+                v[0] += f[0]; v[1] += f[1]; v[2] += f[2]; v[3] += f[3];
+            }
+            if (p.act == 1) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+            } else if (p.act == 2) {
+                const float4 sl = *(const float4*)(p.slope + n);
+                const float s4[4] = {sl.x, sl.y, sl.z, sl.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * s4[e];
+            }
+            float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+            const uint4 pk = T::pack8(o8);
+            *(uint2*)(p.y + pix * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
+            if (p.y2) {
+                const float4 a = *(const float4*)(p.aff_s + n), c = *(const float4*)(p.aff_b + n);
+                float u8[8] = {v[0] * a.x + c.x, v[1] * a.y + c.y, v[2] * a.z + c.z, v[3] * a.w + c.w, 0, 0, 0, 0};
+                const uint4 pk2 = T::pack8(u8);
+                *(uint2*)(p.y2 + pix * p.Cy2 + p.y2_off + n) = make_uint2(pk2.x, pk2.y);
+            }
+        }
+    }
+}
+
+// Supported bands: (W, TH) with TH*(W+2)-2 <= the variant's MFMA rows.
+//   variant 0: 2x4 waves, FM 7, FN 4 -> 224 pixel rows x 256 channels
+//   variant 1: 2x4 waves, FM 7, FN 2 -> 224 x 128
+//   variant 2: 4x2 waves, FM 4, FN 2 -> 256 x 64
+template <bool F16, int W, int TH, int V, int WS>
+static hipError_t launch_band_k(const ConvArgs& a, hipStream_t s) {
+    constexpr int WM = V == 2 ? 4 : 2, WN = V == 2 ? 2 : 4, FM = V == 2 ? 4 : 7, FN = V == 0 ? 4 : 2;
+    constexpr int BN = 16 * FN * WN;
+    constexpr int P64 = ((TH + 2) * (W + 2) + 63) / 64 * 64;
+    constexpr int LDS = 2 * 8 * P64 * 16 + WS * BN * 128;
+    static_assert(LDS <= 160 * 1024, "band LDS budget");
+    auto k = conv3x3_band_kernel<F16, W, TH, WM, WN, FM, FN, WS>;
+    static bool attr = false;  // opt in to > 64 KiB dynamic LDS once per instantiation
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+        attr = true;
+    }
+    const int ntn = (a.Cout + BN - 1) / BN;
+    dim3 grid(a.B * (a.H / TH) * ntn);
+    hipLaunchKernelGGL(k, grid, dim3(64 * WM * WN), LDS, s, a, ntn);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// Applicability: 3x3 / stride 1 / pad 1, Cin % 64 == 0, a supported (W, TH) band, Cout a multiple of
+// the variant's BN.  Returns the band config id (see launch_conv_band).
+bool band_plan(const ConvArgs& a, int* cfg, int* variant) {
+    if (a.Kh != 3 || a.Kw != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1) return false;
+    if (a.Cin % 64 != 0 || a.Ho != a.H || a.Wo != a.W || a.partial) return false;
+    int v;
+    if (a.Cout % 256 == 0) v = 0;
+    else if (a.Cout % 128 == 0) v = 1;
+    else if (a.Cout % 64 == 0) v = 2;
+    else return false;
+    int c;
+    if (a.W == 14 && a.H % 14 == 0) c = 0;
+    else if (a.W == 28 && a.H % 7 == 0) c = 1;
+    else if (a.W == 56 && a.H % 4 == 0) c = 2;
+    else if (a.W == 112 && a.H % 2 == 0) c = 3;
+    else return false;
+    if (c == 0 && v == 2) return false;  // 14x14x64: 196 rows of a 256-row tile, not worth it
+    if ((c == 2 || c == 3) && v != 2) return false;  // 4x58 / 2x114 rows exceed the 224-row variants
+    *cfg = c;
+    *variant = v;
+    return true;
+}
+
+template <bool F16>
+static hipError_t launch_band_t(const ConvArgs& a, int c, int v, hipStream_t s) {
+    switch (c * 3 + v) {
+        case 0: return launch_band_k<F16, 14, 14, 0, 3>(a, s);
+        case 1: return launch_band_k<F16, 14, 14, 1, 3>(a, s);
+        case 3: return launch_band_k<F16, 28, 7, 0, 2>(a, s);
+        case 4: return launch_band_k<F16, 28, 7, 1, 3>(a, s);
+        case 5: return launch_band_k<F16, 28, 7, 2, 3>(a, s);
+        case 8: return launch_band_k<F16, 56, 4, 2, 3>(a, s);
+        case 11: return launch_band_k<F16, 112, 2, 2, 2>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_conv_band(const ConvArgs& a, int cfg, int variant, hipStream_t s) {
+    return a.f16 ? launch_band_t<true>(a, cfg, variant, s) : launch_band_t<false>(a, cfg, variant, s);
+}
+
+}  // namespace fr

@@ -20,6 +20,8 @@
 // FASTK (Cin % 64 == 0): a K-step is one (r, s) tap and 64 channels, tracked in scalars.
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace fr {
 
 namespace {
@@ -70,18 +72,31 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, float* v, int m, in
     }
 }
 
-template <bool F16, int BM, int BN, int WM, int WN, bool FASTK>
-__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
-    static_assert(WM * WN == 4, "4 waves");
+template <int BM, int BN, int WM, int WN, int STAGES>
+struct ConvGeom {
+    static constexpr int NW = WM * WN, NT = 64 * NW;
+    static constexpr int STAGE = (BM + BN) * BK * 2;  // bytes per LDS stage
+    static constexpr int LDS_A = STAGES * STAGE, LDS_E = BM * (BN + 4) * 4;
+    static constexpr int LDS_BYTES = LDS_A > LDS_E ? LDS_A : LDS_E;
+    static constexpr int BLOCKS_PER_CU = (160 * 1024) / LDS_BYTES > 2 ? 2 : (160 * 1024) / LDS_BYTES;
+    static constexpr int MIN_WAVES_PER_SIMD = BLOCKS_PER_CU * NW / 4;
+};
+
+template <bool F16, int BM, int BN, int WM, int WN, int STAGES, bool FASTK>
+__global__ __launch_bounds__(64 * WM * WN, (ConvGeom<BM, BN, WM, WN, STAGES>::MIN_WAVES_PER_SIMD))
+void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
+    typedef ConvGeom<BM, BN, WM, WN, STAGES> Gm;
+    constexpr int NW = Gm::NW, NT = Gm::NT;
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     typedef Num<F16> T;
     typedef typename T::frag frag;
     constexpr int TWM = BM / WM, TWN = BN / WN;  // wave tile (pixels, channels)
     constexpr int FM = TWM / 16, FN = TWN / 16;  // MFMA tiles per wave
-    constexpr int NA = BM / 32, NB = BN / 32;    // DMA instructions per wave per K-step
-    constexpr int STAGE_A = BM * BK * 2, STAGE = (BM + BN) * BK * 2;  // bytes
+    constexpr int NA = BM / (8 * NW), NB = BN / (8 * NW);  // DMA instructions per wave per K-step
+    static_assert(NA * 8 * NW == BM && NB * 8 * NW == BN, "tile rows must split evenly over the waves");
+    constexpr int STAGE_A = BM * BK * 2, STAGE = Gm::STAGE;
     constexpr int EPI_LD = BN + 4;
-    constexpr int LDS_A = 2 * STAGE, LDS_E = BM * EPI_LD * 4;
-    constexpr int LDS_BYTES = LDS_A > LDS_E ? LDS_A : LDS_E;
+    constexpr int LDS_BYTES = Gm::LDS_BYTES;
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];  // the ONLY LDS object (guide §5 trap 4a)
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -95,8 +110,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
     const int kt0 = split * kt_per_split;
     const int kt1 = min(nkt, kt0 + kt_per_split);
 
-    // Lane's DMA slot: rows 8*(wave + 4i) + (lane>>3); the logical chunk it fetches is the same for
-    // every i (the swizzle term (row>>1)&7 = (4*wave + (lane>>4)) & 7 does not depend on i).
+    // Lane's DMA slot: rows 8*(wave + NW*i) + (lane>>3); the logical chunk it fetches is the same for
+    // every i (the swizzle term (row>>1)&7 = (4*wave + 4*NW*i + (lane>>4)) & 7 does not depend on i).
     const int lrow = lane >> 3;
     const int cl = (lane & 7) ^ ((4 * wave + (lane >> 4)) & 7);
 
@@ -110,7 +125,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
     uint32_t a_base[NA];  // byte offset of (b, ih0, iw0, x_off [+ 8*cl]) — wraps if ih0/iw0 < 0, only used when valid
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-        const int m = m0 + 8 * (wave + 4 * i) + lrow;
+        const int m = m0 + 8 * (wave + NW * i) + lrow;
         if (m < p.M) {
             const int b = m / HoWo, r = m - b * HoWo;
             const int oh = r / p.Wo, ow = r - oh * p.Wo;
@@ -127,7 +142,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
     }
     uint32_t b_base[NB];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) b_base[j] = (uint32_t)(((n0 + 8 * (wave + 4 * j) + lrow) * p.Kpad + 8 * cl) * 2);
+    for (int j = 0; j < NB; ++j) b_base[j] = (uint32_t)(((n0 + 8 * (wave + NW * j) + lrow) * p.Kpad + 8 * cl) * 2);
 
     // K-step position: FASTK → wave-uniform (r, s, c0); generic → per-lane (r, s, c) of k = kt*64 + 8*cl.
     int r_cur, s_cur, c_cur;
@@ -150,10 +165,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
             bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
             if (!FASTK) ok = ok && k_cur < p.K;
             const uint32_t off = ok ? a_base[i] + (uint32_t)soff : OOB;
-            dma16(xr, sA + (wave + 4 * i) * 1024, off);
+            dma16(xr, sA + (wave + NW * i) * 1024, off);
         }
 #pragma unroll
-        for (int j = 0; j < NB; ++j) dma16(wr, sB + (wave + 4 * j) * 1024, b_base[j] + (uint32_t)(kt * BK * 2));
+        for (int j = 0; j < NB; ++j) dma16(wr, sB + (wave + NW * j) * 1024, b_base[j] + (uint32_t)(kt * BK * 2));
         // advance one K-step
         if (FASTK) {
             c_cur += BK;
@@ -177,14 +192,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-    if (kt0 < kt1) {
-        issue(kt0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-        if (kt + 1 < kt1) issue(kt + 1, buf ^ 1);
+    auto compute = [&](int buf) {
         const bf16_t* sA = (const bf16_t*)(smem + buf * STAGE);
         const bf16_t* sW = (const bf16_t*)(smem + buf * STAGE + STAGE_A);
 #pragma unroll
@@ -206,9 +214,48 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
 #pragma unroll
                 for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next stage landed (this wave's DMA)
-        __syncthreads();                     // ... and every other wave's; stage `buf` free again
-        buf ^= 1;
+    };
+
+    if (STAGES == 2) {
+        // DMA for step t+1 overlaps the MFMAs of step t; one vmcnt(0) + barrier per step.
+        if (kt0 < kt1) {
+            issue(kt0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        int buf = 0;
+        for (int kt = kt0; kt < kt1; ++kt) {
+            if (kt + 1 < kt1) issue(kt + 1, buf ^ 1);
+            compute(buf);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next stage landed (this wave's DMA)
+            __syncthreads();                                   // ... and every wave's; stage `buf` free
+            buf ^= 1;
+        }
+    } else {
+        // 3-stage ring: two K-steps of DMA in flight; at step t wait only for step t's group
+        // (vmcnt(NA+NB) leaves step t+1's group outstanding), raw s_barrier (no vmcnt drain), then
+        // issue step t+2 into the stage step t-1 used (every wave has passed its MFMAs).
+        constexpr int GROUP = NA + NB;
+        if (kt0 < kt1) issue(kt0, 0);
+        if (kt0 + 1 < kt1) issue(kt0 + 1, 1);
+        int buf = 0;
+        for (int kt = kt0; kt < kt1; ++kt) {
+            if (kt + 1 < kt1) {
+                if constexpr (GROUP == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else if constexpr (GROUP == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                else if constexpr (GROUP == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else if constexpr (GROUP == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt + 2 < kt1) issue(kt + 2, buf == 0 ? 2 : buf - 1);
+            compute(buf);
+            buf = buf == 2 ? 0 : buf + 1;
+        }
+        __syncthreads();
     }
 
     // Epilogue: accumulators → LDS f32 tile [BM][EPI_LD] → coalesced 8-channel groups.
@@ -223,7 +270,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs p, int tile
         }
     __syncthreads();
     constexpr int G = BN / 8;
-    for (int it = tid; it < BM * G; it += 256) {
+    for (int it = tid; it < BM * G; it += NT) {
         const int ml = it / G, g = it - ml * G;
         const int m = m0 + ml, n = n0 + g * 8;
         if (m >= p.M || n >= p.Cout) continue;
@@ -257,53 +304,85 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(ConvArgs p) {
     }
 }
 
-template <bool F16, int BM, int BN, int WM, int WN>
+template <bool F16, int BM, int BN, int WM, int WN, int STAGES>
 hipError_t launch_variant(const ConvArgs& a, hipStream_t s) {
     const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.Cout + BN - 1) / BN;
     const int nkt = a.Kpad / BK;
     const int split = a.split_k > 1 ? a.split_k : 1;
     const int per = (nkt + split - 1) / split;
     dim3 grid(tiles_m * tiles_n, split);
+    dim3 block(64 * WM * WN);
     if (a.Cin % 64 == 0)
-        hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN, true>), grid, dim3(256), 0, s, a, tiles_n, per);
+        hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN, STAGES, true>), grid, block, 0, s, a, tiles_n, per);
     else
-        hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN, false>), grid, dim3(256), 0, s, a, tiles_n, per);
+        hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN, STAGES, false>), grid, block, 0, s, a, tiles_n, per);
     return hipGetLastError();
 }
 
 template <bool F16>
 hipError_t launch_dtype(const ConvArgs& a, hipStream_t s) {
     switch (a.tile) {
-        case TILE_256x64: return launch_variant<F16, 256, 64, 4, 1>(a, s);
-        case TILE_128x64: return launch_variant<F16, 128, 64, 2, 2>(a, s);
-        case TILE_64x128: return launch_variant<F16, 64, 128, 2, 2>(a, s);
-        default: return launch_variant<F16, 128, 128, 2, 2>(a, s);
+        case TILE_256x64: return launch_variant<F16, 256, 64, 4, 1, 2>(a, s);
+        case TILE_128x64: return launch_variant<F16, 128, 64, 2, 2, 2>(a, s);
+        case TILE_64x128: return launch_variant<F16, 64, 128, 2, 2, 2>(a, s);
+        case TILE_128x128_S3: return launch_variant<F16, 128, 128, 2, 2, 3>(a, s);
+        case TILE_256x128: return launch_variant<F16, 256, 128, 4, 2, 3>(a, s);
+        case TILE_128x256: return launch_variant<F16, 128, 256, 2, 4, 3>(a, s);
+        default: return launch_variant<F16, 128, 128, 2, 2, 2>(a, s);
     }
 }
 
 }  // namespace
 
-int conv_tile_bm(int tile) { return tile == TILE_256x64 ? 256 : tile == TILE_64x128 ? 64 : 128; }
-int conv_tile_bn(int tile) { return (tile == TILE_256x64 || tile == TILE_128x64) ? 64 : 128; }
+int conv_tile_bm(int tile) {
+    switch (tile) {
+        case TILE_256x64: case TILE_256x128: return 256;
+        case TILE_64x128: return 64;
+        default: return 128;
+    }
+}
+int conv_tile_bn(int tile) {
+    switch (tile) {
+        case TILE_256x64: case TILE_128x64: return 64;
+        case TILE_128x256: return 256;
+        default: return 128;
+    }
+}
+static int tile_blocks_per_cu(int tile) {
+    switch (tile) {
+        case TILE_128x128_S3: case TILE_256x128: case TILE_128x256: return 1;
+        default: return 2;
+    }
+}
 
-// Tile + split-K choice: minimise (rounds of resident blocks) x (tile area / tile efficiency),
-// where a round is 2 blocks per CU on 256 CUs.  Small-M layers get split-K to fill the chip.
+// Tile + split-K choice: minimise rounds-of-resident-blocks x per-block work / tile efficiency,
+// plus a charge for split-K (partials round trip + reduce kernel + prologue/epilogue amortised over
+// fewer K-steps).  A forced variant via FR_CONV_TILE=<id> (env) is honoured for experiments.
 void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
-    static const int tiles[4] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128};
-    static const double eff[4] = {1.0, 0.95, 0.8, 0.8};
+    static const int env_tile = [] {
+        const char* e = getenv("FR_CONV_TILE");
+        return e ? atoi(e) : -1;
+    }();
+    static const int tiles[] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128, TILE_128x128_S3, TILE_256x128,
+                                TILE_128x256};
+    static const double eff[] = {1.0, 0.95, 0.8, 0.8, 1.05, 1.15, 1.15};
     const int nkt = Kpad / BK;
     double best = 1e30;
     int bt = TILE_128x128, bs = 1;
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < 7; ++v) {
+        if (env_tile >= 0 && tiles[v] != env_tile) continue;
         const int BM = conv_tile_bm(tiles[v]), BN = conv_tile_bn(tiles[v]);
-        if (BN == 128 && Cout <= 64) continue;
+        if (BN >= 128 && Cout <= 64) continue;
+        if (BN == 256 && Cout <= 128) continue;
         const long nt = (long)((M + BM - 1) / BM) * ((Cout + BN - 1) / BN);
+        const int slots = 256 * tile_blocks_per_cu(tiles[v]);
         for (int sk = 1; sk <= 16; sk *= 2) {
-            if (sk > 1 && nkt / sk < 4) break;
+            if (sk > 1 && nkt / sk < 8) break;
             const long blocks = nt * sk;
-            const double rounds = (double)((blocks + 511) / 512);
-            const double per_block = (double)BM * BN * ((nkt + sk - 1) / sk) / eff[v];
-            const double cost = rounds * per_block + (sk > 1 ? 0.02 * nt * BM * BN / 512.0 : 0.0);
+            const double rounds = (double)((blocks + slots - 1) / slots);
+            const double ksteps = (double)((nkt + sk - 1) / sk) + 6.0;  // + prologue/epilogue ~ 6 K-steps
+            const double per_block = (double)BM * BN * ksteps / eff[v] / (512.0 / slots);
+            const double cost = rounds * per_block + (sk > 1 ? 0.25 * (double)M * Cout * sk / 2048.0 : 0.0);
             if (cost < best * 0.999) { best = cost; bt = tiles[v]; bs = sk; }
         }
     }

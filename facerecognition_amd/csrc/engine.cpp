@@ -10,6 +10,8 @@
 // (facerecognition_amd/weights.py); this file only knows tensor names.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -542,7 +544,29 @@ int reserve(fr_handle* h, int maxB) {
     return FR_OK;
 }
 
+bool band_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_BAND");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
+int conv_dbg() {
+    static const int d = [] {
+        const char* e = getenv("FR_CONV_DBG");
+        return e ? atoi(e) : 0;
+    }();
+    return d;
+}
+
 int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
+    a.dbg = conv_dbg();
+    int TH, variant;
+    if (band_enabled() && band_plan(a, &TH, &variant)) {
+        FR_HIP_CHECK(launch_conv_band(a, TH, variant, s));
+        return FR_OK;
+    }
     int tile, split;
     conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
     a.tile = tile;
@@ -814,6 +838,28 @@ int fr_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, i
     return FR_OK;
 }
 
+int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
+    if (!h || !buf || n == 0 || B <= 0) { set_error("fr_debug_plan: bad argument"); return FR_ERR_ARG; }
+    std::string out;
+    for (const auto& op : h->ops) {
+        if (op.kind != OP_CONV && op.kind != OP_HEAD) {
+            out += std::string(op.kind == OP_PRE ? "pre" : op.kind == OP_MAXPOOL ? "maxpool" : "avgpool") + "\n";
+            continue;
+        }
+        const auto& cw = h->convw[op.wi];
+        const int M = op.kind == OP_HEAD ? B : B * h->tensors[op.out].H * h->tensors[op.out].W;
+        int tile, sp;
+        conv_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
+        const std::string nm = op.kind == OP_HEAD ? "head" : h->tensors[op.out].name;
+        out += (op.kind == OP_HEAD ? "head " : "conv ") + std::to_string(M) + " " + std::to_string(cw.Cout) + " " +
+               std::to_string(cw.K) + " " + std::to_string(cw.Kpad) + " " + std::to_string(tile) + " " +
+               std::to_string(sp) + " " + std::to_string(op.kh) + "x" + std::to_string(op.kw) + " " +
+               (nm.empty() ? "-" : nm) + "\n";
+    }
+    std::snprintf(buf, n, "%s", out.c_str());
+    return out.size() + 1 <= n ? FR_OK : FR_ERR_ARG;
+}
+
 int fr_debug_tensor_count(const fr_handle* h) { return h ? (int)h->tensors.size() : 0; }
 
 const char* fr_debug_tensor_name(const fr_handle* h, int t) {
@@ -859,8 +905,14 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
     a.y = (bf16_t*)d->y; a.Cy = d->Cy; a.y_off = d->y_off;
     a.y2 = (bf16_t*)d->y2; a.Cy2 = d->Cy2; a.y2_off = d->y2_off; a.aff_s = d->aff_s; a.aff_b = d->aff_b;
     a.f16 = d->dtype == FR_DTYPE_F16;
+    if (d->tile == FR_TILE_BAND + 1) {
+        int TH, variant;
+        if (!band_plan(a, &TH, &variant)) { set_error("fr_op_conv2d: band kernel not applicable"); return FR_ERR_ARG; }
+        FR_HIP_CHECK(launch_conv_band(a, TH, variant, (hipStream_t)stream));
+        return FR_OK;
+    }
     if (d->tile > 0) {
-        if (d->tile > 4) { set_error("fr_op_conv2d: bad tile"); return FR_ERR_ARG; }
+        if (d->tile > 7) { set_error("fr_op_conv2d: bad tile"); return FR_ERR_ARG; }
         a.tile = d->tile - 1;
     } else {
         int tile, sp;

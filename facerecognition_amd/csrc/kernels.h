@@ -6,7 +6,8 @@
 namespace fr {
 
 // Conv tile variants (BM pixels x BN channels, 4 waves each).
-enum { TILE_128x128 = 0, TILE_256x64 = 1, TILE_128x64 = 2, TILE_64x128 = 3 };
+enum { TILE_128x128 = 0, TILE_256x64 = 1, TILE_128x64 = 2, TILE_64x128 = 3,
+       TILE_128x128_S3 = 4, TILE_256x128 = 5, TILE_128x256 = 6 };  // *_S3 / 8-wave tiles: 3-stage DMA ring
 
 // Implicit-GEMM convolution, NHWC bf16 in/out, f32 accumulate, fused epilogue.
 // GEMM view: M = B*Ho*Wo output pixels, N = Cout, K = Kh*Kw*Cin (c fastest).
@@ -21,6 +22,7 @@ struct ConvArgs {
     float* partial; int split_k;  // partial != null: raw f32 partials [split][M][Npad], no epilogue
     int f16;                      // 0: bf16 storage + bf16 MFMA; 1: f16 storage + f16 MFMA
     int tile;                     // TILE_* variant (conv_plan)
+    int dbg;                      // experiment switches (FR_CONV_DBG env; 0 in production)
 };
 
 // Choose tile variant and split-K factor for a GEMM of M x Cout x Kpad.
@@ -30,6 +32,9 @@ int conv_tile_bn(int tile);
 
 // Launches a.tile with a.split_k; returns hipError_t.
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
+// Row-band direct 3x3/s1/p1 conv (conv_band.hip): applicability/params, launch.
+bool band_plan(const ConvArgs& a, int* cfg, int* variant);
+hipError_t launch_conv_band(const ConvArgs& a, int cfg, int variant, hipStream_t s);
 // Split-K reduction + the same fused epilogue as the conv kernel.
 hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
 // Number of K-tiles of 64 (for split-k planning).

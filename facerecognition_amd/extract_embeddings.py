@@ -1,0 +1,322 @@
+"""Drop-in for the reference's ``inference/extract_embeddings.py`` (same names, arguments, return
+values and error conventions), with every forward pass and every gallery reduction on the MI355X
+through libfrhip.so.
+
+Reference → here:
+  load_arcface_model  :80-123   checkpoint schema read with torch.load(weights_only=True); arch
+                                 auto-detected (ResNet-50 ArcFace / IResNet100 / InceptionResnetV1)
+  load_facenet_model  :126-167  FaceNet state_dict (model.* / backbone.* prefixes, logits ignored)
+  get_transform / get_facenet_transform :170-185   Resize(PIL bilinear)+ToTensor+Normalize(0.5)
+  extract_embedding_single :348-389   one image → np.f32 [512] or None on any error
+  extract_embeddings_batch :392-443   (emb [M,512], valid_paths); bad files skipped; empty → (array([]), [])
+  extract_embedding_for_folder :714-762   per-identity mean + renorm — batched: ONE fr_embed for the
+                                 folder instead of one forward per image
+  compute_prototypes :555-592 / build_faiss_index :595-645 (→ DeviceGallery, IndexFlatIP surface)
+  build_db :765-835, extract_embeddings_from_csv :446-552, full_pipeline :838-888
+Face detection/alignment (FacePreprocessor, MTCNN) and t-SNE plotting are out of scope (SURVEY.md
+§2.1 rows 1/11): requesting them prints a warning and the raw image is used, exactly as the reference
+does when its detector is unavailable.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import weights as Wt
+
+ARCFACE_TEMPLATE = np.array([[38.2946, 51.6963], [73.5318, 51.5014], [56.0252, 71.7366],
+                             [41.5493, 92.3655], [70.7299, 92.2041]], dtype=np.float32)
+IMG_EXTS = (".jpg", ".jpeg", ".png", ".webp")
+
+
+def _device_index(device) -> int:
+    """'cuda', 'cuda:1', torch.device or int → HIP device index.  There is no CPU path."""
+    if device is None:
+        return 0
+    if isinstance(device, int):
+        return device
+    s = str(device)
+    if s.startswith("cuda"):
+        return int(s.split(":")[1]) if ":" in s else 0
+    raise ValueError(f"device {device!r}: facerecognition_amd runs on a ROCm GPU ('cuda[:N]'); "
+                     "there is deliberately no CPU fallback")
+
+
+# ---------------------------------------------------------------------------------------- models
+def load_arcface_model(model_path: str, device: str = "cuda"):
+    """Returns (model, info) like the reference; model(x, labels=None) → un-normalized embedding."""
+    from .model import FRModel
+
+    if not os.path.exists(model_path):
+        raise FileNotFoundError(f"Model khong ton tai: {model_path}")
+    sd, ck = Wt.load_checkpoint(model_path)
+    arch = Wt.detect_arch(sd)
+    config = ck.get("config") or {}
+    num_classes = config.get("num_classes", ck.get("num_classes") or 100)
+    embedding_size = (config.get("model") or {}).get("embedding_size", 512)
+    model = FRModel(arch, sd, device=_device_index(device))
+    info = {"num_classes": num_classes, "embedding_size": embedding_size, "arch": arch,
+            "epoch": ck.get("epoch") if ck.get("epoch") is not None else "N/A",
+            "val_acc": ck.get("val_acc") if ck.get("val_acc") is not None else "N/A",
+            "best_val_acc": ck.get("best_val_acc") if ck.get("best_val_acc") is not None else "N/A"}
+    print(f"Loaded model from {model_path} ({arch}, {model.dtype})")
+    return model, info
+
+
+def load_facenet_model(model_path: str, device: str = "cuda"):
+    model, info = load_arcface_model(model_path, device)
+    if model.arch != "irv1_facenet":
+        raise ValueError(f"{model_path} is not an InceptionResnetV1 (FaceNet) checkpoint ({model.arch})")
+    return model, {k: info[k] for k in ("embedding_size", "epoch", "best_val_acc")}
+
+
+# ---------------------------------------------------------------------------------------- transforms
+class _Transform:
+    """Resize((S,S)) with PIL bilinear (identity when already S x S) + ToTensor + Normalize(0.5, 0.5)."""
+
+    def __init__(self, image_size: int):
+        self.size = image_size
+
+    def resize(self, img):
+        from PIL import Image
+        img = img.convert("RGB")
+        if img.size != (self.size, self.size):
+            img = img.resize((self.size, self.size), Image.BILINEAR)
+        return img
+
+    def __call__(self, img):
+        import torch
+        a = np.asarray(self.resize(img), dtype=np.uint8)
+        t = torch.from_numpy(a.copy()).permute(2, 0, 1).contiguous().float().div(255)
+        return (t - 0.5) / 0.5
+
+
+def get_transform(image_size: int = 112):
+    return _Transform(image_size)
+
+
+def get_facenet_transform(image_size: int = 160):
+    return _Transform(image_size)
+
+
+def _load_u8(img_input, transform) -> np.ndarray:
+    """PIL/path → resized RGB u8 HWC (the fused u8 path of fr_embed does ToTensor+Normalize exactly)."""
+    from PIL import Image
+    img = Image.open(img_input) if isinstance(img_input, str) else img_input
+    if isinstance(transform, _Transform):
+        return np.asarray(transform.resize(img), dtype=np.uint8)
+    raise TypeError("transform must come from get_transform()/get_facenet_transform()")
+
+
+def _embed_u8(model, u8: np.ndarray) -> np.ndarray:
+    import torch
+    return model.embed(torch.from_numpy(np.ascontiguousarray(u8)), normalize=True).cpu().numpy()
+
+
+# ---------------------------------------------------------------------------------------- extraction
+def extract_embedding_single(img_input, model, transform, device: str = "cuda",
+                             model_type: str = "arcface") -> Optional[np.ndarray]:
+    try:
+        u8 = _load_u8(img_input, transform)
+        return _embed_u8(model, u8[None])[0].astype(np.float32).flatten()
+    except Exception as e:  # reference: any failure → None (extract_embeddings.py:386-389)
+        if isinstance(img_input, str):
+            print(f"Loi xu ly {img_input}: {e}")
+        return None
+
+
+def extract_embeddings_batch(image_paths: List[str], model, transform, device: str = "cuda",
+                             batch_size: int = 64, model_type: str = "arcface") -> Tuple[np.ndarray, List[str]]:
+    embeddings, valid_paths = [], []
+    for i in range(0, len(image_paths), batch_size):
+        imgs, paths = [], []
+        for path in image_paths[i:i + batch_size]:
+            try:
+                imgs.append(_load_u8(path, transform))
+                paths.append(path)
+            except Exception as e:
+                print(f"Skip {path}: {e}")
+        if not imgs:
+            continue
+        embeddings.append(_embed_u8(model, np.stack(imgs)))
+        valid_paths.extend(paths)
+    if not embeddings:
+        return np.array([]), []
+    return np.vstack(embeddings).astype(np.float32), valid_paths
+
+
+def _mean_renorm(embs: np.ndarray) -> np.ndarray:
+    m = np.mean(np.stack(list(embs), axis=0), axis=0)
+    return m / (np.linalg.norm(m) + 1e-8)
+
+
+def extract_embedding_for_folder(folder: str, model, transform, device: str = "cuda", preprocessor=None,
+                                 model_type: str = "arcface") -> Optional[np.ndarray]:
+    if not os.path.exists(folder):
+        return None
+    if preprocessor is not None:
+        print("[WARN] face detection/alignment is out of scope for facerecognition_amd; using raw images")
+    paths = [os.path.join(folder, f) for f in os.listdir(folder) if f.lower().endswith(IMG_EXTS)]
+    imgs = []
+    for p in paths:  # os.listdir order, as the reference
+        try:
+            imgs.append(_load_u8(p, transform))
+        except Exception as e:
+            print(f"Loi xu ly {p}: {e}")
+    if not imgs:
+        return None
+    return _mean_renorm(_embed_u8(model, np.stack(imgs))).astype(np.float32)
+
+
+def compute_prototypes(embeddings: np.ndarray, labels: np.ndarray, output_path: str = None) -> np.ndarray:
+    print("\n=== COMPUTING PROTOTYPES ===")
+    unique_labels = np.unique(labels)
+    prototypes = np.zeros((len(unique_labels), embeddings.shape[1]), dtype=np.float32)
+    for label in unique_labels:
+        p = embeddings[labels == label].mean(axis=0)
+        prototypes[label] = p / (np.linalg.norm(p) + 1e-8)
+    print(f"Computed {len(unique_labels)} prototypes")
+    if output_path:
+        np.save(output_path, prototypes)
+        print(f"Saved prototypes: {output_path}")
+    return prototypes
+
+
+def build_faiss_index(embeddings: np.ndarray, output_path: str = None, use_gpu: bool = True):
+    """IndexFlatIP equivalent on the GPU: rows L2-normalized (+1e-8) like the reference; saved as an
+    .npz (rows) because the FAISS binary format needs faiss, which is not part of this path."""
+    from .gallery import DeviceGallery
+
+    print("\n=== BUILDING DEVICE INDEX (IndexFlatIP semantics) ===")
+    e = np.asarray(embeddings, dtype=np.float32)
+    e = e / (np.linalg.norm(e, axis=1, keepdims=True) + 1e-8)
+    index = DeviceGallery(e, dim=e.shape[1])
+    print(f"Index built: {index.ntotal} vectors, {e.shape[1]}D")
+    if output_path:
+        np.savez(output_path if output_path.endswith(".npz") else output_path + ".npz", rows=e)
+        print(f"Saved index: {output_path}")
+    return index
+
+
+def read_index(path: str):
+    """Load an index written by build_faiss_index (the .faiss path of the reference maps to .npz)."""
+    from .gallery import DeviceGallery
+    p = path if os.path.exists(path) else (path + ".npz")
+    with np.load(p, allow_pickle=False) as z:
+        rows = z["rows"]
+    return DeviceGallery(rows, dim=rows.shape[1])
+
+
+def visualize_tsne(*_a, **_k):
+    raise NotImplementedError("t-SNE plotting is out of scope for facerecognition_amd (SURVEY.md §2.1 row 1)")
+
+
+# ---------------------------------------------------------------------------------------- drivers
+def build_db(model_path: str, root_folder: str = "data/celeb", save_path: str = "data/arcface_embeddings_db.npy",
+             device: str = None, use_face_detection: bool = True, model_type: str = "arcface") -> None:
+    print("=" * 60)
+    print(f"EXTRACT EMBEDDINGS DATABASE ({model_type.upper()})")
+    print("=" * 60)
+    device = device or "cuda"
+    if not os.path.exists(root_folder):
+        print(f"Root folder khong ton tai: {root_folder}")
+        return
+    if model_type == "facenet":
+        model, _ = load_facenet_model(model_path, device)
+        transform = get_facenet_transform()
+    else:
+        model, _ = load_arcface_model(model_path, device)
+        transform = get_transform(Wt.INPUT_SIZE[model.arch])
+    if use_face_detection:
+        print("[WARN] face detection/alignment is out of scope for facerecognition_amd; using raw images")
+    db: Dict[str, np.ndarray] = {}
+    persons = [p for p in os.listdir(root_folder) if os.path.isdir(os.path.join(root_folder, p))]
+    print(f"\nTim thay {len(persons)} celebrities")
+    for person in persons:
+        emb = extract_embedding_for_folder(os.path.join(root_folder, person), model, transform, device, None,
+                                           model_type)
+        if emb is not None:
+            db[person] = emb
+    if not db:
+        print("\nKhong co embeddings nao duoc tao!")
+        return
+    os.makedirs(os.path.dirname(save_path) or ".", exist_ok=True)
+    np.save(save_path, db)
+    print(f"\nDa luu {len(db)} embeddings vao {save_path}")
+    print(f"Success rate: {len(db)}/{len(persons)} ({100 * len(db) / len(persons):.1f}%)")
+
+
+def extract_embeddings_from_csv(model_path: str, csv_path: str, data_root: str = None,
+                                output_dir: str = "data/embeddings", device: str = None, batch_size: int = 64) -> Dict:
+    import pandas as pd
+
+    os.makedirs(output_dir, exist_ok=True)
+    model, _ = load_arcface_model(model_path, device or "cuda")
+    transform = get_transform(Wt.INPUT_SIZE[model.arch])
+    df = pd.read_csv(csv_path)
+    path_col = "image_path" if "image_path" in df.columns else ("image" if "image" in df.columns else None)
+    id_col = "identity_name" if "identity_name" in df.columns else ("person_id" if "person_id" in df.columns else None)
+    if path_col is None:
+        raise ValueError(f"CSV khong co cot path. Columns: {list(df.columns)}")
+    if id_col is None:
+        raise ValueError(f"CSV khong co cot identity. Columns: {list(df.columns)}")
+    image_paths = [os.path.join(data_root, p) for p in df[path_col]] if data_root else df[path_col].tolist()
+    identities = df[id_col].astype(str).tolist()
+    unique_ids = sorted(set(identities))
+    id_to_label = {id_: i for i, id_ in enumerate(unique_ids)}
+    labels = [id_to_label[i] for i in identities]
+    embeddings, valid_paths = extract_embeddings_batch(image_paths, model, transform, device, batch_size)
+    index_of = {p: i for i, p in enumerate(image_paths)}
+    valid_idx = [index_of[p] for p in valid_paths]
+    valid_labels = [labels[i] for i in valid_idx]
+    valid_ids = [identities[i] for i in valid_idx]
+    np.save(os.path.join(output_dir, "arcface_train_embeddings.npy"), embeddings)
+    pd.DataFrame({"image_path": valid_paths, "identity": valid_ids, "label": valid_labels}).to_csv(
+        os.path.join(output_dir, "embeddings_metadata.csv"), index=False)
+    np.save(os.path.join(output_dir, "label_mapping.npy"),
+            {"id_to_label": id_to_label, "label_to_id": {v: k for k, v in id_to_label.items()}})
+    return {"embeddings": embeddings, "labels": np.array(valid_labels), "identities": valid_ids,
+            "paths": valid_paths, "id_to_label": id_to_label}
+
+
+def full_pipeline(model_path: str, csv_path: str, data_root: str = None, output_dir: str = "data/embeddings",
+                  device: str = None, batch_size: int = 64):
+    result = extract_embeddings_from_csv(model_path, csv_path, data_root, output_dir, device, batch_size)
+    prototypes = compute_prototypes(result["embeddings"], result["labels"],
+                                    os.path.join(output_dir, "arcface_prototypes.npy"))
+    build_faiss_index(prototypes, os.path.join(output_dir, "arcface_index.npz"))
+    print("t-SNE visualization skipped (out of scope)")
+    return result
+
+
+def main(argv=None):
+    import argparse
+    ap = argparse.ArgumentParser(description="Extract embeddings (MI355X)")
+    ap.add_argument("--model-path", default="models/checkpoints/arcface/arcface_best.pth")
+    ap.add_argument("--mode", choices=["db", "csv", "full"], default="full")
+    ap.add_argument("--csv-path", default=None)
+    ap.add_argument("--data-root", default=None)
+    ap.add_argument("--data-dir", default="data/celeb")
+    ap.add_argument("--output-dir", default="data/embeddings")
+    ap.add_argument("--output-path", default="data/arcface_embeddings_db.npy")
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--batch-size", type=int, default=64)
+    ap.add_argument("--use-face-detection", action="store_true", default=True)
+    ap.add_argument("--no-face-detection", action="store_true")
+    ap.add_argument("--model-type", choices=["arcface", "facenet"], default="arcface")
+    a = ap.parse_args(argv)
+    use_fd = a.use_face_detection and not a.no_face_detection
+    if a.mode == "db":
+        build_db(a.model_path, a.data_dir, a.output_path, a.device, use_fd, a.model_type)
+    elif a.csv_path is None:
+        print("Vui long cung cap --csv-path")
+    elif a.mode == "csv":
+        extract_embeddings_from_csv(a.model_path, a.csv_path, a.data_root, a.output_dir, a.device, a.batch_size)
+    else:
+        full_pipeline(a.model_path, a.csv_path, a.data_root, a.output_dir, a.device, a.batch_size)
+
+
+if __name__ == "__main__":
+    main()

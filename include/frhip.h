@@ -146,6 +146,10 @@ typedef struct fr_conv_desc {
 #define FR_TILE_256x64 1
 #define FR_TILE_128x64 2
 #define FR_TILE_64x128 3
+#define FR_TILE_128x128_S3 4 /* 3-stage DMA ring, 1 block/CU */
+#define FR_TILE_256x128 5    /* 8 waves, 3-stage ring */
+#define FR_TILE_128x256 6    /* 8 waves, 3-stage ring */
+#define FR_TILE_BAND 7       /* row-band direct 3x3/s1/p1 kernel (conv_band.hip); auto-selected when applicable */
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 
@@ -170,6 +174,9 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * Tensor names are the reference/oracle module whose output the tensor equals
  * (e.g. "backbone.layer2.0", "layer3.7.prelu", "model.repeat_1.2"); "" for internal buffers. */
 int fr_debug_tensor_count(const fr_handle* h);
+/* Text dump of the forward plan at batch B, one line per op:
+ * "conv|head M N K Kpad tile split KhxKw name" or "pre|maxpool|avgpool". */
+int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n);
 const char* fr_debug_tensor_name(const fr_handle* h, int t);
 int fr_debug_tensor_shape(const fr_handle* h, int t, int* H, int* W, int* C);
 /* Copy the first B samples of tensor t (bf16 NHWC) to dst (device) after an fr_embed. */

@@ -61,7 +61,7 @@ def test_conv_parity(gpu, case, dtype):
     _close(y, ref, tol=1e-2 if dtype == "bf16" else 2e-3)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("case", [(2, 14, 14, 256, 256, 3, 3, (1, 1), (1, 1)), (2, 19, 19, 80, 192, 3, 3, (1, 1), (0, 0)),
                                   (3, 9, 9, 64, 64, 1, 1, (2, 2), (0, 0))])
 def test_conv_every_tile(gpu, case, tile):
@@ -71,6 +71,33 @@ def test_conv_every_tile(gpu, case, tile):
     w = torch.randn(Cout, Cin, kh, kw, generator=g) / np.sqrt(Cin * kh * kw)
     y = conv_op(x, w, stride=stride, pad=pad, act=1, tile=tile)
     _close(y, conv_ref(x, w, stride=stride, pad=pad, act=1))
+
+
+BAND_CASES = [(2, 14, 14, 256, 256), (2, 28, 28, 128, 128), (2, 56, 56, 64, 64), (1, 112, 112, 64, 64),
+              (2, 14, 14, 128, 256), (2, 28, 28, 64, 128), (2, 28, 28, 128, 256), (2, 28, 28, 64, 64)]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("case", BAND_CASES)
+def test_conv_band(gpu, case, dtype):
+    """Row-band direct 3x3/s1/p1 kernel (forced) with the IResNet epilogue: bias + residual +
+    PReLU + second affine output."""
+    B, H, W, Cin, Cout = case
+    g = torch.Generator().manual_seed(Cin + Cout + H)
+    x = torch.randn(B, H, W, Cin, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    slope = torch.rand(Cout, generator=g) * 0.5
+    res = torch.randn(B, H, W, Cout, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    s = torch.rand(Cout, generator=g) + 0.5
+    t = torch.randn(Cout, generator=g) * 0.1
+    y2 = torch.zeros(B, H, W, Cout, dtype=TORCH_DT[dtype], device=gpu)
+    y = conv_op(x, w, pad=(1, 1), bias=bias, act=2, slope=slope, res=res, y2=y2, aff_s=s, aff_b=t, dtype=dtype,
+                tile=N.FR_TILE_BAND)
+    ref = conv_ref(x, w, pad=(1, 1), bias=bias, act=2, slope=slope, res=res, dtype=dtype)
+    tol = 1e-2 if dtype == "bf16" else 2e-3
+    _close(y, ref, tol=tol)
+    _close(y2, y.float().cpu() * s + t, tol=tol)
 
 
 def test_conv_residual_prelu_dual_output(gpu):
