@@ -31,6 +31,24 @@ IRESNET100_GFLOP_PER_FACE = 24.179  # 2 * (conv + fc MACs)
 BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
 
 
+def pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py:
+    FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE, separate --pmc passes of this same
+    command), or None when no summary for this workload exists."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("arch") == args.arch and d.get("dtype") == args.dtype and d.get("batch") == args.batch:
+            k = d.get("kernels", {}).get(kernel)
+            if k:
+                return k["hbm_bytes_per_launch"]
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -43,6 +61,7 @@ def parse():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prof", action="store_true", help="skip the per-kernel event timing (roofline)")
     return ap.parse_args()
 
 
@@ -91,6 +110,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
+    from facerecognition_amd.distributed import ShardedMatcher, shard_range
     from facerecognition_amd.gallery import DeviceGallery
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
@@ -102,18 +122,14 @@ def main():
     u8 = torch.from_numpy(synthetic_crops(B, size, seed=100 + rank)).to(dev)  # HBM-resident input
     # gallery: rows [r*rows/N, (r+1)*rows/N) on rank r; global indices via index_base
     rows = args.gallery_rows
-    lo, hi = rank * rows // world, (rank + 1) * rows // world
+    lo, hi = shard_range(rows, rank, world)
     g = np.random.default_rng(1).standard_normal((rows, 512)).astype(np.float32)[lo:hi]
     g /= np.linalg.norm(g, axis=1, keepdims=True)
     gallery = DeviceGallery(g, device=local, index_base=lo)
     emb = torch.empty((B, 512), dtype=torch.float32, device=dev)
-    all_emb = torch.empty((world * B, 512), dtype=torch.float32, device=dev)
-    cand_s = torch.empty((world, world * B, K), dtype=torch.float32, device=dev)
-    cand_i = torch.empty((world, world * B, K), dtype=torch.int32, device=dev)
-    fin_s = torch.empty((world * B, K), dtype=torch.float32, device=dev)
-    fin_i = torch.empty((world * B, K), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    matcher = ShardedMatcher(B, 512, K, lambda p: gallery.search_device(p, K), dev)
 
     def step(i=None):
         if i is not None:
@@ -121,22 +137,7 @@ def main():
         model.embed(u8, out=emb)
         if i is not None:
             ev[i][1].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(all_emb, emb)
-            probes = all_emb
-        else:
-            probes = emb
-        s, idx = gallery.search_device(probes, K)
-        if world > 1:
-            dist.all_gather_into_tensor(cand_s.view(-1), s.contiguous().view(-1))
-            dist.all_gather_into_tensor(cand_i.view(-1), idx.contiguous().view(-1))
-            # candidates [rank][probe][k] -> [probe][rank][k] for the merge
-            cs = cand_s.permute(1, 0, 2).contiguous()
-            ci = cand_i.permute(1, 0, 2).contiguous()
-            N.check(N.lib().fr_topk_merge(cs.data_ptr(), ci.data_ptr(), world * B, world, K, fin_s.data_ptr(),
-                                          fin_i.data_ptr(), N.stream_ptr(dev)), "fr_topk_merge")
-            return fin_s, fin_i
-        return s, idx
+        return matcher.search(emb)  # N > 1: RCCL all-gather + shard top-k + all-gather + merge
 
     for _ in range(args.warmup):
         step()
@@ -144,6 +145,24 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    kclasses_all = {}
+    dominant = None
+    if not args.no_prof:
+        # untimed pass with every launch bracketed -> per-class breakdown and the dominant class;
+        # the timed steps then bracket only the dominant class's launches (event pairs serialize the
+        # stream a little, ~1.5 us each)
+        L = N.lib()
+        N.check(L.fr_prof_enable(model.handle, 1), "fr_prof_enable")
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize(dev)
+        kclasses_all = N.prof_read(model.handle)
+        dominant = max(kclasses_all.items(), key=lambda kv: kv[1][0])[0]
+        N.check(L.fr_prof_enable(model.handle, 1), "fr_prof_enable")
+        N.check(L.fr_prof_only(model.handle, dominant.encode()), "fr_prof_only")
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         out_s, out_i = step(i)
@@ -152,6 +171,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    kclasses = {}
+    if not args.no_prof:
+        kclasses = N.prof_read(model.handle)
+        N.check(N.lib().fr_prof_enable(model.handle, 0), "fr_prof_enable")
+        N.check(N.lib().fr_prof_only(model.handle, None), "fr_prof_only")
     embed_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))  # forward duration on its stream
     if dist:
         t = torch.tensor([elapsed, embed_ms], dtype=torch.float64, device=dev)
@@ -175,12 +199,25 @@ def main():
                    "parallelism": f"dp{world}"},
     }
     if flop_fwd:
-        achieved = flop_fwd / (embed_ms * 1e-3) / 1e12
-        result["roofline"] = {"bound": "mfma", "kernel": "fr_embed forward (conv_igemm MFMA launches + "
-                              "preprocess/split-K/head), HIP events on the embed stream",
-                              "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                              "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": None,
-                              "embed_ms": round(embed_ms, 4)}
+        result["forward"] = {"embed_ms": round(embed_ms, 4),
+                             "tflops": round(flop_fwd / (embed_ms * 1e-3) / 1e12, 2)}
+    if kclasses:
+        # dominant kernel = the class with the most GPU time; achieved = its algorithmic FLOPs per
+        # launch (2*M*N*K of the conv it computes) / its mean launch duration (HIP events on the
+        # stream it is launched on, over the timed steps)
+        name = dominant
+        ms, launches, flops = kclasses[name]
+        achieved = flops / (ms * 1e-3) / 1e12
+        result["roofline"] = {
+            "bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
+            "traffic": pmc_traffic(name, args), "launches_per_step": launches // args.steps,
+            "us_per_launch": round(ms / launches * 1e3, 2), "gflop_per_launch": round(flops / launches / 1e9, 3),
+            "share_of_forward": round(ms / args.steps / embed_ms, 4)}
+        # per-class breakdown from the untimed all-launch pass (2 steps)
+        result["kernels"] = {k: {"ms_per_step": round(v[0] / 2, 4), "launches": v[1] // 2,
+                                 "tflops": round(v[2] / (v[0] * 1e-3) / 1e12, 1) if v[2] else None}
+                             for k, v in sorted(kclasses_all.items(), key=lambda kv: -kv[1][0])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.arch, args.cpu_seconds)
     if rank == 0:

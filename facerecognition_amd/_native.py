@@ -60,6 +60,11 @@ _SIGS = {
     "fr_segment_mean_normalize": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "fr_debug_tensor_count": (c_int, [c_void_p]),
     "fr_debug_plan": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t]),
+    "fr_prof_enable": (c_int, [c_void_p, c_int]),
+    "fr_prof_collect": (c_int, [c_void_p]),
+    "fr_prof_only": (c_int, [c_void_p, ctypes.c_char_p]),
+    "fr_prof_get": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t, ctypes.POINTER(ctypes.c_double),
+                            ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "fr_debug_tensor_name": (ctypes.c_char_p, [c_void_p, c_int]),
     "fr_debug_tensor_shape": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                       ctypes.POINTER(c_int)]),
@@ -116,3 +121,17 @@ def ptr(t) -> int:
 def stream_ptr(device=None) -> int:
     import torch
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def prof_read(handle):
+    """fr_prof_collect + fr_prof_get for every class → {name: (total_ms, launches, flops)}."""
+    L = lib()
+    n = L.fr_prof_collect(handle)
+    check(n if n < 0 else 0, "fr_prof_collect")
+    out = {}
+    for i in range(n):
+        name = ctypes.create_string_buffer(128)
+        ms, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        check(L.fr_prof_get(handle, i, name, 128, ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(fl)), "fr_prof_get")
+        out[name.value.decode()] = (ms.value, cnt.value, fl.value)
+    return out

@@ -365,7 +365,9 @@ void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
     }();
     static const int tiles[] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128, TILE_128x128_S3, TILE_256x128,
                                 TILE_128x256};
-    static const double eff[] = {1.0, 0.95, 0.8, 0.8, 1.05, 1.15, 1.15};
+    // relative MFMA efficiency per tile, calibrated on the IResNet100 bs=256 per-layer sweep
+    // (tools/tile_sweep.sh, profiles/r01_tile_sweep.txt); the 3-stage 128x128 ring is the slowest
+    static const double eff[] = {1.0, 0.93, 0.92, 0.9, 0.7, 0.9, 0.92};
     const int nkt = Kpad / BK;
     double best = 1e30;
     int bt = TILE_128x128, bs = 1;

@@ -90,6 +90,14 @@ struct fr_handle {
     float* cand_s = nullptr;
     int32_t* cand_i = nullptr;
     size_t cand_cap = 0;
+    // per-kernel-class event timing (fr_prof_*): events recorded on the launching stream
+    struct ProfRec { std::string cls; hipEvent_t a, b; double flops; };
+    struct ProfAcc { double ms = 0; int64_t launches = 0; double flops = 0; };
+    bool prof = false;
+    std::string prof_only;  // non-empty: time only this kernel class
+    std::vector<hipEvent_t> ev_free;
+    std::vector<ProfRec> prof_pending;
+    std::vector<std::pair<std::string, ProfAcc>> prof_acc;
 };
 
 namespace {
@@ -560,10 +568,44 @@ int conv_dbg() {
     return d;
 }
 
+hipEvent_t prof_event(fr_handle* h) {
+    if (!h->ev_free.empty()) { hipEvent_t e = h->ev_free.back(); h->ev_free.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Brackets one launch with two events when profiling is on; `cls` names the kernel instantiation so
+// the totals line up with rocprofv3's per-kernel rows.
+struct ProfScope {
+    fr_handle* h; hipStream_t s; hipEvent_t a = nullptr; std::string cls; double flops = 0;
+    ProfScope(fr_handle* h_, hipStream_t s_) : h(h_), s(s_) {}
+    // call right before the launch(es), once the class name is known
+    void start(const std::string& c) {
+        cls = c;
+        if (!h->prof || (!h->prof_only.empty() && h->prof_only != cls)) return;
+        if ((a = prof_event(h))) (void)hipEventRecord(a, s);
+    }
+    ~ProfScope() {
+        if (!a) return;
+        hipEvent_t b = prof_event(h);
+        if (!b) { h->ev_free.push_back(a); return; }
+        (void)hipEventRecord(b, s);
+        h->prof_pending.push_back({cls, a, b, flops});
+    }
+};
+
+double conv_flops(const ConvArgs& a) { return 2.0 * (double)a.M * a.Cout * ((double)a.Cin * a.Kh * a.Kw); }
+
 int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     a.dbg = conv_dbg();
+    ProfScope ps(h, s);
+    ps.flops = conv_flops(a);
     int TH, variant;
-    if (band_enabled() && band_plan(a, &TH, &variant)) {
+    // auto policy (measured, profiles/r01_layers.txt): the row-band kernel beats the implicit GEMM
+    // only on the 14x14 stage (layer3, 45% of IResNet100 FLOPs); W=28/56/112 stay on igemm tiles
+    if (band_enabled() && a.W == 14 && band_plan(a, &TH, &variant)) {
+        ps.start("conv3x3_band W" + std::to_string(a.W) + " v" + std::to_string(variant));
         FR_HIP_CHECK(launch_conv_band(a, TH, variant, s));
         return FR_OK;
     }
@@ -573,6 +615,7 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) split /= 2;
     if (split > 1) a.partial = h->partial;
     a.split_k = split;
+    ps.start("conv_igemm tile" + std::to_string(tile) + (split > 1 ? " splitk" : ""));
     FR_HIP_CHECK(launch_conv(a, s));
     if (split > 1 && a.y) FR_HIP_CHECK(launch_splitk_epilogue(a, s));
     return FR_OK;
@@ -583,6 +626,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
     for (const auto& op : h->ops) {
         switch (op.kind) {
             case OP_PRE: {
+                ProfScope ps(h, s);
+                ps.start("preprocess");
                 const auto& t = h->tensors[op.out];
                 FR_HIP_CHECK(launch_preprocess(in, in_fmt, B, t.H, t.W, t.dev, f16, s));
                 break;
@@ -609,6 +654,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 break;
             }
             case OP_MAXPOOL: {
+                ProfScope ps(h, s);
+                ps.start("maxpool");
                 const auto& ti = h->tensors[op.in];
                 const auto& to = h->tensors[op.out];
                 FR_HIP_CHECK(launch_maxpool(ti.dev, B, ti.H, ti.W, ti.C, 0, ti.C, op.pk, op.ps, op.pp, to.dev, to.C,
@@ -616,13 +663,18 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 break;
             }
             case OP_AVGPOOL: {
+                ProfScope ps(h, s);
+                ps.start("avgpool");
                 const auto& ti = h->tensors[op.in];
                 FR_HIP_CHECK(launch_avgpool(ti.dev, B, ti.H, ti.W, ti.C, h->tensors[op.out].dev, f16, s));
                 break;
             }
             case OP_HEAD: {
+                ProfScope ps(h, s);
+                ps.start("head");
                 const auto& cw = h->convw[op.wi];
                 const auto& ti = h->tensors[op.in];
+                ps.flops = 2.0 * B * cw.Cout * (double)cw.K;
                 ConvArgs a{};
                 a.f16 = f16;
                 a.x = ti.dev; a.B = B; a.H = 1; a.W = 1; a.Cx = cw.K; a.x_off = 0; a.Cin = cw.K;
@@ -684,6 +736,8 @@ void fr_destroy(fr_handle* h) {
     if (h->gallery) (void)hipFree(h->gallery);
     if (h->cand_s) (void)hipFree(h->cand_s);
     if (h->cand_i) (void)hipFree(h->cand_i);
+    for (auto& r : h->prof_pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (auto e : h->ev_free) (void)hipEventDestroy(e);
     delete h;
 }
 
@@ -858,6 +912,61 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
     }
     std::snprintf(buf, n, "%s", out.c_str());
     return out.size() + 1 <= n ? FR_OK : FR_ERR_ARG;
+}
+
+int fr_prof_enable(fr_handle* h, int on) {
+    if (!h) { set_error("fr_prof_enable: null handle"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    for (auto& r : h->prof_pending) {
+        (void)hipEventSynchronize(r.b);
+        h->ev_free.push_back(r.a);
+        h->ev_free.push_back(r.b);
+    }
+    h->prof_pending.clear();
+    h->prof_acc.clear();
+    h->prof = on != 0;
+    return FR_OK;
+}
+
+int fr_prof_only(fr_handle* h, const char* kernel_class) {
+    if (!h) { set_error("fr_prof_only: null handle"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->prof_only = kernel_class ? kernel_class : "";
+    return FR_OK;
+}
+
+int fr_prof_collect(fr_handle* h) {
+    if (!h) { set_error("fr_prof_collect: null handle"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    for (auto& r : h->prof_pending) {
+        FR_HIP_CHECK(hipEventSynchronize(r.b));
+        float ms = 0.f;
+        FR_HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
+        size_t i = 0;
+        while (i < h->prof_acc.size() && h->prof_acc[i].first != r.cls) ++i;
+        if (i == h->prof_acc.size()) h->prof_acc.push_back({r.cls, {}});
+        auto& acc = h->prof_acc[i].second;
+        acc.ms += ms;
+        acc.launches += 1;
+        acc.flops += r.flops;
+        h->ev_free.push_back(r.a);
+        h->ev_free.push_back(r.b);
+    }
+    h->prof_pending.clear();
+    return (int)h->prof_acc.size();
+}
+
+int fr_prof_get(const fr_handle* h, int i, char* name, size_t n, double* total_ms, int64_t* launches,
+                double* flops) {
+    if (!h || i < 0 || i >= (int)h->prof_acc.size()) { set_error("fr_prof_get: bad index"); return FR_ERR_ARG; }
+    const auto& e = h->prof_acc[i];
+    if (name && n) { std::strncpy(name, e.first.c_str(), n - 1); name[n - 1] = 0; }
+    if (total_ms) *total_ms = e.second.ms;
+    if (launches) *launches = e.second.launches;
+    if (flops) *flops = e.second.flops;
+    return FR_OK;
 }
 
 int fr_debug_tensor_count(const fr_handle* h) { return h ? (int)h->tensors.size() : 0; }

@@ -1,0 +1,81 @@
+"""Data-parallel embed + sharded gallery match across ranks.
+
+One process per GPU.  Rank r embeds its own batch of faces; the gallery is row-sharded (rank r holds
+global rows [lo_r, hi_r), searched with ``index_base = lo_r``).  The one real exchange step:
+
+  1. all-gather the L2-normalized embeddings  [B, D] per rank → [world*B, D] on every rank
+  2. every rank: local top-k of ALL gathered probes against its shard (global indices)
+  3. all-gather the candidates [world*B, k] (score, idx) per rank → [world, world*B, k]
+  4. every rank: deterministic merge per probe, (score desc, global index asc)
+
+Because the ordering is total and every candidate list is itself exact, the merged top-k equals the
+single-device top-k over the whole gallery bit for bit (tests/test_distributed.py checks this with
+world_size 2 on gloo).  On GPUs the collectives are RCCL over xGMI (backend "nccl") and steps 2/4 are
+``fr_match_topk`` / ``fr_topk_merge``; on CPU (tests) the same protocol runs with numpy callables.
+
+The reference has no multi-process path; this is the scale-out the north star asks for.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import torch
+
+
+def shard_range(rows: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous, balanced row range of `rank` (sizes differ by at most one row)."""
+    return rank * rows // world, (rank + 1) * rows // world
+
+
+def _all_gather(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, inp.contiguous(), group=group)
+    else:  # gloo: list form
+        world = dist.get_world_size(group)
+        parts = list(out.view(world, *inp.shape).unbind(0))
+        dist.all_gather(parts, inp.contiguous(), group=group)
+
+
+def native_merge(cand_s: torch.Tensor, cand_i: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fr_topk_merge on the device: cand_* [P, n_lists, k] → [P, k]."""
+    from . import _native as N
+    P, n_lists = int(cand_s.shape[0]), int(cand_s.shape[1])
+    s = torch.empty((P, k), dtype=torch.float32, device=cand_s.device)
+    i = torch.empty((P, k), dtype=torch.int32, device=cand_s.device)
+    N.check(N.lib().fr_topk_merge(N.ptr(cand_s), N.ptr(cand_i), P, n_lists, k, N.ptr(s), N.ptr(i),
+                                  N.stream_ptr(cand_s.device)), "fr_topk_merge")
+    return s, i
+
+
+class ShardedMatcher:
+    """Steps 1-4 above with preallocated buffers (no allocation per call).
+
+    local_search(probes [P, D]) -> (scores [P, k] f32, idx [P, k] int32, global indices)
+    merge(cand_s [P, world, k], cand_i [P, world, k], k) -> ([P, k], [P, k])
+    """
+
+    def __init__(self, batch: int, dim: int, k: int, local_search: Callable, device: torch.device,
+                 merge: Optional[Callable] = None, group=None):
+        import torch.distributed as dist
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.group, self.k, self.B = group, k, batch
+        self.local_search = local_search
+        self.merge = merge or native_merge
+        W = self.world
+        self.all_emb = torch.empty((W * batch, dim), dtype=torch.float32, device=device)
+        self.cand_s = torch.empty((W, W * batch, k), dtype=torch.float32, device=device)
+        self.cand_i = torch.empty((W, W * batch, k), dtype=torch.int32, device=device)
+
+    def search(self, emb: torch.Tensor):
+        """emb: this rank's normalized embeddings [B, D] → top-k of every rank's probes, identical on
+        all ranks: (scores [world*B, k], idx [world*B, k]); row j*B + b is rank j's probe b."""
+        if self.world == 1:
+            return self.local_search(emb)
+        _all_gather(self.all_emb, emb, self.group)
+        s, i = self.local_search(self.all_emb)
+        _all_gather(self.cand_s.view(-1), s.contiguous().view(-1), self.group)
+        _all_gather(self.cand_i.view(-1), i.contiguous().view(-1), self.group)
+        cs = self.cand_s.permute(1, 0, 2).contiguous()  # [probe][rank][k]
+        ci = self.cand_i.permute(1, 0, 2).contiguous()
+        return self.merge(cs, ci, self.k)

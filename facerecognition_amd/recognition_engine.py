@@ -1,0 +1,349 @@
+"""Drop-in for the reference's ``inference/recognition_engine.py`` (RecognitionEngine, cosine_similarity,
+create_engine_from_embeddings_dir) with embedding and gallery matching on the MI355X.
+
+Reference → here:
+  cosine_similarity :41-63            unchanged host function (a10)
+  RecognitionEngine.__init__ :75-140  same arguments; dict db (.npy) and/or index + prototypes + mapping
+  extract_embedding :244-265          fr_embed via extract_embedding_single (a7)
+  recognize_with_db :267-289          ONE fr_match_topk against the device copy of the db (dict order =
+                                       row order; (score desc, index asc) = the stable sort), top-5,
+                                       ``best < threshold`` → "Unknown"; no db → ("No database", 0.0, [])
+  recognize_with_faiss :291-326       probe / (‖p‖+1e-8), exact inner-product top-k on the device
+                                       index; names ``id_to_label.get(idx, f"ID_{idx}")`` (reference quirk kept)
+  recognize :328-381                  same result dict / status / message
+  recognize_batch :383-389            batched: all images in one fr_embed + one fr_match_topk (§8f row 1)
+  add_to_db / save_db / get_db_identities / set_threshold :391-435, :165-167
+Face detection/alignment (MTCNN) is out of scope: with ``use_face_detection=True`` the engine reports the
+detector as unavailable and continues without it — the reference's own fallback (:122-124).
+
+The device gallery is rebuilt lazily whenever the db changes (``engine.db = {...}``, ``add_to_db``, or
+item assignment on ``engine.db``).  Scores are f32 inner products computed on the GPU; they agree with
+the reference's numpy ``cosine_similarity`` to ~1e-6 (accumulation order), and ranks are identical
+except between rows whose scores differ by less than that.
+"""
+from __future__ import annotations
+
+import io
+import os
+import pickle
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import weights as Wt
+from .extract_embeddings import (_device_index, _embed_u8, _load_u8, extract_embedding_single,
+                                 get_transform, load_arcface_model, read_index)
+
+MAX_K = 16  # fr_match_topk limit
+
+
+def cosine_similarity(a: np.ndarray, b: np.ndarray) -> float:
+    a = a.flatten().astype(np.float32)
+    b = b.flatten().astype(np.float32)
+    na, nb = np.linalg.norm(a), np.linalg.norm(b)
+    if na == 0 or nb == 0:
+        return 0.0
+    if abs(na - 1.0) < 1e-3 and abs(nb - 1.0) < 1e-3:
+        return float(np.dot(a, b))
+    return float(np.dot(a, b) / (na * nb))
+
+
+# ---------------------------------------------------------------------------------------- db files
+class _NumpyOnlyUnpickler(pickle.Unpickler):
+    """The reference stores its db / label mapping as ``np.save(path, dict)`` (a pickled 0-d object
+    array).  Load those with an unpickler that can only rebuild numpy arrays, dtypes and plain
+    containers — never arbitrary callables."""
+    ALLOWED = {("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+               ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+               ("numpy", "ndarray"), ("numpy", "dtype"), ("builtins", "dict"), ("builtins", "list"),
+               ("builtins", "tuple"), ("builtins", "str"), ("builtins", "int"), ("builtins", "float"),
+               ("collections", "OrderedDict"), ("_codecs", "encode")}
+
+    def find_class(self, module, name):
+        if (module, name) in self.ALLOWED or (module.startswith("numpy") and name.startswith("dtype")):
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"refusing to load {module}.{name} from a db file")
+
+
+def load_npy_object(path: str):
+    """np.load(path, allow_pickle=True).item() restricted to numpy/builtin types."""
+    from numpy.lib import format as npf
+    with open(path, "rb") as f:
+        version = npf.read_magic(f)
+        read_header = npf.read_array_header_1_0 if version == (1, 0) else npf.read_array_header_2_0
+        _shape, _fortran, dtype = read_header(f)
+        if dtype != object:
+            return np.load(path, allow_pickle=False)
+        arr = _NumpyOnlyUnpickler(io.BytesIO(f.read())).load()
+    return arr.item() if isinstance(arr, np.ndarray) and arr.shape == () else arr
+
+
+class _TrackedDB(dict):
+    """dict that counts mutations so the device copy knows when to refresh."""
+    version = 0
+
+    def _bump(self):
+        self.version += 1
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v)
+        self._bump()
+
+    def __delitem__(self, k):
+        super().__delitem__(k)
+        self._bump()
+
+    def update(self, *a, **k):
+        super().update(*a, **k)
+        self._bump()
+
+    def pop(self, *a):
+        r = super().pop(*a)
+        self._bump()
+        return r
+
+    def popitem(self):
+        r = super().popitem()
+        self._bump()
+        return r
+
+    def clear(self):
+        super().clear()
+        self._bump()
+
+    def setdefault(self, k, v=None):
+        r = super().setdefault(k, v)
+        self._bump()
+        return r
+
+
+class RecognitionEngine:
+    def __init__(self, model_path: str = "models/checkpoints/arcface/arcface_best.pth", db_path: str = None,
+                 faiss_index_path: str = None, prototypes_path: str = None, label_mapping_path: str = None,
+                 device: str = None, threshold: float = 0.5, use_face_detection: bool = True, model=None):
+        self.device = device or "cuda"
+        self.threshold = threshold
+        self.use_face_detection = use_face_detection
+        self.model, self.model_info = None, None
+        if model is not None:  # an already-built FRModel (tests, services sharing one model)
+            self.model = model
+        elif model_path and os.path.exists(model_path):
+            self.model, self.model_info = load_arcface_model(model_path, self.device)
+        self.transform = get_transform(Wt.INPUT_SIZE[self.model.arch] if self.model is not None else 112)
+        self.face_detector = None
+        if self.use_face_detection:
+            print("Khong the khoi tao Face Detector: face detection is out of scope for facerecognition_amd")
+            self.use_face_detection = False
+        self._db = None
+        self._g = None          # (key, DeviceGallery, names)
+        self.faiss_index = None
+        self.prototypes = None
+        self.label_to_id = None
+        self.id_to_label = None
+        if db_path and os.path.exists(db_path):
+            self.db = load_npy_object(db_path)
+            print(f"Loaded database: {len(self.db)} identities")
+        if faiss_index_path and (os.path.exists(faiss_index_path) or os.path.exists(faiss_index_path + ".npz")):
+            self._load_faiss(faiss_index_path, prototypes_path, label_mapping_path)
+
+    # ------------------------------------------------------------------ state
+    @property
+    def db(self):
+        return self._db
+
+    @db.setter
+    def db(self, value):
+        self._db = None if value is None else (value if isinstance(value, _TrackedDB) else _TrackedDB(value))
+        self._g = None
+
+    def _load_faiss(self, index_path: str, prototypes_path: str = None, mapping_path: str = None):
+        try:
+            self.faiss_index = read_index(index_path)
+            print(f"Loaded index: {self.faiss_index.ntotal} vectors")
+        except Exception as e:
+            print(f"Loi load FAISS: {e}")
+            return
+        if prototypes_path and os.path.exists(prototypes_path):
+            self.prototypes = np.load(prototypes_path)
+            print(f"Loaded prototypes: {self.prototypes.shape}")
+        if mapping_path and os.path.exists(mapping_path):
+            mapping = load_npy_object(mapping_path)
+            self.label_to_id = mapping.get("label_to_id", {})
+            self.id_to_label = mapping.get("id_to_label", {})
+            print(f"Loaded label mapping: {len(self.label_to_id)} classes")
+
+    def set_threshold(self, threshold: float):
+        self.threshold = threshold
+        print(f"Threshold set to: {threshold}")
+
+    def align_face(self, image, landmarks):  # detector-based alignment: out of scope
+        return None
+
+    def detect_and_align(self, img_input):  # MTCNN: out of scope
+        return None
+
+    def _db_gallery(self):
+        from .gallery import DeviceGallery
+        key = (id(self._db), self._db.version)
+        if self._g is None or self._g[0] != key:
+            names = list(self._db.keys())
+            rows = np.stack([np.asarray(v, dtype=np.float32).reshape(-1) for v in self._db.values()])
+            dev = self.model.device.index if self.model is not None else _device_index(self.device)
+            self._g = (key, DeviceGallery(rows, dim=rows.shape[1], device=dev), names)
+        return self._g[1], self._g[2]
+
+    # ------------------------------------------------------------------ embedding
+    def extract_embedding(self, img_input) -> Optional[np.ndarray]:
+        if self.model is None:
+            print("Model chua duoc load")
+            return None
+        return extract_embedding_single(img_input, self.model, self.transform, self.device)
+
+    # ------------------------------------------------------------------ matching
+    @staticmethod
+    def _as_probes(E: np.ndarray) -> np.ndarray:
+        """Probe rows in cosine_similarity semantics: rows whose norm is not within 1e-3 of 1 are
+        divided by it (the gallery side is prepared the same way by fr_gallery_set)."""
+        E = np.asarray(E, dtype=np.float32).reshape(len(E), -1).copy()
+        n = np.linalg.norm(E, axis=1)
+        fix = (np.abs(n - 1.0) >= 1e-3) & (n > 0)
+        E[fix] /= n[fix, None]
+        return E
+
+    def _db_topk(self, E: np.ndarray, k: int):
+        import torch
+        g, names = self._db_gallery()
+        k = min(k, g.ntotal)
+        P = torch.from_numpy(self._as_probes(E)).to(g.device)
+        s, i = g.search_device(P, k)
+        return s.cpu().numpy(), i.cpu().numpy(), names
+
+    def _result_db(self, s_row, i_row, names):
+        top = [(names[j], float(v)) for v, j in zip(s_row, i_row)]
+        best_name, best_score = top[0]
+        if best_score < self.threshold:
+            return "Unknown", best_score, top
+        return best_name, best_score, top
+
+    def recognize_with_db(self, embedding: np.ndarray) -> Tuple[str, float, List[Tuple[str, float]]]:
+        if self.db is None:
+            return "No database", 0.0, []
+        s, i, names = self._db_topk(np.asarray(embedding)[None], 5)
+        return self._result_db(s[0], i[0], names)
+
+    def _faiss_topk(self, E: np.ndarray, k: int):
+        import torch
+        if k > MAX_K:
+            raise ValueError(f"k={k} > {MAX_K} is not supported by fr_match_topk")
+        E = np.asarray(E, dtype=np.float32).reshape(len(E), -1)
+        E = E / (np.linalg.norm(E, axis=1, keepdims=True) + 1e-8)
+        P = torch.from_numpy(np.ascontiguousarray(E)).to(self.faiss_index.device)
+        s, i = self.faiss_index.search_device(P, k)
+        return s.cpu().numpy(), i.cpu().numpy()
+
+    def _result_faiss(self, s_row, i_row):
+        results = []
+        for idx, score in zip(i_row, s_row):
+            if idx == -1:
+                continue
+            name = self.id_to_label.get(int(idx), f"ID_{idx}") if self.id_to_label else f"ID_{idx}"
+            results.append((name, float(score)))
+        if not results:
+            return "Unknown", 0.0, []
+        best_name, best_score = results[0]
+        if best_score < self.threshold:
+            return "Unknown", best_score, results
+        return best_name, best_score, results
+
+    def recognize_with_faiss(self, embedding: np.ndarray, k: int = 5) -> Tuple[str, float, List[Tuple[str, float]]]:
+        if self.faiss_index is None:
+            return "No FAISS index", 0.0, []
+        s, i = self._faiss_topk(np.asarray(embedding)[None], k)
+        return self._result_faiss(s[0], i[0])
+
+    # ------------------------------------------------------------------ end-to-end
+    def recognize(self, img_input, use_faiss: bool = None, k: int = 5) -> Dict:
+        return self.recognize_batch([img_input], use_faiss, k)[0]
+
+    def recognize_batch(self, img_inputs: List, use_faiss: bool = None, k: int = 5) -> List[Dict]:
+        results = [{"identity": "Unknown", "confidence": 0.0, "top_k": [], "embedding": None, "status": "success"}
+                   for _ in img_inputs]
+        ok, crops = [], []
+        if self.model is not None:
+            for n, img in enumerate(img_inputs):
+                try:
+                    crops.append(_load_u8(img, self.transform))
+                    ok.append(n)
+                except Exception as e:
+                    if isinstance(img, str):
+                        print(f"Loi xu ly {img}: {e}")
+        else:
+            print("Model chua duoc load")
+        for n in range(len(img_inputs)):
+            if n not in ok:
+                results[n]["status"] = "error"
+                results[n]["message"] = "Cannot extract embedding (no face or invalid image)"
+        if not ok:
+            return results
+        mb = max(1, getattr(self.model, "max_batch", 256) or 256)
+        E = np.concatenate([_embed_u8(self.model, np.stack(crops[j:j + mb])) for j in range(0, len(crops), mb)])
+        if use_faiss is None:
+            use_faiss = self.faiss_index is not None
+        if use_faiss and self.faiss_index is not None:
+            s, i = self._faiss_topk(E, k)
+            ident = [self._result_faiss(s[r], i[r]) for r in range(len(ok))]
+        elif self.db is not None:
+            s, i, names = self._db_topk(E, 5)
+            ident = [self._result_db(s[r], i[r], names) for r in range(len(ok))]
+        else:
+            for r, n in enumerate(ok):
+                results[n]["embedding"] = E[r]
+                results[n]["status"] = "error"
+                results[n]["message"] = "No database loaded"
+            return results
+        for r, n in enumerate(ok):
+            results[n]["embedding"] = E[r].astype(np.float32)
+            results[n]["identity"], results[n]["confidence"], results[n]["top_k"] = ident[r]
+        return results
+
+    def add_to_db(self, name: str, img_inputs: List) -> bool:
+        crops = []
+        if self.model is not None:
+            for img in img_inputs:
+                try:
+                    crops.append(_load_u8(img, self.transform))
+                except Exception as e:
+                    if isinstance(img, str):
+                        print(f"Loi xu ly {img}: {e}")
+        if not crops:
+            print(f"Khong the extract embedding cho {name}")
+            return False
+        E = _embed_u8(self.model, np.stack(crops))
+        m = np.mean(np.stack(list(E)), axis=0)
+        m = m / (np.linalg.norm(m) + 1e-8)
+        if self.db is None:
+            self.db = {}
+        self.db[name] = m
+        print(f"Added {name} to database (from {len(crops)} images)")
+        return True
+
+    def save_db(self, path: str):
+        if self.db:
+            os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+            np.save(path, dict(self.db))
+            print(f"Saved database: {path}")
+
+    def get_db_identities(self) -> List[str]:
+        return list(self.db.keys()) if self.db else []
+
+
+
+def create_engine_from_embeddings_dir(model_path: str, embeddings_dir: str, threshold: float = 0.5,
+                                      device: str = None) -> RecognitionEngine:
+    idx = os.path.join(embeddings_dir, "arcface_index.npz")
+    protos = os.path.join(embeddings_dir, "arcface_prototypes.npy")
+    mapping = os.path.join(embeddings_dir, "label_mapping.npy")
+    return RecognitionEngine(model_path=model_path, faiss_index_path=idx if os.path.exists(idx) else None,
+                             prototypes_path=protos if os.path.exists(protos) else None,
+                             label_mapping_path=mapping if os.path.exists(mapping) else None,
+                             threshold=threshold, device=device)

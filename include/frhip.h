@@ -173,6 +173,20 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
 /* ---- debug: named intermediate tensors of the forward plan (per-layer drift tests) ----
  * Tensor names are the reference/oracle module whose output the tensor equals
  * (e.g. "backbone.layer2.0", "layer3.7.prelu", "model.repeat_1.2"); "" for internal buffers. */
+/* ---- measurement: per-kernel-class timing with HIP events (bench.py roofline) --------------
+ * No reference counterpart (the reference has no profiler hook); used by bench.py to time the
+ * dominant kernel live, on the stream it is launched on.  fr_prof_enable(h, 1) resets and starts
+ * recording an event pair around every launch of fr_embed; fr_prof_collect() waits for the pending
+ * events and returns the number of kernel classes; fr_prof_get() reads class i: name (matches the
+ * kernel instantiation), summed milliseconds, launch count, summed algorithmic FLOPs (2*M*N*K). */
+int fr_prof_enable(fr_handle* h, int on);
+/* Restrict timing to one kernel class (name as returned by fr_prof_get; NULL or "" = all).
+ * Each event pair serializes the stream slightly, so bench.py times only the dominant class. */
+int fr_prof_only(fr_handle* h, const char* kernel_class);
+int fr_prof_collect(fr_handle* h);
+int fr_prof_get(const fr_handle* h, int i, char* name, size_t n, double* total_ms, int64_t* launches,
+                double* flops);
+
 int fr_debug_tensor_count(const fr_handle* h);
 /* Text dump of the forward plan at batch B, one line per op:
  * "conv|head M N K Kpad tile split KhxKw name" or "pre|maxpool|avgpool". */

@@ -76,3 +76,15 @@ def compute_prototypes(embeddings: np.ndarray, labels: np.ndarray) -> np.ndarray
         p = embeddings[labels == lab].mean(axis=0)
         protos[lab] = p / (np.linalg.norm(p) + 1e-8)
     return protos
+
+
+def merge_topk(cand_s: np.ndarray, cand_i: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Merge of per-shard candidate lists [P, n_lists, k] → [P, k] with the same total order as
+    topk_dot (score desc, global index asc; (-inf, -1) padding sorts last).  No reference
+    counterpart: this is the exchange step of the multi-GPU design."""
+    P = cand_s.shape[0]
+    s = cand_s.reshape(P, -1).astype(np.float32)
+    i = cand_i.reshape(P, -1).astype(np.int64)
+    key_i = np.where(i < 0, np.iinfo(np.int64).max, i)
+    order = np.lexsort((key_i, -s), axis=1)[:, :k]
+    return np.take_along_axis(s, order, 1), np.take_along_axis(i, order, 1)

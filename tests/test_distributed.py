@@ -1,0 +1,96 @@
+"""The multi-GPU exchange protocol (facerecognition_amd/distributed.py) on CPU with
+gloo, world_size 2: all-gather of embeddings → shard-local top-k with global indices → all-gather of
+candidates → merge.  The merged result must equal the single-device exact top-k over the whole
+gallery bit for bit, including ties that straddle shard boundaries.
+
+Scores are made exact (entries are multiples of 1/8 with small magnitude, so every f32 dot product is
+exact whatever the accumulation order), hence a bit-exact comparison is meaningful."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle.match import merge_topk, topk_dot
+
+D, B, K, ROWS = 64, 6, 5, 203
+
+
+def _data():
+    rng = np.random.default_rng(5)
+    G = (rng.integers(-4, 5, size=(ROWS, D)) / 8).astype(np.float32)
+    G[150] = G[17]            # exact tie across the shard boundary (rank 0 row vs rank 1 row)
+    G[101] = G[100]           # tie inside one shard... and at the boundary for world 2 (101 = split)
+    P = (rng.integers(-4, 5, size=(2 * B, D)) / 8).astype(np.float32)
+    P[3] = G[17]              # probe whose best match is the tied pair
+    P[7] = G[100]
+    return G, P
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from facerecognition_amd.distributed import ShardedMatcher, shard_range
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        G, P = _data()
+        lo, hi = shard_range(ROWS, rank, world)
+        shard = G[lo:hi]
+
+        def local_search(probes):
+            s, i = topk_dot(probes.numpy(), shard, K)
+            i = np.where(i >= 0, i + lo, -1)
+            return torch.from_numpy(s), torch.from_numpy(i.astype(np.int32))
+
+        def merge(cs, ci, k):
+            s, i = merge_topk(cs.numpy(), ci.numpy(), k)
+            return torch.from_numpy(s), torch.from_numpy(i.astype(np.int32))
+
+        m = ShardedMatcher(B, D, K, local_search, torch.device("cpu"), merge=merge)
+        s, i = m.search(torch.from_numpy(P[rank * B:(rank + 1) * B]))
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), s=s.numpy(), i=i.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_range_partitions_rows():
+    from facerecognition_amd.distributed import shard_range
+    for rows in (0, 1, 7, 203, 10000):
+        for world in (1, 2, 3, 8):
+            r = [shard_range(rows, k, world) for k in range(world)]
+            assert r[0][0] == 0 and r[-1][1] == rows
+            assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+            assert max(h - l for l, h in r) - min(h - l for l, h in r) <= 1
+
+
+def test_merge_oracle_matches_global_topk():
+    G, P = _data()
+    lists = [topk_dot(P, G[lo:hi], K) for lo, hi in ((0, 90), (90, 91), (91, ROWS))]
+    cs = np.stack([s for s, _ in lists], 1)
+    ci = np.stack([np.where(i >= 0, i + lo, -1) for (_, i), lo in zip(lists, (0, 90, 91))], 1)
+    s, i = merge_topk(cs, ci, K)
+    gs, gi = topk_dot(P, G, K)
+    assert np.array_equal(i, gi) and np.array_equal(s, gs)
+
+
+@pytest.mark.timeout(180)
+def test_sharded_match_world2_gloo_equals_single_device():
+    G, P = _data()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        r0, r1 = (np.load(os.path.join(d, f"r{r}.npz")) for r in (0, 1))
+        gs, gi = topk_dot(P, G, K)
+        for r in (r0, r1):  # every rank holds the full, identical answer
+            assert np.array_equal(r["i"], gi.astype(np.int32))
+            assert np.array_equal(r["s"], gs)
+        assert list(gi[3][:2]) == [17, 150] and list(gi[7][:2]) == [100, 101]

@@ -1,0 +1,140 @@
+"""The reference-compatible host API end to end on the GPU, checked against the reference's own
+outputs (tests/golden/arcface_r50_golden.npz, produced by importing the reference's
+ArcFaceModel / extract_embedding_single / RecognitionEngine.recognize_with_db; tools/gen_golden.py).
+
+Tolerances: embeddings within 1e-3 cosine distance of the reference's (north star);
+match scores of given embeddings within 1e-5 (f32 dot products, different summation order);
+indices / names identical."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "arcface_r50_golden.npz")
+COS_TOL = 1e-3
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with np.load(GOLD, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def r50(gold, gpu):
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.weights import synth_state_dict
+    sd = synth_state_dict("resnet50_arcface", seed=int(gold["seed"]), num_classes=int(gold["num_classes"]))
+    return FRModel("resnet50_arcface", sd, max_batch=64)
+
+
+@pytest.fixture(scope="module")
+def names_db(gold):
+    from facerecognition_amd.synthetic import planted_gallery
+    G = planted_gallery(gold["emb_batch"], int(gold["gallery_rows"]), seed=int(gold["gallery_seed"]))
+    names = [f"id_{i:04d}" for i in range(len(G))]
+    return names, {n: G[i] for i, n in enumerate(names)}
+
+
+def _cos_dist(a, b):
+    a = a / np.linalg.norm(a, axis=-1, keepdims=True)
+    b = b / np.linalg.norm(b, axis=-1, keepdims=True)
+    return 1 - (a * b).sum(-1)
+
+
+def test_extract_embedding_single_vs_reference(gold, r50):
+    from PIL import Image
+    from facerecognition_amd.extract_embeddings import extract_embedding_single, get_transform
+    t = get_transform()
+    got = np.stack([extract_embedding_single(Image.fromarray(p), r50, t) for p in gold["probes"]])
+    assert got.dtype == np.float32 and got.shape == (8, 512)
+    assert _cos_dist(got, gold["emb_single"]).max() <= COS_TOL
+
+
+def test_natural_image_tensor_vs_reference(gold, r50):
+    """uploads/anh1.jpg after the reference transform (f32 NCHW input path of fr_embed)."""
+    import torch
+    e = r50.embed(torch.from_numpy(gold["natural_tensor"])[None]).cpu().numpy()[0]
+    assert _cos_dist(e, gold["natural_emb"]) <= COS_TOL
+
+
+def test_raw_forward_vs_reference(gold, r50):
+    import torch
+    raw = r50(torch.from_numpy(gold["probes"])).cpu().numpy()  # ArcFaceModel(x, labels=None): unnormalized
+    assert _cos_dist(raw, gold["emb_raw"]).max() <= COS_TOL
+    n_ref, n = np.linalg.norm(gold["emb_raw"], axis=1), np.linalg.norm(raw, axis=1)
+    assert np.allclose(n, n_ref, rtol=5e-3)
+
+
+def test_recognize_with_db_vs_reference(gold, names_db):
+    from facerecognition_amd.recognition_engine import RecognitionEngine
+    names, db = names_db
+    eng = RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.5)
+    eng.db = db
+    for p in range(8):
+        name, score, top5 = eng.recognize_with_db(gold["emb_single"][p])
+        assert name == str(gold["best_name"][p])
+        assert [names.index(t[0]) for t in top5] == list(gold["top5_idx"][p])
+        assert np.allclose([t[1] for t in top5], gold["top5_scores"][p], atol=1e-5)
+    eng.db = {"dup_a": db["id_0003"], "dup_b": db["id_0003"].copy(), "other": db["id_0005"]}
+    name, _, top = eng.recognize_with_db(gold["emb_single"][3])
+    assert name == str(gold["tie_name"]) and [t[0] for t in top] == list(gold["tie_top"])
+    eng.db = db
+    eng.set_threshold(0.999)
+    name, score, _ = eng.recognize_with_db(gold["emb_single"][0])
+    assert name == "Unknown" and abs(score - float(gold["unknown_score"])) < 1e-5
+
+
+def test_recognize_batch_end_to_end(gold, r50, names_db):
+    from PIL import Image
+    from facerecognition_amd.recognition_engine import RecognitionEngine
+    _, db = names_db
+    eng = RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.5, model=r50)
+    eng.db = db
+    imgs = [Image.fromarray(p) for p in gold["probes"]] + ["/nonexistent.jpg"]
+    res = eng.recognize_batch(imgs)
+    assert [r["identity"] for r in res[:8]] == [str(n) for n in gold["best_name"]]
+    assert res[8]["status"] == "error" and res[8]["embedding"] is None
+    single = eng.recognize(imgs[2])
+    assert single["identity"] == res[2]["identity"] and abs(single["confidence"] - res[2]["confidence"]) < 1e-6
+    assert _cos_dist(res[2]["embedding"], gold["emb_single"][2]) <= COS_TOL
+    # in-place db edit is picked up by the device copy
+    eng.db["zz_probe2"] = res[2]["embedding"]
+    assert eng.recognize(imgs[2])["identity"] == "zz_probe2"
+
+
+def test_folder_db_build_and_faiss_path(gold, r50, tmp_path):
+    from PIL import Image
+    import torch
+    from facerecognition_amd import extract_embeddings as EE
+    from facerecognition_amd.recognition_engine import RecognitionEngine, create_engine_from_embeddings_dir
+    from oracle.match import faiss_flat_ip_search, folder_mean
+    for person, idx in (("p0", [0, 1, 2]), ("p1", [3, 4]), ("p2", [5, 6, 7])):
+        os.makedirs(tmp_path / "celeb" / person)
+        for i in idx:
+            Image.fromarray(gold["probes"][i]).save(tmp_path / "celeb" / person / f"{i}.png")
+    t = EE.get_transform()
+    e = EE.extract_embedding_for_folder(str(tmp_path / "celeb" / "p1"), r50, t)
+    assert _cos_dist(e, folder_mean(gold["emb_single"][[3, 4]])) <= COS_TOL
+    # checkpoint in the reference's schema -> build_db -> RecognitionEngine(db_path)
+    from facerecognition_amd.weights import synth_state_dict
+    sd = synth_state_dict("resnet50_arcface", seed=int(gold["seed"]), num_classes=int(gold["num_classes"]))
+    ck = str(tmp_path / "arcface_best.pth")
+    torch.save({"model_state_dict": {k: torch.as_tensor(v) for k, v in sd.items()},
+                "config": {"num_classes": 100, "model": {"embedding_size": 512}}, "epoch": 3}, ck)
+    dbp = str(tmp_path / "db.npy")
+    EE.build_db(ck, str(tmp_path / "celeb"), dbp, "cuda", use_face_detection=False)
+    eng = RecognitionEngine(model_path=ck, db_path=dbp, use_face_detection=False, threshold=0.3)
+    assert sorted(eng.get_db_identities()) == ["p0", "p1", "p2"]
+    assert eng.recognize(Image.fromarray(gold["probes"][4]))["identity"] == "p1"
+    # FAISS-style index over the same identities
+    protos = np.stack([eng.db[k] for k in ("p0", "p1", "p2")])
+    os.makedirs(tmp_path / "emb")
+    EE.build_faiss_index(protos, str(tmp_path / "emb" / "arcface_index.npz"))
+    eng2 = create_engine_from_embeddings_dir(ck, str(tmp_path / "emb"), threshold=0.3)
+    name, score, res = eng2.recognize_with_faiss(gold["emb_single"][6], k=3)
+    s_ref, i_ref = faiss_flat_ip_search(protos, gold["emb_single"][6], 3)
+    assert [r[0] for r in res] == [f"ID_{i}" for i in i_ref[0]]
+    assert np.allclose([r[1] for r in res], s_ref[0], atol=1e-5)

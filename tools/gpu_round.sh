@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-end measurement on the GPU box (repo root):  tools/gpu_round.sh TAG [skip-tests]
+#   1. pytest -m gpu           -> gpurun_out/TAG/tests.log
+#   2. bench.py (default args) -> gpurun_out/TAG/bench.json  (+ --no-prof line for the event overhead)
+#   3. rocprofv3 --kernel-trace --stats of the same bench command -> gpurun_out/TAG/prof/
+#   4. two separate --pmc passes (FETCH_SIZE, WRITE_SIZE) -> profiles-ready traffic JSON
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+T=${1:?tag}; SKIP_TESTS=${2:-}
+R=$(pwd); O=$R/gpurun_out/$T
+mkdir -p $O
+step() { local name=$1 lim=$2; shift 2; echo "[$(date +%T)] $name"; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; if [ $rc -ne 0 ]; then echo "$name failed rc=$rc"; tail -20 $O/$name.log; exit $rc; fi; }
+if [ -z "$SKIP_TESTS" ]; then
+  step tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x
+  tail -3 $O/tests.log
+fi
+step bench 400 python bench.py
+tail -1 $O/bench.log > $O/bench.json; cat $O/bench.json
+step bench_noprof 300 python bench.py --no-prof --no-cpu-baseline
+tail -1 $O/bench_noprof.log
+BCMD="$R/bench.py --steps 10 --warmup 3 --no-cpu-baseline"
+cd /tmp && export TMPDIR=/tmp
+step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $BCMD
+step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pf -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-prof
+step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pw -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-prof
+cd $R
+python tools/pmc_traffic.py --fetch $O/pf --write $O/pw --out $O/pmc_traffic.json
+find $O/prof -name "*kernel_stats.csv" | head -1 | xargs -r head -12
+echo "[$(date +%T)] done"
