@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "aligned faces/sec (embed+match) ArcFace@112 bs=256, 1/2/4/8 MI355X"
-IRESNET100_GFLOP_PER_FACE = 24.179  # 2 * (conv + fc MACs)
+GFLOP_PER_FACE = {"iresnet100": 24.179, "resnet50_arcface": 2.154, "irv1_facenet": 2.835}
 BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
 
 
@@ -58,10 +58,13 @@ def parse():
     ap.add_argument("--gallery-rows", type=int, default=10000)
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--arch", default="iresnet100")
-    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dtype", default=None, help="bf16 | f16 (default: the arch's parity dtype)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip the per-kernel event timing (roofline)")
+    ap.add_argument("--host-input", action="store_true",
+                    help="crops start in pinned host memory and are copied H2D inside each step "
+                         "(PCIe-inclusive rate, DESIGN.md; never the headline value)")
     return ap.parse_args()
 
 
@@ -92,7 +95,7 @@ def cpu_baseline(arch, seconds):
             break
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 3), "unit": "faces/s", "cores": threads, "kind": "port",
-            "sample": f"{done} synthetic 112x112 crops in batches of {bs}: {arch} fp32 forward + F.normalize "
+            "sample": f"{done} synthetic {s}x{s} crops in batches of {bs}: {arch} fp32 forward + F.normalize "
                       f"+ np.dot top-5 vs 1000x512 gallery, torch {threads} threads, {dt:.1f}s"}
 
 
@@ -118,6 +121,7 @@ def main():
 
     B, K = args.batch, args.k
     model = FRModel.synthetic(args.arch, device=local, max_batch=B, dtype=args.dtype)
+    args.dtype = model.dtype
     size = model.input_size
     u8 = torch.from_numpy(synthetic_crops(B, size, seed=100 + rank)).to(dev)  # HBM-resident input
     # gallery: rows [r*rows/N, (r+1)*rows/N) on rank r; global indices via index_base
@@ -131,7 +135,11 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     matcher = ShardedMatcher(B, 512, K, lambda p: gallery.search_device(p, K), dev)
 
+    u8_host = u8.cpu().pin_memory() if args.host_input else None
+
     def step(i=None):
+        if u8_host is not None:
+            u8.copy_(u8_host, non_blocking=True)
         if i is not None:
             ev[i][0].record(stream)
         model.embed(u8, out=emb)
@@ -186,13 +194,13 @@ def main():
 
     faces = world * B * args.steps
     value = faces / elapsed
-    flop_fwd = IRESNET100_GFLOP_PER_FACE * 1e9 * B if args.arch == "iresnet100" else None
+    flop_fwd = GFLOP_PER_FACE[args.arch] * 1e9 * B
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "faces/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-        "data": "synthetic u8 112x112x3 aligned crops (HBM-resident), random-init BN-calibrated weights, "
-                "random unit-norm gallery",
+        "data": f"synthetic u8 {size}x{size}x3 aligned crops ({'pinned host, H2D per step' if args.host_input else 'HBM-resident'}), "
+                "random-init BN-calibrated weights, random unit-norm gallery",
         "config": {"workload": f"{args.arch} {args.dtype} embed bs={B}/GPU + top-{K} match vs "
                                f"{rows}x512 f32 gallery (row-sharded over {world} GPU(s))",
                    "batch_per_gpu": B, "global_batch": world * B, "gallery_rows": rows, "k": K,

@@ -17,6 +17,8 @@
 // LDS rows are 128 B (64 channels); chunk index XOR (row>>1)&7, applied to the per-lane DMA source.
 #include "kernels.h"
 
+#include <hip/hip_ext.h>
+
 namespace fr {
 namespace {
 
@@ -284,7 +286,10 @@ static hipError_t launch_band_k(const ConvArgs& a, hipStream_t s) {
     }
     const int ntn = (a.Cout + BN - 1) / BN;
     dim3 grid(a.B * (a.H / TH) * ntn);
-    hipLaunchKernelGGL(k, grid, dim3(64 * WM * WN), LDS, s, a, ntn);
+    if (a.ev0)
+        hipExtLaunchKernelGGL(k, grid, dim3(64 * WM * WN), LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, ntn);
+    else
+        hipLaunchKernelGGL(k, grid, dim3(64 * WM * WN), LDS, s, a, ntn);
     return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@
 // FASTK (Cin % 64 == 0): a K-step is one (r, s) tap and 64 channels, tracked in scalars.
 #include "kernels.h"
 
+#include <hip/hip_ext.h>
+
 #include <cstdlib>
 
 namespace fr {
@@ -312,10 +314,12 @@ hipError_t launch_variant(const ConvArgs& a, hipStream_t s) {
     const int per = (nkt + split - 1) / split;
     dim3 grid(tiles_m * tiles_n, split);
     dim3 block(64 * WM * WN);
-    if (a.Cin % 64 == 0)
-        hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN, STAGES, true>), grid, block, 0, s, a, tiles_n, per);
+    auto k = a.Cin % 64 == 0 ? conv_igemm_kernel<F16, BM, BN, WM, WN, STAGES, true>
+                             : conv_igemm_kernel<F16, BM, BN, WM, WN, STAGES, false>;
+    if (a.ev0)
+        hipExtLaunchKernelGGL(k, grid, block, 0, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, tiles_n, per);
     else
-        hipLaunchKernelGGL((conv_igemm_kernel<F16, BM, BN, WM, WN, STAGES, false>), grid, block, 0, s, a, tiles_n, per);
+        hipLaunchKernelGGL(k, grid, block, 0, s, a, tiles_n, per);
     return hipGetLastError();
 }
 

@@ -578,19 +578,24 @@ hipEvent_t prof_event(fr_handle* h) {
 // Brackets one launch with two events when profiling is on; `cls` names the kernel instantiation so
 // the totals line up with rocprofv3's per-kernel rows.
 struct ProfScope {
-    fr_handle* h; hipStream_t s; hipEvent_t a = nullptr; std::string cls; double flops = 0;
+    fr_handle* h; hipStream_t s; hipEvent_t a = nullptr, b = nullptr; bool stamped = false;
+    std::string cls; double flops = 0;
     ProfScope(fr_handle* h_, hipStream_t s_) : h(h_), s(s_) {}
-    // call right before the launch(es), once the class name is known
-    void start(const std::string& c) {
+    // Call right before the launch once the class is known.  With `ka` the pair is handed to the
+    // conv launcher, which stamps it from the dispatch packet (hipExtLaunchKernel: no extra stream
+    // commands); otherwise the pair is recorded around the launch(es) with hipEventRecord.
+    void start(const std::string& c, ConvArgs* ka = nullptr) {
         cls = c;
         if (!h->prof || (!h->prof_only.empty() && h->prof_only != cls)) return;
-        if ((a = prof_event(h))) (void)hipEventRecord(a, s);
+        a = prof_event(h);
+        b = a ? prof_event(h) : nullptr;
+        if (!b) { if (a) h->ev_free.push_back(a); a = nullptr; return; }
+        if (ka) { ka->ev0 = a; ka->ev1 = b; stamped = true; }
+        else (void)hipEventRecord(a, s);
     }
     ~ProfScope() {
         if (!a) return;
-        hipEvent_t b = prof_event(h);
-        if (!b) { h->ev_free.push_back(a); return; }
-        (void)hipEventRecord(b, s);
+        if (!stamped) (void)hipEventRecord(b, s);
         h->prof_pending.push_back({cls, a, b, flops});
     }
 };
@@ -605,7 +610,7 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     // auto policy (measured, profiles/r01_layers.txt): the row-band kernel beats the implicit GEMM
     // only on the 14x14 stage (layer3, 45% of IResNet100 FLOPs); W=28/56/112 stay on igemm tiles
     if (band_enabled() && a.W == 14 && band_plan(a, &TH, &variant)) {
-        ps.start("conv3x3_band W" + std::to_string(a.W) + " v" + std::to_string(variant));
+        ps.start("conv3x3_band W" + std::to_string(a.W) + " v" + std::to_string(variant), &a);
         FR_HIP_CHECK(launch_conv_band(a, TH, variant, s));
         return FR_OK;
     }
@@ -615,7 +620,7 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) split /= 2;
     if (split > 1) a.partial = h->partial;
     a.split_k = split;
-    ps.start("conv_igemm tile" + std::to_string(tile) + (split > 1 ? " splitk" : ""));
+    ps.start("conv_igemm tile" + std::to_string(tile) + (split > 1 ? " splitk" : ""), &a);
     FR_HIP_CHECK(launch_conv(a, s));
     if (split > 1 && a.y) FR_HIP_CHECK(launch_splitk_epilogue(a, s));
     return FR_OK;

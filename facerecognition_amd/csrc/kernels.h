@@ -23,6 +23,8 @@ struct ConvArgs {
     int f16;                      // 0: bf16 storage + bf16 MFMA; 1: f16 storage + f16 MFMA
     int tile;                     // TILE_* variant (conv_plan)
     int dbg;                      // experiment switches (FR_CONV_DBG env; 0 in production)
+    void* ev0;                    // optional hipEvent_t pair stamped by the dispatch itself
+    void* ev1;                    //   (hipExtLaunchKernel; fr_prof_* timing), null normally
 };
 
 // Choose tile variant and split-K factor for a GEMM of M x Cout x Kpad.

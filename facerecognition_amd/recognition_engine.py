@@ -347,3 +347,8 @@ def create_engine_from_embeddings_dir(model_path: str, embeddings_dir: str, thre
                              prototypes_path=protos if os.path.exists(protos) else None,
                              label_mapping_path=mapping if os.path.exists(mapping) else None,
                              threshold=threshold, device=device)
+
+
+# The north star names "UnifiedRecognitionEngine"; the reference's README calls recognition_engine.py the
+# "Unified Recognition Engine" (README.md:202) but the class is RecognitionEngine (SURVEY.md §0 note 3).
+UnifiedRecognitionEngine = RecognitionEngine

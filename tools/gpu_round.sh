@@ -18,6 +18,10 @@ step bench 400 python bench.py
 tail -1 $O/bench.log > $O/bench.json; cat $O/bench.json
 step bench_noprof 300 python bench.py --no-prof --no-cpu-baseline
 tail -1 $O/bench_noprof.log
+step bench_host 300 python bench.py --no-cpu-baseline --host-input
+step bench_irv1 300 python bench.py --no-cpu-baseline --arch irv1_facenet
+step bench_r50 300 python bench.py --no-cpu-baseline --arch resnet50_arcface
+for b in bench_host bench_irv1 bench_r50; do tail -1 $O/$b.log | cut -c1-400; done
 BCMD="$R/bench.py --steps 10 --warmup 3 --no-cpu-baseline"
 cd /tmp && export TMPDIR=/tmp
 step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $BCMD
