@@ -19,6 +19,8 @@
 
 #include <hip/hip_ext.h>
 
+#include <cstdlib>
+
 namespace fr {
 namespace {
 
@@ -45,6 +47,70 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 constexpr int MAXPW = 8;  // max patch DMA instructions per wave per chunk
+
+// Fused epilogue straight from registers (lane = 4 consecutive channels of one pixel): bias, residual,
+// ReLU/PReLU, bf16/f16 store, optional second affine output.  Channel-outer so the per-channel vectors
+// load once per fragment column; residual loads are unconditional (invalid lanes read pixel 0) so the
+// FM loads of a column are in flight together; only the stores are predicated.
+template <class T, int W, int Wp, int Mv, int FM, int FN>
+__device__ __forceinline__ void band_epilogue(const ConvArgs& p, const f32x4_t (&acc)[FN][FM], int lane, int wm,
+                                              int wn, size_t pix0, int n0) {
+    int pix_off[FM];
+    bool pv[FM];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+        const int m = 16 * (wm * FM + j) + (lane & 15);
+        const int r = m / Wp, c = m - r * Wp;
+        pv[j] = m < Mv && c < W;
+        pix_off[j] = pv[j] ? r * W + c : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+        const int n_raw = n0 + wn * 16 * FN + 16 * i + 4 * (lane >> 4);
+        const bool nv = n_raw < p.Cout;
+        const int n = nv ? n_raw : 0;
+        float4 bb = make_float4(0.f, 0.f, 0.f, 0.f), sl = bb, as = bb, ab = bb;
+        if (p.bias) bb = *(const float4*)(p.bias + n);
+        if (p.act == 2) sl = *(const float4*)(p.slope + n);
+        if (p.y2) { as = *(const float4*)(p.aff_s + n); ab = *(const float4*)(p.aff_b + n); }
+        uint2 rr[FM];
+        if (p.res) {
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+                rr[j] = *(const uint2*)(p.res + (pix0 + pix_off[j]) * p.Cres + p.res_off + n);
+        }
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
+            if (p.res) {
+                float f[8];
+                T::unpack8(make_uint4(rr[j].x, rr[j].y, 0, 0), f);
+                v[0] += f[0]; v[1] += f[1]; v[2] += f[2]; v[3] += f[3];
+            }
+            if (p.act == 1) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+            } else if (p.act == 2) {
+                v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
+                v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
+                v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
+                v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
+            }
+            if (pv[j] && nv) {
+                const size_t pix = pix0 + pix_off[j];
+                float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+                const uint4 pk = T::pack8(o8);
+                *(uint2*)(p.y + pix * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
+                if (p.y2) {
+                    float u8[8] = {v[0] * as.x + ab.x, v[1] * as.y + ab.y, v[2] * as.z + ab.z, v[3] * as.w + ab.w,
+                                   0, 0, 0, 0};
+                    const uint4 pk2 = T::pack8(u8);
+                    *(uint2*)(p.y2 + pix * p.Cy2 + p.y2_off + n) = make_uint2(pk2.x, pk2.y);
+                }
+            }
+        }
+    }
+}
 
 // Patch LDS image, chunk-major: [8 chunks of 8 channels][P64 positions][16 B].  A tap shift is then a
 // pure position offset, i.e. an immediate on ds_read_b128, and 16 lanes reading 16 consecutive
@@ -223,48 +289,227 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_band_kernel(ConvArgs 
         }
     }
 
-    // Fused epilogue straight from registers: lane = 4 consecutive channels of one pixel.
+    band_epilogue<T, W, Wp, Mv, FM, FN>(p, acc, lane, wm, wn, (size_t)(b * H + oh0) * W, n0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmn() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Software-pipelined band kernel: one wave per SIMD (4 waves, 512-register budget), each wave owning
+// a 16*FM (pixel rows) x 16*FN (channels) register tile.  Per K-step s = (chunk, tap), K = 64 as two
+// MFMA k-halves:
+//   [ DMA slice s+2 | (tap 0) DMA next patch ]  [ ds_read k-half 1 frags | 56 MFMA on k-half 0 ]
+//   s_waitcnt vmcnt(younger than slice s+1), lgkmcnt(0); s_barrier (raw: no vmcnt(0) drain)
+//   [ ds_read next step's k-half 0 frags | 56 MFMA on k-half 1 ]
+// so LDS reads always overlap MFMAs, the weight ring keeps two slices in flight across the barrier,
+// and every DMA count is static (the last steps re-fetch the final slice / patch into free buffers
+// instead of skipping, keeping the vmcnt arithmetic compile-time).
+template <bool F16, int W, int TH, int WM, int WN, int FM, int FN>
+__global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs p, int ntn) {
+    constexpr int NW = WM * WN;
+    constexpr int BN = 16 * FN * WN;
+    constexpr int Wp = W + 2;
+    constexpr int P = (TH + 2) * Wp;
+    constexpr int P64 = (P + 63) / 64 * 64;
+    constexpr int PLANE = P64 * 16;
+    constexpr int PATCH = 8 * PLANE;
+    constexpr int NPB = P64 / 64;
+    constexpr int PI = 8 * NPB;
+    static_assert(PI % NW == 0, "patch DMA must split evenly over waves");
+    constexpr int NPW = PI / NW;
+    constexpr int WSL = BN * 128;
+    constexpr int NWI = BN / 8 / NW;
+    static_assert(NWI * 8 * NW == BN, "weight slice rows must split evenly over waves");
+    static_assert(NWI + 2 * NPW <= 63, "vmcnt range");
+    constexpr int Mv = TH * Wp - 2;
+    static_assert(16 * FM * WM >= Mv, "MFMA rows must cover the band");
+    typedef Num<F16> T;
+    typedef typename T::frag frag;
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [patch0][patch1][wsl0][wsl1][wsl2]
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int H = p.H;
+    const int bands = H / TH;
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tn = lid % ntn;
+    const int rest = lid / ntn;
+    const int band = rest % bands, b = rest / bands;
+    const int oh0 = band * TH, n0 = tn * BN;
+
+    const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * H * W * p.Cx * 2);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
+    const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
+
+    uint32_t psrc[NPW];
+#pragma unroll
+    for (int u = 0; u < NPW; ++u) {
+        const int q = wave + NW * u;
+        const int c = q / NPB, pos = 64 * (q - c * NPB) + lane;
+        const int ih = oh0 - 1 + pos / Wp, iw = pos % Wp - 1;
+        const bool ok = pos < P && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        psrc[u] = ok ? (uint32_t)((((b * H + ih) * W + iw) * p.Cx + p.x_off + 8 * c) * 2) : OOB;
+    }
+    uint32_t woff[NWI];
+#pragma unroll
+    for (int u = 0; u < NWI; ++u) {
+        const int row = 8 * (wave + NW * u) + (lane >> 3);
+        const int cl = (lane & 7) ^ ((row >> 1) & 7);
+        woff[u] = (uint32_t)(((n0 + row) * p.Kpad + 8 * cl) * 2);
+    }
+    int aoff[FM];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
         const int m = 16 * (wm * FM + j) + (lane & 15);
-        const int r = m / Wp, c = m - r * Wp;
-        if (m >= Mv || c >= W) continue;
-        const size_t pix = (size_t)(b * H + oh0 + r) * W + c;
+        aoff[j] = (lane >> 4) * PLANE + (m < Mv ? m : 0) * 16;
+    }
+    int boff[FN], boff1[FN];  // k-half 1 = chunk ^ 4 = byte bit 6 of the swizzled row
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+        const int row = wn * 16 * FN + 16 * i + (lane & 15);
+        boff[i] = row * 128 + swzb(row, lane >> 4) * 16;
+        boff1[i] = boff[i] ^ 64;
+    }
+
+    auto issue_patch = [&](int chunk, int pb) {
+        const uint32_t cadd = (uint32_t)(chunk * 64 * 2);
+        char* dst = smem + pb * PATCH;
+#pragma unroll
+        for (int u = 0; u < NPW; ++u) dma16(xr, dst + (wave + NW * u) * 1024, psrc[u] == OOB ? OOB : psrc[u] + cadd);
+    };
+    auto issue_w = [&](int chunk, int tap, int wb) {
+        const uint32_t kadd = (uint32_t)((tap * p.Cin + chunk * 64) * 2);
+        char* dst = smem + 2 * PATCH + wb * WSL;
+#pragma unroll
+        for (int u = 0; u < NWI; ++u) dma16(wr, dst + (wave + NW * u) * 1024, woff[u] + kadd);
+    };
+
+    f32x4_t acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+    // Fragments: the 7 patch fragments are double-buffered (pA / pB by k-half parity); each of the 8
+    // weight fragments is refilled in place for the next k-half right after its last MFMA use.  Every
+    // LDS read is (per-lane base) + (compile-time immediate) after the unrolling below.
+    frag wf[FN], pA[FM], pB[FM];
+    auto wread = [&](frag& f, int i, int wslot, int kk) {
+        f = *(const frag*)(smem + 2 * PATCH + wslot * WSL + (kk ? boff1[i] : boff[i]));
+    };
+    auto pread = [&](frag (&pf)[FM], int pbuf, int kk, int tap) {
+        const int shift = ((tap / 3) * Wp + (tap % 3)) * 16;
+        const char* pa = smem + pbuf * PATCH + kk * 4 * PLANE + shift;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) pf[j] = *(const frag*)(pa + aoff[j]);
+    };
+    // one k-half: MFMAs on (wf, cur) while the next k-half's patch fragments land in `nxt` and each wf[i]
+    // is reloaded (from wslot_n / kk_n) after its 7 MFMAs; `has_next` false on the very last half
+    auto half_step = [&](frag (&cur)[FM], frag (&nxt)[FM], bool has_next, int pbuf_n, int wslot_n, int kk_n,
+                         int tap_n, int n_dma) {
+        if (has_next) pread(nxt, pbuf_n, kk_n, tap_n);
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
-            const int n = n0 + wn * 16 * FN + 16 * i + 4 * (lane >> 4);
-            if (n >= p.Cout) continue;
-            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            if (p.bias) {
-                const float4 bb = *(const float4*)(p.bias + n);
-                v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-            }
-            if (p.res) {
-                const uint2 r = *(const uint2*)(p.res + pix * p.Cres + p.res_off + n);
-                float f[8];
-                T::unpack8(make_uint4(r.x, r.y, 0, 0), f);
-                v[0] += f[0]; v[1] += f[1]; v[2] += f[2]; v[3] += f[3];
-            }
-            if (p.act == 1) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-            } else if (p.act == 2) {
-                const float4 sl = *(const float4*)(p.slope + n);
-                const float s4[4] = {sl.x, sl.y, sl.z, sl.w};
+            for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
+            if (has_next) wread(wf[i], i, wslot_n, kk_n);
+        }
+        // issue order: the step's DMAs, then one patch read per MFMA gap, then one weight refill after
+        // each weight fragment's 7 MFMAs (its last use)
+        if (n_dma == NWI + NPW) __builtin_amdgcn_sched_group_barrier(0x020, NWI + NPW, 0);
+        else if (n_dma == NWI) __builtin_amdgcn_sched_group_barrier(0x020, NWI, 0);
+        if (has_next) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * s4[e];
+            for (int q = 0; q < FM; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
-            float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
-            const uint4 pk = T::pack8(o8);
-            *(uint2*)(p.y + pix * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
-            if (p.y2) {
-                const float4 a = *(const float4*)(p.aff_s + n), c = *(const float4*)(p.aff_b + n);
-                float u8[8] = {v[0] * a.x + c.x, v[1] * a.y + c.y, v[2] * a.z + c.z, v[3] * a.w + c.w, 0, 0, 0, 0};
-                const uint4 pk2 = T::pack8(u8);
-                *(uint2*)(p.y2 + pix * p.Cy2 + p.y2_off + n) = make_uint2(pk2.x, pk2.y);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+            for (int i = 1; i < FN; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, FM, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
+        } else {
+            __builtin_amdgcn_sched_group_barrier(0x008, FN * FM, 0);
+        }
+    };
+
+    const int nchunk = p.Cin / 64;
+    issue_patch(0, 0);
+    issue_w(0, 0, 0);
+    issue_w(0, 1, 1);
+    {  // warm this XCD's L2 with a 1/32 share of the block's weight panel (see conv3x3_band_kernel)
+        const uint32_t panel = (uint32_t)BN * p.Kpad * 2;
+        const uint32_t share = (panel + 31) / 32;
+        const uint32_t base = (uint32_t)n0 * p.Kpad * 2 + (uint32_t)((blockIdx.x / 8) % 32) * share;
+        const uint32_t stride = (uint32_t)NW * 64 * 128;
+        unsigned dummy;
+        for (uint32_t o = (uint32_t)(wave * 64 + lane) * 128; o < share; o += stride) {
+            asm volatile("buffer_load_dword %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)"
+                         : "=&v"(dummy) : "v"(base + o), "s"(wr) : "memory");
         }
     }
+    wait_vmn<0>();
+    asm volatile("s_barrier" ::: "memory");
+    pread(pA, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < FN; ++i) wread(wf[i], i, 0, 0);
+
+    for (int chunk = 0; chunk < nchunk; ++chunk) {
+        const int pb = chunk & 1;
+        const bool last_chunk = chunk + 1 == nchunk;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            // ring slot of step (chunk, tap) = tap % 3 because 9 % 3 == 0
+            {
+                const int t2 = tap + 2 < 9 ? tap + 2 : tap - 7;
+                const int c2n = tap + 2 < 9 ? chunk : chunk + 1;
+                const bool ok = c2n < nchunk;
+                issue_w(ok ? c2n : nchunk - 1, ok ? t2 : 8, (tap + 2) % 3);  // static count at the tail
+            }
+            if (tap == 0) issue_patch(last_chunk ? chunk : chunk + 1, pb ^ 1);
+            // k-half 0 (fragments in pA / wf); prefetch k-half 1 of the same step
+            half_step(pA, pB, true, pb, tap % 3, 1, tap, NWI + (tap == 0 ? NPW : 0));
+            // slice step+1 (and, before a new chunk, its patch: older) has landed for this wave;
+            // younger: slice step+2 (+ the patch issued at tap 0 / at the previous step's tap 0)
+            if (tap == 0 || tap == 1) wait_vmn<NWI + NPW>();
+            else wait_vmn<NWI>();
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            // k-half 1; prefetch k-half 0 of the next step
+            const bool nxt = tap < 8 || !last_chunk;
+            half_step(pB, pA, nxt, tap < 8 ? pb : pb ^ 1, (tap + 1) % 3, 0, tap < 8 ? tap + 1 : 0, 0);
+        }
+    }
+    wait_vmn<0>();  // the tail re-fetches must land before the workgroup's LDS is released
+
+    band_epilogue<T, W, Wp, Mv, FM, FN>(p, acc, lane, wm, wn, (size_t)(b * H + oh0) * W, n0);
+}
+
+template <bool F16, int W, int TH>
+static hipError_t launch_bandp_k(const ConvArgs& a, hipStream_t s) {
+    constexpr int WM = 2, WN = 2, FM = 7, FN = 8;
+    constexpr int BN = 16 * FN * WN;
+    constexpr int P64 = ((TH + 2) * (W + 2) + 63) / 64 * 64;
+    constexpr int LDS = 2 * 8 * P64 * 16 + 3 * BN * 128;
+    static_assert(LDS <= 160 * 1024, "band LDS budget");
+    auto k = conv3x3_bandp_kernel<F16, W, TH, WM, WN, FM, FN>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+        attr = true;
+    }
+    const int ntn = (a.Cout + BN - 1) / BN;
+    dim3 grid(a.B * (a.H / TH) * ntn);
+    if (a.ev0)
+        hipExtLaunchKernelGGL(k, grid, dim3(64 * WM * WN), LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, ntn);
+    else
+        hipLaunchKernelGGL(k, grid, dim3(64 * WM * WN), LDS, s, a, ntn);
+    return hipGetLastError();
 }
 
 // Supported bands: (W, TH) with TH*(W+2)-2 <= the variant's MFMA rows.
@@ -297,6 +542,14 @@ static hipError_t launch_band_k(const ConvArgs& a, hipStream_t s) {
 
 // Applicability: 3x3 / stride 1 / pad 1, Cin % 64 == 0, a supported (W, TH) band, Cout a multiple of
 // the variant's BN.  Returns the band config id (see launch_conv_band).
+static bool band_legacy() {
+    static const bool on = [] {
+        const char* e = getenv("FR_BAND_LEGACY");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 bool band_plan(const ConvArgs& a, int* cfg, int* variant) {
     if (a.Kh != 3 || a.Kw != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1) return false;
     if (a.Cin % 64 != 0 || a.Ho != a.H || a.Wo != a.W || a.partial) return false;
@@ -312,6 +565,7 @@ bool band_plan(const ConvArgs& a, int* cfg, int* variant) {
     else if (a.W == 112 && a.H % 2 == 0) c = 3;
     else return false;
     if (c == 0 && v == 2) return false;  // 14x14x64: 196 rows of a 256-row tile, not worth it
+    if (c == 0 && v == 0 && a.Cin % 128 == 0 && !band_legacy()) v = 3;  // software-pipelined 4-wave variant
     if ((c == 2 || c == 3) && v != 2) return false;  // 4x58 / 2x114 rows exceed the 224-row variants
     *cfg = c;
     *variant = v;
@@ -320,6 +574,7 @@ bool band_plan(const ConvArgs& a, int* cfg, int* variant) {
 
 template <bool F16>
 static hipError_t launch_band_t(const ConvArgs& a, int c, int v, hipStream_t s) {
+    if (v == 3) return c == 0 ? launch_bandp_k<F16, 14, 14>(a, s) : hipErrorInvalidValue;
     switch (c * 3 + v) {
         case 0: return launch_band_k<F16, 14, 14, 0, 3>(a, s);
         case 1: return launch_band_k<F16, 14, 14, 1, 3>(a, s);

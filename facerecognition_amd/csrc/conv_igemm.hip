@@ -271,20 +271,82 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
             *(f32x4_t*)(sE + ml * EPI_LD + nl) = acc[i][j];
         }
     __syncthreads();
-    constexpr int G = BN / 8;
-    for (int it = tid; it < BM * G; it += NT) {
-        const int ml = it / G, g = it - ml * G;
-        const int m = m0 + ml, n = n0 + g * 8;
-        if (m >= p.M || n >= p.Cout) continue;
-        const float4 v0 = *(const float4*)(sE + ml * EPI_LD + g * 8);
-        const float4 v1 = *(const float4*)(sE + ml * EPI_LD + g * 8 + 4);
-        if (p.partial) {
+    constexpr int G = BN / 8;            // 8-channel groups per tile row
+    constexpr int RS = NT / G;           // tile rows per pass
+    constexpr int ITER = BM / RS;        // passes
+    static_assert(NT % G == 0 && BM % RS == 0, "epilogue mapping");
+    const int g = tid % G, ml0 = tid / G;
+    const int n = n0 + g * 8;
+    const bool nv = n < p.Cout;
+    if (p.partial) {
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+            const int ml = ml0 + it * RS, m = m0 + ml;
+            if (m >= p.M || !nv) continue;
+            const float4 v0 = *(const float4*)(sE + ml * EPI_LD + g * 8);
+            const float4 v1 = *(const float4*)(sE + ml * EPI_LD + g * 8 + 4);
             float* dst = p.partial + ((size_t)split * p.M + m) * p.Npad + n;
             *(float4*)dst = v0;
             *(float4*)(dst + 4) = v1;
-        } else {
-            float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-            epilogue8<F16>(p, v, m, n);
+        }
+        return;
+    }
+    // this thread's 8 channels are fixed: per-channel vectors load once; residual loads of all passes
+    // are issued together (rows past M read row 0), stores are predicated
+    const int nn = nv ? n : 0;
+    float bias8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sl8[8], as8[8], ab8[8];
+    if (p.bias) {
+        const float4 b0 = *(const float4*)(p.bias + nn), b1 = *(const float4*)(p.bias + nn + 4);
+        bias8[0] = b0.x; bias8[1] = b0.y; bias8[2] = b0.z; bias8[3] = b0.w;
+        bias8[4] = b1.x; bias8[5] = b1.y; bias8[6] = b1.z; bias8[7] = b1.w;
+    }
+    if (p.act == 2) {
+        const float4 s0 = *(const float4*)(p.slope + nn), s1 = *(const float4*)(p.slope + nn + 4);
+        sl8[0] = s0.x; sl8[1] = s0.y; sl8[2] = s0.z; sl8[3] = s0.w;
+        sl8[4] = s1.x; sl8[5] = s1.y; sl8[6] = s1.z; sl8[7] = s1.w;
+    }
+    if (p.y2) {
+        const float4 a0 = *(const float4*)(p.aff_s + nn), a1 = *(const float4*)(p.aff_s + nn + 4);
+        const float4 c0 = *(const float4*)(p.aff_b + nn), c1 = *(const float4*)(p.aff_b + nn + 4);
+        as8[0] = a0.x; as8[1] = a0.y; as8[2] = a0.z; as8[3] = a0.w; as8[4] = a1.x; as8[5] = a1.y; as8[6] = a1.z; as8[7] = a1.w;
+        ab8[0] = c0.x; ab8[1] = c0.y; ab8[2] = c0.z; ab8[3] = c0.w; ab8[4] = c1.x; ab8[5] = c1.y; ab8[6] = c1.z; ab8[7] = c1.w;
+    }
+    uint4 rr[ITER];
+    if (p.res) {
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+            const int m = m0 + ml0 + it * RS;
+            rr[it] = *(const uint4*)(p.res + (size_t)(m < p.M ? m : 0) * p.Cres + p.res_off + nn);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const int ml = ml0 + it * RS, m = m0 + ml;
+        const float4 v0 = *(const float4*)(sE + ml * EPI_LD + g * 8);
+        const float4 v1 = *(const float4*)(sE + ml * EPI_LD + g * 8 + 4);
+        float v[8] = {v0.x + bias8[0], v0.y + bias8[1], v0.z + bias8[2], v0.w + bias8[3],
+                      v1.x + bias8[4], v1.y + bias8[5], v1.z + bias8[6], v1.w + bias8[7]};
+        if (p.res) {
+            float f[8];
+            T::unpack8(rr[it], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += f[e];
+        }
+        if (p.act == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        } else if (p.act == 2) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sl8[e];
+        }
+        if (m < p.M && nv) {
+            *(uint4*)(p.y + (size_t)m * p.Cy + p.y_off + n) = T::pack8(v);
+            if (p.y2) {
+                float u[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) u[e] = v[e] * as8[e] + ab8[e];
+                *(uint4*)(p.y2 + (size_t)m * p.Cy2 + p.y2_off + n) = T::pack8(u);
+            }
         }
     }
 }

@@ -74,7 +74,8 @@ def test_conv_every_tile(gpu, case, tile):
 
 
 BAND_CASES = [(2, 14, 14, 256, 256), (2, 28, 28, 128, 128), (2, 56, 56, 64, 64), (1, 112, 112, 64, 64),
-              (2, 14, 14, 128, 256), (2, 28, 28, 64, 128), (2, 28, 28, 128, 256), (2, 28, 28, 64, 64)]
+              (2, 14, 14, 128, 256), (2, 28, 28, 64, 128), (2, 28, 28, 128, 256), (2, 28, 28, 64, 64),
+              (3, 14, 14, 512, 256), (1, 14, 14, 256, 512), (2, 14, 14, 192, 256)]
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
