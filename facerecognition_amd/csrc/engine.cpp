@@ -607,9 +607,9 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     ProfScope ps(h, s);
     ps.flops = conv_flops(a);
     int TH, variant;
-    // auto policy (measured, profiles/r01_layers.txt): the row-band kernel beats the implicit GEMM
-    // only on the 14x14 stage (layer3, 45% of IResNet100 FLOPs); W=28/56/112 stay on igemm tiles
-    if (band_enabled() && a.W == 14 && band_plan(a, &TH, &variant)) {
+    // auto policy (measured, profiles/r01_tile_sweep.txt): the software-pipelined row-band variants
+    // (3: 14x14, 4: 28x28) beat the implicit GEMM; the legacy 8-wave variants do not
+    if (band_enabled() && band_plan(a, &TH, &variant) && variant >= 3) {
         ps.start("conv3x3_band W" + std::to_string(a.W) + " v" + std::to_string(variant), &a);
         FR_HIP_CHECK(launch_conv_band(a, TH, variant, s));
         return FR_OK;
