@@ -394,6 +394,8 @@ hipError_t launch_dtype(const ConvArgs& a, hipStream_t s) {
         case TILE_128x128_S3: return launch_variant<F16, 128, 128, 2, 2, 3>(a, s);
         case TILE_256x128: return launch_variant<F16, 256, 128, 4, 2, 3>(a, s);
         case TILE_128x256: return launch_variant<F16, 128, 256, 2, 4, 3>(a, s);
+        case TILE_128x64_S3: return launch_variant<F16, 128, 64, 2, 2, 3>(a, s);
+        case TILE_64x128_S3: return launch_variant<F16, 64, 128, 2, 2, 3>(a, s);
         default: return launch_variant<F16, 128, 128, 2, 2, 2>(a, s);
     }
 }
@@ -403,13 +405,13 @@ hipError_t launch_dtype(const ConvArgs& a, hipStream_t s) {
 int conv_tile_bm(int tile) {
     switch (tile) {
         case TILE_256x64: case TILE_256x128: return 256;
-        case TILE_64x128: return 64;
+        case TILE_64x128: case TILE_64x128_S3: return 64;
         default: return 128;
     }
 }
 int conv_tile_bn(int tile) {
     switch (tile) {
-        case TILE_256x64: case TILE_128x64: return 64;
+        case TILE_256x64: case TILE_128x64: case TILE_128x64_S3: return 64;
         case TILE_128x256: return 256;
         default: return 128;
     }
@@ -424,21 +426,44 @@ static int tile_blocks_per_cu(int tile) {
 // Tile + split-K choice: minimise rounds-of-resident-blocks x per-block work / tile efficiency,
 // plus a charge for split-K (partials round trip + reduce kernel + prologue/epilogue amortised over
 // fewer K-steps).  A forced variant via FR_CONV_TILE=<id> (env) is honoured for experiments.
-void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
-    static const int env_tile = [] {
+static int env_tile_id() {
+    static const int t = [] {
         const char* e = getenv("FR_CONV_TILE");
         return e ? atoi(e) : -1;
     }();
+    return t;
+}
+
+bool conv_tile_forced() { return env_tile_id() >= 0; }
+
+// Tiles worth timing for a conv with Cout output channels (the autotuner's candidate set).
+int conv_tile_candidates(int Cout, int* out) {
+    static const int tiles[] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128, TILE_256x128, TILE_128x256};
+    int n = 0;
+    for (int t : tiles) {
+        const int BN = conv_tile_bn(t);
+        if (BN >= 128 && Cout <= 64) continue;
+        if (BN == 256 && Cout <= 128) continue;
+        out[n++] = t;
+    }
+    return n;
+}
+
+void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
+    const int env_tile = env_tile_id();
     static const int tiles[] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128, TILE_128x128_S3, TILE_256x128,
-                                TILE_128x256};
+                                TILE_128x256, TILE_128x64_S3, TILE_64x128_S3};
     // relative MFMA efficiency per tile, calibrated on the IResNet100 bs=256 per-layer sweep
     // (tools/tile_sweep.sh, profiles/r01_tile_sweep.txt); the 3-stage 128x128 ring is the slowest
-    static const double eff[] = {1.0, 0.93, 0.92, 0.9, 0.7, 0.9, 0.92};
+    // (0 = only when forced: not yet calibrated)
+    static const double eff[] = {1.0, 0.93, 0.92, 0.9, 0.7, 0.9, 0.92, 0.0, 0.0};
+    constexpr int NV = sizeof(tiles) / sizeof(tiles[0]);
     const int nkt = Kpad / BK;
     double best = 1e30;
     int bt = TILE_128x128, bs = 1;
-    for (int v = 0; v < 7; ++v) {
+    for (int v = 0; v < NV; ++v) {
         if (env_tile >= 0 && tiles[v] != env_tile) continue;
+        if (env_tile < 0 && eff[v] == 0.0) continue;
         const int BM = conv_tile_bm(tiles[v]), BN = conv_tile_bn(tiles[v]);
         if (BN >= 128 && Cout <= 64) continue;
         if (BN == 256 && Cout <= 128) continue;
@@ -449,7 +474,7 @@ void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
             const long blocks = nt * sk;
             const double rounds = (double)((blocks + slots - 1) / slots);
             const double ksteps = (double)((nkt + sk - 1) / sk) + 6.0;  // + prologue/epilogue ~ 6 K-steps
-            const double per_block = (double)BM * BN * ksteps / eff[v] / (512.0 / slots);
+            const double per_block = (double)BM * BN * ksteps / (eff[v] > 0.0 ? eff[v] : 1.0) / (512.0 / slots);
             const double cost = rounds * per_block + (sk > 1 ? 0.25 * (double)M * Cout * sk / 2048.0 : 0.0);
             if (cost < best * 0.999) { best = cost; bt = tiles[v]; bs = sk; }
         }

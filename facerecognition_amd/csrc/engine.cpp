@@ -94,10 +94,24 @@ struct fr_handle {
     struct ProfRec { std::string cls; hipEvent_t a, b; double flops; };
     struct ProfAcc { double ms = 0; int64_t launches = 0; double flops = 0; };
     bool prof = false;
+    int prof_stride = 1;        // time every n-th matching launch (sampling keeps the overhead small)
+    uint64_t prof_seen = 0;
     std::string prof_only;  // non-empty: time only this kernel class
     std::vector<hipEvent_t> ev_free;
     std::vector<ProfRec> prof_pending;
     std::vector<std::pair<std::string, ProfAcc>> prof_acc;
+    // forward replays as hipGraphs, keyed by the call's pointers / shape (captured on the second call
+    // with a key; the first call runs eagerly and warms per-kernel attributes)
+    struct GraphEnt { const void* in; float* out; int fmt, B, flags; hipGraphExec_t exec; bool no_graph; uint64_t used; };
+    std::vector<GraphEnt> graphs;
+    hipStream_t cap_stream = nullptr;
+    uint64_t tick = 0;
+    // per-shape igemm tile autotuning (numerically invisible: every tile accumulates K in the same
+    // order; split-K choices stay with the cost model)
+    struct Tuned { int key[10]; int tile; };
+    std::vector<Tuned> tuned;
+    std::vector<int> tuned_batches;
+    bool tuning = false;
 };
 
 namespace {
@@ -124,7 +138,16 @@ int upload(fr_handle* h, T** dst, const std::vector<T>& src) {
     return FR_OK;
 }
 
+void drop_graphs(fr_handle* h) {
+    if (h->graphs.empty()) return;
+    (void)hipDeviceSynchronize();  // no exec may be destroyed while a replay of it is in flight
+    for (auto& g : h->graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    h->graphs.clear();
+}
+
 void free_acts(fr_handle* h) {
+    drop_graphs(h);
     for (void* p : h->act_allocs) (void)hipFree(p);
     h->act_allocs.clear();
     for (auto& t : h->tensors) t.dev = nullptr;
@@ -134,6 +157,7 @@ void free_acts(fr_handle* h) {
 }
 
 void free_weights(fr_handle* h) {
+    drop_graphs(h);
     for (void* p : h->weight_allocs) (void)hipFree(p);
     h->weight_allocs.clear();
     h->convw.clear();
@@ -587,6 +611,7 @@ struct ProfScope {
     void start(const std::string& c, ConvArgs* ka = nullptr) {
         cls = c;
         if (!h->prof || (!h->prof_only.empty() && h->prof_only != cls)) return;
+        if (h->prof_seen++ % h->prof_stride != 0) return;
         a = prof_event(h);
         b = a ? prof_event(h) : nullptr;
         if (!b) { if (a) h->ev_free.push_back(a); a = nullptr; return; }
@@ -602,6 +627,59 @@ struct ProfScope {
 
 double conv_flops(const ConvArgs& a) { return 2.0 * (double)a.M * a.Cout * ((double)a.Cin * a.Kh * a.Kw); }
 
+bool autotune_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_AUTOTUNE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+void shape_key(const ConvArgs& a, int* k) {
+    const int v[10] = {a.M, a.Cout, a.Kpad, a.Cin, a.Kh, a.Kw, a.sh, a.sw, a.res ? 1 : 0, a.y2 ? 1 : 0};
+    for (int i = 0; i < 10; ++i) k[i] = v[i];
+}
+
+int find_tuned(const fr_handle* h, const ConvArgs& a) {
+    int k[10];
+    shape_key(a, k);
+    for (const auto& t : h->tuned)
+        if (std::memcmp(t.key, k, sizeof(k)) == 0) return t.tile;
+    return -1;
+}
+
+// Time every applicable tile on this conv (1 warm + 3 timed launches each, HIP events on `s`) and
+// remember the fastest for the shape.  Runs only inside the eager tuning pass of embed_locked.
+int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
+    int cand[16];
+    const int nc = conv_tile_candidates(a.Cout, cand);
+    hipEvent_t e0, e1;
+    FR_HIP_CHECK(hipEventCreate(&e0));
+    FR_HIP_CHECK(hipEventCreate(&e1));
+    int best = -1;
+    float best_ms = 1e30f;
+    a.split_k = 1;
+    a.partial = nullptr;
+    for (int c = 0; c < nc; ++c) {
+        a.tile = cand[c];
+        FR_HIP_CHECK(launch_conv(a, s));
+        FR_HIP_CHECK(hipEventRecord(e0, s));
+        for (int r = 0; r < 3; ++r) FR_HIP_CHECK(launch_conv(a, s));
+        FR_HIP_CHECK(hipEventRecord(e1, s));
+        FR_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        FR_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best_ms * 0.99f) { best_ms = ms; best = cand[c]; }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    fr_handle::Tuned t;
+    shape_key(a, t.key);
+    t.tile = best;
+    h->tuned.push_back(t);
+    return FR_OK;
+}
+
 int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     a.dbg = conv_dbg();
     ProfScope ps(h, s);
@@ -616,6 +694,15 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     }
     int tile, split;
     conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
+    if (split == 1 && autotune_enabled() && !conv_tile_forced()) {
+        int t = find_tuned(h, a);
+        if (t < 0 && h->tuning) {
+            int rc = tune_conv(h, a, s);
+            if (rc) return rc;
+            t = find_tuned(h, a);
+        }
+        if (t >= 0) tile = t;
+    }
     a.tile = tile;
     while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) split /= 2;
     if (split > 1) a.partial = h->partial;
@@ -741,6 +828,8 @@ void fr_destroy(fr_handle* h) {
     if (h->gallery) (void)hipFree(h->gallery);
     if (h->cand_s) (void)hipFree(h->cand_s);
     if (h->cand_i) (void)hipFree(h->cand_i);
+    drop_graphs(h);
+    if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     for (auto& r : h->prof_pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : h->ev_free) (void)hipEventDestroy(e);
     delete h;
@@ -785,6 +874,58 @@ int fr_reserve(fr_handle* h, int max_batch) {
 int fr_embed_dim(const fr_handle* h) { return h ? h->embed_dim : 0; }
 int fr_input_size(const fr_handle* h) { return h ? h->in_size : 0; }
 
+static bool graphs_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_GRAPH");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
+// The ~110-launch forward replayed as one hipGraph: captured on an internal non-blocking stream (the
+// caller's stream may be the legacy null stream, which cannot be captured) and launched on the
+// caller's stream.  Eager when profiling (per-launch events) or when capture fails.
+static int forward_graph(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
+    if (!graphs_enabled() || h->prof) return forward(h, in, in_fmt, B, out, flags, s);
+    fr_handle::GraphEnt* e = nullptr;
+    for (auto& g : h->graphs)
+        if (g.in == in && g.out == out && g.fmt == in_fmt && g.B == B && g.flags == flags) e = &g;
+    if (!e) {
+        if (h->graphs.size() >= 8) {  // evict the least recently used
+            auto lru = h->graphs.begin();
+            for (auto it = h->graphs.begin(); it != h->graphs.end(); ++it)
+                if (it->used < lru->used) lru = it;
+            if (lru->exec) {
+                (void)hipDeviceSynchronize();
+                (void)hipGraphExecDestroy(lru->exec);
+            }
+            h->graphs.erase(lru);
+        }
+        h->graphs.push_back({in, out, in_fmt, B, flags, nullptr, false, ++h->tick});
+        return forward(h, in, in_fmt, B, out, flags, s);  // first sighting: eager
+    }
+    e->used = ++h->tick;
+    if (e->no_graph) return forward(h, in, in_fmt, B, out, flags, s);
+    if (!e->exec) {
+        if (!h->cap_stream) FR_HIP_CHECK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+        FR_HIP_CHECK(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+        const int rc = forward(h, in, in_fmt, B, out, flags, h->cap_stream);
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(h->cap_stream, &g);
+        hipGraphExec_t x = nullptr;
+        if (rc == FR_OK && ec == hipSuccess && g && hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess) {
+            e->exec = x;
+        } else {
+            e->no_graph = true;
+            (void)hipGetLastError();
+        }
+        if (g) (void)hipGraphDestroy(g);
+        if (!e->exec) return forward(h, in, in_fmt, B, out, flags, s);
+    }
+    FR_HIP_CHECK(hipGraphLaunch(e->exec, s));
+    return FR_OK;
+}
+
 static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, float* out, int flags,
                         void* stream) {
     if (!h->loaded) { set_error("fr_embed: weights not loaded"); return FR_ERR_STATE; }
@@ -800,7 +941,18 @@ static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, 
         int rc = reserve(h, B);
         if (rc) return rc;
     }
-    return forward(h, in, in_fmt, B, out, flags, (hipStream_t)stream);
+    if (autotune_enabled() && !h->prof &&
+        std::find(h->tuned_batches.begin(), h->tuned_batches.end(), B) == h->tuned_batches.end()) {
+        // first call at this batch size: eager forward that times the tile candidates of every igemm
+        // shape on the way (results are exact: the last launch of each conv uses the chosen tile)
+        h->tuning = true;
+        const int rc = forward(h, in, in_fmt, B, out, flags, (hipStream_t)stream);
+        h->tuning = false;
+        if (rc) return rc;
+        h->tuned_batches.push_back(B);
+        return FR_OK;
+    }
+    return forward_graph(h, in, in_fmt, B, out, flags, (hipStream_t)stream);
 }
 
 int fr_embed(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, float* out, int flags, void* stream) {
@@ -909,6 +1061,17 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
         const int M = op.kind == OP_HEAD ? B : B * h->tensors[op.out].H * h->tensors[op.out].W;
         int tile, sp;
         conv_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
+        if (op.kind == OP_CONV) {
+            ConvArgs a{};
+            a.M = M; a.Cout = cw.Cout; a.Kpad = cw.Kpad; a.Cin = op.cin; a.Kh = op.kh; a.Kw = op.kw;
+            a.sh = op.sh; a.sw = op.sw; a.H = h->tensors[op.in].H; a.W = h->tensors[op.in].W;
+            a.Ho = h->tensors[op.out].H; a.Wo = h->tensors[op.out].W; a.ph = op.ph; a.pw = op.pw;
+            a.res = op.res >= 0 ? (const bf16_t*)1 : nullptr;
+            a.y2 = op.out2 >= 0 ? (bf16_t*)1 : nullptr;
+            int TH, variant;
+            if (band_enabled() && band_plan(a, &TH, &variant) && variant >= 3) tile = FR_TILE_BAND;
+            else if (sp == 1 && autotune_enabled() && !conv_tile_forced() && find_tuned(h, a) >= 0) tile = find_tuned(h, a);
+        }
         const std::string nm = op.kind == OP_HEAD ? "head" : h->tensors[op.out].name;
         out += (op.kind == OP_HEAD ? "head " : "conv ") + std::to_string(M) + " " + std::to_string(cw.Cout) + " " +
                std::to_string(cw.K) + " " + std::to_string(cw.Kpad) + " " + std::to_string(tile) + " " +
@@ -930,7 +1093,9 @@ int fr_prof_enable(fr_handle* h, int on) {
     }
     h->prof_pending.clear();
     h->prof_acc.clear();
-    h->prof = on != 0;
+    h->prof = on > 0;
+    h->prof_stride = on > 0 ? on : 1;
+    h->prof_seen = 0;
     return FR_OK;
 }
 
@@ -1026,7 +1191,7 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         return FR_OK;
     }
     if (d->tile > 0) {
-        if (d->tile > 7) { set_error("fr_op_conv2d: bad tile"); return FR_ERR_ARG; }
+        if (d->tile > NUM_TILE_IDS) { set_error("fr_op_conv2d: bad tile"); return FR_ERR_ARG; }
         a.tile = d->tile - 1;
     } else {
         int tile, sp;

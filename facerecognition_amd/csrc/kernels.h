@@ -7,7 +7,8 @@ namespace fr {
 
 // Conv tile variants (BM pixels x BN channels, 4 waves each).
 enum { TILE_128x128 = 0, TILE_256x64 = 1, TILE_128x64 = 2, TILE_64x128 = 3,
-       TILE_128x128_S3 = 4, TILE_256x128 = 5, TILE_128x256 = 6 };  // *_S3 / 8-wave tiles: 3-stage DMA ring
+       TILE_128x128_S3 = 4, TILE_256x128 = 5, TILE_128x256 = 6,  // *_S3 / 8-wave tiles: 3-stage DMA ring
+       TILE_128x64_S3 = 8, TILE_64x128_S3 = 9, NUM_TILE_IDS = 10 };   // (7 = the band kernel's id in the ABI)
 
 // Implicit-GEMM convolution, NHWC bf16 in/out, f32 accumulate, fused epilogue.
 // GEMM view: M = B*Ho*Wo output pixels, N = Cout, K = Kh*Kw*Cin (c fastest).
@@ -28,6 +29,8 @@ struct ConvArgs {
 };
 
 // Choose tile variant and split-K factor for a GEMM of M x Cout x Kpad.
+bool conv_tile_forced();
+int conv_tile_candidates(int Cout, int* out);
 void conv_plan(int M, int Cout, int Kpad, int* tile, int* split);
 int conv_tile_bm(int tile);
 int conv_tile_bn(int tile);

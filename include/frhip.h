@@ -150,6 +150,8 @@ typedef struct fr_conv_desc {
 #define FR_TILE_256x128 5    /* 8 waves, 3-stage ring */
 #define FR_TILE_128x256 6    /* 8 waves, 3-stage ring */
 #define FR_TILE_BAND 7       /* row-band direct 3x3/s1/p1 kernel (conv_band.hip); auto-selected when applicable */
+#define FR_TILE_128x64_S3 8  /* 3-stage DMA ring, 2 blocks/CU */
+#define FR_TILE_64x128_S3 9  /* 3-stage DMA ring, 2 blocks/CU */
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 
@@ -175,8 +177,10 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * (e.g. "backbone.layer2.0", "layer3.7.prelu", "model.repeat_1.2"); "" for internal buffers. */
 /* ---- measurement: per-kernel-class timing with HIP events (bench.py roofline) --------------
  * No reference counterpart (the reference has no profiler hook); used by bench.py to time the
- * dominant kernel live, on the stream it is launched on.  fr_prof_enable(h, 1) resets and starts
- * recording an event pair around every launch of fr_embed; fr_prof_collect() waits for the pending
+ * dominant kernel live, on the stream it is launched on.  fr_prof_enable(h, n) (n >= 1) resets and
+ * starts recording an event pair around every n-th launch of fr_embed (conv launches are stamped by
+ * their dispatch via hipExtLaunchKernel; n > 1 samples to keep the overhead small); n = 0 stops.
+ * Profiled forwards launch eagerly (no hipGraph replay).  fr_prof_collect() waits for the pending
  * events and returns the number of kernel classes; fr_prof_get() reads class i: name (matches the
  * kernel instantiation), summed milliseconds, launch count, summed algorithmic FLOPs (2*M*N*K). */
 int fr_prof_enable(fr_handle* h, int on);

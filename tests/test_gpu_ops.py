@@ -61,7 +61,7 @@ def test_conv_parity(gpu, case, dtype):
     _close(y, ref, tol=1e-2 if dtype == "bf16" else 2e-3)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 8, 9])
 @pytest.mark.parametrize("case", [(2, 14, 14, 256, 256, 3, 3, (1, 1), (1, 1)), (2, 19, 19, 80, 192, 3, 3, (1, 1), (0, 0)),
                                   (3, 9, 9, 64, 64, 1, 1, (2, 2), (0, 0))])
 def test_conv_every_tile(gpu, case, tile):

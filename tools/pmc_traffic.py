@@ -28,6 +28,8 @@ def class_pattern(cls: str, f16: bool) -> str:
     m = re.match(r"conv3x3_band W(\d+) v(\d+)", cls)
     if m:
         W, v = int(m.group(1)), int(m.group(2))
+        if v == 3:  # software-pipelined 4-wave variant
+            return f"conv3x3_bandp_kernel<{str(f16).lower()}, {W}, {BAND_TH[W]}, 2, 2, 7, 8>"
         wm, wn, fm, fn = BAND_VARIANT[v]
         return f"conv3x3_band_kernel<{str(f16).lower()}, {W}, {BAND_TH[W]}, {wm}, {wn}, {fm}, {fn},"
     raise KeyError(cls)
@@ -53,7 +55,7 @@ def main():
     ap.add_argument("--arch", default="iresnet100")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--classes", nargs="*", default=["conv3x3_band W14 v0"])
+    ap.add_argument("--classes", nargs="*", default=["conv3x3_band W14 v3"])
     ap.add_argument("--flops-per-launch", type=float, default=2.0 * 50176 * 256 * 2304,
                     help="algorithmic FLOPs per launch of the first class (intensity report)")
     a = ap.parse_args()
