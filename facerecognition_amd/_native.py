@@ -38,6 +38,7 @@ class FrConvDesc(ctypes.Structure):
         ("y2", c_void_p), ("Cy2", c_int), ("y2_off", c_int), ("aff_s", c_void_p), ("aff_b", c_void_p),
         ("Ho", c_int), ("Wo", c_int),
         ("split_k", c_int), ("partial", c_void_p), ("dtype", c_int), ("tile", c_int),
+        ("bias9", c_void_p),
     ]
 
 

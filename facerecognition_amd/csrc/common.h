@@ -124,6 +124,14 @@ struct Num<true> {  // f16
     }
 };
 
+// Border class of output pixel (oh, ow) for a bias9 table (3x3 / stride 1 / pad 1 with the input BN
+// folded into the weights): 3*rc + cc, rc = 0 top row, 1 interior, 2 bottom row (cc for columns).
+__device__ __forceinline__ int border_class(int oh, int ow, int Ho, int Wo) {
+    const int rc = oh == 0 ? 0 : (oh == Ho - 1 ? 2 : 1);
+    const int cc = ow == 0 ? 0 : (ow == Wo - 1 ? 2 : 1);
+    return 3 * rc + cc;
+}
+
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5, "XCD swizzle must be
 // bijective"): blocks that share an XCD (raw id ≡ mod 8) get consecutive logical ids.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

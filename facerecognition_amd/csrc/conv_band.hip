@@ -33,6 +33,12 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const char* l
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
 }
 
+// ... with a wave-uniform byte offset in soffset (memory address only; the instruction's immediate
+// offset would also shift the LDS destination)
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, soff, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -70,7 +76,7 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& p, const f32x4_t (
         const bool nv = n_raw < p.Cout;
         const int n = nv ? n_raw : 0;
         float4 bb = make_float4(0.f, 0.f, 0.f, 0.f), sl = bb, as = bb, ab = bb;
-        if (p.bias) bb = *(const float4*)(p.bias + n);
+        if (p.bias && !p.bias9) bb = *(const float4*)(p.bias + n);
         if (p.act == 2) sl = *(const float4*)(p.slope + n);
         if (p.y2) { as = *(const float4*)(p.aff_s + n); ab = *(const float4*)(p.aff_b + n); }
         uint2 rr[FM];
@@ -82,6 +88,11 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& p, const f32x4_t (
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
             float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
+            if (p.bias9) {
+                const int po = pix_off[j], oh = (int)((pix0 / W) % p.Ho) + po / W;
+                const float4 b9 = *(const float4*)(p.bias9 + (size_t)border_class(oh, po % W, p.Ho, W) * p.Npad + n);
+                v[0] += b9.x; v[1] += b9.y; v[2] += b9.z; v[3] += b9.w;
+            }
             if (p.res) {
                 float f[8];
                 T::unpack8(make_uint4(rr[j].x, rr[j].y, 0, 0), f);
@@ -112,11 +123,11 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& p, const f32x4_t (
     }
 }
 
-// LDS-staged epilogue for the 4-wave band kernel: two passes (one per wn channel half of 16*FN
-// channels); the owning waves park their f32 accumulators in LDS (rows of 16*FN floats, padded by 16 B
-// against bank conflicts), then all threads emit coalesced 8-channel groups: 16-B loads of the
-// residual (issued before the LDS round trip), 16-B stores of y / y2, per-channel vectors loaded once
-// per thread (its channel group is fixed).  Replaces 8-B stores scattered over 16 pixels.
+// LDS-staged epilogue for the 4-wave band kernel.  Passes over (channel half wn, row group mp): the
+// owning waves park their f32 accumulators in LDS (rows of 16*FN floats, padded by 16 B against bank
+// conflicts), then all threads emit coalesced 8-channel groups: 16-B loads of the residual (issued
+// before the LDS round trip), 16-B stores of y / y2, per-channel vectors loaded once per pass (a
+// thread's channel group is fixed).  Row groups (MP > 1) keep the staged rows within the LDS.
 template <class T, int W, int Wp, int Mv, int FM, int FN, int WM, int WN>
 __device__ __forceinline__ void band_epilogue_lds(const ConvArgs& p, const f32x4_t (&acc)[FN][FM], char* smem,
                                                   int tid, int lane, int wm, int wn, size_t pix0, int n0) {
@@ -125,14 +136,18 @@ __device__ __forceinline__ void band_epilogue_lds(const ConvArgs& p, const f32x4
     constexpr int G = CH / 8;                // 8-channel groups per row
     constexpr int ROWS = 16 * FM * WM;       // MFMA rows (pixel positions incl. the discarded columns)
     constexpr int LD = CH * 4 + 16;          // bytes per LDS row
-    static_assert(ROWS * LD <= 160 * 1024, "epilogue staging fits LDS");
+    constexpr int MP = ROWS * LD <= 160 * 1024 ? 1 : 2;  // row groups
+    constexpr int GR = ROWS / MP;            // staged rows per pass
+    static_assert(GR * LD <= 160 * 1024 && WM % MP == 0, "epilogue staging fits LDS");
     static_assert(NT % G == 0, "fixed channel group per thread");
     constexpr int RS = NT / G;               // rows per sweep
-    constexpr int IT = (Mv + RS - 1) / RS;   // sweeps over the valid row range
+    constexpr int IT = (GR + RS - 1) / RS;   // sweeps over a row group
     const int g = tid % G, r0 = tid / G;
 #pragma unroll 1
-    for (int pass = 0; pass < WN; ++pass) {
-        const int n = n0 + pass * CH + 8 * g;
+    for (int pass = 0; pass < WN * MP; ++pass) {
+        const int pn = pass / MP, mp = pass % MP;
+        const int mbase = mp * GR;
+        const int n = n0 + pn * CH + 8 * g;
         const bool nv = n < p.Cout;
         const int nn = nv ? n : 0;
         // residual of this thread's rows first: its latency overlaps the LDS round trip
@@ -141,14 +156,14 @@ __device__ __forceinline__ void band_epilogue_lds(const ConvArgs& p, const f32x4
         bool ok[IT];
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int m = r0 + it * RS;
+            const int m = mbase + r0 + it * RS;
             const int r = m / Wp, c = m - r * Wp;
-            ok[it] = m < Mv && c < W && nv;
+            ok[it] = r0 + it * RS < GR && m < Mv && c < W && nv;
             pixo[it] = ok[it] ? r * W + c : 0;
             if (p.res) rr[it] = *(const uint4*)(p.res + (pix0 + pixo[it]) * p.Cres + p.res_off + nn);
         }
         float b8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s8[8], as8[8], ab8[8];
-        if (p.bias) {
+        if (p.bias && !p.bias9) {
             const float4 x0 = *(const float4*)(p.bias + nn), x1 = *(const float4*)(p.bias + nn + 4);
             b8[0] = x0.x; b8[1] = x0.y; b8[2] = x0.z; b8[3] = x0.w; b8[4] = x1.x; b8[5] = x1.y; b8[6] = x1.z; b8[7] = x1.w;
         }
@@ -162,24 +177,31 @@ __device__ __forceinline__ void band_epilogue_lds(const ConvArgs& p, const f32x4
             as8[0] = x0.x; as8[1] = x0.y; as8[2] = x0.z; as8[3] = x0.w; as8[4] = x1.x; as8[5] = x1.y; as8[6] = x1.z; as8[7] = x1.w;
             ab8[0] = y0.x; ab8[1] = y0.y; ab8[2] = y0.z; ab8[3] = y0.w; ab8[4] = y1.x; ab8[5] = y1.y; ab8[6] = y1.z; ab8[7] = y1.w;
         }
-        if (wn == pass) {
+        if (wn == pn && wm / (WM / MP) == mp) {
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
                 for (int j = 0; j < FM; ++j) {
-                    const int m = 16 * (wm * FM + j) + (lane & 15);
+                    const int m = 16 * (wm * FM + j) + (lane & 15) - mbase;
                     *(f32x4_t*)(smem + m * LD + (16 * i + 4 * (lane >> 4)) * 4) = acc[i][j];
                 }
         }
         __syncthreads();
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int m = r0 + it * RS;
-            if (m < ROWS) {
-                const float4 v0 = *(const float4*)(smem + m * LD + g * 32);
-                const float4 v1 = *(const float4*)(smem + m * LD + g * 32 + 16);
+            const int ml = r0 + it * RS;
+            if (ml < GR) {
+                const float4 v0 = *(const float4*)(smem + ml * LD + g * 32);
+                const float4 v1 = *(const float4*)(smem + ml * LD + g * 32 + 16);
                 float v[8] = {v0.x + b8[0], v0.y + b8[1], v0.z + b8[2], v0.w + b8[3],
                               v1.x + b8[4], v1.y + b8[5], v1.z + b8[6], v1.w + b8[7]};
+                if (p.bias9) {
+                    const int po = pixo[it], oh = (int)((pix0 / W) % p.Ho) + po / W;
+                    const float* bb = p.bias9 + (size_t)border_class(oh, po % W, p.Ho, W) * p.Npad + nn;
+                    const float4 x0 = *(const float4*)bb, x1 = *(const float4*)(bb + 4);
+                    v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
+                    v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+                }
                 if (p.res) {
                     float f[8];
                     T::unpack8(rr[it], f);
@@ -403,8 +425,9 @@ __device__ __forceinline__ void wait_vmn() {
 // so LDS reads always overlap MFMAs, the weight ring keeps two slices in flight across the barrier,
 // and every DMA count is static (the last steps re-fetch the final slice / patch into free buffers
 // instead of skipping, keeping the vmcnt arithmetic compile-time).
-template <bool F16, int W, int TH, int WM, int WN, int FM, int FN>
+template <bool F16, int W, int TH, int WM, int WN, int FM, int FN, int WS>
 __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs p, int ntn) {
+    static_assert(WS == 2 || WS == 3, "weight ring depth");
     constexpr int NW = WM * WN;
     constexpr int BN = 16 * FN * WN;
     constexpr int Wp = W + 2;
@@ -416,10 +439,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
     constexpr int PI = 8 * NPB;
     static_assert(PI % NW == 0, "patch DMA must split evenly over waves");
     constexpr int NPW = PI / NW;
+    static_assert(NPW <= 2 * FN && BN / 8 / NW <= 2 * FN, "at most two DMA pieces per MFMA group");
     constexpr int WSL = BN * 128;
     constexpr int NWI = BN / 8 / NW;
     static_assert(NWI * 8 * NW == BN, "weight slice rows must split evenly over waves");
-    static_assert(NWI + 2 * NPW <= 63, "vmcnt range");
+    static_assert((WS - 2) * NWI + 2 * NPW <= 63, "vmcnt range");
     constexpr int Mv = TH * Wp - 2;
     static_assert(16 * FM * WM >= Mv, "MFMA rows must cover the band");
     typedef Num<F16> T;
@@ -442,22 +466,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
     const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
 
-    uint32_t psrc[NPW];
+    // Patch DMA: wave w owns position blocks w*NBW .. w*NBW+NBW-1 (64 positions each) of all 8 channel
+    // planes; a piece's plane only changes the source channel offset, carried in soffset.
+    static_assert(NPB % NW == 0, "patch position blocks must split evenly over waves");
+    constexpr int NBW = NPB / NW;
+    uint32_t psrc[NBW];
 #pragma unroll
-    for (int u = 0; u < NPW; ++u) {
-        const int q = wave + NW * u;
-        const int c = q / NPB, pos = 64 * (q - c * NPB) + lane;
+    for (int u = 0; u < NBW; ++u) {
+        const int pos = 64 * (wave * NBW + u) + lane;
         const int ih = oh0 - 1 + pos / Wp, iw = pos % Wp - 1;
         const bool ok = pos < P && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-        psrc[u] = ok ? (uint32_t)((((b * H + ih) * W + iw) * p.Cx + p.x_off + 8 * c) * 2) : OOB;
+        psrc[u] = ok ? (uint32_t)((((b * H + ih) * W + iw) * p.Cx + p.x_off) * 2) : OOB;
     }
-    uint32_t woff[NWI];
-#pragma unroll
-    for (int u = 0; u < NWI; ++u) {
-        const int row = 8 * (wave + NW * u) + (lane >> 3);
-        const int cl = (lane & 7) ^ ((row >> 1) & 7);
-        woff[u] = (uint32_t)(((n0 + row) * p.Kpad + 8 * cl) * 2);
-    }
+    // Weight DMA: piece u covers rows 8*(wave + NW*u) + lane/8 -> a constant row stride per piece.
+    const int wrow0 = 8 * wave + (lane >> 3);
+    const uint32_t woff0 = (uint32_t)(((n0 + wrow0) * p.Kpad + 8 * ((lane & 7) ^ ((wrow0 >> 1) & 7))) * 2);
+    const uint32_t wstride = (uint32_t)(8 * NW * p.Kpad * 2);
     int aoff[FM];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
@@ -473,19 +497,24 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
     }
 
     const int dbg = p.dbg;  // timing-only experiment switches (FR_CONV_DBG), 0 in production
+    // one 1-KiB DMA piece of the next chunk's patch / of a weight slice (u < NPW / NWI); the pieces are
+    // issued one per 7-MFMA group inside the k-halves so their issue cost hides behind MFMAs
+    auto patch_piece = [&](int chunk, int pb, int u) {
+        const int c = u % 8, blk = u / 8;
+        dma16s(xr, smem + pb * PATCH + c * PLANE + (wave * NBW + blk) * 1024, psrc[blk],
+               (uint32_t)(chunk * 64 * 2 + c * 16));
+    };
+    auto w_piece = [&](int chunk, int tap, int wb, int u) {
+        const uint32_t kadd = (uint32_t)((tap * p.Cin + chunk * 64) * 2);
+        dma16s(wr, smem + 2 * PATCH + wb * WSL + (wave + NW * u) * 1024, woff0, kadd + u * wstride);
+    };
     auto issue_patch = [&](int chunk, int pb) {
-        if ((dbg & 2) && chunk > 0) return;
-        const uint32_t cadd = (uint32_t)(chunk * 64 * 2);
-        char* dst = smem + pb * PATCH;
 #pragma unroll
-        for (int u = 0; u < NPW; ++u) dma16(xr, dst + (wave + NW * u) * 1024, psrc[u] == OOB ? OOB : psrc[u] + cadd);
+        for (int u = 0; u < NPW; ++u) patch_piece(chunk, pb, u);
     };
     auto issue_w = [&](int chunk, int tap, int wb) {
-        if ((dbg & 1) && (chunk > 0 || tap > 1)) return;
-        const uint32_t kadd = (uint32_t)((tap * p.Cin + chunk * 64) * 2);
-        char* dst = smem + 2 * PATCH + wb * WSL;
 #pragma unroll
-        for (int u = 0; u < NWI; ++u) dma16(wr, dst + (wave + NW * u) * 1024, woff[u] + kadd);
+        for (int u = 0; u < NWI; ++u) w_piece(chunk, tap, wb, u);
     };
 
     f32x4_t acc[FN][FM];
@@ -498,6 +527,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
     // weight fragments is refilled in place for the next k-half right after its last MFMA use.  Every
     // LDS read is (per-lane base) + (compile-time immediate) after the unrolling below.
     frag wf[FN], pA[FM], pB[FM];
+    // ring slot of step s = s % WS: with WS = 3 this is tap % 3 (9 % 3 == 0, compile-time); with
+    // WS = 2 it is (chunk + tap) & 1 (runtime parity, an add per weight read)
     auto wread = [&](frag& f, int i, int wslot, int kk) {
         f = *(const frag*)(smem + 2 * PATCH + wslot * WSL + (kk ? boff1[i] : boff[i]));
     };
@@ -509,40 +540,43 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
     };
     // one k-half: MFMAs on (wf, cur) while the next k-half's patch fragments land in `nxt` and each wf[i]
     // is reloaded (from wslot_n / kk_n) after its 7 MFMAs; `has_next` false on the very last half
+    // one k-half: MFMAs on (wf, cur) while the next k-half's patch fragments land in `nxt`, each wf[i] is
+    // reloaded (wslot_n / kk_n) after its 7 MFMAs, and DMA piece i (dma(i), i < n_dma) is issued after
+    // group i.  Program order keeps LDS reads before the DMAs that may overwrite LDS; the sched-group
+    // pattern places one LDS read per MFMA gap in group 0 and one read + one DMA after every group.
     auto half_step = [&](frag (&cur)[FM], frag (&nxt)[FM], bool has_next, int pbuf_n, int wslot_n, int kk_n,
-                         int tap_n, int n_dma) {
+                         int tap_n, int n_dma, auto&& dma) {
         if (has_next) pread(nxt, pbuf_n, kk_n, tap_n);
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
             if (has_next) wread(wf[i], i, wslot_n, kk_n);
+#pragma unroll
+            for (int d = 0; d < (NPW > FN || NWI > FN ? 2 : 1); ++d)
+                if (i + d * FN < n_dma) dma(i + d * FN);
         }
-        // issue order: the step's DMAs, then one patch read per MFMA gap, then one weight refill after
-        // each weight fragment's 7 MFMAs (its last use)
-        if (n_dma == NWI + NPW) __builtin_amdgcn_sched_group_barrier(0x020, NWI + NPW, 0);
-        else if (n_dma == NWI) __builtin_amdgcn_sched_group_barrier(0x020, NWI, 0);
-        if (has_next) {
 #pragma unroll
-            for (int q = 0; q < FM; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int i = 0; i < FN; ++i) {
+            if (i == 0 && has_next) {
 #pragma unroll
-            for (int i = 1; i < FN; ++i) {
+                for (int q = 0; q < FM; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+            } else {
                 __builtin_amdgcn_sched_group_barrier(0x008, FM, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
-        } else {
-            __builtin_amdgcn_sched_group_barrier(0x008, FN * FM, 0);
+            if (has_next) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            if (i + FN < n_dma) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+            else if (i < n_dma) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
         }
     };
 
     const int nchunk = p.Cin / 64;
     issue_patch(0, 0);
-    issue_w(0, 0, 0);
-    issue_w(0, 1, 1);
+#pragma unroll
+    for (int t = 0; t < WS; ++t) issue_w(0, t, t);
     {  // warm this XCD's L2 with a 1/32 share of the block's weight panel (see conv3x3_band_kernel)
         const uint32_t panel = (uint32_t)BN * p.Kpad * 2;
         const uint32_t share = (panel + 31) / 32;
@@ -560,30 +594,50 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
 #pragma unroll
     for (int i = 0; i < FN; ++i) wread(wf[i], i, 0, 0);
 
-    for (int chunk = 0; chunk < nchunk; ++chunk) {
-        const int pb = chunk & 1;
-        const bool last_chunk = chunk + 1 == nchunk;
+    // one K-step (chunk, tap): slot / slot_n = ring slots of this and the next step
+    auto kstep = [&](int chunk, int tap, int pb, bool last_chunk, int slot, int slot_n) {
+        // k-half 0: prefetch k-half 1 of this step; at tap 0 the next chunk's patch DMA rides along
+        // (the last chunk re-fetches its own patch into the free buffer: static vmcnt counts)
+        const int pch = last_chunk ? chunk : chunk + 1;
+        half_step(pA, pB, true, pb, slot, 1, tap, tap == 0 ? NPW : 0,
+                  [&](int u) { patch_piece(pch, pb ^ 1, u); });
+        // slice step+1 (and, before a new chunk, its patch: older) has landed for this wave.
+        // Younger: slices step+2 .. step+WS-1 and the patch pieces issued in the last WS-1 steps
+        // (at tap 0 of this chunk).
+        if (WS == 3) {
+            if (tap == 0 || tap == 1) wait_vmn<(WS - 2) * NWI + NPW>();
+            else wait_vmn<(WS - 2) * NWI>();
+        } else {
+            if (tap == 0) wait_vmn<NPW>();
+            else wait_vmn<0>();
+        }
+        if (dbg & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        // k-half 1: prefetch k-half 0 of the next step; this step's slot (read-complete before the
+        // barrier) receives slice step+WS (clamped to the last slice at the tail)
+        const bool nxt = tap < 8 || !last_chunk;
+        const int tw = tap + WS < 9 ? tap + WS : tap + WS - 9;
+        const int cw = tap + WS < 9 ? chunk : chunk + 1;
+        const bool okw = cw < nchunk;
+        half_step(pB, pA, nxt, tap < 8 ? pb : pb ^ 1, slot_n, 0, tap < 8 ? tap + 1 : 0, NWI,
+                  [&](int u) { w_piece(okw ? cw : nchunk - 1, okw ? tw : 8, slot, u); });
+    };
+    if constexpr (WS == 3) {
+        // ring slot of step (chunk, tap) = tap % 3 because 9 % 3 == 0
+        for (int chunk = 0; chunk < nchunk; ++chunk) {
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            // ring slot of step (chunk, tap) = tap % 3 because 9 % 3 == 0
-            {
-                const int t2 = tap + 2 < 9 ? tap + 2 : tap - 7;
-                const int c2n = tap + 2 < 9 ? chunk : chunk + 1;
-                const bool ok = c2n < nchunk;
-                issue_w(ok ? c2n : nchunk - 1, ok ? t2 : 8, (tap + 2) % 3);  // static count at the tail
-            }
-            if (tap == 0) issue_patch(last_chunk ? chunk : chunk + 1, pb ^ 1);
-            // k-half 0 (fragments in pA / wf); prefetch k-half 1 of the same step
-            half_step(pA, pB, true, pb, tap % 3, 1, tap, NWI + (tap == 0 ? NPW : 0));
-            // slice step+1 (and, before a new chunk, its patch: older) has landed for this wave;
-            // younger: slice step+2 (+ the patch issued at tap 0 / at the previous step's tap 0)
-            if (tap == 0 || tap == 1) wait_vmn<NWI + NPW>();
-            else wait_vmn<NWI>();
-            if (dbg & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            // k-half 1; prefetch k-half 0 of the next step
-            const bool nxt = tap < 8 || !last_chunk;
-            half_step(pB, pA, nxt, tap < 8 ? pb : pb ^ 1, (tap + 1) % 3, 0, tap < 8 ? tap + 1 : 0, 0);
+            for (int tap = 0; tap < 9; ++tap) kstep(chunk, tap, chunk & 1, chunk + 1 == nchunk, tap % 3, (tap + 1) % 3);
+        }
+    } else {
+        // two chunks (18 steps) per iteration: patch buffer and ring slot are compile-time (Cin % 128 == 0)
+        for (int c2 = 0; c2 < nchunk; c2 += 2) {
+#pragma unroll
+            for (int half = 0; half < 2; ++half)
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) {
+                    const int st = half * 9 + tap;
+                    kstep(c2 + half, tap, half, c2 + half + 1 == nchunk, st & 1, (st + 1) & 1);
+                }
         }
     }
     wait_vmn<0>();  // the tail re-fetches must land before the workgroup's LDS is released
@@ -602,14 +656,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
                                                      (size_t)(b * H + oh0) * W, n0);
 }
 
-template <bool F16, int W, int TH, int FN>
+template <bool F16, int W, int TH, int WM, int WN, int FM, int FN, int WS>
 static hipError_t launch_bandp_k(const ConvArgs& a, hipStream_t s) {
-    constexpr int WM = 2, WN = 2, FM = 7;
     constexpr int BN = 16 * FN * WN;
     constexpr int P64 = ((TH + 2) * (W + 2) + 63) / 64 * 64;
-    constexpr int LDS = 2 * 8 * P64 * 16 + 3 * BN * 128;
+    constexpr int LDS = 2 * 8 * P64 * 16 + WS * BN * 128;
     static_assert(LDS <= 160 * 1024, "band LDS budget");
-    auto k = conv3x3_bandp_kernel<F16, W, TH, WM, WN, FM, FN>;
+    auto k = conv3x3_bandp_kernel<F16, W, TH, WM, WN, FM, FN, WS>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -677,8 +730,9 @@ bool band_plan(const ConvArgs& a, int* cfg, int* variant) {
     else if (a.W == 112 && a.H % 2 == 0) c = 3;
     else return false;
     if (c == 0 && v == 2) return false;  // 14x14x64: 196 rows of a 256-row tile, not worth it
-    // software-pipelined 4-wave variant 3 = 14x14 x 256 channels (a 28x28 x 128 instance of the same
-    // template measured 612 TFLOP/s vs 648 for the igemm 128x64 tile on layer2, so it is not used)
+    // software-pipelined 4-wave variant 3 = 14x14 x 256 channels.  (A 28x28 instance -- 14-row bands,
+    // 4x1 waves, 2-slot ring -- measured 610 TFLOP/s on layer2 vs 692 for the igemm 128x128 tile:
+    // half-length blocks in two rounds pay the prologue/epilogue twice; not instantiated.)
     if (!band_legacy() && c == 0 && v == 0) v = 3;
     if ((c == 2 || c == 3) && v != 2) return false;  // 4x58 / 2x114 rows exceed the 224-row variants
     *cfg = c;
@@ -688,7 +742,8 @@ bool band_plan(const ConvArgs& a, int* cfg, int* variant) {
 
 template <bool F16>
 static hipError_t launch_band_t(const ConvArgs& a, int c, int v, hipStream_t s) {
-    if (v == 3) return c == 0 ? launch_bandp_k<F16, 14, 14, 8>(a, s) : hipErrorInvalidValue;
+    // 3: 14x14 images, 2x2 waves of 112 rows x 128 channels, 3-slot weight ring
+    if (v == 3) return c == 0 ? launch_bandp_k<F16, 14, 14, 2, 2, 7, 8, 3>(a, s) : hipErrorInvalidValue;
     switch (c * 3 + v) {
         case 0: return launch_band_k<F16, 14, 14, 0, 3>(a, s);
         case 1: return launch_band_k<F16, 14, 14, 1, 3>(a, s);

@@ -42,6 +42,7 @@ struct DevConvW {
     float* slope = nullptr;
     float* aff_s = nullptr;
     float* aff_b = nullptr;
+    float* bias9 = nullptr;  // [9][Npad] border-class bias (input BN folded into a 3x3/s1/p1 conv)
     int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0;
 };
 
@@ -293,6 +294,20 @@ struct Builder {
         bias.resize(cw.Npad, 0.f);
         if ((rc = upload(h, &cw.w, packed))) return -1;
         if ((rc = upload(h, &cw.bias, bias))) return -1;
+        if (names.size() == 1) {
+            const HostT* b9 = find(names[0] + ".b9");
+            if (b9) {
+                if (b9->dims.size() != 2 || b9->dims[0] != 9 || b9->dims[1] != cout || kh != 3 || kw != 3) {
+                    set_error("weights: mis-shaped " + names[0] + ".b9 (expects [9, Cout] on a 3x3 conv)");
+                    rc = FR_ERR_WEIGHTS;
+                    return -1;
+                }
+                std::vector<float> t9((size_t)9 * cw.Npad, 0.f);
+                for (int c = 0; c < 9; ++c)
+                    for (int o = 0; o < cout; ++o) t9[(size_t)c * cw.Npad + o] = b9->v[(size_t)c * cout + o];
+                if ((rc = upload(h, &cw.bias9, t9))) return -1;
+            }
+        }
         if (act == 2) {
             slope.resize(cw.Npad, 0.f);
             if ((rc = upload(h, &cw.slope, slope))) return -1;
@@ -382,9 +397,12 @@ void build_iresnet100(Builder& b) {
     h->in_size = 112;
     const int in = b.tensor(112, 112, 8);
     h->ops.push_back(Op{OP_PRE, -1, 0, 0, in});
-    int x = b.tensor(112, 112, 64, "prelu"), xb = b.tensor(112, 112, 64, L(1, 0) + ".bn1");
+    // Each block's pre-conv bn1 is folded into its conv1 (weights scaled per input channel, the shift in
+    // a border-class bias table .b9: weights.fold_state_dict), so conv1 reads the previous block's output
+    // directly and no producer writes a second (bn1) output.
+    int x = b.tensor(112, 112, 64, "prelu");
     b.stem = true;
-    b.conv({"conv1"}, in, 0, 8, x, 0, 3, 3, 1, 1, 1, 1, 2, -1, 0, xb, L(1, 0) + ".bn1");
+    b.conv({"conv1"}, in, 0, 8, x, 0, 3, 3, 1, 1, 1, 1, 2);
     const int planes[4] = {64, 128, 256, 512}, nblk[4] = {3, 13, 30, 3};
     int H = 112, C = 64;
     for (int l = 0; l < 4; ++l) {
@@ -393,20 +411,15 @@ void build_iresnet100(Builder& b) {
             const std::string pre = L(l + 1, i);
             const int Hin = i == 0 ? H : Ho, st = i == 0 ? 2 : 1;
             const int hmid = b.tensor(Hin, Hin, P, pre + ".prelu");
-            b.conv({pre + ".conv1"}, xb, 0, C, hmid, 0, 3, 3, 1, 1, 1, 1, 2);
+            b.conv({pre + ".conv1"}, x, 0, C, hmid, 0, 3, 3, 1, 1, 1, 1, 2);
             int res = x;
             if (i == 0) {
                 res = b.tensor(Ho, Ho, P, pre + ".downsample");
                 b.conv({pre + ".downsample"}, x, 0, C, res, 0, 1, 1, 2, 2, 0, 0, 0);
             }
-            std::string next;
-            if (i + 1 < nblk[l]) next = L(l + 1, i + 1) + ".bn1";
-            else if (l + 1 < 4) next = L(l + 2, 0) + ".bn1";
             const int y = b.tensor(Ho, Ho, P, pre);
-            const int yb = next.empty() ? -1 : b.tensor(Ho, Ho, P, next);
-            b.conv({pre + ".conv2"}, hmid, 0, P, y, 0, 3, 3, st, st, 1, 1, 0, res, 0, yb, next);
+            b.conv({pre + ".conv2"}, hmid, 0, P, y, 0, 3, 3, st, st, 1, 1, 0, res, 0);
             x = y;
-            xb = yb;
             C = P;
         }
         H = Ho;
@@ -734,7 +747,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.w = cw.w; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
                 a.K = cw.K; a.Kpad = cw.Kpad;
                 a.Ho = to.H; a.Wo = to.W; a.M = B * to.H * to.W; a.Cout = cw.Cout; a.Npad = cw.Npad;
-                a.bias = cw.bias; a.slope = cw.slope; a.act = op.act;
+                a.bias = cw.bias; a.slope = cw.slope; a.act = op.act; a.bias9 = cw.bias9;
                 if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
                 a.y = to.dev; a.Cy = to.C; a.y_off = op.out_off;
                 if (op.out2 >= 0) {
@@ -1179,7 +1192,7 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
     a.Ho = d->Ho ? d->Ho : (d->H + 2 * d->pad_h - d->Kh) / d->stride_h + 1;
     a.Wo = d->Wo ? d->Wo : (d->W + 2 * d->pad_w - d->Kw) / d->stride_w + 1;
     a.M = d->B * a.Ho * a.Wo; a.Cout = d->Cout; a.Npad = d->Npad;
-    a.bias = d->bias; a.slope = d->slope; a.act = d->act;
+    a.bias = d->bias; a.slope = d->slope; a.act = d->act; a.bias9 = d->bias9;
     a.res = (const bf16_t*)d->res; a.Cres = d->Cres; a.res_off = d->res_off;
     a.y = (bf16_t*)d->y; a.Cy = d->Cy; a.y_off = d->y_off;
     a.y2 = (bf16_t*)d->y2; a.Cy2 = d->Cy2; a.y2_off = d->y2_off; a.aff_s = d->aff_s; a.aff_b = d->aff_b;

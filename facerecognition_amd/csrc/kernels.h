@@ -17,6 +17,7 @@ struct ConvArgs {
     const bf16_t* w; int Kh, Kw, sh, sw, ph, pw, K, Kpad;
     int Ho, Wo, M, Cout, Npad;
     const float* bias; const float* slope; int act;  // act: 0 none, 1 relu, 2 prelu
+    const float* bias9;           // [9][Npad] border-class bias (replaces bias; see frhip.h), or null
     const bf16_t* res; int Cres, res_off;
     bf16_t* y; int Cy, y_off;
     bf16_t* y2; int Cy2, y2_off; const float* aff_s; const float* aff_b;

@@ -250,6 +250,25 @@ def _put_conv(out: dict, name: str, w: np.ndarray, s: Optional[np.ndarray], t: O
         out[name + ".slope"] = _np(slope).astype(np.float32)
 
 
+def _fold_pre_bn_3x3(out: dict, name: str, w: np.ndarray, s1, t1, s2, t2, slope) -> None:
+    """IBasicBlock conv1 with its PRE-conv BN folded in: bn2(conv(pad0(s1*x + t1))).
+
+    Zero padding is applied after bn1, so its shift t1 only reaches the taps that land inside the image:
+        conv(pad0(s1*x + t1), W) = conv(pad0(x), W*s1) + sum_{taps inside} sum_c W[o,c,tap] t1[c].
+    The second term depends only on the output pixel's border class (top / interior / bottom row x left /
+    interior / right column for 3x3, stride 1, pad 1), so it becomes a [9, Cout] bias table '.b9'
+    (class 3*rc + cc).  bn2 folds into the output side as usual.  w: [Cout, 3, 3, Cin] (KRSC), f64."""
+    ws = w * s2[:, None, None, None]                       # bn2 (output side)
+    T = np.einsum("orsc,c->ors", ws, t1)                   # bn1 shift through each tap: [Cout, 3, 3]
+    valid = ((1, 2), (0, 1, 2), (0, 1))                    # taps inside the image for rc / cc = 0, 1, 2
+    b9 = np.stack([t2 + T[:, list(valid[rc]), :][:, :, list(valid[cc])].sum(axis=(1, 2))
+                   for rc in range(3) for cc in range(3)])
+    out[name + ".w"] = (ws * s1[None, None, None, :]).astype(np.float32)
+    out[name + ".b"] = b9[4].astype(np.float32)            # interior class (reference only)
+    out[name + ".b9"] = b9.astype(np.float32)
+    out[name + ".slope"] = _np(slope).astype(np.float32)
+
+
 def fold_state_dict(arch: str, sd) -> Dict[str, np.ndarray]:
     """Eval-mode BN folding (f64) → the tensor names of csrc/engine.cpp's plans."""
     eps = BN_EPS[arch]
@@ -279,11 +298,10 @@ def fold_state_dict(arch: str, sd) -> Dict[str, np.ndarray]:
         for li, blocks in enumerate([3, 13, 30, 3]):
             for i in range(blocks):
                 p = f"layer{li + 1}.{i}"
-                s, t = _bn_affine(sd, p + ".bn1", eps)  # pre-conv BN: applied as the producer's 2nd output
-                out[p + ".bn1.s"] = s.astype(np.float32)
-                out[p + ".bn1.t"] = t.astype(np.float32)
-                s, t = _bn_affine(sd, p + ".bn2", eps)
-                _put_conv(out, p + ".conv1", _krsc(sd[p + ".conv1.weight"]), s, t, sd[p + ".prelu.weight"])
+                s1, t1 = _bn_affine(sd, p + ".bn1", eps)
+                s2, t2 = _bn_affine(sd, p + ".bn2", eps)
+                _fold_pre_bn_3x3(out, p + ".conv1", _krsc(sd[p + ".conv1.weight"]), s1, t1, s2, t2,
+                                 sd[p + ".prelu.weight"])
                 s, t = _bn_affine(sd, p + ".bn3", eps)
                 _put_conv(out, p + ".conv2", _krsc(sd[p + ".conv2.weight"]), s, t)
                 if i == 0:

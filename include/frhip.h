@@ -139,6 +139,11 @@ typedef struct fr_conv_desc {
     float* partial;      /* workspace [split_k, B*Ho*Wo, Npad] f32 when split_k > 1 */
     int dtype;           /* FR_DTYPE_BF16 / FR_DTYPE_F16: element type of x, w, res, y, y2 */
     int tile;            /* 0 = automatic (cost model); 1 + FR_TILE_* forces a tile variant */
+    /* Border-class bias for a 3x3 / stride 1 / pad 1 conv whose input BN was folded into the weights
+     * (the BN shift meets the zero padding only at the image border): [9][Npad] f32, class
+     * 3*rc + cc with rc = 0 / 1 / 2 for output row 0 / interior / Ho-1 (cc likewise for columns).
+     * When set it replaces `bias`.  NULL otherwise. */
+    const float* bias9;
 } fr_conv_desc;
 
 /* conv tile variants (pixels x channels per 256-thread block) */

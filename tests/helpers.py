@@ -34,7 +34,7 @@ def pack_weight(w: torch.Tensor, device, dtype: str = "bf16") -> tuple:
 
 def conv_op(x_nhwc, w, *, stride=(1, 1), pad=(0, 0), bias=None, act=0, slope=None, res=None, res_off=0,
             x_off=0, cin=None, y=None, y_off=0, y2=None, aff_s=None, aff_b=None, split_k=1, dtype="bf16",
-            tile=None):
+            tile=None, bias9=None):
     """Run fr_op_conv2d. x_nhwc: cuda 16-bit [B,H,W,Cx] of `dtype`; w: cpu f32 [Cout,Cin,kh,kw]."""
     dev = x_nhwc.device
     assert x_nhwc.dtype == TORCH_DT[dtype]
@@ -60,6 +60,10 @@ def conv_op(x_nhwc, w, *, stride=(1, 1), pad=(0, 0), bias=None, act=0, slope=Non
         return t.data_ptr()
 
     d.bias = dptr(bias)
+    if bias9 is not None:  # [9, Cout] -> [9, Npad]
+        b9 = torch.zeros((9, npad), dtype=torch.float32)
+        b9[:, :cout] = bias9
+        d.bias9 = dptr(b9)
     d.act = act
     d.slope = dptr(slope)
     if res is not None:

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from facerecognition_amd import _native as N
-from tests.helpers import TORCH_DT, bf16_round, conv_op, conv_ref
+from tests.helpers import TORCH_DT, bf16_round, conv_op, conv_ref, q16
 
 pytestmark = pytest.mark.gpu
 
@@ -75,7 +75,7 @@ def test_conv_every_tile(gpu, case, tile):
 
 BAND_CASES = [(2, 14, 14, 256, 256), (2, 28, 28, 128, 128), (2, 56, 56, 64, 64), (1, 112, 112, 64, 64),
               (2, 14, 14, 128, 256), (2, 28, 28, 64, 128), (2, 28, 28, 128, 256), (2, 28, 28, 64, 64),
-              (3, 14, 14, 512, 256), (1, 14, 14, 256, 512), (2, 14, 14, 192, 256)]
+              (3, 14, 14, 512, 256), (1, 14, 14, 256, 512), (2, 14, 14, 192, 256), (1, 28, 28, 256, 128)]
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
@@ -288,3 +288,42 @@ def test_segment_mean_normalize(gpu):
     for s in range(3):
         ref = folder_mean(E[seg[s]:seg[s + 1]])
         assert np.allclose(out[s].cpu().numpy(), ref, atol=1e-6)
+
+
+def _border_class(H, W):
+    rc = torch.ones(H, dtype=torch.long)
+    rc[0], rc[-1] = 0, 2
+    cc = torch.ones(W, dtype=torch.long)
+    cc[0], cc[-1] = 0, 2
+    return 3 * rc[:, None] + cc[None, :]
+
+
+BIAS9_CASES = [(2, 14, 14, 256, 256, None), (2, 14, 14, 256, 256, N.FR_TILE_BAND), (2, 28, 28, 128, 128, None),
+               (2, 56, 56, 64, 64, 2), (2, 28, 28, 128, 128, 0)]
+
+
+@pytest.mark.parametrize("case", BIAS9_CASES)
+def test_conv_bias9_prefolded_bn(gpu, case):
+    """Pre-conv BN folded into a 3x3/s1/p1 conv: bias9[border class] replaces bias (every kernel path:
+    band, igemm tiles, split-K reduce).  Reference: conv(pad0(s*x + t)) in f32."""
+    B, H, W, C, Cout, tile = case
+    g = torch.Generator().manual_seed(H + C)
+    x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(Cout, C, 3, 3, generator=g) / np.sqrt(C * 9)
+    s = torch.rand(C, generator=g) + 0.5
+    t = torch.randn(C, generator=g)
+    slope = torch.rand(Cout, generator=g) * 0.5
+    wf = w * s[None, :, None, None]
+    T = torch.einsum("ocrs,c->ors", w, t)
+    valid = [(1, 2), (0, 1, 2), (0, 1)]
+    b9 = torch.stack([T[:, list(valid[rc])][:, :, list(valid[cc])].sum((1, 2)) for rc in range(3) for cc in range(3)])
+    y = conv_op(x, wf, pad=(1, 1), act=2, slope=slope, bias9=b9, tile=tile)
+    xf = x.float().cpu().permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(xf * s[None, :, None, None] + t[None, :, None, None], q16(w), padding=1)
+    ref = torch.nn.functional.prelu(ref, slope).permute(0, 2, 3, 1)
+    got = y.float().cpu()
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-2, err
+    # border rows/cols really use their own class (a wrong class would be off by O(|T|))
+    cls = _border_class(H, W)
+    assert set(cls.unique().tolist()) == set(range(9))
