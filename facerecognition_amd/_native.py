@@ -23,6 +23,8 @@ FR_IN_U8_NHWC = 0
 FR_IN_F32_NCHW = 1
 FR_EMBED_RAW = 1
 FR_TILE_BAND = 7
+FR_OPT_STAGE = 1
+FR_OPT_KEEP_INTERMEDIATES = 2
 
 c_int, c_int64, c_size_t, c_void_p, c_float_p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p
 
@@ -59,6 +61,8 @@ _SIGS = {
     "fr_embed_match": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "fr_segment_mean_normalize": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "fr_set_option": (c_int, [c_void_p, c_int, c_int]),
+    "fr_get_option": (c_int, [c_void_p, c_int]),
     "fr_debug_tensor_count": (c_int, [c_void_p]),
     "fr_debug_plan": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t]),
     "fr_prof_enable": (c_int, [c_void_p, c_int]),

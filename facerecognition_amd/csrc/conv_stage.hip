@@ -1,0 +1,301 @@
+// LDS-resident stage kernel for the stride-1 IBasicBlocks of IResNet100 layer3 (14x14x256).
+//
+// Replaces, per image, the chain of 2*nblk row-band convolutions of layer3.1 .. layer3.29
+// (insightface IBasicBlock: bn1 -> conv3x3 -> bn2 -> PReLU -> conv3x3 -> bn3 -> + identity; the BNs are
+// folded into the conv weights by weights.fold_state_dict, bn1 as a border-class bias table).  These
+// convs are 55 % of the network's FLOPs.  As separate launches every conv pays a lockstep prologue
+// (patch + first weight slices, cold) and a lockstep epilogue (residual read + output write) on all
+// 256 CUs at once: measured ~15 us of a ~65 us launch (profiles/r01_*).  A layer3 conv of image b only
+// reads image b's previous activation, so one workgroup per image runs the whole stage:
+//   * the activation lives in LDS as 14 rows x 16 positions (columns 0 and 15 are the zero left/right
+//     halo) of all 256 channels ([32 planes of 8 channels][224 positions][16 B] = 112 KiB); the
+//     top/bottom halo rows are not stored: the two (wave, m-frag, tap) combinations that read them
+//     (wave-uniform) read the zero slot at position 0 instead; conv1's epilogue writes t =
+//     PReLU(conv1(x)) straight into it, after reading x from the same positions to seed conv2's
+//     accumulators (the identity), and conv2's epilogue writes x' = (x + conv2(t)) + bias back: no
+//     global traffic at all between the first patch load and the last block's NHWC store;
+//   * the weights stream through a 3-slot LDS ring of 16 KiB K-steps (32 input channels x one tap x 256
+//     output channels), pre-packed in exactly the LDS image so each DMA piece is a contiguous 1 KiB;
+//     the DMA stream runs three K-steps ahead across conv boundaries (two steps of latency cover), so a
+//     new conv never waits for its first weights;
+//   * one s_barrier per K-step, mid-step: after it the slice of step s+1 has landed everywhere and the
+//     slot of step s is free for step s+3; the weight fragments of step s+1 are refilled in place as
+//     each one retires, the patch fragments of step s+1 are read during step s.
+// MFMA geometry = conv3x3_bandp_kernel<14,14,2,2,7,8>: 2x2 waves, each 112 patch positions (7 m-frags,
+// columns 14/15 computed and discarded) x 128 channels (8 n-frags), v_mfma_f32_16x16x32_{bf16,f16};
+// operand A = weight rows, operand B = patch positions, so a lane ends with 4 consecutive channels of
+// one pixel.
+#include "kernels.h"
+
+#include <hip/hip_ext.h>
+
+#include <type_traits>
+
+namespace fr {
+namespace {
+
+constexpr int SW = 14;                       // image width = height
+constexpr int SWP = 16;                      // patch row stride (positions)
+constexpr int SC = 256;                      // channels
+constexpr int SPIX = SW * SW;                // 196
+constexpr int PPOS = SW * SWP;               // 224 stored positions per plane (rows 0..13)
+constexpr int PLANE_B = PPOS * 16;           // 3584: one 8-channel plane
+constexpr int PATCH_B = (SC / 8) * PLANE_B;  // 114688
+constexpr int SLICE_B = 4 * 256 * 16;        // 16384: [4 groups of 8 ch][256 rows][16 B]
+constexpr int NSLOT = 3;
+constexpr int STAGE_LDS = PATCH_B + NSLOT * SLICE_B;  // 163840 = the whole 160 KiB
+constexpr int KSTEPS = (SC / 32) * 9;        // 72 per conv
+constexpr uint32_t OOB = 0x80000000u;
+
+#ifndef FR_STAGE_SCHED
+#define FR_STAGE_SCHED 0  // explicit MFMA / ds_read / DMA interleave (sched_group_barrier)
+#endif
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, soff, 0, 0);
+}
+
+template <bool F16>
+__global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
+    typedef Num<F16> T;
+    typedef typename T::frag frag;
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [patch][slot0][slot1][slot2]
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    const int b = blockIdx.x;
+    const int nconv = 2 * p.nblk;
+    const int total = nconv * KSTEPS;
+
+    const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)total * SLICE_B);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
+
+    // ---- initial patch: x of this image; the patch is 7168 16-B slots (plane-major), 112 pieces of 64
+    {
+        const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * SPIX * SC * 2);
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
+        for (int u = 0; u < PATCH_B / 1024 / 4; ++u) {
+            const int piece = wave + 4 * u, q = piece * 64 + lane;
+            const int plane = q / PPOS, pos = q - plane * PPOS, r = pos / SWP, c = pos % SWP - 1;
+            const uint32_t src = (unsigned)c < (unsigned)SW ? (uint32_t)((((b * SPIX + r * SW + c) * SC) + plane * 8) * 2) : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(smem + piece * 1024), 16, src, 0, 0, 0);
+        }
+    }
+    // weight slices of global K-steps 0..2 (4 pieces per wave each)
+    auto issue_w = [&](int g, int slot) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            dma16s(wr, smem + PATCH_B + slot * SLICE_B + (wave * 4 + u) * 1024, (uint32_t)((wave * 4 + u) * 1024 + lane * 16),
+                   (uint32_t)g * SLICE_B);
+    };
+    issue_w(0, 0);
+    issue_w(1, 1);
+    issue_w(2, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // fragment addresses: B (patch) rows m = wm*112 + 16j + (lane&15) at plane (lane>>4) of the group;
+    // A (weights) rows n = wn*128 + 16i + (lane&15) in group (lane>>4)
+    int aoff[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) aoff[j] = (lane >> 4) * PLANE_B + ((wm * 7 + j) * SWP + (lane & 15)) * 16;
+    const int zoff = (lane >> 4) * PLANE_B;  // position 0 = left halo of row 0: a zero slot in every plane
+    const int boff = PATCH_B + (lane >> 4) * 4096 + (wn * 128 + (lane & 15)) * 16;
+
+    f32x4_t acc[8][7];
+    frag wf[8], pA[7], pB[7];
+    // patch fragments of (cg, tap): output row r = wm*7 + j reads source row r + dh - 1; rows -1 and 14
+    // (wave 0 frag 0 at dh = 0, wave 1 frag 6 at dh = 2) are halo -> the zero slot
+    auto pread = [&](frag (&pf)[7], int cg, int tap) {
+        const int dh = tap / 3, dw = tap % 3;
+        const char* pl = smem + cg * 4 * PLANE_B;
+        const char* pa = pl + ((dh - 1) * SWP + dw) * 16;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            const char* a = pa + aoff[j];
+            if (j == 0 && dh == 0) a = wm == 0 ? pl + zoff : a;
+            if (j == 6 && dh == 2) a = wm == 1 ? pl + zoff : a;
+            pf[j] = *(const frag*)a;
+        }
+    };
+    auto wread = [&](int i, int slot) { wf[i] = *(const frag*)(smem + boff + slot * SLICE_B + i * 256); };
+
+    // one K-step: MFMAs on (wf, cur); nxt <- patch fragments of (cg_n, tap_n) when has_next; mid-step
+    // barrier; DMA of global step g+3 into this step's slot; wf <- slice of step g+1 in place.  The
+    // slot of step s is s % 3 = tap % 3 (9 and 72 are multiples of 3): compile-time after unrolling.
+    auto kstep = [&](int g, int slot, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
+        pread(nxt, cg_n, tap_n);  // (after a conv's last step: unused reads, no branch)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
+#if FR_STAGE_SCHED
+        // first half: one patch read after every 4 MFMAs
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#endif
+        // slice g+1 landed (this wave); the 4 pieces of slice g+2 may stay in flight.  Branch-free: the
+        // tail re-fetches the last slice into the free slot and reads clamped slots (static counts)
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        issue_w(g + 3 < total ? g + 3 : total - 1, slot);
+        const int nslot = slot == NSLOT - 1 ? 0 : slot + 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wread(i, nslot);
+#pragma unroll
+        for (int i = 4; i < 8; ++i) {
+#pragma unroll
+            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
+            wread(i, nslot);
+        }
+#if FR_STAGE_SCHED
+        // second half: refills of wf[0..3] and the 4 DMA pieces spread over the first 8 MFMAs, then
+        // each wf[4..7] refill right after its 7th MFMA
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#endif
+    };
+
+    const size_t img = (size_t)b * SPIX * SC;
+    auto run_conv = [&](int cv, auto second_tag) {
+        constexpr bool second = decltype(second_tag)::value;
+        const StageConv c = p.conv[cv];
+        if (!second) {  // conv2 starts from the identity seeded by conv1's epilogue
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 7; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        }
+        pread(pA, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wread(i, 0);  // step 0 of every conv sits in slot 0 (72 % 3 == 0)
+        const int g0 = cv * KSTEPS;
+#pragma unroll 1
+        for (int cg = 0; cg < SC / 32; cg += 2) {
+#pragma unroll
+            for (int t = 0; t < 18; ++t) {
+                const int cgl = cg + t / 9, tap = t % 9;
+                const int cgn = t == 8 ? cg + 1 : (t == 17 ? cg + 2 : cgl);
+                const int tapn = t == 8 || t == 17 ? 0 : tap + 1;
+                if (t & 1) kstep(g0 + cgl * 9 + tap, tap % 3, pB, pA, cgn, tapn);
+                else kstep(g0 + cgl * 9 + tap, tap % 3, pA, pB, cgn, tapn);
+            }
+        }
+        // ---- epilogue: every wave is past its last patch read before the patch is overwritten.
+        // conv1: t = PReLU(acc + bias9) -> patch; the lane first reads x (the same positions and
+        //        channels it is about to overwrite -- no other lane touches them) and seeds its
+        //        accumulators with it, so conv2 accumulates onto the identity: x' = (x + conv2(t)) + b.
+        // conv2: x' -> patch (and NHWC global for the last block / intermediates).
+        // No global loads or stores between the stage's first patch load and its last block.
+        // (opaque lane copy: keeps the ~100 per-(i,j) addresses from being hoisted and spilled)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_barrier(0);
+            const int n = wn * 128 + 16 * i + 4 * (ln >> 4);
+            float4 sl = make_float4(0.f, 0.f, 0.f, 0.f), bb = sl;
+            if (c.slope) sl = *(const float4*)(c.slope + n);
+            if (c.bias) bb = *(const float4*)(c.bias + n);
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const int m = wm * 112 + 16 * j + (ln & 15), r = m >> 4, cc = m & 15;
+                const bool ok = r < SW && cc < SW;
+                char* slot = smem + (n >> 3) * PLANE_B + (m + 1) * 16 + (n & 7) * 2;
+                uint2 xin = make_uint2(0u, 0u);
+                if (!second && ok) xin = *(const uint2*)slot;
+                float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
+                if (c.bias9) {
+                    const float4 b9 = *(const float4*)(c.bias9 + border_class(r, cc, SW, SW) * SC + n);
+                    v[0] += b9.x; v[1] += b9.y; v[2] += b9.z; v[3] += b9.w;
+                }
+                if (c.act == 2) {
+                    v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
+                    v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
+                    v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
+                    v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
+                } else if (c.act == 1) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                }
+                float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+                const uint4 pk = T::pack8(o8);
+                const uint2 pk2 = make_uint2(pk.x, pk.y);
+                if (!second) {
+                    float f[8];
+                    T::unpack8(make_uint4(xin.x, xin.y, 0, 0), f);
+                    acc[i][j] = (f32x4_t){f[0], f[1], f[2], f[3]};
+                }
+                if (ok) {
+                    *(uint2*)slot = pk2;
+                    const size_t go = img + (size_t)(r * SW + cc) * SC + n;
+                    if (second && cv == nconv - 1) *(uint2*)(p.y + go) = pk2;
+                    if (p.dbg_x) {
+                        bf16_t* dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
+                        if (dbg) *(uint2*)(dbg + go) = pk2;
+                    }
+                }
+            }
+        }
+        __syncthreads();  // the new activation is visible to every wave before the next conv reads it
+    };
+#pragma unroll 1
+    for (int blk = 0; blk < p.nblk; ++blk) {
+        run_conv(2 * blk, std::false_type{});
+        run_conv(2 * blk + 1, std::true_type{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs land before the LDS is released
+}
+
+}  // namespace
+
+bool stage_supported(int B, int H, int W, int C) { return B > 0 && H == SW && W == SW && C == SC; }
+
+size_t stage_weight_bytes(int nconv) { return (size_t)nconv * KSTEPS * SLICE_B; }
+
+// Packs one conv's [256][Kpad] row-major weights (K order (kh, kw, c)) into the stage's K-step
+// image: step s = cg*9 + tap, [4 groups g][256 rows n][8 channels] with channel 32cg + 8g + e.
+void stage_pack_weights(const bf16_t* rows, int Kpad, bf16_t* out) {
+    for (int cg = 0; cg < SC / 32; ++cg)
+        for (int tap = 0; tap < 9; ++tap) {
+            bf16_t* s = out + (size_t)(cg * 9 + tap) * (SLICE_B / 2);
+            for (int g = 0; g < 4; ++g)
+                for (int n = 0; n < SC; ++n)
+                    for (int e = 0; e < 8; ++e)
+                        s[(g * 256 + n) * 8 + e] = rows[(size_t)n * Kpad + tap * SC + cg * 32 + g * 8 + e];
+        }
+}
+
+hipError_t launch_stage(const StageArgs& a, hipStream_t s) {
+    auto k = a.f16 ? stage_kernel<true> : stage_kernel<false>;
+    static bool attr[2] = {false, false};
+    if (!attr[a.f16 ? 1 : 0]) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, STAGE_LDS);
+        attr[a.f16 ? 1 : 0] = true;
+    }
+    if (a.ev0)
+        hipExtLaunchKernelGGL(k, dim3(a.B), dim3(256), STAGE_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
+    else
+        hipLaunchKernelGGL(k, dim3(a.B), dim3(256), STAGE_LDS, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace fr

@@ -52,7 +52,7 @@ struct TensorDesc {
     std::string name;  // oracle module whose output this tensor equals ("" = internal)
 };
 
-enum OpKind { OP_PRE, OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD };
+enum OpKind { OP_PRE, OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_STAGE };
 
 struct Op {
     OpKind kind;
@@ -64,6 +64,17 @@ struct Op {
     int act = 0;
     int wi = -1;
     int pk = 0, ps = 0, pp = 0;
+    int stage = -1;  // OP_STAGE: its StageRec; OP_CONV: the stage that covers it (skipped when stages run)
+};
+
+// One LDS-resident stage (conv_stage.hip): blocks [first, first+nblk) of a 14x14x256 layer.
+struct StageRec {
+    int in = -1, out = -1, nblk = 0;
+    std::vector<int> conv_ops;            // member OP_CONV indices, conv1/conv2 alternating
+    std::vector<int> t_tensors, x_tensors;  // per block: conv1 output, block output
+    bf16_t* w = nullptr;                  // packed K-step weight images
+    StageConv* table = nullptr;           // [2*nblk]
+    bf16_t** dbg = nullptr;               // [2*nblk] device pointer table: x outputs then t outputs
 };
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -113,6 +124,10 @@ struct fr_handle {
     std::vector<Tuned> tuned;
     std::vector<int> tuned_batches;
     bool tuning = false;
+    // LDS-resident stage kernels (fr_set_option FR_OPT_STAGE / FR_OPT_KEEP_INTERMEDIATES)
+    std::vector<StageRec> stages;
+    bool use_stage = true;
+    bool keep_inter = false;
 };
 
 namespace {
@@ -390,6 +405,51 @@ struct Builder {
     }
 };
 
+// Packs a stage's weights (from the member convs' [Npad][Kpad] device images) and its epilogue table.
+int build_stage(fr_handle* h, StageRec& r) {
+    const int nconv = 2 * r.nblk;
+    std::vector<bf16_t> packed(stage_weight_bytes(nconv) / sizeof(bf16_t));
+    std::vector<StageConv> tab(nconv);
+    const size_t per = packed.size() / nconv;
+    for (int c = 0; c < nconv; ++c) {
+        const Op& op = h->ops[r.conv_ops[c]];
+        const DevConvW& cw = h->convw[op.wi];
+        if (cw.Cout != 256 || cw.Npad != 256 || cw.Kh != 3 || cw.Kw != 3 || cw.Cin != 256) {
+            set_error("plan: stage member conv is not 3x3 256->256");
+            return FR_ERR_ARG;
+        }
+        std::vector<bf16_t> rows((size_t)cw.Npad * cw.Kpad);
+        FR_HIP_CHECK(hipMemcpy(rows.data(), cw.w, rows.size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
+        stage_pack_weights(rows.data(), cw.Kpad, packed.data() + c * per);
+        tab[c].bias = cw.bias9 ? nullptr : cw.bias;
+        tab[c].bias9 = cw.bias9;
+        tab[c].slope = cw.slope;
+        tab[c].act = op.act;
+    }
+    int rc = upload(h, &r.w, packed);
+    if (rc) return rc;
+    rc = upload(h, &r.table, tab);
+    if (rc) return rc;
+    void* d = nullptr;
+    if ((rc = dev_alloc(&d, (size_t)nconv * sizeof(bf16_t*)))) return rc;
+    h->weight_allocs.push_back(d);
+    r.dbg = (bf16_t**)d;
+    return FR_OK;
+}
+
+// Device pointer table of a stage's intermediate tensors (filled after every activation reserve).
+int fill_stage_dbg(fr_handle* h) {
+    for (auto& r : h->stages) {
+        std::vector<bf16_t*> p(2 * r.nblk);
+        for (int i = 0; i < r.nblk; ++i) {
+            p[i] = h->tensors[r.x_tensors[i]].dev;
+            p[r.nblk + i] = h->tensors[r.t_tensors[i]].dev;
+        }
+        FR_HIP_CHECK(hipMemcpy(r.dbg, p.data(), p.size() * sizeof(bf16_t*), hipMemcpyHostToDevice));
+    }
+    return FR_OK;
+}
+
 std::string L(int l, int i) { return "layer" + std::to_string(l) + "." + std::to_string(i); }
 
 void build_iresnet100(Builder& b) {
@@ -407,7 +467,18 @@ void build_iresnet100(Builder& b) {
     int H = 112, C = 64;
     for (int l = 0; l < 4; ++l) {
         const int P = planes[l], Ho = H / 2;
+        // layer3 blocks 1.. (stride 1, 14x14x256): also emitted as one LDS-resident stage op
+        int st_op = -1;
+        StageRec rec;
         for (int i = 0; i < nblk[l]; ++i) {
+            if (i == 1 && stage_supported(1, Ho, Ho, P) && P == C) {
+                st_op = (int)h->ops.size();
+                rec.in = x;
+                Op op;
+                op.kind = OP_STAGE;
+                op.stage = (int)h->stages.size();
+                h->ops.push_back(op);
+            }
             const std::string pre = L(l + 1, i);
             const int Hin = i == 0 ? H : Ho, st = i == 0 ? 2 : 1;
             const int hmid = b.tensor(Hin, Hin, P, pre + ".prelu");
@@ -419,8 +490,21 @@ void build_iresnet100(Builder& b) {
             }
             const int y = b.tensor(Ho, Ho, P, pre);
             b.conv({pre + ".conv2"}, hmid, 0, P, y, 0, 3, 3, st, st, 1, 1, 0, res, 0);
+            if (st_op >= 0 && !b.rc) {
+                rec.conv_ops.push_back((int)h->ops.size() - 2);
+                rec.conv_ops.push_back((int)h->ops.size() - 1);
+                rec.t_tensors.push_back(hmid);
+                rec.x_tensors.push_back(y);
+            }
             x = y;
             C = P;
+        }
+        if (st_op >= 0 && !b.rc) {
+            rec.out = x;
+            rec.nblk = (int)rec.t_tensors.size();
+            for (int oi : rec.conv_ops) h->ops[oi].stage = h->ops[st_op].stage;
+            b.rc = build_stage(h, rec);
+            h->stages.push_back(rec);
         }
         H = Ho;
     }
@@ -586,7 +670,7 @@ int reserve(fr_handle* h, int maxB) {
     h->partial = (float*)p;
     h->partial_floats = need;
     h->max_batch = maxB;
-    return FR_OK;
+    return fill_stage_dbg(h);
 }
 
 bool band_enabled() {
@@ -600,6 +684,14 @@ bool band_enabled() {
 int conv_dbg() {
     static const int d = [] {
         const char* e = getenv("FR_CONV_DBG");
+        return e ? atoi(e) : 0;
+    }();
+    return d;
+}
+
+int stage_dbg() {
+    static const int d = [] {
+        const char* e = getenv("FR_STAGE_DBG");
         return e ? atoi(e) : 0;
     }();
     return d;
@@ -729,7 +821,26 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
 int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
     const int f16 = h->dtype == FR_DTYPE_F16;
     for (const auto& op : h->ops) {
+        if (op.kind == OP_STAGE ? !h->use_stage : (op.stage >= 0 && h->use_stage)) continue;
         switch (op.kind) {
+            case OP_STAGE: {
+                const StageRec& r = h->stages[op.stage];
+                StageArgs a{};
+                a.x = h->tensors[r.in].dev;
+                a.y = h->tensors[r.out].dev;
+                a.w = r.w;
+                a.conv = r.table;
+                if (h->keep_inter) { a.dbg_x = r.dbg; a.dbg_t = r.dbg + r.nblk; }
+                a.B = B;
+                a.nblk = r.nblk;
+                a.f16 = f16;
+                a.dbg = stage_dbg();
+                ProfScope ps(h, s);
+                ps.flops = 2.0 * r.nblk * 2.0 * B * 196.0 * 256.0 * 2304.0;
+                ps.start("stage layer3");
+                FR_HIP_CHECK(launch_stage(a, s));
+                break;
+            }
             case OP_PRE: {
                 ProfScope ps(h, s);
                 ps.start("preprocess");
@@ -811,6 +922,11 @@ extern "C" {
 const char* fr_last_error(void) { return g_err.c_str(); }
 int fr_abi_version(void) { return FR_ABI_VERSION; }
 
+static bool stage_default() {
+    const char* e = getenv("FR_NO_STAGE");
+    return !(e && e[0] == '1');
+}
+
 int fr_create(fr_handle** out, int device, int arch, int dtype) {
     if (!out || !valid_arch(arch) || (dtype != FR_DTYPE_BF16 && dtype != FR_DTYPE_F16)) {
         set_error("fr_create: bad argument (arch/dtype)");
@@ -828,6 +944,7 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->arch = arch;
     h->dtype = dtype;
     h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
+    h->use_stage = stage_default();
     *out = h;
     return FR_OK;
 }
@@ -1066,6 +1183,13 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
     if (!h || !buf || n == 0 || B <= 0) { set_error("fr_debug_plan: bad argument"); return FR_ERR_ARG; }
     std::string out;
     for (const auto& op : h->ops) {
+        if (op.kind == OP_STAGE ? !h->use_stage : (op.stage >= 0 && h->use_stage)) continue;
+        if (op.kind == OP_STAGE) {
+            const StageRec& r = h->stages[op.stage];
+            out += "stage " + std::to_string(B * 196) + " 256 2304 2304 " + std::to_string(2 * r.nblk) + " 1 3x3 " +
+                   h->tensors[r.out].name + "\n";
+            continue;
+        }
         if (op.kind != OP_CONV && op.kind != OP_HEAD) {
             out += std::string(op.kind == OP_PRE ? "pre" : op.kind == OP_MAXPOOL ? "maxpool" : "avgpool") + "\n";
             continue;
@@ -1093,6 +1217,27 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
     }
     std::snprintf(buf, n, "%s", out.c_str());
     return out.size() + 1 <= n ? FR_OK : FR_ERR_ARG;
+}
+
+int fr_set_option(fr_handle* h, int option, int value) {
+    if (!h) { set_error("fr_set_option: null handle"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    switch (option) {
+        case FR_OPT_STAGE: h->use_stage = value != 0; break;
+        case FR_OPT_KEEP_INTERMEDIATES: h->keep_inter = value != 0; break;
+        default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;
+    }
+    drop_graphs(h);  // captured replays bake in the plan
+    return FR_OK;
+}
+
+int fr_get_option(const fr_handle* h, int option) {
+    if (!h) return FR_ERR_ARG;
+    switch (option) {
+        case FR_OPT_STAGE: return h->use_stage && !h->stages.empty() ? 1 : 0;
+        case FR_OPT_KEEP_INTERMEDIATES: return h->keep_inter ? 1 : 0;
+        default: return FR_ERR_ARG;
+    }
 }
 
 int fr_prof_enable(fr_handle* h, int on) {

@@ -41,6 +41,29 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
 // Row-band direct 3x3/s1/p1 conv (conv_band.hip): applicability/params, launch.
 bool band_plan(const ConvArgs& a, int* cfg, int* variant);
 hipError_t launch_conv_band(const ConvArgs& a, int cfg, int variant, hipStream_t s);
+// LDS-resident stage kernel (conv_stage.hip): the stride-1 IBasicBlocks of a 14x14x256 stage, one
+// workgroup per image, activation kept in LDS across all 2*nblk convs.
+struct StageConv {
+    const float* bias;   // [256] (null when bias9 carries the full bias)
+    const float* bias9;  // [9][256] border-class bias (conv1: folded pre-conv BN), or null
+    const float* slope;  // [256] PReLU slopes (act == 2), or null
+    int act, pad_;
+};
+struct StageArgs {
+    const bf16_t* x;           // stage input [B][14][14][256]
+    bf16_t* y;                 // stage output [B][14][14][256] (written by the last block)
+    const bf16_t* w;           // packed K-step images of all convs (stage_pack_weights)
+    const StageConv* conv;     // [2*nblk] device table
+    bf16_t* const* dbg_x;      // optional [nblk] per-block outputs / [nblk] conv1 outputs (device
+    bf16_t* const* dbg_t;      //   pointer tables; null = do not materialise intermediates)
+    int B, nblk, f16, dbg;     // dbg: timing-only experiment switches (FR_STAGE_DBG), 0 in production
+    void* ev0;
+    void* ev1;
+};
+bool stage_supported(int B, int H, int W, int C);
+size_t stage_weight_bytes(int nconv);
+void stage_pack_weights(const bf16_t* rows, int Kpad, bf16_t* out);
+hipError_t launch_stage(const StageArgs& a, hipStream_t s);
 // Split-K reduction + the same fused epilogue as the conv kernel.
 hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
 // Number of K-tiles of 64 (for split-k planning).

@@ -61,6 +61,13 @@ class FRModel:
         N.check(N.lib().fr_load_weights(self._h, buf, len(blob)), "fr_load_weights")
         self.embedding_size = N.lib().fr_embed_dim(self._h)
 
+    def set_option(self, option: int, value: int) -> None:
+        """fr_set_option (FR_OPT_STAGE, FR_OPT_KEEP_INTERMEDIATES; include/frhip.h)."""
+        N.check(N.lib().fr_set_option(self._h, int(option), int(value)), "fr_set_option")
+
+    def get_option(self, option: int) -> int:
+        return int(N.lib().fr_get_option(self._h, int(option)))
+
     def reserve(self, max_batch: int) -> None:
         N.check(N.lib().fr_reserve(self._h, int(max_batch)), "fr_reserve")
 

@@ -177,6 +177,19 @@ int fr_op_avgpool(const void* x, int B, int H, int W, int C, void* y, int dtype,
 int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, int Kpad,
                  const float* bias, int normalize, float* out, int split_k, float* partial, int dtype, void* stream);
 
+/* ---- execution options (no reference counterpart: plan choices of this build) ----------------
+ * FR_OPT_STAGE (default 1; env FR_NO_STAGE=1 starts at 0): run the stride-1 IResNet100 layer3 blocks
+ *   as one LDS-resident stage kernel per image instead of 58 separate conv launches.  Numerically the
+ *   same op sequence and bf16 rounding points (f32 accumulation in a different K order).
+ * FR_OPT_KEEP_INTERMEDIATES (default 0): the stage kernel also writes every block output and conv1
+ *   output to its named tensor (per-layer drift tests; costs HBM writes).
+ * Changing an option drops the captured hipGraph replays.  fr_get_option returns the value (FR_OPT_STAGE
+ * reads 0 when the plan has no stage) or FR_ERR_ARG. */
+#define FR_OPT_STAGE 1
+#define FR_OPT_KEEP_INTERMEDIATES 2
+int fr_set_option(fr_handle* h, int option, int value);
+int fr_get_option(const fr_handle* h, int option);
+
 /* ---- debug: named intermediate tensors of the forward plan (per-layer drift tests) ----
  * Tensor names are the reference/oracle module whose output the tensor equals
  * (e.g. "backbone.layer2.0", "layer3.7.prelu", "model.repeat_1.2"); "" for internal buffers. */
@@ -198,7 +211,8 @@ int fr_prof_get(const fr_handle* h, int i, char* name, size_t n, double* total_m
 
 int fr_debug_tensor_count(const fr_handle* h);
 /* Text dump of the forward plan at batch B, one line per op:
- * "conv|head M N K Kpad tile split KhxKw name" or "pre|maxpool|avgpool". */
+ * "conv|head M N K Kpad tile split KhxKw name", "stage M 256 2304 2304 nconv 1 3x3 name" or
+ * "pre|maxpool|avgpool". */
 int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n);
 const char* fr_debug_tensor_name(const fr_handle* h, int t);
 int fr_debug_tensor_shape(const fr_handle* h, int t, int* H, int* W, int* C);

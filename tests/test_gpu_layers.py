@@ -25,6 +25,7 @@ def stage_report(arch, B=2, seed=0):
     u8 = synthetic_crops(B, INPUT_SIZE[arch], seed=seed)
     sd = synth_state_dict(arch)
     m = FRModel(arch, sd)
+    m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)  # the layer3 stage kernel materialises its blocks too
     dt = torch.float16 if m.dtype == "f16" else torch.bfloat16
     m.embed(torch.from_numpy(u8))
     torch.cuda.synchronize()
