@@ -1,0 +1,12 @@
+#!/bin/bash
+# Copy a tools/gpu_round.sh TAG run from gpurun_out/ into the tracked profiles/ (round-named files).
+#   tools/collect_profiles.sh TAG ROUND   e.g. tools/collect_profiles.sh r01b r01
+T=${1:?tag}; R=${2:?round prefix}; O=gpurun_out/$T
+set -e
+cp $O/bench.json profiles/${R}_bench.json
+: > profiles/${R}_bench_runs.jsonl
+for b in bench bench_noprof bench_host bench_irv1 bench_r50; do tail -1 $O/$b.log >> profiles/${R}_bench_runs.jsonl; done
+cp "$(find $O/prof -name '*kernel_stats.csv' | head -1)" profiles/${R}_bench_kernel_stats.csv
+cp $O/pmc_traffic.json profiles/${R}_pmc_traffic.json
+grep -v "^\s*$" $O/tests.log | tail -40 > profiles/${R}_gpu_tests.log
+echo "collected $T -> profiles/${R}_*"

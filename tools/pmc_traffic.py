@@ -25,11 +25,13 @@ BAND_TH = {14: 14, 28: 7, 56: 4, 112: 2}
 
 
 def class_pattern(cls: str, f16: bool) -> str:
+    if cls == "stage layer3":
+        return f"stage_kernel<{str(f16).lower()}>"
     m = re.match(r"conv3x3_band W(\d+) v(\d+)", cls)
     if m:
         W, v = int(m.group(1)), int(m.group(2))
         if v == 3:  # software-pipelined 4-wave variant
-            return f"conv3x3_bandp_kernel<{str(f16).lower()}, {W}, {BAND_TH[W]}, 2, 2, 7, 8>"
+            return f"conv3x3_bandp_kernel<{str(f16).lower()}, {W}, {BAND_TH[W]}, 2, 2, 7, 8,"
         wm, wn, fm, fn = BAND_VARIANT[v]
         return f"conv3x3_band_kernel<{str(f16).lower()}, {W}, {BAND_TH[W]}, {wm}, {wn}, {fm}, {fn},"
     raise KeyError(cls)
@@ -55,7 +57,7 @@ def main():
     ap.add_argument("--arch", default="iresnet100")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--classes", nargs="*", default=["conv3x3_band W14 v3"])
+    ap.add_argument("--classes", nargs="*", default=["stage layer3", "conv3x3_band W14 v3"])
     ap.add_argument("--flops-per-launch", type=float, default=2.0 * 50176 * 256 * 2304,
                     help="algorithmic FLOPs per launch of the first class (intensity report)")
     a = ap.parse_args()
@@ -72,7 +74,7 @@ def main():
             continue
         fb = sum(fetch[k][0] for k in fk) / sum(fetch[k][1] for k in fk) * 1024 * 2
         wb = sum(write[k][0] for k in wk) / sum(write[k][1] for k in wk) * 1024
-        out["kernels"][cls] = {"rocprof_kernel": fk[0].split("(")[0], "fetch_bytes_per_launch": round(fb),
+        out["kernels"][cls] = {"rocprof_kernel": fk[0].split("(fr::")[0], "fetch_bytes_per_launch": round(fb),
                                "write_bytes_per_launch": round(wb), "hbm_bytes_per_launch": round(fb + wb),
                                "dispatches": sum(fetch[k][1] for k in fk)}
         print(cls, out["kernels"][cls])
