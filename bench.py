@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 METRIC = "aligned faces/sec (embed+match) ArcFace@112 bs=256, 1/2/4/8 MI355X"
 GFLOP_PER_FACE = {"iresnet100": 24.179, "resnet50_arcface": 2.154, "irv1_facenet": 2.835}
 BF16_DENSE_PEAK_TFLOPS = 2500.0
+FP8_DENSE_PEAK_TFLOPS = 5000.0  # MI355X_MICROARCH.md: ~5 PF dense fp8 (block-scaled f8f6f4 MFMA)
 PROF_STRIDE = 8  # roofline: sample every 8th dominant-kernel launch (event overhead ~0.5 % instead of ~4 %)     # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
 
 
@@ -59,7 +60,8 @@ def parse():
     ap.add_argument("--gallery-rows", type=int, default=10000)
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--arch", default="iresnet100")
-    ap.add_argument("--dtype", default=None, help="bf16 | f16 (default: the arch's parity dtype)")
+    ap.add_argument("--dtype", default=None,
+                    help="bf16 | f16 | fp8 (default: the arch's parity dtype; fp8 = BASELINE config 5)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip the per-kernel event timing (roofline)")
@@ -219,9 +221,10 @@ def main():
         name = dominant
         ms, launches, flops = kclasses[name]
         achieved = flops / (ms * 1e-3) / 1e12
+        peak = FP8_DENSE_PEAK_TFLOPS if name.startswith("conv_fp8") else BF16_DENSE_PEAK_TFLOPS
         result["roofline"] = {
-            "bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
+            "bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": pmc_traffic(name, args), "sampled_launches": launches, "sample_stride": PROF_STRIDE,
             "us_per_launch": round(ms / launches * 1e3, 2), "gflop_per_launch": round(flops / launches / 1e9, 3),
             "share_of_forward": round(kclasses_all[name][0] / 2 / embed_ms, 4)}

@@ -18,7 +18,8 @@ FR_OK = 0
 FR_ARCH = {"resnet50_arcface": 0, "iresnet100": 1, "irv1_facenet": 2}
 FR_DTYPE_BF16 = 0
 FR_DTYPE_F16 = 1
-FR_DTYPE = {"bf16": FR_DTYPE_BF16, "f16": FR_DTYPE_F16}
+FR_DTYPE_FP8 = 2
+FR_DTYPE = {"bf16": FR_DTYPE_BF16, "f16": FR_DTYPE_F16, "fp8": FR_DTYPE_FP8}
 FR_IN_U8_NHWC = 0
 FR_IN_F32_NCHW = 1
 FR_EMBED_RAW = 1
@@ -41,6 +42,7 @@ class FrConvDesc(ctypes.Structure):
         ("Ho", c_int), ("Wo", c_int),
         ("split_k", c_int), ("partial", c_void_p), ("dtype", c_int), ("tile", c_int),
         ("bias9", c_void_p),
+        ("wscale", c_void_p), ("x_amax", c_void_p), ("y_amax", c_void_p),
     ]
 
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cmath>
 #include <string>
 
 typedef uint16_t bf16_t;  // 16-bit activation/weight storage (bf16 or f16 bits, per handle dtype)
@@ -30,6 +31,26 @@ static inline bf16_t host_f2bf(float f) {
     if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
     u += 0x7fffu + ((u >> 16) & 1u);
     return (bf16_t)(u >> 16);
+}
+
+// f32 -> OCP e4m3fn (gfx950 fp8) round-to-nearest-even on the host, saturating to +-448 (no NaN from
+// weights).  Exact for values that are already e4m3-representable (weights.quantize_fp8 output).
+static inline uint8_t host_f2e4m3(float f) {
+    const uint8_t s = f < 0.f ? 0x80 : 0;
+    float a = f < 0.f ? -f : f;
+    if (!(a == a)) return 0x7f;
+    if (a >= 448.f) return s | 0x7e;
+    int e;
+    const float m = frexpf(a, &e);  // a = m * 2^e, m in [0.5, 1)
+    int E = e - 1;                  // a = (2m) * 2^E, 2m in [1, 2)
+    if (a == 0.f || E < -6) {       // subnormal: step 2^-9
+        const int q = (int)nearbyintf(a * 512.f);
+        return s | (uint8_t)q;      // q == 8 is the smallest normal (exp 1, mantissa 0): same bits
+    }
+    int q = (int)nearbyintf((2.f * m - 1.f) * 8.f);
+    if (q == 8) { q = 0; ++E; }
+    if (E > 8 || (E == 8 && q == 7)) return s | 0x7e;
+    return s | (uint8_t)(((E + 7) << 3) | q);
 }
 
 // f32 -> f16 round-to-nearest-even on the host, saturating to ±65504 (no inf from weights).

@@ -350,6 +350,7 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
         }
         return;
     }
+    float amax = 0.f;  // max |y| of this thread's stores (fp8 consumers' dynamic activation scale)
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
         const int ml = ml0 + it * RS, m = m0 + ml;
@@ -378,6 +379,8 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
             for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sl8[e];
         }
         if (m < p.M && nv) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
             *(uint4*)(p.y + (size_t)m * p.Cy + p.y_off + n) = T::pack8(v);
             if (p.y2) {
                 float u[8];
@@ -386,6 +389,13 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
                 *(uint4*)(p.y2 + (size_t)m * p.Cy2 + p.y2_off + n) = T::pack8(u);
             }
         }
+    }
+    if (p.y_amax) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+        if ((tid & 63) == 0)
+            atomicMax((unsigned int*)p.y_amax + (blockIdx.x + gridDim.x * blockIdx.y) % max(p.amax_slots, 1),
+                      __float_as_uint(amax));
     }
 }
 

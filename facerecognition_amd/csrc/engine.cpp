@@ -43,7 +43,9 @@ struct DevConvW {
     float* aff_s = nullptr;
     float* aff_b = nullptr;
     float* bias9 = nullptr;  // [9][Npad] border-class bias (input BN folded into a 3x3/s1/p1 conv)
-    int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0;
+    uint8_t* w8 = nullptr;   // FR_DTYPE_FP8: e4m3 [Npad][Kpad8] + per-channel scale
+    float* wscale = nullptr;
+    int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0, Kpad8 = 0;
 };
 
 struct TensorDesc {
@@ -126,6 +128,12 @@ struct fr_handle {
     bool tuning = false;
     // LDS-resident stage kernels (fr_set_option FR_OPT_STAGE / FR_OPT_KEEP_INTERMEDIATES)
     std::vector<StageRec> stages;
+    // FaceNet projection (Linear(512, d) + F.normalize after IRV1's own L2; facenet_model.py:20-23,32-35)
+    float* proj_w = nullptr;
+    float* proj_b = nullptr;
+    int proj_d = 0;
+    float* emb_pre = nullptr;  // [max_batch][512] IRV1 output before the projection
+    float* amax = nullptr;     // FR_DTYPE_FP8: per-tensor max |x| of the current forward [ntensors]
     bool use_stage = true;
     bool keep_inter = false;
 };
@@ -169,6 +177,8 @@ void free_acts(fr_handle* h) {
     for (auto& t : h->tensors) t.dev = nullptr;
     h->partial = nullptr;
     h->partial_floats = 0;
+    h->emb_pre = nullptr;
+    h->amax = nullptr;
     h->max_batch = 0;
 }
 
@@ -177,6 +187,9 @@ void free_weights(fr_handle* h) {
     for (void* p : h->weight_allocs) (void)hipFree(p);
     h->weight_allocs.clear();
     h->convw.clear();
+    h->stages.clear();
+    h->proj_w = h->proj_b = nullptr;
+    h->proj_d = 0;
 }
 
 // ------------------------------------------------------------------ weight blob
@@ -242,7 +255,7 @@ struct Builder {
 
     bool stem = false;  // next conv is the network stem: fold 1/255 + hi/lo split (see launch_preprocess)
 
-    float round16(float v) const {
+    float round16(float v) const {  // stem hi/lo split in the activation dtype (bf16 for FR_DTYPE_FP8)
         return h->dtype == FR_DTYPE_F16 ? host_h2f(host_f2h(v)) : host_bf2f(host_f2bf(v));
     }
 
@@ -308,6 +321,33 @@ struct Builder {
             }
         bias.resize(cw.Npad, 0.f);
         if ((rc = upload(h, &cw.w, packed))) return -1;
+        if (h->dtype == FR_DTYPE_FP8 && names.size() == 1 && !stem_split && cin % 64 == 0) {
+            const HostT* ws = find(names[0] + ".wscale");
+            if (ws) {  // e4m3 weights: the blob carries e4m3-representable values w/s and the scales s
+                if ((int)ws->v.size() != cout) {
+                    set_error("weights: mis-sized " + names[0] + ".wscale");
+                    rc = FR_ERR_WEIGHTS;
+                    return -1;
+                }
+                cw.Kpad8 = round_up(cw.K, 128);
+                std::vector<uint8_t> q((size_t)cw.Npad * cw.Kpad8, 0);
+                for (int o = 0; o < cout; ++o)
+                    for (int k = 0; k < cw.K; ++k) q[(size_t)o * cw.Kpad8 + k] = host_f2e4m3(wrows[(size_t)o * cw.K + k]);
+                std::vector<float> sc(ws->v);
+                sc.resize(cw.Npad, 0.f);
+                if ((rc = upload(h, &cw.w8, q))) return -1;
+                if ((rc = upload(h, &cw.wscale, sc))) return -1;
+                // the bf16 copy (debug / op paths) holds the dequantized weights
+                for (int o = 0; o < cout; ++o)
+                    for (int k = 0; k < cw.K; ++k)
+                        packed[(size_t)o * cw.Kpad + k] = host_f2bf(wrows[(size_t)o * cw.K + k] * ws->v[o]);
+                if (hipMemcpy(cw.w, packed.data(), packed.size() * sizeof(bf16_t), hipMemcpyHostToDevice) != hipSuccess) {
+                    set_error("hipMemcpy of dequantized fp8 weights failed");
+                    rc = FR_ERR_HIP;
+                    return -1;
+                }
+            }
+        }
         if ((rc = upload(h, &cw.bias, bias))) return -1;
         if (names.size() == 1) {
             const HostT* b9 = find(names[0] + ".b9");
@@ -403,6 +443,22 @@ struct Builder {
         h->embed_dim = h->convw[op.wi].Cout;
         h->ops.push_back(op);
     }
+    // optional FaceNet projection "proj.w" [d, 512] + "proj.b" [d] after the (L2-normalized) head
+    void projection() {
+        if (rc) return;
+        const HostT* w = find("proj.w");
+        if (!w) return;
+        const HostT* bb = find("proj.b");
+        if (w->dims.size() != 2 || w->dims[1] != h->embed_dim || w->dims[1] > 1024 || !bb ||
+            (int64_t)bb->v.size() != w->dims[0]) {
+            set_error("weights: mis-shaped proj.w / proj.b (expects [d, " + std::to_string(h->embed_dim) + "], [d])");
+            rc = FR_ERR_WEIGHTS;
+            return;
+        }
+        if ((rc = upload(h, &h->proj_w, w->v))) return;
+        if ((rc = upload(h, &h->proj_b, bb->v))) return;
+        h->proj_d = (int)w->dims[0];
+    }
 };
 
 // Packs a stage's weights (from the member convs' [Npad][Kpad] device images) and its epilogue table.
@@ -471,7 +527,7 @@ void build_iresnet100(Builder& b) {
         int st_op = -1;
         StageRec rec;
         for (int i = 0; i < nblk[l]; ++i) {
-            if (i == 1 && stage_supported(1, Ho, Ho, P) && P == C) {
+            if (i == 1 && h->dtype != FR_DTYPE_FP8 && stage_supported(1, Ho, Ho, P) && P == C) {
                 st_op = (int)h->ops.size();
                 rec.in = x;
                 Op op;
@@ -635,6 +691,7 @@ void build_irv1(Builder& b) {
     const int pool = b.tensor(1, 1, 1792, m + "avgpool_1a");
     b.avgpool(x, pool);
     b.head(pool);
+    b.projection();
 }
 
 // ------------------------------------------------------------------ execution
@@ -670,6 +727,20 @@ int reserve(fr_handle* h, int maxB) {
     h->partial = (float*)p;
     h->partial_floats = need;
     h->max_batch = maxB;
+    if (h->dtype == FR_DTYPE_FP8) {
+        void* q = nullptr;
+        rc = dev_alloc(&q, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float));
+        if (rc) { free_acts(h); return rc; }
+        h->act_allocs.push_back(q);
+        h->amax = (float*)q;
+    }
+    if (h->proj_d) {
+        void* q = nullptr;
+        rc = dev_alloc(&q, (size_t)maxB * h->embed_dim * sizeof(float));
+        if (rc) { free_acts(h); return rc; }
+        h->act_allocs.push_back(q);
+        h->emb_pre = (float*)q;
+    }
     return fill_stage_dbg(h);
 }
 
@@ -789,10 +860,17 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     a.dbg = conv_dbg();
     ProfScope ps(h, s);
     ps.flops = conv_flops(a);
+    if (a.w8) {  // FR_DTYPE_FP8 conv (conv_fp8.hip)
+        a.tile = conv_fp8_tile(a.M, a.Cout);
+        a.split_k = 1;
+        ps.start("conv_fp8 tile" + std::to_string(a.tile), &a);
+        FR_HIP_CHECK(launch_conv_fp8(a, s));
+        return FR_OK;
+    }
     int TH, variant;
     // auto policy (measured, profiles/r01_tile_sweep.txt): the software-pipelined row-band variants
     // (3: 14x14, 4: 28x28) beat the implicit GEMM; the legacy 8-wave variants do not
-    if (band_enabled() && band_plan(a, &TH, &variant) && variant >= 3) {
+    if (band_enabled() && !a.y_amax && band_plan(a, &TH, &variant) && variant >= 3) {
         ps.start("conv3x3_band W" + std::to_string(a.W) + " v" + std::to_string(variant), &a);
         FR_HIP_CHECK(launch_conv_band(a, TH, variant, s));
         return FR_OK;
@@ -820,6 +898,7 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
 
 int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
     const int f16 = h->dtype == FR_DTYPE_F16;
+    if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s));
     for (const auto& op : h->ops) {
         if (op.kind == OP_STAGE ? !h->use_stage : (op.stage >= 0 && h->use_stage)) continue;
         switch (op.kind) {
@@ -865,6 +944,14 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                     a.y2 = h->tensors[op.out2].dev; a.Cy2 = h->tensors[op.out2].C; a.y2_off = 0;
                     a.aff_s = cw.aff_s; a.aff_b = cw.aff_b;
                 }
+                if (h->amax) {
+                    a.y_amax = h->amax + (size_t)op.out * FR_AMAX_SLOTS;
+                    a.amax_slots = FR_AMAX_SLOTS;
+                    if (cw.w8 && op.in_off == 0) {
+                        a.w8 = cw.w8; a.wscale = cw.wscale; a.Kpad = cw.Kpad8;
+                        a.x_amax = h->amax + (size_t)op.in * FR_AMAX_SLOTS;
+                    }
+                }
                 int rc = run_conv_args(h, a, s);
                 if (rc) return rc;
                 break;
@@ -903,8 +990,14 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.split_k = split;
                 a.partial = h->partial;
                 FR_HIP_CHECK(launch_conv(a, s));
-                FR_HIP_CHECK(launch_head_finalize(h->partial, split, B, cw.Cout, cw.Npad, cw.bias,
-                                                  (flags & FR_EMBED_RAW) ? 0 : 1, out, s));
+                if (h->proj_d) {  // IRV1 L2 (always: InceptionResnetV1 classify=False) -> projection -> L2
+                    FR_HIP_CHECK(launch_head_finalize(h->partial, split, B, cw.Cout, cw.Npad, cw.bias, 1, h->emb_pre, s));
+                    FR_HIP_CHECK(launch_proj_l2(h->emb_pre, B, cw.Cout, h->proj_w, h->proj_b, h->proj_d,
+                                                (flags & FR_EMBED_RAW) ? 0 : 1, out, s));
+                } else {
+                    FR_HIP_CHECK(launch_head_finalize(h->partial, split, B, cw.Cout, cw.Npad, cw.bias,
+                                                      (flags & FR_EMBED_RAW) ? 0 : 1, out, s));
+                }
                 break;
             }
         }
@@ -928,7 +1021,7 @@ static bool stage_default() {
 }
 
 int fr_create(fr_handle** out, int device, int arch, int dtype) {
-    if (!out || !valid_arch(arch) || (dtype != FR_DTYPE_BF16 && dtype != FR_DTYPE_F16)) {
+    if (!out || !valid_arch(arch) || (dtype != FR_DTYPE_BF16 && dtype != FR_DTYPE_F16 && dtype != FR_DTYPE_FP8)) {
         set_error("fr_create: bad argument (arch/dtype)");
         return FR_ERR_ARG;
     }
@@ -1001,7 +1094,7 @@ int fr_reserve(fr_handle* h, int max_batch) {
     return reserve(h, max_batch);
 }
 
-int fr_embed_dim(const fr_handle* h) { return h ? h->embed_dim : 0; }
+int fr_embed_dim(const fr_handle* h) { return h ? (h->proj_d ? h->proj_d : h->embed_dim) : 0; }
 int fr_input_size(const fr_handle* h) { return h ? h->in_size : 0; }
 
 static bool graphs_enabled() {
@@ -1342,6 +1435,19 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
     a.y = (bf16_t*)d->y; a.Cy = d->Cy; a.y_off = d->y_off;
     a.y2 = (bf16_t*)d->y2; a.Cy2 = d->Cy2; a.y2_off = d->y2_off; a.aff_s = d->aff_s; a.aff_b = d->aff_b;
     a.f16 = d->dtype == FR_DTYPE_F16;
+    a.y_amax = d->y_amax;
+    a.amax_slots = 1;
+    if (d->dtype == FR_DTYPE_FP8) {
+        if (!d->wscale || !d->x_amax || d->Cin % 64 || d->Kpad % 128 || d->split_k > 1) {
+            set_error("fr_op_conv2d: fp8 needs wscale, x_amax, Cin % 64 == 0, Kpad % 128 == 0, no split-K");
+            return FR_ERR_ARG;
+        }
+        a.w8 = (const uint8_t*)d->w; a.wscale = d->wscale; a.x_amax = d->x_amax;
+        a.tile = conv_fp8_tile(a.M, a.Cout);
+        if (d->tile > 0) a.tile = d->tile - 1;
+        FR_HIP_CHECK(launch_conv_fp8(a, (hipStream_t)stream));
+        return FR_OK;
+    }
     if (d->tile == FR_TILE_BAND + 1) {
         int TH, variant;
         if (!band_plan(a, &TH, &variant)) { set_error("fr_op_conv2d: band kernel not applicable"); return FR_ERR_ARG; }

@@ -27,7 +27,19 @@ struct ConvArgs {
     int dbg;                      // experiment switches (FR_CONV_DBG env; 0 in production)
     void* ev0;                    // optional hipEvent_t pair stamped by the dispatch itself
     void* ev1;                    //   (hipExtLaunchKernel; fr_prof_* timing), null normally
+    // fp8 path (conv_fp8.hip): e4m3 weights [Npad][Kpad] (Kpad = bytes per row, % 128), per-channel
+    // scale, dynamic per-tensor amax of the input (power-of-two activation scale) and of the output
+    const uint8_t* w8;
+    const float* wscale;
+    const float* x_amax;
+    float* y_amax;                // non-null: the epilogue atomically records max |y| (both dtypes)
+    int amax_slots;               // x_amax / y_amax are arrays of this many partial maxima (block % slots)
 };
+constexpr int FR_AMAX_SLOTS = 64;  // engine: spreads the producers' atomics over 64 addresses
+
+// FP8 (e4m3 x e4m3, v_mfma_scale_f32_16x16x128_f8f6f4) implicit GEMM; Cin % 64 == 0.
+int conv_fp8_tile(int M, int Cout);
+hipError_t launch_conv_fp8(const ConvArgs& a, hipStream_t s);
 
 // Choose tile variant and split-K factor for a GEMM of M x Cout x Kpad.
 bool conv_tile_forced();
@@ -79,6 +91,9 @@ hipError_t launch_avgpool(const bf16_t* x, int B, int H, int W, int C, bf16_t* y
 // Sum split-K partials [split][B][Npad] + bias, optional L2 normalize → out [B][N] f32.
 hipError_t launch_head_finalize(const float* partial, int split, int B, int N, int Npad, const float* bias,
                                 int normalize, float* out, hipStream_t s);
+// FaceNet projection: out = x W^T + bias (f32), optional F.normalize (eps 1e-12).  K <= 1024.
+hipError_t launch_proj_l2(const float* x, int B, int K, const float* W, const float* bias, int N, int normalize,
+                          float* out, hipStream_t s);
 // Row-wise L2 normalize in place (F.normalize, eps 1e-12).
 hipError_t launch_l2norm_rows(float* x, int B, int D, hipStream_t s);
 

@@ -165,7 +165,38 @@ __global__ __launch_bounds__(256) void gallery_prepare_kernel(float* __restrict_
     for (int d = threadIdx.x; d < D; d += 256) row[d] *= inv;
 }
 
+// FaceNetModel.projection + F.normalize (facenet_model.py:32-35): out[b] = W x[b] + bias (f32), then
+// out[b] / max(||out[b]||, 1e-12) when normalize.  x rows are the already L2-normalized IRV1 outputs.
+__global__ __launch_bounds__(256) void proj_l2_kernel(const float* x, int K, const float* W, const float* bias, int N,
+                                                      int normalize, float* out) {
+    __shared__ float xs[1024];
+    __shared__ float red[8];
+    const int b = blockIdx.x;
+    for (int k = threadIdx.x; k < K; k += 256) xs[k] = x[(size_t)b * K + k];
+    __syncthreads();
+    float ss = 0.f;
+    for (int n = threadIdx.x; n < N; n += 256) {
+        const float* w = W + (size_t)n * K;
+        float acc = 0.f;
+        for (int k = 0; k < K; ++k) acc = fmaf(w[k], xs[k], acc);
+        acc += bias ? bias[n] : 0.f;
+        out[(size_t)b * N + n] = acc;
+        ss += acc * acc;
+    }
+    if (!normalize) return;
+    const float inv = 1.0f / fmaxf(sqrtf(block_sum_256(ss, red)), 1e-12f);
+    __syncthreads();
+    for (int n = threadIdx.x; n < N; n += 256) out[(size_t)b * N + n] *= inv;
+}
+
 }  // namespace
+
+hipError_t launch_proj_l2(const float* x, int B, int K, const float* W, const float* bias, int N, int normalize,
+                          float* out, hipStream_t s) {
+    if (K > 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(proj_l2_kernel, dim3(B), dim3(256), 0, s, x, K, W, bias, N, normalize, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_preprocess(const void* in, int in_fmt, int B, int H, int W, bf16_t* out, int f16, hipStream_t s) {
     const int npix = B * H * W;

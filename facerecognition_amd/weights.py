@@ -348,10 +348,31 @@ def fold_state_dict(arch: str, sd) -> Dict[str, np.ndarray]:
         W = _np(sd[m + "last_linear.weight"]).astype(np.float64)
         out["head.w"] = (sl[:, None] * W).astype(np.float32)
         out["head.b"] = tl.astype(np.float32)
-        if "projection.weight" in sd:
-            raise NotImplementedError("FaceNet projection (embedding_size != 512) is not yet on the native path")
+        if "projection.weight" in sd:  # FaceNetModel.projection (facenet_model.py:20-23,32-33), after IRV1's L2
+            out["proj.w"] = _np(sd["projection.weight"]).astype(np.float32)
+            out["proj.b"] = _np(sd["projection.bias"]).astype(np.float32)
     else:
         raise ValueError(arch)
+    return out
+
+
+def quantize_fp8(folded: Dict[str, np.ndarray], min_cin: int = 64) -> Dict[str, np.ndarray]:
+    """FR_DTYPE_FP8 weights (BASELINE config 5): every folded conv weight "<name>.w" [Cout, kh, kw, Cin]
+    with Cin % 64 == 0 becomes per-output-channel scaled OCP e4m3: s[o] = max|w[o]| / 448 (f32),
+    "<name>.w" = e4m3(w / s) as exactly representable f32 values (torch.float8_e4m3fn cast, RNE,
+    saturating), "<name>.wscale" = s.  The stem (Cin 3) and the 2-D head stay bf16.  Dequantized
+    weight = w * s.  Biases, border-class tables and PReLU slopes are unchanged."""
+    import torch
+    out = dict(folded)
+    for k, w in folded.items():
+        if not k.endswith(".w") or w.ndim != 4 or w.shape[3] % min_cin != 0:
+            continue
+        w64 = np.asarray(w, dtype=np.float32)
+        amax = np.abs(w64).reshape(w64.shape[0], -1).max(axis=1)
+        s = np.where(amax > 0, amax / 448.0, 1.0).astype(np.float32)
+        q = torch.from_numpy(w64 / s[:, None, None, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+        out[k] = q.to(torch.float32).numpy()
+        out[k[:-2] + ".wscale"] = s
     return out
 
 

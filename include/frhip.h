@@ -38,6 +38,11 @@ extern "C" {
 
 /* ---- compute dtypes ---- */
 #define FR_DTYPE_BF16 0 /* bf16 activations/weights, f32 accumulate (v_mfma_f32_16x16x32_bf16) */
+#define FR_DTYPE_FP8 2  /* BASELINE config 5: e4m3 weights (per-output-channel scale) x e4m3 activations
+                         * (dynamic per-tensor power-of-two scale) on v_mfma_scale_f32_16x16x128_f8f6f4,
+                         * f32 accumulate; activations stay bf16 in memory (residual stream at bf16);
+                         * the stem and the 25088->512 head stay bf16.  Weight blob convs carrying
+                         * "<name>.wscale" run fp8 (values in "<name>.w" must be e4m3-representable). */
 #define FR_DTYPE_F16 1  /* f16 activations/weights, f32 accumulate (v_mfma_f32_16x16x32_f16): same MFMA
                            rate, 3 more mantissa bits; stores saturate at +-65504 */
 
@@ -144,6 +149,13 @@ typedef struct fr_conv_desc {
      * 3*rc + cc with rc = 0 / 1 / 2 for output row 0 / interior / Ho-1 (cc likewise for columns).
      * When set it replaces `bias`.  NULL otherwise. */
     const float* bias9;
+    /* dtype == FR_DTYPE_FP8: w is e4m3 bytes [Npad][Kpad] (Kpad % 128 == 0, Cin % 64 == 0), wscale [Npad]
+     * per-output-channel f32 scales, x_amax -> the input's max |x| (device f32; the activation scale is
+     * the power of two 2^e with max|x| / 2^e <= 448); x, res, y, y2 are bf16.  y_amax (any dtype, may
+     * be NULL): the epilogue atomically raises it to max |y| of what it stores (caller zeroes it). */
+    const float* wscale;
+    const float* x_amax;
+    float* y_amax;
 } fr_conv_desc;
 
 /* conv tile variants (pixels x channels per 256-thread block) */

@@ -301,7 +301,10 @@ def build_model(arch: str, state_dict=None, num_classes: int = 100) -> nn.Module
     elif arch == "iresnet100":
         m = IResNet100()
     elif arch == "irv1_facenet":
-        m = FaceNetModel()
+        emb = 512
+        if state_dict is not None and "projection.weight" in state_dict:
+            emb = int(np.asarray(state_dict["projection.weight"]).shape[0])
+        m = FaceNetModel(embedding_size=emb)
     else:
         raise ValueError(arch)
     if state_dict is not None:

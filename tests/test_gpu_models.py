@@ -147,3 +147,30 @@ def test_repeated_calls_replay_identically(gpu):
     e2 = m.embed(x2.clone())
     torch.cuda.synchronize()
     assert torch.equal(out, e2) and not torch.equal(out, ref)
+
+
+def test_facenet_projection_head(gpu):
+    """FaceNetModel with embedding_size=128 (projection Linear(512,128) + F.normalize after IRV1's own
+    L2, facenet_model.py:20-23,32-35) vs the oracle, and the raw (pre-normalize) projection output."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.weights import synth_state_dict
+    from oracle import models as M
+    sd = synth_state_dict("irv1_facenet", embedding_size=128)
+    m = FRModel("irv1_facenet", sd)
+    assert m.embedding_size == 128
+    u8 = _probes("irv1_facenet", 4, seed=2)
+    got = m.embed(torch.from_numpy(u8)).cpu().numpy()
+    om = M.build_model("irv1_facenet", sd)
+    ref = M.embed(om, "irv1_facenet", u8)
+    assert got.shape == ref.shape == (4, 128)
+    cos = np.sum(got * ref, axis=1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(ref, axis=1))
+    assert np.all(1 - cos <= COS_TOL), f"projection: 1-cos = {1 - cos}"
+    assert np.allclose(np.linalg.norm(got, axis=1), 1, atol=1e-5)
+    raw = m.embed(torch.from_numpy(u8), normalize=False).cpu().numpy()
+    with torch.no_grad():
+        e = om.model(M.preprocess_u8_nhwc(u8))
+        raw_ref = om.projection(e).numpy()
+    cos = np.sum(raw * raw_ref, axis=1) / (np.linalg.norm(raw, axis=1) * np.linalg.norm(raw_ref, axis=1))
+    assert np.all(1 - cos <= COS_TOL)
+    assert np.allclose(np.linalg.norm(raw, axis=1), np.linalg.norm(raw_ref, axis=1), rtol=2e-2)
+    m.close()

@@ -76,3 +76,39 @@ def test_blob_round_trip_sizes():
     f = W.fold_state_dict("iresnet100", W.synth_state_dict("iresnet100", seed=1, calibrated=False))
     blob = W.pack_blob(f)
     assert blob[:4] == b"FRW1" and int.from_bytes(blob[4:8], "little") == len(f)
+
+
+def test_facenet_projection_fold_and_oracle():
+    """FaceNetModel(embedding_size=128): projection.{weight,bias} pass through as proj.{w,b}; the oracle
+    builds the projection from the state_dict (facenet_model.py:20-23,32-35)."""
+    from oracle import models as M
+    sd = W.synth_state_dict("irv1_facenet", embedding_size=128)
+    out = W.fold_state_dict("irv1_facenet", sd)
+    assert out["proj.w"].shape == (128, 512) and out["proj.b"].shape == (128,)
+    np.testing.assert_array_equal(out["proj.w"], sd["projection.weight"])
+    m = M.build_model("irv1_facenet", sd)
+    assert m.projection is not None and m.projection.out_features == 128
+    x = torch.randn(3, 512)
+    e = torch.nn.functional.normalize(x, dim=1)
+    ref = torch.nn.functional.normalize(m.projection(e), dim=1)
+    got = torch.nn.functional.normalize(e @ torch.tensor(out["proj.w"]).T + torch.tensor(out["proj.b"]), dim=1)
+    assert torch.allclose(got, ref, atol=1e-6)
+
+
+def test_quantize_fp8_weights():
+    """quantize_fp8: per-output-channel scale = max|w| / 448, values e4m3-representable, dequant error
+    within half an e4m3 ulp (2^-4 relative for normals), stem and head untouched."""
+    sd = W.synth_state_dict("iresnet100")
+    f = W.fold_state_dict("iresnet100", sd)
+    q = W.quantize_fp8(f)
+    assert "conv1.wscale" not in q and "head.wscale" not in q
+    k = "layer3.5.conv2"
+    w, qw, s = f[k + ".w"], q[k + ".w"], q[k + ".wscale"]
+    assert s.shape == (w.shape[0],) and np.allclose(s, np.abs(w).reshape(w.shape[0], -1).max(1) / 448)
+    rt = torch.from_numpy(qw).to(torch.float8_e4m3fn).float().numpy()
+    assert np.array_equal(rt, qw)                       # exactly representable
+    assert np.abs(qw).max() <= 448
+    deq = qw * s[:, None, None, None]
+    # half an ulp: 2^-4 relative for normals, 2^-10 (scaled) absolute in the subnormal range
+    bound = 2 ** -4 * np.abs(w) + 2 ** -10 * s[:, None, None, None] * (1 + 1e-5)
+    assert np.all(np.abs(deq - w) <= bound + 1e-12)

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Match-kernel timing at the BASELINE config-4 shapes: per rank, all gathered
+probes (B_total = 8 x 256 = 2048) against one 1M/8 = 125k-row gallery shard, top-5; plus the
+single-GPU whole-gallery case (256 x 1M).  HIP events around fr_match_topk on the launching stream.
+
+    python tools/match_bench.py [--rows 125000 --probes 2048] [--iters 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(rows, probes, k, iters):
+    from facerecognition_amd.gallery import DeviceGallery
+    g = torch.randn(rows, 512, device="cuda")
+    g = g / g.norm(dim=1, keepdim=True)
+    p = torch.randn(probes, 512, device="cuda")
+    p = p / p.norm(dim=1, keepdim=True)
+    gal = DeviceGallery(handle=None)
+    gal.set_device_rows(g)
+    for _ in range(3):
+        gal.search_device(p, k)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        s, i = gal.search_device(p, k)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    # exactness spot check against torch f32 on the GPU (ties aside): top-1 indices
+    ref = (p[:64] @ g.T).argmax(dim=1)
+    agree = float((i[:64, 0] == ref).float().mean())
+    flop = 2.0 * probes * rows * 512
+    gbytes = rows * 512 * 4 / 1e9
+    return {"rows": rows, "probes": probes, "k": k, "ms": round(ms, 4), "tflops_f32": round(flop / ms / 1e9, 2),
+            "gallery_GBps": round(gbytes / ms * 1e3, 1), "top1_agree_torch": agree}
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--k", type=int, default=5)
+    a = ap.parse_args()
+    for rows, probes in ((10000, 256), (125000, 2048), (1000000, 256)):
+        print(json.dumps(run(rows, probes, a.k, a.iters)), flush=True)
