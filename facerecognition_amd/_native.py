@@ -11,7 +11,8 @@ import os
 import re
 import threading
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libfrhip.so")
+LIB_PATH = os.environ.get("FR_LIBFRHIP") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                          "libfrhip.so")  # env: timing-experiment builds
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "frhip.h")
 
 FR_OK = 0
@@ -26,6 +27,8 @@ FR_EMBED_RAW = 1
 FR_TILE_BAND = 7
 FR_OPT_STAGE = 1
 FR_OPT_KEEP_INTERMEDIATES = 2
+FR_OPT_MATCH_EXACT = 3
+FR_OPT_X3_MIN_ROWS = 4
 
 c_int, c_int64, c_size_t, c_void_p, c_float_p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p
 
@@ -65,6 +68,7 @@ _SIGS = {
     "fr_segment_mean_normalize": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "fr_set_option": (c_int, [c_void_p, c_int, c_int]),
     "fr_get_option": (c_int, [c_void_p, c_int]),
+    "fr_debug_match_fallbacks": (c_int, [c_void_p]),
     "fr_debug_tensor_count": (c_int, [c_void_p]),
     "fr_debug_plan": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t]),
     "fr_prof_enable": (c_int, [c_void_p, c_int]),

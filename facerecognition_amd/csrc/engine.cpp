@@ -101,6 +101,11 @@ struct fr_handle {
     int64_t g_rows = 0;
     int g_dim = 0;
     int64_t g_base = 0;
+    bf16_t* g_hi = nullptr;  // bf16 hi/lo split of the prepared gallery (match_x3.hip), N >= X3_MIN_ROWS
+    bf16_t* g_lo = nullptr;
+    int* match_fb = nullptr;  // device counter of exact-rescan fallbacks (fr_debug_match_fallbacks)
+    bool match_exact = false; // FR_OPT_MATCH_EXACT: always the f32-MFMA kernel
+    int64_t x3_min_rows = X3_MIN_ROWS;  // FR_OPT_X3_MIN_ROWS
     float* cand_s = nullptr;
     int32_t* cand_i = nullptr;
     size_t cand_cap = 0;
@@ -1049,6 +1054,9 @@ void fr_destroy(fr_handle* h) {
     free_acts(h);
     free_weights(h);
     if (h->gallery) (void)hipFree(h->gallery);
+    if (h->g_hi) (void)hipFree(h->g_hi);
+    if (h->g_lo) (void)hipFree(h->g_lo);
+    if (h->match_fb) (void)hipFree(h->match_fb);
     if (h->cand_s) (void)hipFree(h->cand_s);
     if (h->cand_i) (void)hipFree(h->cand_i);
     drop_graphs(h);
@@ -1192,6 +1200,8 @@ int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index
     std::lock_guard<std::mutex> lk(h->mu);
     FR_HIP_CHECK(hipSetDevice(h->device));
     if (h->gallery) { (void)hipFree(h->gallery); h->gallery = nullptr; }
+    if (h->g_hi) { (void)hipFree(h->g_hi); h->g_hi = nullptr; }
+    if (h->g_lo) { (void)hipFree(h->g_lo); h->g_lo = nullptr; }
     h->g_rows = 0;
     if (N > 0) {
         void* p = nullptr;
@@ -1201,6 +1211,16 @@ int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index
         FR_HIP_CHECK(hipMemcpy(p, G, (size_t)N * D * sizeof(float),
                                g_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
         FR_HIP_CHECK(launch_gallery_prepare(h->gallery, N, D, nullptr));
+        if (N >= h->x3_min_rows && D == 512) {  // bf16 hi/lo copy for the candidate pass (match_x3.hip)
+            int rc2 = dev_alloc((void**)&h->g_hi, (size_t)N * D * sizeof(bf16_t));
+            if (!rc2) rc2 = dev_alloc((void**)&h->g_lo, (size_t)N * D * sizeof(bf16_t));
+            if (!rc2 && !h->match_fb) {
+                rc2 = dev_alloc((void**)&h->match_fb, sizeof(int));
+                if (!rc2) FR_HIP_CHECK(hipMemset(h->match_fb, 0, sizeof(int)));
+            }
+            if (rc2) return rc2;
+            FR_HIP_CHECK(launch_split_bf16(h->gallery, (size_t)N * D, h->g_hi, h->g_lo, nullptr));
+        }
         FR_HIP_CHECK(hipDeviceSynchronize());
     }
     h->g_rows = N;
@@ -1211,6 +1231,21 @@ int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index
 
 int64_t fr_gallery_rows(const fr_handle* h) { return h ? h->g_rows : 0; }
 
+static int ensure_cand(fr_handle* h, size_t need) {
+    if (need <= h->cand_cap) return FR_OK;
+    if (h->cand_s) (void)hipFree(h->cand_s);
+    if (h->cand_i) (void)hipFree(h->cand_i);
+    h->cand_s = nullptr;
+    h->cand_i = nullptr;
+    h->cand_cap = 0;
+    int rc = dev_alloc((void**)&h->cand_s, need * sizeof(float));
+    if (rc) return rc;
+    rc = dev_alloc((void**)&h->cand_i, need * sizeof(int32_t));
+    if (rc) return rc;
+    h->cand_cap = need;
+    return FR_OK;
+}
+
 static int match_locked(fr_handle* h, const float* P, int B, int k, float* scores, int32_t* idx, void* stream) {
     if (!P || !scores || !idx || B <= 0 || k <= 0 || k > 16) {
         set_error("fr_match_topk: bad argument (1 <= k <= 16)");
@@ -1218,23 +1253,20 @@ static int match_locked(fr_handle* h, const float* P, int B, int k, float* score
     }
     if (!h->gallery || h->g_rows <= 0) { set_error("fr_match_topk: no gallery"); return FR_ERR_STATE; }
     FR_HIP_CHECK(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
     int n_split;
     int64_t rps;
-    match_split_plan(B, h->g_rows, &n_split, &rps);
-    const size_t need = (size_t)B * n_split * k;
-    if (need > h->cand_cap) {
-        if (h->cand_s) (void)hipFree(h->cand_s);
-        if (h->cand_i) (void)hipFree(h->cand_i);
-        h->cand_s = nullptr;
-        h->cand_i = nullptr;
-        h->cand_cap = 0;
-        int rc = dev_alloc((void**)&h->cand_s, need * sizeof(float));
+    if (h->g_hi && !h->match_exact) {  // bf16x3 candidates + exact f32 rescoring (match_x3.hip)
+        match_x3_plan(B, h->g_rows, &n_split, &rps);
+        int rc = ensure_cand(h, (size_t)B * n_split * match_x3_candidates());
         if (rc) return rc;
-        rc = dev_alloc((void**)&h->cand_i, need * sizeof(int32_t));
-        if (rc) return rc;
-        h->cand_cap = need;
+        FR_HIP_CHECK(launch_match_x3(P, B, h->gallery, h->g_hi, h->g_lo, h->g_rows, h->g_dim, k, h->g_base, h->cand_s,
+                                     h->cand_i, n_split, rps, scores, idx, h->match_fb, s));
+        return FR_OK;
     }
-    hipStream_t s = (hipStream_t)stream;
+    match_split_plan(B, h->g_rows, &n_split, &rps);
+    int rc = ensure_cand(h, (size_t)B * n_split * k);
+    if (rc) return rc;
     FR_HIP_CHECK(launch_match_topk(P, B, h->gallery, h->g_rows, h->g_dim, k, h->g_base, h->cand_s, h->cand_i,
                                    n_split, rps, s));
     FR_HIP_CHECK(launch_topk_merge(h->cand_s, h->cand_i, B, n_split, k, scores, idx, s));
@@ -1318,6 +1350,11 @@ int fr_set_option(fr_handle* h, int option, int value) {
     switch (option) {
         case FR_OPT_STAGE: h->use_stage = value != 0; break;
         case FR_OPT_KEEP_INTERMEDIATES: h->keep_inter = value != 0; break;
+        case FR_OPT_MATCH_EXACT: h->match_exact = value != 0; break;
+        case FR_OPT_X3_MIN_ROWS:
+            if (value < 1) { set_error("fr_set_option: FR_OPT_X3_MIN_ROWS must be >= 1"); return FR_ERR_ARG; }
+            h->x3_min_rows = value;
+            break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;
     }
     drop_graphs(h);  // captured replays bake in the plan
@@ -1329,8 +1366,21 @@ int fr_get_option(const fr_handle* h, int option) {
     switch (option) {
         case FR_OPT_STAGE: return h->use_stage && !h->stages.empty() ? 1 : 0;
         case FR_OPT_KEEP_INTERMEDIATES: return h->keep_inter ? 1 : 0;
+        case FR_OPT_MATCH_EXACT: return h->match_exact ? 1 : 0;
+        case FR_OPT_X3_MIN_ROWS: return (int)h->x3_min_rows;
         default: return FR_ERR_ARG;
     }
+}
+
+int fr_debug_match_fallbacks(fr_handle* h) {
+    if (!h) return FR_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->match_fb) return 0;
+    int v = 0;
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    FR_HIP_CHECK(hipDeviceSynchronize());
+    FR_HIP_CHECK(hipMemcpy(&v, h->match_fb, sizeof(int), hipMemcpyDeviceToHost));
+    return v;
 }
 
 int fr_prof_enable(fr_handle* h, int on) {

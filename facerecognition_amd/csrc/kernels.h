@@ -103,6 +103,14 @@ hipError_t launch_match_topk(const float* P, int B, const float* G, int64_t N, i
                              int64_t rows_per_split, hipStream_t s);
 hipError_t launch_topk_merge(const float* cs, const int32_t* ci, int B, int n_lists, int k, float* out_s,
                              int32_t* out_i, hipStream_t s);
+// Large-gallery match (match_x3.hip): bf16x3 candidates, exact f32 rescoring with a proof / fallback.
+constexpr int64_t X3_MIN_ROWS = 32768;  // below: the exact f32 kernel is as fast (10k x 256: 0.105 vs 0.16 ms)
+hipError_t launch_split_bf16(const float* G, size_t n, bf16_t* hi, bf16_t* lo, hipStream_t s);
+void match_x3_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split);
+int match_x3_candidates();
+hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* Gh, const bf16_t* Gl, int64_t N, int D,
+                           int k, int64_t index_base, float* cand_s, int32_t* cand_i, int n_split,
+                           int64_t rows_per_split, float* out_s, int32_t* out_i, int* n_fallback, hipStream_t s);
 // Choose n_split / rows_per_split for a (B, N) match.
 void match_split_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split);
 hipError_t launch_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, int n_seg,

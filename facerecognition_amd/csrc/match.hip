@@ -111,11 +111,24 @@ __global__ __launch_bounds__(256) void match_partial_kernel(const float* __restr
             for (int r = 0; r < 4; ++r)
                 sS[(16 * wave + 4 * (lane >> 4) + r) * (MG + 1) + 16 * j + (lane & 15)] = acc[j][r];
         __syncthreads();
-#pragma unroll 4
-        for (int i = 0; i < 16; ++i) {
-            const int g = my_sub * 16 + i;
-            const int64_t gr = t0 + g;
-            if (gr < g_end) topk_insert<KMAX>(ls, li, sS[my_p * (MG + 1) + g], (int)(gr + index_base));
+        // filter against this lane's current K-th best first: after the lists fill almost no score
+        // qualifies, and the (divergent) sorted insert runs only for the few that do
+        {
+            const float thr = ls[KMAX - 1];
+            const int thri = li[KMAX - 1];
+            uint32_t mask = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int g = my_sub * 16 + i;
+                if (t0 + g < g_end && better(sS[my_p * (MG + 1) + g], (int)(t0 + g + index_base), thr, thri))
+                    mask |= 1u << i;
+            }
+            while (mask) {
+                const int i = __builtin_ctz(mask);
+                mask &= mask - 1;
+                const int g = my_sub * 16 + i;
+                topk_insert<KMAX>(ls, li, sS[my_p * (MG + 1) + g], (int)(t0 + g + index_base));
+            }
         }
         __syncthreads();
     }

@@ -1,0 +1,471 @@
+// Fast exact gallery match for large galleries (BASELINE config 4: 2048 probes x a 125k-row shard of a
+// 1M x 512 gallery per rank).  The exact f32 path (match.hip, v_mfma_f32_16x16x4_f32) runs at the f32
+// MFMA rate, 1/16 of bf16.  Here:
+//   1. candidates: s~ = Ph.Gh + Ph.Gl + Pl.Gh on v_mfma_f32_16x16x32_bf16 (x = xh + xl, both bf16: a
+//      3-product split), |s~ - s| <= eps = 1.25e-4 ||p|| ||g|| (split error 3 * 2^-16 plus two f32
+//      accumulations of 512 terms, worst case); per (probe, split) the top-KO by s~ of four sub-lists
+//      of KP (rows 16j + 4 sub + r of each tile, kept by the lane whose accumulators hold them) and a floor: every row dropped from a sub-list, or by the
+//      filter, has s~ <= floor = the best last entry of the full sub-lists;
+//   2. rescore (one wave per probe): the global top-KC by s~ are rescored exactly with the k-ordered f32
+//      fmaf chain of the exact kernel (same order, so the scores are bit-identical to match.hip) and
+//      the top-k is taken by (score desc, index asc);
+//   3. proof: every row outside the KC candidates has s~ <= T (the KC-th candidate's s~, or the largest
+//      floor if higher), so its exact
+//      score is <= T + eps.  Unless the k-th exact score exceeds T + 2 eps (i.e. more than KC - k rows tie
+//      with it within 2 eps), the wave rescans the whole gallery exactly for that probe (counted).  The
+//      result is therefore always the exact top-k of the f32 scores.
+// Block = 8 waves, 128 probes; each wave keeps its 16 probes' bf16 hi/lo fragments in registers for the
+// whole kernel; gallery hi/lo chunks (64 rows x 64 dims, 16 KiB) stream through a 7-slot LDS-DMA ring
+// six chunks ahead (counted vmcnt, raw barriers; XOR-swizzled 16-B chunks): the ring depth, not HBM,
+// sets the stream rate (in flight / L2 latency).  Blocks of one gallery split share an XCD (xcd_remap), so each XCD streams its
+// splits from HBM once and the other probe blocks hit its L2.
+#include "kernels.h"
+
+#include <float.h>
+#include <stdlib.h>
+#include <limits.h>
+
+namespace fr {
+namespace {
+
+#ifndef FR_X3_EXP
+#define FR_X3_EXP 0  // timing experiments only (tools/x3_exp.sh); 0 in every shipped build
+#endif
+
+constexpr int XW = 8;         // waves per block
+constexpr int XP = 16 * XW;   // probes per block
+constexpr int XG = 64;        // gallery rows per tile
+constexpr int XC = 64;        // dims per LDS chunk
+constexpr int XD = 512;       // embedding dim (the kernel is specialised)
+constexpr int KP = 8;         // candidates per (probe, split, sub-lane): 4 sub-lanes per probe
+constexpr int KO = 16;        // candidates written per (probe, split) ...
+constexpr int KS = KO + 1;    // ... plus one floor entry (index -2)
+constexpr int KC = 16;        // candidates rescored per probe
+
+__device__ __forceinline__ bool better(float s1, int i1, float s2, int i2) {
+    return s1 > s2 || (s1 == s2 && i1 < i2);
+}
+
+template <int KMAX>
+__device__ __forceinline__ void insert(float (&ls)[KMAX], int (&li)[KMAX], float s, int idx) {
+    if (!better(s, idx, ls[KMAX - 1], li[KMAX - 1])) return;
+    float cs = s;
+    int ci = idx;
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {
+        if (better(cs, ci, ls[q], li[q])) {
+            const float ts = ls[q];
+            const int ti = li[q];
+            ls[q] = cs;
+            li[q] = ci;
+            cs = ts;
+            ci = ti;
+        }
+    }
+}
+
+// score-only sorted insert for the candidate scan (ties with the last entry are dropped: the floor
+// covers them)
+template <int KMAX>
+__device__ __forceinline__ void insert_s(float (&ls)[KMAX], int (&li)[KMAX], float s, int idx) {
+    if (!(s > ls[KMAX - 1])) return;
+    float cs = s;
+    int ci = idx;
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {
+        const bool b = cs > ls[q];
+        const float ts = ls[q];
+        const int ti = li[q];
+        ls[q] = b ? cs : ts;
+        li[q] = b ? ci : ti;
+        cs = b ? ts : cs;
+        ci = b ? ti : ci;
+    }
+}
+
+__device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+// G (f32 [N][D]) -> Gh, Gl (bf16): g = gh + gl + r, |r| <= 2^-16 |g|
+__global__ __launch_bounds__(256) void split_bf16_kernel(const float* __restrict__ G, size_t n, bf16_t* __restrict__ hi,
+                                                         bf16_t* __restrict__ lo) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float g = G[i];
+        const uint16_t h = bf16_bits(g);
+        hi[i] = h;
+        lo[i] = bf16_bits(g - __uint_as_float((uint32_t)h << 16));
+    }
+}
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
+
+constexpr int XSLOT = 7;                       // LDS ring depth (chunks): XSLOT - 1 in flight
+constexpr int XCHUNK_B = 2 * XG * XC * 2;      // 16 KiB: [hi 64 rows x 128 B][lo 64 rows x 128 B]
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr uint32_t XOOB = 0x80000000u;
+
+__device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__ P, int B, const bf16_t* __restrict__ Gh,
+                                                       const bf16_t* __restrict__ Gl, int64_t N, int64_t index_base,
+                                                       int64_t rows_per_split, int n_split, int npb,
+                                                       float* __restrict__ cs, int32_t* __restrict__ ci) {
+    // ONE LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads)
+    __shared__ __attribute__((aligned(16))) char smem[XSLOT * XCHUNK_B];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: no waterfall around the DMAs
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = lid / npb, pb = lid - split * npb;
+    const int p0 = pb * XP;
+    const int64_t g_begin = (int64_t)split * rows_per_split;
+    const int64_t g_end = g_begin + rows_per_split < N ? g_begin + rows_per_split : N;
+
+    // probe fragments (the MFMA's B operand): k-step t (32 dims) of probe p0 + 16*wave + (lane&15),
+    // dims 32t + 8(lane>>4) .. +8
+    constexpr int KT = XD / 32;
+    bf8v ph[KT], pl[KT];
+    const int my_q = 16 * wave + (lane & 15);  // this lane's probe (block-local) ...
+    const int my_sub = lane >> 4;              // ... and sub-list: rows 16j + 4*my_sub + r of every tile
+    {
+        const int p = p0 + my_q;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (p < B) {
+                const float* src = P + (size_t)p * XD + 32 * t + 8 * (lane >> 4);
+                const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const __bf16 h = (__bf16)v[e];
+                ph[t][e] = h;
+                pl[t][e] = (__bf16)(v[e] - (float)h);
+            }
+        }
+    }
+
+    float ls[KP];
+    int li[KP];
+#pragma unroll
+    for (int q = 0; q < KP; ++q) { ls[q] = -INFINITY; li[q] = INT_MAX; }
+
+    // LDS-DMA of chunk (tile t0, dims 64c..): 16 pieces of 8 rows x 128 B (hi: pieces 0-7, lo: 8-15);
+    // wave w issues pieces 2w, 2w+1; the source 16-B chunk is XOR-swizzled (read side: xswz)
+    const uint32_t g_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)N * XD * 2);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)Gh, 0, g_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)Gl, 0, g_bytes, 0x00020000);
+    auto issue_chunk = [&](int64_t t0, int c, int slot) {
+#if FR_X3_EXP == 2  // timing experiment: no gallery stream
+        return;
+#endif
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int piece = 2 * wave + u, half = piece >> 3;
+            const int row = 8 * (piece & 7) + (lane >> 3);
+            const int cl = (lane & 7) ^ ((row >> 1) & 7);
+            const int64_t gr = t0 + row;
+            const uint32_t off = gr < g_end ? (uint32_t)((gr * XD + XC * c + 8 * cl) * 2) : XOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(half ? rl : rh, (lds_void*)(smem + slot * XCHUNK_B + piece * 1024),
+                                                     16, off, 0, 0, 0);
+        }
+    };
+    // prologue: the first XSLOT - 1 chunks (slots are uniform run-time values: one VALU add per chunk)
+    int64_t t_issue = g_begin;  // tile of the next chunk to issue
+    int c_issue = 0, s_issue = 0, s_read = 0;
+    auto issue_next = [&]() {
+        issue_chunk(t_issue, c_issue, s_issue);
+        if (++c_issue == XD / XC) { c_issue = 0; t_issue += XG; }
+        if (++s_issue == XSLOT) s_issue = 0;
+    };
+#pragma unroll
+    for (int i = 0; i < XSLOT - 1; ++i) issue_next();
+
+    for (int64_t t0 = g_begin; t0 < g_end; t0 += XG) {
+        f32x4_t acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < XD / XC; ++c) {
+            // chunk c landed (the XSLOT - 2 younger chunks' pieces may stay in flight); every wave is
+            // past chunk c-1, so its slot takes chunk c + XSLOT - 1
+            static_assert(XSLOT == 7, "vmcnt below counts 2 pieces x (XSLOT - 2) younger chunks");
+            asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+            issue_next();
+            const char* ch = smem + s_read * XCHUNK_B;
+            if (++s_read == XSLOT) s_read = 0;
+#pragma unroll
+            for (int tt = 0; tt < XC / 32; ++tt) {
+                const int t = c * (XC / 32) + tt;
+                const int kch = 4 * tt + (lane >> 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int row = 16 * j + (lane & 15);
+                    const int o = row * 128 + xswz(row, kch) * 16;
+                    const bf8v gh = *(const bf8v*)(ch + o);
+                    const bf8v gl = *(const bf8v*)(ch + XCHUNK_B / 2 + o);
+                    // gallery rows as the A operand: D[row][probe], so each lane's accumulators belong to
+                    // ONE probe (its own candidate sub-list) and the filter never leaves the registers
+#if FR_X3_EXP == 1  // timing experiment: no MFMA
+                    acc[j][0] += (float)gh[t & 7] + (float)gl[t & 7];
+#else
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, ph[t], acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl, ph[t], acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, pl[t], acc[j], 0, 0, 0);
+#endif
+                }
+            }
+        }
+        // acc[j][r] = s~(probe my_q, row t0 + 16*j + 4*my_sub + r).  A row not above the best KP-th score
+        // of the probe's 4 sub-lists (lanes lane ^ 16, ^ 32) is never needed: the floor (>= that score)
+        // covers it in the proof -- ties included, so the scan compares scores only.  The sorted insert
+        // runs once per hit of the wave's busiest lane.
+        if (g_end - t0 < XG) {  // last tile of the split: rows past it are zero-filled, never candidates
+            const int lim = (int)(g_end - t0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (16 * j + 4 * my_sub + r >= lim) acc[j][r] = -INFINITY;
+        }
+        // also: when every sub-list holds >= KP/2 entries above x, the probe's top KO = 2 KP (the merge
+        // keeps exactly those) are all above x, so min over the sub-lists of the (KP/2)-th score is a
+        // valid (usually higher) bar too
+        float thr = ls[KP - 1], thr2 = ls[KP / 2 - 1];
+        thr = fmaxf(thr, __shfl_xor(thr, 16));
+        thr2 = fminf(thr2, __shfl_xor(thr2, 16));
+        thr = fmaxf(thr, __shfl_xor(thr, 32));
+        thr2 = fminf(thr2, __shfl_xor(thr2, 32));
+        thr = fmaxf(thr, thr2);
+#if FR_X3_EXP == 3  // timing experiment: no insert (the compares still run)
+        {
+            uint32_t m = 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) m |= (acc[e >> 2][e & 3] > thr) << e;
+            asm volatile("" ::"v"(m));
+        }
+        continue;
+#endif
+        uint32_t m = 0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) m |= acc[e >> 2][e & 3] > thr ? 1u << e : 0u;
+        // one pass per hit of the busiest lane (usually one): pick the score by a select tree
+        while (m) {
+            const int e = __builtin_ctz(m);
+            m &= m - 1;
+            float v8[8], v4[4], v2[2];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v8[q] = (e & 8) ? acc[(q + 8) >> 2][(q + 8) & 3] : acc[q >> 2][q & 3];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v4[q] = (e & 4) ? v8[q + 4] : v8[q];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) v2[q] = (e & 2) ? v4[q + 2] : v4[q];
+            const float sc = (e & 1) ? v2[1] : v2[0];
+            insert_s<KP>(ls, li, sc, (int)(t0 + index_base) + 16 * (e >> 2) + 4 * my_sub + (e & 3));
+        }
+    }
+    // the look-ahead DMAs (zeros past the split) land everywhere before the ring is reused as scratch
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    // merge the 4 sub-lists of each probe into its top KO: park them in the (drained) ring and let
+    // lane my_sub == 0 insert all four (a rolled loop: one inlined insert)
+    float* ms = (float*)smem;                    // [XP][4][KP] scores (the drained DMA ring)
+    int* mi = (int*)(smem + XP * 4 * KP * 4);    // [XP][4][KP] indices
+    static_assert(2 * XP * 4 * KP * 4 <= XSLOT * XCHUNK_B, "merge scratch fits the ring");
+    static_assert(KO == 2 * KP, "the scan's second bar assumes 4 sub-lists x KP/2 = KO");
+#pragma unroll
+    for (int q = 0; q < KP; ++q) {
+        ms[(my_q * 4 + my_sub) * KP + q] = ls[q];
+        mi[(my_q * 4 + my_sub) * KP + q] = li[q];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int p = p0 + my_q;
+    if (my_sub == 0 && p < B) {
+        float os[KO];
+        int oi[KO];
+#pragma unroll
+        for (int q = 0; q < KO; ++q) { os[q] = -INFINITY; oi[q] = INT_MAX; }
+        float floor_s = -INFINITY;
+#pragma unroll 1
+        for (int e = 0; e < 4 * KP; ++e) {
+            const float sc = ms[my_q * 4 * KP + e];
+            const int ix = mi[my_q * 4 * KP + e];
+            if (ix == INT_MAX) continue;
+            insert<KO>(os, oi, sc, ix);
+            // a full sub-list may have dropped rows scoring up to its last entry
+            if (e % KP == KP - 1) floor_s = fmaxf(floor_s, sc);
+        }
+        const size_t o = ((size_t)p * n_split + split) * KS;
+#pragma unroll
+        for (int q = 0; q < KO; ++q) {
+            const bool valid = oi[q] != INT_MAX;
+            cs[o + q] = valid ? os[q] : -INFINITY;
+            ci[o + q] = valid ? oi[q] : -1;
+        }
+        cs[o + KO] = floor_s;
+        ci[o + KO] = -2;
+    }
+}
+
+// Exact score in the order of match.hip's v_mfma_f32_16x16x4_f32 sequence: per 16-dim block t16 the
+// MFMAs take components comp = 0..3 of the lanes' float4 k-groups kq = 0..3, each a k-ordered fmaf chain.
+__device__ __forceinline__ float exact_dot(const float* __restrict__ p, const float* __restrict__ g) {
+    float acc = 0.f;
+#pragma unroll 2
+    for (int t16 = 0; t16 < XD / 16; ++t16) {
+        float4 a[4], b[4];
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) {
+            a[kq] = *(const float4*)(p + 16 * t16 + 4 * kq);
+            b[kq] = *(const float4*)(g + 16 * t16 + 4 * kq);
+        }
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].x, b[kq].x, acc);
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].y, b[kq].y, acc);
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].z, b[kq].z, acc);
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].w, b[kq].w, acc);
+    }
+    return acc;
+}
+
+// wave-wide pop of the best (score desc, index asc) entry of per-lane sorted lists
+template <int KMAX>
+__device__ __forceinline__ void wave_pop(float (&ls)[KMAX], int (&li)[KMAX], int& head, float& ws, int& wi) {
+    float bs = -INFINITY;
+    int bi = INT_MAX;
+#pragma unroll
+    for (int h = 0; h < KMAX; ++h)
+        if (h == head) { bs = ls[h]; bi = li[h]; }
+    ws = bs;
+    wi = bi;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float os = __shfl_xor(ws, o);
+        const int oi = __shfl_xor(wi, o);
+        if (better(os, oi, ws, wi)) { ws = os; wi = oi; }
+    }
+    if (wi == bi && bi != INT_MAX) ++head;  // indices are unique: the owner pops
+}
+
+__global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ P, int B, const float* __restrict__ G,
+                                                      int64_t N, int64_t index_base, const float* __restrict__ cs,
+                                                      const int32_t* __restrict__ ci, int n_lists, int k,
+                                                      float* __restrict__ out_s, int32_t* __restrict__ out_i,
+                                                      int* __restrict__ n_fallback) {
+    const int lane = threadIdx.x & 63;
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= B) return;
+    const float* prow = P + (size_t)p * XD;
+    // (a) global top-KC by approximate score; T = the KC-th (or -inf with fewer candidates)
+    float ls[KC];
+    int li[KC];
+#pragma unroll
+    for (int q = 0; q < KC; ++q) { ls[q] = -INFINITY; li[q] = INT_MAX; }
+    const int n = n_lists * KS;
+    float floor_s = -INFINITY;  // every row no list holds has s~ <= floor_s
+    for (int c = lane; c < n; c += 64) {
+        const int idx = ci[(size_t)p * n + c];
+        if (idx >= 0) insert<KC>(ls, li, cs[(size_t)p * n + c], idx);
+        else if (idx == -2) floor_s = fmaxf(floor_s, cs[(size_t)p * n + c]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) floor_s = fmaxf(floor_s, __shfl_xor(floor_s, o));
+    int head = 0, my_idx = -1;
+    float T = -INFINITY;
+    for (int q = 0; q < KC; ++q) {
+        float ws;
+        int wi;
+        wave_pop<KC>(ls, li, head, ws, wi);
+        if (lane == q) my_idx = wi == INT_MAX ? -1 : wi;
+        if (q == KC - 1) T = wi == INT_MAX ? -INFINITY : ws;
+    }
+    T = fmaxf(T, floor_s);
+    // (b) exact rescoring: lane q < KC holds candidate q
+    float rs[1] = {-INFINITY};
+    int ri[1] = {INT_MAX};
+    if (lane < KC && my_idx >= 0) {
+        rs[0] = exact_dot(prow, G + (size_t)(my_idx - index_base) * XD);
+        ri[0] = my_idx;
+    }
+    float pp = 0.f;
+    for (int d = lane; d < XD; d += 64) pp = fmaf(prow[d], prow[d], pp);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pp += __shfl_xor(pp, o);
+    const float eps = 1.25e-4f * sqrtf(pp) * 1.001f;  // rows are unit norm within 1e-3 (or zero)
+    // (c) exact top-k among the candidates
+    int h1 = 0;
+    float kth = INFINITY, outs = -INFINITY;
+    int outi = -1;
+    for (int q = 0; q < k; ++q) {
+        float ws;
+        int wi;
+        wave_pop<1>(rs, ri, h1, ws, wi);
+        if (lane == q) {
+            outs = wi == INT_MAX ? -INFINITY : ws;
+            outi = wi == INT_MAX ? -1 : wi;
+        }
+        if (q == k - 1) kth = ws;
+    }
+    // (d) an excluded row scores <= T + eps; ties need the index order, so require kth > T + 2 eps
+    if (!(T == -INFINITY || kth > T + 2.f * eps)) {
+        if (lane == 0 && n_fallback) atomicAdd(n_fallback, 1);
+        float fs[KC];
+        int fi[KC];
+#pragma unroll
+        for (int q = 0; q < KC; ++q) { fs[q] = -INFINITY; fi[q] = INT_MAX; }
+#pragma unroll 1
+        for (int64_t r = lane; r < N; r += 64)
+            insert<KC>(fs, fi, exact_dot(prow, G + (size_t)r * XD), (int)(r + index_base));
+        int hh = 0;
+        for (int q = 0; q < k; ++q) {
+            float ws;
+            int wi;
+            wave_pop<KC>(fs, fi, hh, ws, wi);
+            if (lane == q) {
+                outs = wi == INT_MAX ? -INFINITY : ws;
+                outi = wi == INT_MAX ? -1 : wi;
+            }
+        }
+    }
+    if (lane < k) {
+        out_s[(size_t)p * k + lane] = outs;
+        out_i[(size_t)p * k + lane] = outi;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_split_bf16(const float* G, size_t n, bf16_t* hi, bf16_t* lo, hipStream_t s) {
+    int blocks = (int)((n + 255) / 256);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(split_bf16_kernel, dim3(blocks), dim3(256), 0, s, G, n, hi, lo);
+    return hipGetLastError();
+}
+
+void match_x3_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split) {
+    const int npb = (B + XP - 1) / XP;
+    int64_t want = (256 + npb - 1) / npb;  // one 512-thread block per CU
+    const int64_t tiles = (N + XG - 1) / XG;
+    if (want > tiles) want = tiles;
+    if (want < 1) want = 1;
+    const int64_t rps = ((tiles + want - 1) / want) * XG;
+    *rows_per_split = rps;
+    *n_split = (int)((N + rps - 1) / rps);
+}
+
+int match_x3_candidates() { return KS; }
+
+hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* Gh, const bf16_t* Gl, int64_t N, int D,
+                           int k, int64_t index_base, float* cand_s, int32_t* cand_i, int n_split,
+                           int64_t rows_per_split, float* out_s, int32_t* out_i, int* n_fallback, hipStream_t s) {
+    if (D != XD || k > KC || k < 1) return hipErrorInvalidValue;
+    const int npb = (B + XP - 1) / XP;
+    hipLaunchKernelGGL(match_x3_kernel, dim3(npb * n_split), dim3(512), 0, s, P, B, Gh, Gl, N, index_base,
+                       rows_per_split, n_split, npb, cand_s, cand_i);
+    hipLaunchKernelGGL(rescore_kernel, dim3((B + 3) / 4), dim3(256), 0, s, P, B, G, N, index_base, cand_s, cand_i,
+                       n_split, k, out_s, out_i, n_fallback);
+    return hipGetLastError();
+}
+
+}  // namespace fr

@@ -21,7 +21,8 @@ from . import _native as N
 
 
 class DeviceGallery:
-    def __init__(self, rows=None, dim: int = 512, device: int = 0, index_base: int = 0, handle=None):
+    def __init__(self, rows=None, dim: int = 512, device: int = 0, index_base: int = 0, handle=None,
+                 x3_min_rows: Optional[int] = None):
         import torch
 
         if not torch.cuda.is_available():
@@ -35,6 +36,8 @@ class DeviceGallery:
             N.check(N.lib().fr_create(ctypes.byref(h), device, 0, N.FR_DTYPE_BF16), "fr_create")
             handle = h
         self._h = handle
+        if x3_min_rows is not None:  # FR_OPT_X3_MIN_ROWS: smallest gallery given the bf16x3 path
+            N.check(N.lib().fr_set_option(self._h, N.FR_OPT_X3_MIN_ROWS, int(x3_min_rows)), "fr_set_option")
         self._rows = torch.empty((0, dim), dtype=torch.float32)
         if rows is not None:
             self.add(rows)
@@ -67,6 +70,15 @@ class DeviceGallery:
     def _upload(self) -> None:
         N.check(N.lib().fr_gallery_set(self._h, N.ptr(self._rows), self.ntotal, self.d, self.index_base, 0),
                 "fr_gallery_set")
+
+    def set_exact(self, exact: bool) -> None:
+        """FR_OPT_MATCH_EXACT: force the f32-MFMA kernel (default: bf16x3 candidates + exact rescoring
+        for galleries of >= FR_OPT_X3_MIN_ROWS rows; both return the exact f32 top-k)."""
+        N.check(N.lib().fr_set_option(self._h, N.FR_OPT_MATCH_EXACT, int(bool(exact))), "fr_set_option")
+
+    def fallbacks(self) -> int:
+        """Probes whose bf16x3 candidate proof failed and were rescanned exactly (device sync)."""
+        return int(N.lib().fr_debug_match_fallbacks(self._h))
 
     def search_device(self, probes_dev, k: int):
         """probes_dev: cuda f32 [B, D] → (scores [B,k] f32, idx [B,k] int32) on the device."""

@@ -199,8 +199,19 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * reads 0 when the plan has no stage) or FR_ERR_ARG. */
 #define FR_OPT_STAGE 1
 #define FR_OPT_KEEP_INTERMEDIATES 2
+/* FR_OPT_MATCH_EXACT (default 0): galleries of >= FR_OPT_X3_MIN_ROWS rows (D = 512) are matched by a bf16x3 candidate
+ * pass (|error| <= 1.25e-4 ||p||) plus exact f32 rescoring of the top-16 candidates per probe, with a
+ * per-probe proof that no excluded row can enter the top-k (else an exact rescan of that probe): the
+ * results equal the exact f32 kernel's.  1 forces the f32-MFMA kernel for every gallery. */
+#define FR_OPT_MATCH_EXACT 3
+/* FR_OPT_X3_MIN_ROWS (default 32768): smallest gallery given the bf16x3 path (its hi/lo copy is made by
+ * the next fr_gallery_set); below it the f32 kernel is as fast. */
+#define FR_OPT_X3_MIN_ROWS 4
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);
+/* Number of probes (since the gallery was first split) whose bf16x3 candidate proof failed and were
+ * rescanned exactly (synchronizes the device). */
+int fr_debug_match_fallbacks(fr_handle* h);
 
 /* ---- debug: named intermediate tensors of the forward plan (per-layer drift tests) ----
  * Tensor names are the reference/oracle module whose output the tensor equals

@@ -327,3 +327,66 @@ def test_conv_bias9_prefolded_bn(gpu, case):
     # border rows/cols really use their own class (a wrong class would be off by O(|T|))
     cls = _border_class(H, W)
     assert set(cls.unique().tolist()) == set(range(9))
+
+
+@pytest.mark.parametrize("B,Ng,k", [(256, 10000, 5), (2048, 20000, 5), (33, 5000, 16), (1, 4096, 1)])
+def test_match_x3_equals_exact(gpu, B, Ng, k):
+    """bf16x3 candidates + exact rescoring (match_x3.hip) == the f32-MFMA kernel, bit for bit."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(B * 7 + Ng)
+    G = _norm(rng.standard_normal((Ng, 512)))
+    P = _norm(rng.standard_normal((B, 512)))
+    m = min(B, Ng) // 2
+    P[:m] = _norm(G[:m] + 0.05 * rng.standard_normal((m, 512)))
+    gal = DeviceGallery(G, x3_min_rows=4096)
+    s3, i3 = gal.search(P, k)
+    gal.set_exact(True)
+    se, ie = gal.search(P, k)
+    assert np.array_equal(i3, ie)
+    assert np.array_equal(s3, se)  # identical f32 fmaf chains
+    rs, ri = _np_topk(P, G, k)
+    assert np.allclose(s3, rs, atol=1e-5)
+    gal.close()
+
+
+def test_match_x3_fallback_on_ties(gpu):
+    """40 identical copies of a row: more than KC - k candidates tie within 2 eps, so the candidate
+    proof fails and the probe is rescanned exactly -- lowest indices first, like the f32 kernel."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(5)
+    G = _norm(rng.standard_normal((6000, 512)))
+    G[100:140] = G[7]
+    P = _norm(G[[7, 11]] + 0.01 * rng.standard_normal((2, 512)))
+    gal = DeviceGallery(G, x3_min_rows=4096)
+    s3, i3 = gal.search(P, 5)
+    assert gal.fallbacks() >= 1
+    assert list(i3[0]) == [7, 100, 101, 102, 103]
+    gal.set_exact(True)
+    se, ie = gal.search(P, 5)
+    assert np.array_equal(i3, ie) and np.array_equal(s3, se)
+    gal.close()
+
+
+def test_match_x3_sublist_overflow_floor(gpu):
+    """Twelve graded near-duplicates of the probe in rows 16*(i//4) + i%4 -- all in ONE candidate
+    sub-list (rows 16j + 4*sub + r of a tile; KP = 8 entries), which overflows: its floor enters the proof.  k = 5 is provable from the candidates (no rescan);
+    k = 10 needs rows the sub-list dropped, so the proof fails and the probe is rescanned exactly.
+    Both equal the exact f32 kernel bit for bit."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(9)
+    G = _norm(rng.standard_normal((8192, 512)))
+    P = _norm(rng.standard_normal((3, 512)))
+    rows = [16 * (i // 4) + i % 4 for i in range(12)]
+    for i, r in enumerate(rows):
+        G[r] = _norm(P[:1] + (0.1 + 0.05 * i) * _norm(rng.standard_normal((1, 512))))[0]
+    gal = DeviceGallery(G, x3_min_rows=4096)
+    for k, want_fb in ((5, 0), (10, 1)):
+        gal.set_exact(False)
+        fb0 = gal.fallbacks()
+        s3, i3 = gal.search(P, k)
+        assert list(i3[0]) == rows[:k]
+        assert gal.fallbacks() - fb0 == want_fb
+        gal.set_exact(True)
+        se, ie = gal.search(P, k)
+        assert np.array_equal(i3, ie) and np.array_equal(s3, se)
+    gal.close()
