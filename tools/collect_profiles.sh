@@ -5,8 +5,9 @@ T=${1:?tag}; R=${2:?round prefix}; O=gpurun_out/$T
 set -e
 cp $O/bench.json profiles/${R}_bench.json
 : > profiles/${R}_bench_runs.jsonl
-for b in bench bench_noprof bench_host bench_irv1 bench_r50; do tail -1 $O/$b.log >> profiles/${R}_bench_runs.jsonl; done
+for b in bench bench_noprof bench_host bench_irv1 bench_r50 bench_fp8 bench_1m; do tail -1 $O/$b.log >> profiles/${R}_bench_runs.jsonl; done
 cp "$(find $O/prof -name '*kernel_stats.csv' | head -1)" profiles/${R}_bench_kernel_stats.csv
+grep '^{' $O/match_bench.log > profiles/${R}_match_bench.jsonl
 cp $O/pmc_traffic.json profiles/${R}_pmc_traffic.json
 grep -v "^\s*$" $O/tests.log | tail -40 > profiles/${R}_gpu_tests.log
 echo "collected $T -> profiles/${R}_*"

@@ -3,6 +3,7 @@
 #   1. pytest -m gpu           -> gpurun_out/TAG/tests.log
 #   2. bench.py (default args) -> gpurun_out/TAG/bench.json  (+ --no-prof line for the event overhead)
 #   3. rocprofv3 --kernel-trace --stats of the same bench command -> gpurun_out/TAG/prof/
+#   (+ host-input, IRV1, ResNet-50, fp8 and 1M-gallery bench lines, tools/match_bench.py)
 #   4. two separate --pmc passes (FETCH_SIZE, WRITE_SIZE) -> profiles-ready traffic JSON
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
@@ -11,7 +12,7 @@ R=$(pwd); O=$R/gpurun_out/$T
 mkdir -p $O
 step() { local name=$1 lim=$2; shift 2; echo "[$(date +%T)] $name"; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; if [ $rc -ne 0 ]; then echo "$name failed rc=$rc"; tail -20 $O/$name.log; exit $rc; fi; }
 if [ -z "$SKIP_TESTS" ]; then
-  step tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x
+  step tests 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread
   tail -3 $O/tests.log
 fi
 step bench 400 python bench.py
@@ -21,7 +22,10 @@ tail -1 $O/bench_noprof.log
 step bench_host 300 python bench.py --no-cpu-baseline --host-input
 step bench_irv1 300 python bench.py --no-cpu-baseline --arch irv1_facenet
 step bench_r50 300 python bench.py --no-cpu-baseline --arch resnet50_arcface
-for b in bench_host bench_irv1 bench_r50; do tail -1 $O/$b.log | cut -c1-400; done
+step bench_fp8 300 python bench.py --no-cpu-baseline --dtype fp8
+step bench_1m 300 python bench.py --no-cpu-baseline --gallery-rows 1000000
+step match_bench 300 python tools/match_bench.py
+for b in bench_host bench_irv1 bench_r50 bench_fp8 bench_1m; do tail -1 $O/$b.log | cut -c1-400; done
 BCMD="$R/bench.py --steps 10 --warmup 3 --no-cpu-baseline"
 cd /tmp && export TMPDIR=/tmp
 step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $BCMD

@@ -16,7 +16,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(rows, probes, k, iters):
+def run(rows, probes, k, iters, exact=False):
     from facerecognition_amd.gallery import DeviceGallery
     g = torch.randn(rows, 512, device="cuda")
     g = g / g.norm(dim=1, keepdim=True)
@@ -24,6 +24,7 @@ def run(rows, probes, k, iters):
     p = p / p.norm(dim=1, keepdim=True)
     gal = DeviceGallery(handle=None)
     gal.set_device_rows(g)
+    gal.set_exact(exact)
     for _ in range(3):
         gal.search_device(p, k)
     torch.cuda.synchronize()
@@ -39,7 +40,7 @@ def run(rows, probes, k, iters):
     agree = float((i[:64, 0] == ref).float().mean())
     flop = 2.0 * probes * rows * 512
     gbytes = rows * 512 * 4 / 1e9
-    return {"rows": rows, "probes": probes, "k": k, "ms": round(ms, 4), "tflops_f32": round(flop / ms / 1e9, 2),
+    return {"rows": rows, "probes": probes, "k": k, "path": "exact-f32" if exact or rows < 32768 else "bf16x3", "ms": round(ms, 4), "tflops_f32": round(flop / ms / 1e9, 2),
             "gallery_GBps": round(gbytes / ms * 1e3, 1), "top1_agree_torch": agree}
 
 
@@ -47,6 +48,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--k", type=int, default=5)
+    ap.add_argument("--exact", action="store_true", help="force the f32-MFMA kernel (FR_OPT_MATCH_EXACT)")
     a = ap.parse_args()
     for rows, probes in ((10000, 256), (125000, 2048), (1000000, 256)):
-        print(json.dumps(run(rows, probes, a.k, a.iters)), flush=True)
+        print(json.dumps(run(rows, probes, a.k, a.iters, a.exact)), flush=True)
