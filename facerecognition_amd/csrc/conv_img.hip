@@ -1,0 +1,293 @@
+// Image-per-workgroup direct 3x3 convolution (stride 1, pad 1) for the 28x28x128 IBasicBlock convs of
+// IResNet100 layer2 (layer2.1 .. layer2.12: 24 convs, 22.9 % of the network's FLOPs).
+//
+// As an implicit GEMM these convs re-gather every input pixel for all 9 taps (9x the activation bytes
+// L2 -> LDS: at the MFMA rate ~99 GB/s per CU, above the ~70 GB/s an LDS-DMA gather sustains per CU,
+// MI355X_MICROARCH.md "Indexed rows"), and 200704 output rows quantize badly on 256 CUs (3.06 rounds
+// of 256-row tiles).  Here one workgroup owns one image (bs = 256 -> exactly one round on 256 CUs) and
+// walks it as two 14-row halves:
+//   * per 32-input-channel chunk the (14+2) x (28+2) zero-haloed patch is DMA'd into LDS once
+//     ([4 planes of 8 channels][480 positions][16 B], plane stride a multiple of 256 B) and read by all
+//     9 taps at shifted positions; the next chunk's patch (double buffer) streams in during the
+//     current chunk's 9 K-steps, across the half boundary too;
+//   * per K-step (chunk, tap) the [128 out][32 in] weight slice (8 KiB) is gathered straight from the
+//     implicit-GEMM weight rows [Npad][Kpad] (K order (kh, kw, c)) into a 4-slot LDS ring, three steps
+//     ahead; one s_barrier per K-step;
+//   * 2x4 waves, two per SIMD (the second hides the other's LDS latency): wave (wm, wn) computes rows
+//     7wm..7wm+6 of the half (196 pixels = 13 m-frags, the last one 4/16 valid) x output channels
+//     32wn..32wn+31 (2 n-frags): 26 v_mfma_f32_16x16x32_{bf16,f16} per K-step, 104 f32 accumulators;
+//   * operand A = weight rows, operand B = patch positions, so a lane ends with 4 consecutive channels
+//     of one pixel; the epilogue (bias or border-class bias9, residual, ReLU/PReLU) stores 8 B per lane.
+#include "kernels.h"
+
+#include <hip/hip_ext.h>
+
+#include <cstdlib>
+
+namespace fr {
+namespace {
+
+#ifndef FR_IMG_EXP
+#define FR_IMG_EXP 0  // timing experiments only (tools/img_exp.sh: 1 no weight DMA, 2 no patch DMA, 4 neither); 0 in every shipped build
+#endif
+
+constexpr int IW = 28;                   // image width = height
+constexpr int IC = 128;                  // input = output channels
+constexpr int HR = 14;                   // output rows per half
+constexpr int PC = 32;                   // patch row stride in positions (col c+1 = image col c; 0, 29 halo)
+constexpr int PPOS = (HR + 2) * PC;      // 512 positions per plane
+constexpr int PLANE_B = PPOS * 16;       // 8192
+constexpr int PATCH_B = 4 * PLANE_B;     // 32768: one 32-channel chunk = 32 pieces of 1 KiB
+constexpr int SLICE_B = 4 * IC * 16;     // 8192: [4 groups of 8 ch][128 rows][16 B]
+constexpr int NSLOT = 3;
+constexpr int IMG_LDS = 2 * PATCH_B + NSLOT * SLICE_B;  // 90112
+constexpr int NCH = IC / 32;             // 4 chunks of 32 input channels
+constexpr int HSTEPS = NCH * 9;          // 36 K-steps per half
+constexpr int FM = 7;                    // virtual-pixel frags per wave (4 waves x 7 x 16 = 14 rows x 32)
+constexpr int FN = 8;                    // channel frags per wave (all 128)
+constexpr uint32_t OOB = 0x80000000u;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// LDS-DMA of 16 B per lane; soff: a wave-uniform byte offset (memory address only)
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, soff, 0, 0);
+}
+
+// RES: residual input (IBasicBlock conv2); B9: border-class bias table (conv1 with bn1 folded).  The
+// epilogue is specialised on them so its loads issue together instead of behind per-pixel branches.
+template <bool F16, bool RES, bool B9>
+__global__ __launch_bounds__(256, 1) void conv_img28_kernel(ConvArgs p) {
+    typedef Num<F16> T;
+    typedef typename T::frag frag;
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [patch 0][patch 1][slot 0..2]
+    char* const slots = smem + 2 * PATCH_B;
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.x;
+
+    const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * IW * IW * p.Cx * 2);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
+    const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
+
+    // patch of chunk q = 4h + cc (half h, input channels 32cc..): 8 pieces per wave, plane-major
+    // [4 planes][16 rows][32 positions][16 B]; halo and pad positions read out of range (zeros).
+    // Offsets are recomputed per chunk (VALU every 9 K-steps, no live registers); the chunk's channel
+    // offset goes in the scalar offset (rows stay in voff: a negative voff would wrap).
+    auto issue_patch = [&](int q, int buf) {
+#if FR_IMG_EXP == 2 || FR_IMG_EXP == 4  // timing experiment: no patch stream (after the first chunk)
+        if (q > 0) return;
+#endif
+        const int h = q >> 2, cc = q & 3;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));  // opaque copy: the offsets are not hoisted (registers for the MFMAs)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int piece = 4 * u + wave, sl = piece * 64 + ln;
+            const int plane = sl / PPOS, pos = sl % PPOS, pr = pos / PC, pc = pos % PC;
+            const int ir = HR * h - 1 + pr, ic = pc - 1;
+            const bool in = (unsigned)ir < (unsigned)IW && (unsigned)ic < (unsigned)IW;
+            const uint32_t off =
+                in ? (uint32_t)((((size_t)b * IW * IW + ir * IW + ic) * p.Cx + p.x_off + plane * 8) * 2) : OOB;
+            dma16s(xr, smem + buf * PATCH_B + piece * 1024, off, (uint32_t)(cc * 32 * 2));
+        }
+    };
+    // weight slice of K-step s (chunk cc = s / 9, tap = s % 9) gathered from the [Npad][Kpad] rows,
+    // LDS image [g][n][16 B]: pieces 2wave, 2wave+1 = (group g, rows 64nh..); the step in soffset
+    uint32_t wv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int piece = 2 * wave + u;
+        wv[u] = (uint32_t)(((size_t)(64 * (piece & 1) + lane) * p.Kpad + (piece >> 1) * 8) * 2);
+    }
+    auto issue_w = [&](int s, int slot) {
+#if FR_IMG_EXP == 1 || FR_IMG_EXP == 4  // timing experiment: no weight stream (after the first slices)
+        if (s > 2) return;
+#endif
+        const int cc = s / 9, tap = s - cc * 9;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            dma16s(wr, slots + slot * SLICE_B + (2 * wave + u) * 1024, wv[u], (uint32_t)((tap * IC + cc * 32) * 2));
+    };
+
+    // fragment addresses: B (patch) virtual frag f = 7*wave + j -> positions 16f + (lane&15) (row f/2,
+    // columns 16(f%2)..: linear, so one base + compile-time offsets), plane (lane>>4); A (weights)
+    // rows 16i + (lane&15), group (lane>>4)
+    const int pbase = (lane >> 4) * PLANE_B + (112 * wave + (lane & 15)) * 16;
+    const int woff = (lane >> 4) * (IC * 16) + (lane & 15) * 16;
+
+    f32x4_t acc[FN][FM];
+    frag wf[FN], pA[FM], pB[FM];
+    auto pread = [&](frag (&pf)[FM], int buf, int tap) {
+        const int dh = tap / 3, dw = tap % 3;
+        const char* a = smem + buf * PATCH_B + pbase + (dh * PC + dw) * 16;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) pf[j] = *(const frag*)(a + j * 256);
+    };
+    auto wread = [&](int i, int slot) { wf[i] = *(const frag*)(slots + slot * SLICE_B + woff + i * 256); };
+
+    // prologue: chunk 0's patch and the first three weight slices
+    issue_patch(0, 0);
+    issue_w(0, 0);
+    issue_w(1, 1);
+    issue_w(2, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    pread(pA, 0, 0);
+#pragma unroll
+    for (int i = 0; i < FN; ++i) wread(i, 0);
+
+    // one K-step (the stage kernel's schedule, conv_stage.hip): step s of half h (G = 36h + s; slot
+    // s % 3, chunk c = s / 9, tap t = s % 9; compile-time but h).  nxt <- patch fragments of step G+1;
+    // MFMAs of weight frags 0..3; mid-step barrier: this wave's slice G+1 landed (younger: slice G+2
+    // and the 8 patch pieces issued at a chunk start in step G-2 or G-1), every wave is past its reads
+    // of slot s % 3 and of the previous chunk's patch buffer; DMA of slice G+3 into slot s % 3 and, at
+    // t == 0, of the next chunk's patch; wf <- slice G+1 (0..3 now, 4..7 in place after their MFMAs).
+    // The next chunk's patch is read at the start of its t == 8 step: the t == 7 barrier covered it.
+    auto kstep = [&](int h, int s, frag (&cur)[FM], frag (&nxt)[FM]) {
+        const int t = s % 9, c = s / 9, slot = s % NSLOT, nslot = (s + 1) % NSLOT;
+        pread(nxt, t == 8 ? (c + 1) & 1 : c & 1, t == 8 ? 0 : t + 1);  // (tail: unused reads)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
+        // first half: one patch read after every 4 MFMAs (the compiler would sink them to the end)
+#pragma unroll
+        for (int q = 0; q < FM; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if (t == 1 || t == 2) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        issue_w(s + 3 < HSTEPS ? s + 3 : (h == 0 ? s + 3 - HSTEPS : HSTEPS - 1), slot);  // tail: re-fetch
+        if (t == 0) {
+            const int qn = 4 * h + c + 1;
+            issue_patch(qn < 2 * NCH ? qn : 2 * NCH - 1, (c + 1) & 1);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wread(i, nslot);
+#pragma unroll
+        for (int i = 4; i < FN; ++i) {
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
+            wread(i, nslot);
+        }
+        // second half: the wf[0..3] refills spread over the first 8 MFMAs, then each wf[4..7] refill
+        // right after its 7th MFMA
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    };
+
+    const size_t img = (size_t)b * IW * IW;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        // 36 steps, unrolled so slots / taps / buffers are compile-time (36 % 3 == 0, 36 % 2 == 0)
+#pragma unroll
+        for (int s = 0; s < HSTEPS; s += 2) {
+            kstep(h, s, pA, pB);
+            kstep(h, s + 1, pB, pA);
+        }
+        // ---- epilogue: straight from the accumulators (no LDS), 8 B per lane and (i, j).  Per channel
+        // group i the 7 residual / bias9 loads issue together (pad columns read a valid pixel and skip
+        // only the store).
+        int ln = lane;
+        asm volatile("" : "+v"(ln));  // opaque copy: keeps the per-(i, j) addresses from being hoisted
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+            const int n = 16 * i + 4 * (ln >> 4);
+            float4 sl = make_float4(0.f, 0.f, 0.f, 0.f), bb = sl;
+            if (p.act == 2) sl = *(const float4*)(p.slope + n);
+            if (!B9 && p.bias) bb = *(const float4*)(p.bias + n);
+            size_t m[FM];
+            int cls[FM];
+            bool ok[FM];
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                const int f = FM * wave + j, c = 16 * (f & 1) + (ln & 15), r = HR * h + (f >> 1);
+                ok[j] = c < IW;
+                m[j] = img + r * IW + (ok[j] ? c : 0);
+                cls[j] = border_class(r, c, IW, IW);
+            }
+            uint2 rr[FM];
+            float4 b9[FM];
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                if (RES) rr[j] = *(const uint2*)(p.res + m[j] * p.Cres + p.res_off + n);
+                if (B9) b9[j] = *(const float4*)(p.bias9 + cls[j] * p.Npad + n);
+            }
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
+                if (B9) { v[0] += b9[j].x; v[1] += b9[j].y; v[2] += b9[j].z; v[3] += b9[j].w; }
+                if (RES) {
+                    float f8[8];
+                    T::unpack8(make_uint4(rr[j].x, rr[j].y, 0, 0), f8);
+                    v[0] += f8[0]; v[1] += f8[1]; v[2] += f8[2]; v[3] += f8[3];
+                }
+                if (p.act == 2) {
+                    v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
+                    v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
+                    v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
+                    v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
+                } else if (p.act == 1) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                }
+                float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+                const uint4 pk = T::pack8(o8);
+#if FR_IMG_EXP == 5  // timing experiment: epilogue stores only where the value is a NaN
+                if (ok[j] && v[0] != v[0]) *(uint2*)(p.y + m[j] * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
+#else
+                if (ok[j]) *(uint2*)(p.y + m[j] * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
+#endif
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs land before the LDS is released
+}
+
+}  // namespace
+
+bool img28_supported(const ConvArgs& a) {
+    return a.Kh == 3 && a.Kw == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.H == IW && a.W == IW &&
+           a.Ho == IW && a.Wo == IW && a.Cin == IC && a.Cout == IC && a.Npad >= IC && a.Kpad >= 9 * IC &&
+           a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.x_off + IC <= a.Cx && a.Cy % 4 == 0 && a.y_off % 4 == 0 &&
+           a.y_off + IC <= a.Cy && !a.y2 && !a.partial && !a.w8 && !a.y_amax && a.B > 0 && !a.f16 &&
+           !(a.res && a.bias9) &&
+           (!a.res || (a.Cres % 4 == 0 && a.res_off % 4 == 0 && a.res_off + IC <= a.Cres));
+}
+
+hipError_t launch_conv_img28(const ConvArgs& a, hipStream_t s) {
+    if (!img28_supported(a)) return hipErrorInvalidValue;
+    auto k = a.res ? conv_img28_kernel<false, true, false>
+                   : (a.bias9 ? conv_img28_kernel<false, false, true> : conv_img28_kernel<false, false, false>);
+    const int v = a.res ? 0 : (a.bias9 ? 1 : 2);
+    static bool attr[3] = {false, false, false};
+    if (!attr[v]) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, IMG_LDS);
+        attr[v] = true;
+    }
+    if (a.ev0)
+        hipExtLaunchKernelGGL(k, dim3(a.B), dim3(256), IMG_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
+    else
+        hipLaunchKernelGGL(k, dim3(a.B), dim3(256), IMG_LDS, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace fr

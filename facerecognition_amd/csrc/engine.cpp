@@ -749,6 +749,16 @@ int reserve(fr_handle* h, int maxB) {
     return fill_stage_dbg(h);
 }
 
+// The image-per-workgroup layer2 kernel (conv_img.hip) is opt-in (FR_IMG28=1): measured 94 us per
+// conv vs 86 us for the implicit GEMM (profiles/r01_img28.txt)
+bool img28_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_IMG28");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 bool band_enabled() {
     static const bool on = [] {
         const char* e = getenv("FR_NO_BAND");
@@ -870,6 +880,11 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
         a.split_k = 1;
         ps.start("conv_fp8 tile" + std::to_string(a.tile), &a);
         FR_HIP_CHECK(launch_conv_fp8(a, s));
+        return FR_OK;
+    }
+    if (img28_enabled() && img28_supported(a)) {  // layer2 3x3 128->128 @28x28: one image per workgroup
+        ps.start("conv3x3_img W28", &a);
+        FR_HIP_CHECK(launch_conv_img28(a, s));
         return FR_OK;
     }
     int TH, variant;
@@ -1330,8 +1345,12 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
             a.Ho = h->tensors[op.out].H; a.Wo = h->tensors[op.out].W; a.ph = op.ph; a.pw = op.pw;
             a.res = op.res >= 0 ? (const bf16_t*)1 : nullptr;
             a.y2 = op.out2 >= 0 ? (bf16_t*)1 : nullptr;
+            a.Npad = cw.Npad; a.B = B;
+            a.Cx = h->tensors[op.in].C; a.x_off = op.in_off; a.Cy = h->tensors[op.out].C; a.y_off = op.out_off;
+            if (op.res >= 0) { a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
             int TH, variant;
-            if (band_enabled() && band_plan(a, &TH, &variant) && variant >= 3) tile = FR_TILE_BAND;
+            if (img28_enabled() && img28_supported(a)) tile = FR_TILE_IMG28;
+            else if (band_enabled() && band_plan(a, &TH, &variant) && variant >= 3) tile = FR_TILE_BAND;
             else if (sp == 1 && autotune_enabled() && !conv_tile_forced() && find_tuned(h, a) >= 0) tile = find_tuned(h, a);
         }
         const std::string nm = op.kind == OP_HEAD ? "head" : h->tensors[op.out].name;
@@ -1502,6 +1521,11 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         int TH, variant;
         if (!band_plan(a, &TH, &variant)) { set_error("fr_op_conv2d: band kernel not applicable"); return FR_ERR_ARG; }
         FR_HIP_CHECK(launch_conv_band(a, TH, variant, (hipStream_t)stream));
+        return FR_OK;
+    }
+    if (d->tile == FR_TILE_IMG28 + 1) {
+        if (!img28_supported(a)) { set_error("fr_op_conv2d: img28 kernel not applicable"); return FR_ERR_ARG; }
+        FR_HIP_CHECK(launch_conv_img28(a, (hipStream_t)stream));
         return FR_OK;
     }
     if (d->tile > 0) {

@@ -53,6 +53,9 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
 // Row-band direct 3x3/s1/p1 conv (conv_band.hip): applicability/params, launch.
 bool band_plan(const ConvArgs& a, int* cfg, int* variant);
 hipError_t launch_conv_band(const ConvArgs& a, int cfg, int variant, hipStream_t s);
+// Image-per-workgroup direct 3x3/s1/p1 conv for 28x28, 128 -> 128 channels (conv_img.hip).
+bool img28_supported(const ConvArgs& a);
+hipError_t launch_conv_img28(const ConvArgs& a, hipStream_t s);
 // LDS-resident stage kernel (conv_stage.hip): the stride-1 IBasicBlocks of a 14x14x256 stage, one
 // workgroup per image, activation kept in LDS across all 2*nblk convs.
 struct StageConv {

@@ -34,8 +34,10 @@ def pack_weight(w: torch.Tensor, device, dtype: str = "bf16") -> tuple:
 
 def conv_op(x_nhwc, w, *, stride=(1, 1), pad=(0, 0), bias=None, act=0, slope=None, res=None, res_off=0,
             x_off=0, cin=None, y=None, y_off=0, y2=None, aff_s=None, aff_b=None, split_k=1, dtype="bf16",
-            tile=None, bias9=None):
-    """Run fr_op_conv2d. x_nhwc: cuda 16-bit [B,H,W,Cx] of `dtype`; w: cpu f32 [Cout,Cin,kh,kw]."""
+            tile=None, bias9=None, timed_iters=0):
+    """Run fr_op_conv2d. x_nhwc: cuda 16-bit [B,H,W,Cx] of `dtype`; w: cpu f32 [Cout,Cin,kh,kw].
+    timed_iters > 0 (tools/conv_bench.py): also relaunch it that many times, timed one by one with
+    events on the launching stream; returns (y, [ms, ...])."""
     dev = x_nhwc.device
     assert x_nhwc.dtype == TORCH_DT[dtype]
     B, H, W, Cx = x_nhwc.shape
@@ -81,6 +83,16 @@ def conv_op(x_nhwc, w, *, stride=(1, 1), pad=(0, 0), bias=None, act=0, slope=Non
         d.split_k, d.partial = split_k, part.data_ptr()
     N.check(N.lib().fr_op_conv2d(ctypes.byref(d), N.stream_ptr(dev)), "fr_op_conv2d")
     torch.cuda.synchronize(dev)
+    if timed_iters:
+        ms = []
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(timed_iters):
+            e0.record()
+            N.check(N.lib().fr_op_conv2d(ctypes.byref(d), N.stream_ptr(dev)), "fr_op_conv2d")
+            e1.record()
+            torch.cuda.synchronize(dev)
+            ms.append(e0.elapsed_time(e1))
+        return y, ms
     return y
 
 

@@ -101,6 +101,40 @@ def test_conv_band(gpu, case, dtype):
     _close(y2, y.float().cpu() * s + t, tol=tol)
 
 
+@pytest.mark.parametrize("dtype", ["bf16"])  # (f16 nets have no 28x28x128 convs: the kernel is bf16-only)
+@pytest.mark.parametrize("B", [1, 3])
+def test_conv_img28(gpu, B, dtype):
+    """Image-per-workgroup layer2 kernel (conv_img.hip, forced): 3x3/s1/p1 28x28 128->128 with the
+    IResNet conv2 epilogue (bias + residual) and the conv1 one (PReLU)."""
+    g = torch.Generator().manual_seed(28 + B)
+    x = torch.randn(B, 28, 28, 128, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    w = torch.randn(128, 128, 3, 3, generator=g) / np.sqrt(128 * 9)
+    bias = torch.randn(128, generator=g) * 0.1
+    slope = torch.rand(128, generator=g) * 0.5
+    res = torch.randn(B, 28, 28, 128, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    tol = 1e-2 if dtype == "bf16" else 2e-3
+    y = conv_op(x, w, pad=(1, 1), bias=bias, res=res, dtype=dtype, tile=N.FR_TILE_IMG28)
+    _close(y, conv_ref(x, w, pad=(1, 1), bias=bias, res=res, dtype=dtype), tol=tol)
+    y = conv_op(x, w, pad=(1, 1), bias=bias, act=2, slope=slope, dtype=dtype, tile=N.FR_TILE_IMG28)
+    _close(y, conv_ref(x, w, pad=(1, 1), bias=bias, act=2, slope=slope, dtype=dtype), tol=tol)
+
+
+def test_conv_img28_channel_slices_and_applicability(gpu):
+    """img28 reads channels [128:256) of a 256-ch buffer and writes [64:192) of another; other shapes
+    are refused (fail loudly, no silent fallback)."""
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(2, 28, 28, 256, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(128, 128, 3, 3, generator=g) / 34
+    out = torch.randn(2, 28, 28, 256, generator=g).to(torch.bfloat16).to(gpu)
+    before = out.clone()
+    conv_op(x, w, pad=(1, 1), x_off=128, cin=128, act=1, y=out, y_off=64, tile=N.FR_TILE_IMG28)
+    _close(out[..., 64:192], conv_ref(x, w, pad=(1, 1), x_off=128, cin=128, act=1))
+    assert torch.equal(out[..., :64], before[..., :64]) and torch.equal(out[..., 192:], before[..., 192:])
+    x14 = torch.randn(2, 14, 14, 128, generator=g).to(torch.bfloat16).to(gpu)
+    with pytest.raises(RuntimeError, match="img28"):
+        conv_op(x14, w, pad=(1, 1), tile=N.FR_TILE_IMG28)
+
+
 def test_conv_residual_prelu_dual_output(gpu):
     g = torch.Generator().manual_seed(5)
     B, H, Cin, Cout = 2, 14, 128, 128
@@ -299,7 +333,7 @@ def _border_class(H, W):
 
 
 BIAS9_CASES = [(2, 14, 14, 256, 256, None), (2, 14, 14, 256, 256, N.FR_TILE_BAND), (2, 28, 28, 128, 128, None),
-               (2, 56, 56, 64, 64, 2), (2, 28, 28, 128, 128, 0)]
+               (2, 56, 56, 64, 64, 2), (2, 28, 28, 128, 128, 0), (2, 28, 28, 128, 128, N.FR_TILE_IMG28)]
 
 
 @pytest.mark.parametrize("case", BIAS9_CASES)
