@@ -67,6 +67,7 @@ struct Op {
     int wi = -1;
     int pk = 0, ps = 0, pp = 0;
     int stage = -1;  // OP_STAGE: its StageRec; OP_CONV: the stage that covers it (skipped when stages run)
+    bool fuse_stem = false;  // OP_PRE of IResNet100: u8 input runs preprocess + the next (stem) conv fused
 };
 
 // One LDS-resident stage (conv_stage.hip): blocks [first, first+nblk) of a 14x14x256 layer.
@@ -524,6 +525,7 @@ void build_iresnet100(Builder& b) {
     int x = b.tensor(112, 112, 64, "prelu");
     b.stem = true;
     b.conv({"conv1"}, in, 0, 8, x, 0, 3, 3, 1, 1, 1, 1, 2);
+    h->ops[h->ops.size() - 2].fuse_stem = true;  // conv_stem.hip (u8 input)
     const int planes[4] = {64, 128, 256, 512}, nblk[4] = {3, 13, 30, 3};
     int H = 112, C = 64;
     for (int l = 0; l < 4; ++l) {
@@ -759,6 +761,14 @@ bool img28_enabled() {
     return on;
 }
 
+bool stem_fuse_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_STEM_FUSE");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 bool band_enabled() {
     static const bool on = [] {
         const char* e = getenv("FR_NO_BAND");
@@ -919,7 +929,10 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
 int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
     const int f16 = h->dtype == FR_DTYPE_F16;
     if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s));
-    for (const auto& op : h->ops) {
+    bool skip_next = false;
+    for (size_t oi = 0; oi < h->ops.size(); ++oi) {
+        const Op& op = h->ops[oi];
+        if (skip_next) { skip_next = false; continue; }
         if (op.kind == OP_STAGE ? !h->use_stage : (op.stage >= 0 && h->use_stage)) continue;
         switch (op.kind) {
             case OP_STAGE: {
@@ -942,6 +955,23 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
             }
             case OP_PRE: {
                 ProfScope ps(h, s);
+                // u8 crops: preprocess + stem conv in one launch (conv_stem.hip).  Not under fp8, whose
+                // next conv needs the stem output's amax from the conv epilogue.
+                if (op.fuse_stem && in_fmt == FR_IN_U8_NHWC && !h->amax && stem_fuse_enabled() && oi + 1 < h->ops.size() &&
+                    h->ops[oi + 1].kind == OP_CONV) {
+                    const Op& cv = h->ops[oi + 1];
+                    const auto& cw = h->convw[cv.wi];
+                    const auto& to = h->tensors[cv.out];
+                    if (stem_u8_supported(to.H, to.W, cv.cin, cw.K, cw.Kpad, cw.Cout, to.C, cv.out_off) && !cw.bias9 &&
+                        cv.res < 0 && cv.out2 < 0 && cv.sh == 1 && cv.ph == 1 && cv.kh == 3 && cv.kw == 3) {
+                        ps.flops = 2.0 * B * to.H * to.W * cw.Cout * 27.0;
+                        ps.start("stem u8 fused");
+                        FR_HIP_CHECK(launch_stem_u8((const uint8_t*)in, B, cw.w, cw.Kpad, cw.bias, cw.slope, cv.act,
+                                                    to.dev, to.C, cv.out_off, f16, s));
+                        skip_next = true;
+                        break;
+                    }
+                }
                 ps.start("preprocess");
                 const auto& t = h->tensors[op.out];
                 FR_HIP_CHECK(launch_preprocess(in, in_fmt, B, t.H, t.W, t.dev, f16, s));

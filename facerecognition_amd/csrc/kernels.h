@@ -88,6 +88,10 @@ inline int conv_k_tiles(int Kpad) { return Kpad / 64; }
 // q = 255*x (normalized f32).  The stem conv folds 1/255 and a hi/lo weight split into the
 // duplicated channels, so x = (u/255-0.5)/0.5 enters the first conv without rounding.
 hipError_t launch_preprocess(const void* in, int in_fmt, int B, int H, int W, bf16_t* out, int f16, hipStream_t s);
+// Fused u8 preprocess + IResNet stem conv (conv_stem.hip).
+bool stem_u8_supported(int H, int W, int Cin, int K, int Kpad, int Cout, int Cy, int y_off);
+hipError_t launch_stem_u8(const uint8_t* in, int B, const bf16_t* w, int Kpad, const float* bias, const float* slope,
+                          int act, bf16_t* y, int Cy, int y_off, int f16, hipStream_t s);
 hipError_t launch_maxpool(const bf16_t* x, int B, int H, int W, int Cx, int x_off, int C, int k, int stride,
                           int pad, bf16_t* y, int Cy, int y_off, int Ho, int Wo, int f16, hipStream_t s);
 hipError_t launch_avgpool(const bf16_t* x, int B, int H, int W, int C, bf16_t* y, int f16, hipStream_t s);
