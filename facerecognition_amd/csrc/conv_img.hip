@@ -1,21 +1,19 @@
-// Image-per-workgroup direct 3x3 convolution (stride 1, pad 1) for the 28x28x128 IBasicBlock convs of
-// IResNet100 layer2 (layer2.1 .. layer2.12: 24 convs, 22.9 % of the network's FLOPs).
+// Row-band direct 3x3 convolution (stride 1, pad 1) for the 28x28x128 IBasicBlock convs of IResNet100
+// layer2 (layer2.1 .. layer2.12: 24 convs, 22.9 % of the network's FLOPs).
 //
 // As an implicit GEMM these convs re-gather every input pixel for all 9 taps (9x the activation bytes
 // L2 -> LDS: at the MFMA rate ~99 GB/s per CU, above the ~70 GB/s an LDS-DMA gather sustains per CU,
-// MI355X_MICROARCH.md "Indexed rows"), and 200704 output rows quantize badly on 256 CUs (3.06 rounds
-// of 256-row tiles).  Here one workgroup owns one image (bs = 256 -> exactly one round on 256 CUs) and
-// walks it as two 14-row halves:
-//   * per 32-input-channel chunk the (14+2) x (28+2) zero-haloed patch is DMA'd into LDS once
-//     ([4 planes of 8 channels][480 positions][16 B], plane stride a multiple of 256 B) and read by all
-//     9 taps at shifted positions; the next chunk's patch (double buffer) streams in during the
-//     current chunk's 9 K-steps, across the half boundary too;
+// MI355X_MICROARCH.md "Indexed rows").  Here a workgroup owns a quarter image (7 output rows x 28) x
+// all 128 output channels, two workgroups per CU (4B workgroups = 4 per CU at bs = 256, so one
+// workgroup's epilogue overlaps the other's main loop):
+//   * per 32-input-channel chunk the 9 x 30 zero-haloed patch is DMA'd into LDS once ([4 planes of 8
+//     channels][9 rows][32 positions][16 B]) and read by all 9 taps at shifted positions; the next
+//     chunk's patch (double buffer) streams in during the current chunk's 9 K-steps;
 //   * per K-step (chunk, tap) the [128 out][32 in] weight slice (8 KiB) is gathered straight from the
-//     implicit-GEMM weight rows [Npad][Kpad] (K order (kh, kw, c)) into a 4-slot LDS ring, three steps
-//     ahead; one s_barrier per K-step;
-//   * 2x4 waves, two per SIMD (the second hides the other's LDS latency): wave (wm, wn) computes rows
-//     7wm..7wm+6 of the half (196 pixels = 13 m-frags, the last one 4/16 valid) x output channels
-//     32wn..32wn+31 (2 n-frags): 26 v_mfma_f32_16x16x32_{bf16,f16} per K-step, 104 f32 accumulators;
+//     implicit-GEMM weight rows [Npad][Kpad] (K order (kh, kw, c)) into a 3-slot LDS ring, three steps
+//     ahead; one mid-step s_barrier per K-step (the stage kernel's schedule, conv_stage.hip);
+//   * 2x2 waves: wave (wm, wn) computes 7 virtual-pixel frags (rows 0..6 x 32 columns, 28 valid) x
+//     64 output channels (4 n-frags): 28 v_mfma_f32_16x16x32_bf16 per K-step, 112 f32 accumulators;
 //   * operand A = weight rows, operand B = patch positions, so a lane ends with 4 consecutive channels
 //     of one pixel; the epilogue (bias or border-class bias9, residual, ReLU/PReLU) stores 8 B per lane.
 #include "kernels.h"
@@ -33,18 +31,19 @@ namespace {
 
 constexpr int IW = 28;                   // image width = height
 constexpr int IC = 128;                  // input = output channels
-constexpr int HR = 14;                   // output rows per half
+constexpr int QR = 7;                    // output rows per workgroup (a quarter image)
 constexpr int PC = 32;                   // patch row stride in positions (col c+1 = image col c; 0, 29 halo)
-constexpr int PPOS = (HR + 2) * PC;      // 512 positions per plane
-constexpr int PLANE_B = PPOS * 16;       // 8192
-constexpr int PATCH_B = 4 * PLANE_B;     // 32768: one 32-channel chunk = 32 pieces of 1 KiB
+constexpr int PPOS = (QR + 2) * PC;      // 288 positions per plane
+constexpr int PLANE_B = PPOS * 16;       // 4608 = 18 x 256 B
+constexpr int PATCH_PIECES = 20;         // 18 real 1-KiB pieces + 2 zero pieces (5 per wave)
+constexpr int PATCH_B = PATCH_PIECES * 1024;
 constexpr int SLICE_B = 4 * IC * 16;     // 8192: [4 groups of 8 ch][128 rows][16 B]
 constexpr int NSLOT = 3;
-constexpr int IMG_LDS = 2 * PATCH_B + NSLOT * SLICE_B;  // 90112
+constexpr int IMG_LDS = 2 * PATCH_B + NSLOT * SLICE_B;  // 65536: two workgroups per CU
 constexpr int NCH = IC / 32;             // 4 chunks of 32 input channels
-constexpr int HSTEPS = NCH * 9;          // 36 K-steps per half
-constexpr int FM = 7;                    // virtual-pixel frags per wave (4 waves x 7 x 16 = 14 rows x 32)
-constexpr int FN = 8;                    // channel frags per wave (all 128)
+constexpr int NSTEP = NCH * 9;           // 36 K-steps
+constexpr int FM = 7;                    // virtual-pixel frags per wave (2 x 7 x 16 = 7 rows x 32)
+constexpr int FN = 4;                    // channel frags per wave (64 of the 128)
 constexpr uint32_t OOB = 0x80000000u;
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -57,7 +56,7 @@ __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* 
 // RES: residual input (IBasicBlock conv2); B9: border-class bias table (conv1 with bn1 folded).  The
 // epilogue is specialised on them so its loads issue together instead of behind per-pixel branches.
 template <bool F16, bool RES, bool B9>
-__global__ __launch_bounds__(256, 1) void conv_img28_kernel(ConvArgs p) {
+__global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
     extern __shared__ __attribute__((aligned(16))) char smem[];  // [patch 0][patch 1][slot 0..2]
@@ -65,30 +64,29 @@ __global__ __launch_bounds__(256, 1) void conv_img28_kernel(ConvArgs p) {
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = blockIdx.x;
+    const int wm = wave & 1, wn = wave >> 1;  // virtual frags 7wm..7wm+6, output channels 64wn..64wn+63
+    const int b = blockIdx.x >> 2, q = blockIdx.x & 3, r0 = QR * q;
 
     const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * IW * IW * p.Cx * 2);
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
     const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
 
-    // patch of chunk q = 4h + cc (half h, input channels 32cc..): 8 pieces per wave, plane-major
-    // [4 planes][16 rows][32 positions][16 B]; halo and pad positions read out of range (zeros).
-    // Offsets are recomputed per chunk (VALU every 9 K-steps, no live registers); the chunk's channel
-    // offset goes in the scalar offset (rows stay in voff: a negative voff would wrap).
-    auto issue_patch = [&](int q, int buf) {
-#if FR_IMG_EXP == 2 || FR_IMG_EXP == 4  // timing experiment: no patch stream (after the first chunk)
-        if (q > 0) return;
+    // patch of chunk cc (input channels 32cc..): 5 pieces per wave, plane-major [4 planes][9 rows][32
+    // positions][16 B]; halo, pad and the 2 spare pieces read out of range (zeros).  Offsets recomputed
+    // per chunk (no live registers); the chunk's channel offset in the scalar offset.
+    auto issue_patch = [&](int cc, int buf) {
+#if FR_IMG_EXP == 2
+        if (cc > 0) return;
 #endif
-        const int h = q >> 2, cc = q & 3;
         int ln = lane;
         asm volatile("" : "+v"(ln));  // opaque copy: the offsets are not hoisted (registers for the MFMAs)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < PATCH_PIECES / 4; ++u) {
             const int piece = 4 * u + wave, sl = piece * 64 + ln;
             const int plane = sl / PPOS, pos = sl % PPOS, pr = pos / PC, pc = pos % PC;
-            const int ir = HR * h - 1 + pr, ic = pc - 1;
-            const bool in = (unsigned)ir < (unsigned)IW && (unsigned)ic < (unsigned)IW;
+            const int ir = r0 - 1 + pr, ic = pc - 1;
+            const bool in = plane < 4 && (unsigned)ir < (unsigned)IW && (unsigned)ic < (unsigned)IW;
             const uint32_t off =
                 in ? (uint32_t)((((size_t)b * IW * IW + ir * IW + ic) * p.Cx + p.x_off + plane * 8) * 2) : OOB;
             dma16s(xr, smem + buf * PATCH_B + piece * 1024, off, (uint32_t)(cc * 32 * 2));
@@ -103,7 +101,7 @@ __global__ __launch_bounds__(256, 1) void conv_img28_kernel(ConvArgs p) {
         wv[u] = (uint32_t)(((size_t)(64 * (piece & 1) + lane) * p.Kpad + (piece >> 1) * 8) * 2);
     }
     auto issue_w = [&](int s, int slot) {
-#if FR_IMG_EXP == 1 || FR_IMG_EXP == 4  // timing experiment: no weight stream (after the first slices)
+#if FR_IMG_EXP == 1
         if (s > 2) return;
 #endif
         const int cc = s / 9, tap = s - cc * 9;
@@ -112,13 +110,17 @@ __global__ __launch_bounds__(256, 1) void conv_img28_kernel(ConvArgs p) {
             dma16s(wr, slots + slot * SLICE_B + (2 * wave + u) * 1024, wv[u], (uint32_t)((tap * IC + cc * 32) * 2));
     };
 
-    // fragment addresses: B (patch) virtual frag f = 7*wave + j -> positions 16f + (lane&15) (row f/2,
-    // columns 16(f%2)..: linear, so one base + compile-time offsets), plane (lane>>4); A (weights)
-    // rows 16i + (lane&15), group (lane>>4)
-    const int pbase = (lane >> 4) * PLANE_B + (112 * wave + (lane & 15)) * 16;
-    const int woff = (lane >> 4) * (IC * 16) + (lane & 15) * 16;
+    // fragment addresses: B (patch) virtual frag f = 7wm + j -> positions 16f + (lane&15) (row f/2,
+    // columns 16(f%2)..: linear, one base + compile-time offsets), plane (lane>>4); A (weights) rows
+    // 64wn + 16i + (lane&15), group (lane>>4)
+    const int pbase = (lane >> 4) * PLANE_B + (112 * wm + (lane & 15)) * 16;
+    const int woff = (lane >> 4) * (IC * 16) + (64 * wn + (lane & 15)) * 16;
 
     f32x4_t acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     frag wf[FN], pA[FM], pB[FM];
     auto pread = [&](frag (&pf)[FM], int buf, int tap) {
         const int dh = tap / 3, dw = tap % 3;
@@ -139,124 +141,103 @@ __global__ __launch_bounds__(256, 1) void conv_img28_kernel(ConvArgs p) {
 #pragma unroll
     for (int i = 0; i < FN; ++i) wread(i, 0);
 
-    // one K-step (the stage kernel's schedule, conv_stage.hip): step s of half h (G = 36h + s; slot
-    // s % 3, chunk c = s / 9, tap t = s % 9; compile-time but h).  nxt <- patch fragments of step G+1;
-    // MFMAs of weight frags 0..3; mid-step barrier: this wave's slice G+1 landed (younger: slice G+2
-    // and the 8 patch pieces issued at a chunk start in step G-2 or G-1), every wave is past its reads
-    // of slot s % 3 and of the previous chunk's patch buffer; DMA of slice G+3 into slot s % 3 and, at
-    // t == 0, of the next chunk's patch; wf <- slice G+1 (0..3 now, 4..7 in place after their MFMAs).
-    // The next chunk's patch is read at the start of its t == 8 step: the t == 7 barrier covered it.
-    auto kstep = [&](int h, int s, frag (&cur)[FM], frag (&nxt)[FM]) {
+    // one K-step s (slot s % 3, chunk c = s / 9, tap t = s % 9): nxt <- patch fragments of step s+1;
+    // MFMAs of weight frags 0, 1; mid-step barrier: this wave's slice s+1 landed (younger: slice s+2
+    // and the 5 patch pieces of a chunk start at step s-2 or s-1), every wave is past its reads of slot
+    // s % 3 and of the previous chunk's patch buffer; DMA of slice s+3 into slot s % 3 and, at t == 0,
+    // of the next chunk's patch; wf <- slice s+1 (0, 1 now, 2, 3 in place after their MFMAs).  The
+    // next chunk's patch is read at the start of its t == 8 step: the t == 7 barrier covered it.
+    auto kstep = [&](int s, frag (&cur)[FM], frag (&nxt)[FM]) {
         const int t = s % 9, c = s / 9, slot = s % NSLOT, nslot = (s + 1) % NSLOT;
-        pread(nxt, t == 8 ? (c + 1) & 1 : c & 1, t == 8 ? 0 : t + 1);  // (tail: unused reads)
+        if (s + 1 < NSTEP) pread(nxt, t == 8 ? (c + 1) & 1 : c & 1, t == 8 ? 0 : t + 1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
-        // first half: one patch read after every 4 MFMAs (the compiler would sink them to the end)
+        // first half: the 7 next-step patch reads spread over the 14 MFMAs (the compiler would sink them
+        // to the barrier, exposing their latency)
 #pragma unroll
-        for (int q = 0; q < FM; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        for (int qq = 0; qq < FM; ++qq) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        if (t == 1 || t == 2) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (t == 1 || t == 2) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        issue_w(s + 3 < HSTEPS ? s + 3 : (h == 0 ? s + 3 - HSTEPS : HSTEPS - 1), slot);  // tail: re-fetch
-        if (t == 0) {
-            const int qn = 4 * h + c + 1;
-            issue_patch(qn < 2 * NCH ? qn : 2 * NCH - 1, (c + 1) & 1);
-        }
+        issue_w(s + 3 < NSTEP ? s + 3 : NSTEP - 1, slot);  // tail: harmless re-fetch (uniform counts)
+        if (t == 0) issue_patch(c + 1 < NCH ? c + 1 : NCH - 1, (c + 1) & 1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) wread(i, nslot);
+        for (int i = 0; i < 2; ++i) wread(i, nslot);
 #pragma unroll
-        for (int i = 4; i < FN; ++i) {
+        for (int i = 2; i < FN; ++i) {
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
             wread(i, nslot);
         }
-        // second half: the wf[0..3] refills spread over the first 8 MFMAs, then each wf[4..7] refill
-        // right after its 7th MFMA
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
-        }
+        // second half: wf[0], wf[1] refills early, wf[2], wf[3] right after their last MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 11, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     };
+#pragma unroll
+    for (int s = 0; s < NSTEP; s += 2) {
+        kstep(s, pA, pB);
+        kstep(s + 1, pB, pA);
+    }
 
+    // ---- epilogue: straight from the accumulators (no LDS), 8 B per lane and (i, j).  Per channel
+    // group i the 7 residual / bias9 loads issue together (pad columns read a valid pixel and skip
+    // only the store).  The other workgroup on the CU computes meanwhile.
     const size_t img = (size_t)b * IW * IW;
-#pragma unroll 1
-    for (int h = 0; h < 2; ++h) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // opaque copy: keeps the per-(i, j) addresses from being hoisted
 #pragma unroll
-        for (int i = 0; i < FN; ++i)
+    for (int i = 0; i < FN; ++i) {
+        const int n = 64 * wn + 16 * i + 4 * (ln >> 4);
+        float4 sl = make_float4(0.f, 0.f, 0.f, 0.f), bb = sl;
+        if (p.act == 2) sl = *(const float4*)(p.slope + n);
+        if (!B9 && p.bias) bb = *(const float4*)(p.bias + n);
+        size_t m[FM];
+        int cls[FM];
+        bool ok[FM];
 #pragma unroll
-            for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-        // 36 steps, unrolled so slots / taps / buffers are compile-time (36 % 3 == 0, 36 % 2 == 0)
-#pragma unroll
-        for (int s = 0; s < HSTEPS; s += 2) {
-            kstep(h, s, pA, pB);
-            kstep(h, s + 1, pB, pA);
+        for (int j = 0; j < FM; ++j) {
+            const int f = FM * wm + j, c = 16 * (f & 1) + (ln & 15), r = r0 + (f >> 1);
+            ok[j] = c < IW;
+            m[j] = img + r * IW + (ok[j] ? c : 0);
+            cls[j] = border_class(r, c, IW, IW);
         }
-        // ---- epilogue: straight from the accumulators (no LDS), 8 B per lane and (i, j).  Per channel
-        // group i the 7 residual / bias9 loads issue together (pad columns read a valid pixel and skip
-        // only the store).
-        int ln = lane;
-        asm volatile("" : "+v"(ln));  // opaque copy: keeps the per-(i, j) addresses from being hoisted
+        uint2 rr[FM];
+        float4 b9[FM];
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-            const int n = 16 * i + 4 * (ln >> 4);
-            float4 sl = make_float4(0.f, 0.f, 0.f, 0.f), bb = sl;
-            if (p.act == 2) sl = *(const float4*)(p.slope + n);
-            if (!B9 && p.bias) bb = *(const float4*)(p.bias + n);
-            size_t m[FM];
-            int cls[FM];
-            bool ok[FM];
+        for (int j = 0; j < FM; ++j) {
+            if (RES) rr[j] = *(const uint2*)(p.res + m[j] * p.Cres + p.res_off + n);
+            if (B9) b9[j] = *(const float4*)(p.bias9 + cls[j] * p.Npad + n);
+        }
 #pragma unroll
-            for (int j = 0; j < FM; ++j) {
-                const int f = FM * wave + j, c = 16 * (f & 1) + (ln & 15), r = HR * h + (f >> 1);
-                ok[j] = c < IW;
-                m[j] = img + r * IW + (ok[j] ? c : 0);
-                cls[j] = border_class(r, c, IW, IW);
+        for (int j = 0; j < FM; ++j) {
+            float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
+            if (B9) { v[0] += b9[j].x; v[1] += b9[j].y; v[2] += b9[j].z; v[3] += b9[j].w; }
+            if (RES) {
+                float f8[8];
+                T::unpack8(make_uint4(rr[j].x, rr[j].y, 0, 0), f8);
+                v[0] += f8[0]; v[1] += f8[1]; v[2] += f8[2]; v[3] += f8[3];
             }
-            uint2 rr[FM];
-            float4 b9[FM];
+            if (p.act == 2) {
+                v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
+                v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
+                v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
+                v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
+            } else if (p.act == 1) {
 #pragma unroll
-            for (int j = 0; j < FM; ++j) {
-                if (RES) rr[j] = *(const uint2*)(p.res + m[j] * p.Cres + p.res_off + n);
-                if (B9) b9[j] = *(const float4*)(p.bias9 + cls[j] * p.Npad + n);
+                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
             }
-#pragma unroll
-            for (int j = 0; j < FM; ++j) {
-                float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
-                if (B9) { v[0] += b9[j].x; v[1] += b9[j].y; v[2] += b9[j].z; v[3] += b9[j].w; }
-                if (RES) {
-                    float f8[8];
-                    T::unpack8(make_uint4(rr[j].x, rr[j].y, 0, 0), f8);
-                    v[0] += f8[0]; v[1] += f8[1]; v[2] += f8[2]; v[3] += f8[3];
-                }
-                if (p.act == 2) {
-                    v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
-                    v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
-                    v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
-                    v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
-                } else if (p.act == 1) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-                }
-                float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
-                const uint4 pk = T::pack8(o8);
-#if FR_IMG_EXP == 5  // timing experiment: epilogue stores only where the value is a NaN
-                if (ok[j] && v[0] != v[0]) *(uint2*)(p.y + m[j] * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
-#else
-                if (ok[j]) *(uint2*)(p.y + m[j] * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
-#endif
-            }
+            float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+            const uint4 pk = T::pack8(o8);
+            if (ok[j]) *(uint2*)(p.y + m[j] * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs land before the LDS is released
@@ -284,9 +265,9 @@ hipError_t launch_conv_img28(const ConvArgs& a, hipStream_t s) {
         attr[v] = true;
     }
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, dim3(a.B), dim3(256), IMG_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
+        hipExtLaunchKernelGGL(k, dim3(4 * a.B), dim3(256), IMG_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
     else
-        hipLaunchKernelGGL(k, dim3(a.B), dim3(256), IMG_LDS, s, a);
+        hipLaunchKernelGGL(k, dim3(4 * a.B), dim3(256), IMG_LDS, s, a);
     return hipGetLastError();
 }
 
