@@ -29,23 +29,32 @@ namespace {
 #define FR_IMG_EXP 0  // timing experiments only (tools/img_exp.sh: 1 no weight DMA, 2 no patch DMA, 4 neither); 0 in every shipped build
 #endif
 
-constexpr int IW = 28;                   // image width = height
-constexpr int IC = 128;                  // input = output channels
-constexpr int QR = 7;                    // output rows per workgroup (a quarter image)
-constexpr int PC = 32;                   // patch row stride in positions (col c+1 = image col c; 0, 29 halo)
-constexpr int PPOS = (QR + 2) * PC;      // 288 positions per plane
-constexpr int PLANE_B = PPOS * 16;       // 4608 = 18 x 256 B
-constexpr int PATCH_PIECES = 20;         // 18 real 1-KiB pieces + 2 zero pieces (5 per wave)
-constexpr int PATCH_B = PATCH_PIECES * 1024;
-constexpr int SLICE_B = 4 * IC * 16;     // 8192: [4 groups of 8 ch][128 rows][16 B]
-constexpr int NSLOT = 3;
-constexpr int IMG_LDS = 2 * PATCH_B + NSLOT * SLICE_B;  // 65536: two workgroups per CU
-constexpr int NCH = IC / 32;             // 4 chunks of 32 input channels
-constexpr int NSTEP = NCH * 9;           // 36 K-steps
-constexpr int FM = 7;                    // virtual-pixel frags per wave (2 x 7 x 16 = 7 rows x 32)
-constexpr int FN = 4;                    // channel frags per wave (64 of the 128)
-constexpr uint32_t OOB = 0x80000000u;
+// Geometry of one instance: IW x IW images with IC input = output channels; a workgroup owns QR output
+// rows x all IC channels, laid out as QR rows x PCOL virtual columns (IW valid + pad) = 16-pixel frags;
+// 4 waves = PG pixel groups x (4 / PG) channel groups.
+template <int IW_, int IC_, int QR_, int PCOL_, int PG_>
+struct ImgGeo {
+    static constexpr int IW = IW_, IC = IC_, QR = QR_, PC = PCOL_, PG = PG_, CG = 4 / PG_;
+    static constexpr int PPOS = (QR + 2) * PC;                      // positions per plane (halo rows)
+    static constexpr int PLANE_B = PPOS * 16;                       // a multiple of 256 B
+    static constexpr int PATCH_PIECES = (4 * PLANE_B / 1024 + 3) / 4 * 4;  // 1-KiB pieces, 4 | count
+    static constexpr int PATCH_B = PATCH_PIECES * 1024;
+    static constexpr int SLICE_B = 4 * IC * 16;                     // [4 groups of 8 ch][IC rows][16 B]
+    static constexpr int WP = SLICE_B / 1024 / 4;                   // weight pieces per wave per step
+    static constexpr int PP = PATCH_PIECES / 4;                     // patch pieces per wave per chunk
+    static constexpr int NSLOT = 3;
+    static constexpr int LDS = 2 * PATCH_B + NSLOT * SLICE_B;
+    static constexpr int NCH = IC / 32;
+    static constexpr int NSTEP = NCH * 9;
+    static constexpr int FM = QR * PC / 16 / PG;                    // pixel frags per wave
+    static constexpr int FN = IC / 16 / CG;                         // channel frags per wave
+    static constexpr int BANDS = IW / QR;                           // workgroups per image
+    static_assert(PLANE_B % 256 == 0 && IW % QR == 0 && PC % 16 == 0 && PC >= IW + 2 && FN % 2 == 0, "geometry");
+};
+typedef ImgGeo<28, 128, 7, 32, 2> Geo28;  // layer2: 2 x 2 waves of 7 frags x 64 channels, 64 KiB LDS
+typedef ImgGeo<56, 64, 4, 64, 4> Geo56;   // layer1: 4 waves of 4 frags (one virtual row) x 64 channels
 
+constexpr uint32_t OOB = 0x80000000u;
 typedef __attribute__((address_space(3))) void lds_void;
 
 // LDS-DMA of 16 B per lane; soff: a wave-uniform byte offset (memory address only)
@@ -53,27 +62,34 @@ __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* 
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, soff, 0, 0);
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
 // RES: residual input (IBasicBlock conv2); B9: border-class bias table (conv1 with bn1 folded).  The
 // epilogue is specialised on them so its loads issue together instead of behind per-pixel branches.
-template <bool F16, bool RES, bool B9>
-__global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
+template <bool F16, bool RES, bool B9, typename G>
+__global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
+    constexpr int IW = G::IW, IC = G::IC, PC = G::PC, FM = G::FM, FN = G::FN, NCH = G::NCH, NSTEP = G::NSTEP;
+    constexpr int NSLOT = G::NSLOT, PATCH_B = G::PATCH_B, SLICE_B = G::SLICE_B, PLANE_B = G::PLANE_B;
     extern __shared__ __attribute__((aligned(16))) char smem[];  // [patch 0][patch 1][slot 0..2]
     char* const slots = smem + 2 * PATCH_B;
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 1, wn = wave >> 1;  // virtual frags 7wm..7wm+6, output channels 64wn..64wn+63
-    const int b = blockIdx.x >> 2, q = blockIdx.x & 3, r0 = QR * q;
+    const int wm = wave % G::PG, wn = wave / G::PG;  // pixel frags FM*wm.., output channels 16*FN*wn..
+    const int b = blockIdx.x / G::BANDS, r0 = G::QR * (blockIdx.x % G::BANDS);
 
     const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * IW * IW * p.Cx * 2);
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
     const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
 
-    // patch of chunk cc (input channels 32cc..): 5 pieces per wave, plane-major [4 planes][9 rows][32
-    // positions][16 B]; halo, pad and the 2 spare pieces read out of range (zeros).  Offsets recomputed
+    // patch of chunk cc (input channels 32cc..): PP pieces per wave, plane-major [4 planes][QR+2 rows]
+    // [PC positions][16 B]; halo, pad and spare pieces read out of range (zeros).  Offsets recomputed
     // per chunk (no live registers); the chunk's channel offset in the scalar offset.
     auto issue_patch = [&](int cc, int buf) {
 #if FR_IMG_EXP == 2
@@ -82,9 +98,9 @@ __global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
         int ln = lane;
         asm volatile("" : "+v"(ln));  // opaque copy: the offsets are not hoisted (registers for the MFMAs)
 #pragma unroll
-        for (int u = 0; u < PATCH_PIECES / 4; ++u) {
+        for (int u = 0; u < G::PP; ++u) {
             const int piece = 4 * u + wave, sl = piece * 64 + ln;
-            const int plane = sl / PPOS, pos = sl % PPOS, pr = pos / PC, pc = pos % PC;
+            const int plane = sl / G::PPOS, pos = sl % G::PPOS, pr = pos / PC, pc = pos % PC;
             const int ir = r0 - 1 + pr, ic = pc - 1;
             const bool in = plane < 4 && (unsigned)ir < (unsigned)IW && (unsigned)ic < (unsigned)IW;
             const uint32_t off =
@@ -93,12 +109,12 @@ __global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
         }
     };
     // weight slice of K-step s (chunk cc = s / 9, tap = s % 9) gathered from the [Npad][Kpad] rows,
-    // LDS image [g][n][16 B]: pieces 2wave, 2wave+1 = (group g, rows 64nh..); the step in soffset
-    uint32_t wv[2];
+    // LDS image [g][n][16 B]: WP pieces per wave = (group g, rows 64nh..); the step in soffset
+    uint32_t wv[G::WP];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int piece = 2 * wave + u;
-        wv[u] = (uint32_t)(((size_t)(64 * (piece & 1) + lane) * p.Kpad + (piece >> 1) * 8) * 2);
+    for (int u = 0; u < G::WP; ++u) {
+        const int piece = G::WP * wave + u, g = piece / (IC / 64), nh = piece % (IC / 64);
+        wv[u] = (uint32_t)(((size_t)(64 * nh + lane) * p.Kpad + g * 8) * 2);
     }
     auto issue_w = [&](int s, int slot) {
 #if FR_IMG_EXP == 1
@@ -106,15 +122,15 @@ __global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
 #endif
         const int cc = s / 9, tap = s - cc * 9;
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-            dma16s(wr, slots + slot * SLICE_B + (2 * wave + u) * 1024, wv[u], (uint32_t)((tap * IC + cc * 32) * 2));
+        for (int u = 0; u < G::WP; ++u)
+            dma16s(wr, slots + slot * SLICE_B + (G::WP * wave + u) * 1024, wv[u], (uint32_t)((tap * IC + cc * 32) * 2));
     };
 
-    // fragment addresses: B (patch) virtual frag f = 7wm + j -> positions 16f + (lane&15) (row f/2,
-    // columns 16(f%2)..: linear, one base + compile-time offsets), plane (lane>>4); A (weights) rows
-    // 64wn + 16i + (lane&15), group (lane>>4)
-    const int pbase = (lane >> 4) * PLANE_B + (112 * wm + (lane & 15)) * 16;
-    const int woff = (lane >> 4) * (IC * 16) + (64 * wn + (lane & 15)) * 16;
+    // fragment addresses: B (patch) virtual frag f = FM*wm + j -> positions 16f + (lane&15) (linear:
+    // one base + compile-time offsets), plane (lane>>4); A (weights) rows 16*FN*wn + 16i + (lane&15),
+    // group (lane>>4)
+    const int pbase = (lane >> 4) * PLANE_B + (16 * FM * wm + (lane & 15)) * 16;
+    const int woff = (lane >> 4) * (IC * 16) + (16 * FN * wn + (lane & 15)) * 16;
 
     f32x4_t acc[FN][FM];
 #pragma unroll
@@ -142,45 +158,31 @@ __global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
     for (int i = 0; i < FN; ++i) wread(i, 0);
 
     // one K-step s (slot s % 3, chunk c = s / 9, tap t = s % 9): nxt <- patch fragments of step s+1;
-    // MFMAs of weight frags 0, 1; mid-step barrier: this wave's slice s+1 landed (younger: slice s+2
-    // and the 5 patch pieces of a chunk start at step s-2 or s-1), every wave is past its reads of slot
-    // s % 3 and of the previous chunk's patch buffer; DMA of slice s+3 into slot s % 3 and, at t == 0,
-    // of the next chunk's patch; wf <- slice s+1 (0, 1 now, 2, 3 in place after their MFMAs).  The
-    // next chunk's patch is read at the start of its t == 8 step: the t == 7 barrier covered it.
+    // MFMAs of the first half of the weight frags; mid-step barrier: this wave's slice s+1 landed
+    // (younger: slice s+2 and the PP patch pieces of a chunk start at step s-2 or s-1), every wave is
+    // past its reads of slot s % 3 and of the previous chunk's patch buffer; DMA of slice s+3 into slot
+    // s % 3 and, at t == 0, of the next chunk's patch; wf <- slice s+1 (first half now, second half in
+    // place after their MFMAs).  The next chunk's patch is read at the start of its t == 8 step: the
+    // t == 7 barrier covered it.
     auto kstep = [&](int s, frag (&cur)[FM], frag (&nxt)[FM]) {
         const int t = s % 9, c = s / 9, slot = s % NSLOT, nslot = (s + 1) % NSLOT;
         if (s + 1 < NSTEP) pread(nxt, t == 8 ? (c + 1) & 1 : c & 1, t == 8 ? 0 : t + 1);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < FN / 2; ++i)
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
-        // first half: the 7 next-step patch reads spread over the 14 MFMAs (the compiler would sink them
-        // to the barrier, exposing their latency)
-#pragma unroll
-        for (int qq = 0; qq < FM; ++qq) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        if (t == 1 || t == 2) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (t == 1 || t == 2) wait_vm_barrier<G::WP + G::PP>();
+        else wait_vm_barrier<G::WP>();
         issue_w(s + 3 < NSTEP ? s + 3 : NSTEP - 1, slot);  // tail: harmless re-fetch (uniform counts)
         if (t == 0) issue_patch(c + 1 < NCH ? c + 1 : NCH - 1, (c + 1) & 1);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) wread(i, nslot);
+        for (int i = 0; i < FN / 2; ++i) wread(i, nslot);
 #pragma unroll
-        for (int i = 2; i < FN; ++i) {
+        for (int i = FN / 2; i < FN; ++i) {
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
             wread(i, nslot);
         }
-        // second half: wf[0], wf[1] refills early, wf[2], wf[3] right after their last MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 11, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     };
 #pragma unroll
     for (int s = 0; s < NSTEP; s += 2) {
@@ -189,14 +191,14 @@ __global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
     }
 
     // ---- epilogue: straight from the accumulators (no LDS), 8 B per lane and (i, j).  Per channel
-    // group i the 7 residual / bias9 loads issue together (pad columns read a valid pixel and skip
-    // only the store).  The other workgroup on the CU computes meanwhile.
+    // group i the residual / bias9 loads issue together (pad columns read a valid pixel and skip only
+    // the store).  The other workgroup on the CU computes meanwhile.
     const size_t img = (size_t)b * IW * IW;
     int ln = lane;
     asm volatile("" : "+v"(ln));  // opaque copy: keeps the per-(i, j) addresses from being hoisted
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
-        const int n = 64 * wn + 16 * i + 4 * (ln >> 4);
+        const int n = 16 * FN * wn + 16 * i + 4 * (ln >> 4);
         float4 sl = make_float4(0.f, 0.f, 0.f, 0.f), bb = sl;
         if (p.act == 2) sl = *(const float4*)(p.slope + n);
         if (!B9 && p.bias) bb = *(const float4*)(p.bias + n);
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
         bool ok[FM];
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
-            const int f = FM * wm + j, c = 16 * (f & 1) + (ln & 15), r = r0 + (f >> 1);
+            const int f = FM * wm + j, v = 16 * f + (ln & 15), c = v % PC, r = r0 + v / PC;
             ok[j] = c < IW;
             m[j] = img + r * IW + (ok[j] ? c : 0);
             cls[j] = border_class(r, c, IW, IW);
@@ -243,32 +245,44 @@ __global__ __launch_bounds__(256, 2) void conv_img28_kernel(ConvArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs land before the LDS is released
 }
 
-}  // namespace
-
-bool img28_supported(const ConvArgs& a) {
+template <typename G>
+bool img_supported_t(const ConvArgs& a) {
+    constexpr int IW = G::IW, IC = G::IC;
     return a.Kh == 3 && a.Kw == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.H == IW && a.W == IW &&
            a.Ho == IW && a.Wo == IW && a.Cin == IC && a.Cout == IC && a.Npad >= IC && a.Kpad >= 9 * IC &&
            a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.x_off + IC <= a.Cx && a.Cy % 4 == 0 && a.y_off % 4 == 0 &&
            a.y_off + IC <= a.Cy && !a.y2 && !a.partial && !a.w8 && !a.y_amax && a.B > 0 && !a.f16 &&
-           !(a.res && a.bias9) &&
-           (!a.res || (a.Cres % 4 == 0 && a.res_off % 4 == 0 && a.res_off + IC <= a.Cres));
+           !(a.res && a.bias9) && (!a.res || (a.Cres % 4 == 0 && a.res_off % 4 == 0 && a.res_off + IC <= a.Cres));
 }
 
-hipError_t launch_conv_img28(const ConvArgs& a, hipStream_t s) {
-    if (!img28_supported(a)) return hipErrorInvalidValue;
-    auto k = a.res ? conv_img28_kernel<false, true, false>
-                   : (a.bias9 ? conv_img28_kernel<false, false, true> : conv_img28_kernel<false, false, false>);
+template <typename G>
+hipError_t launch_img_t(const ConvArgs& a, hipStream_t s) {
+    auto k = a.res ? conv_img_kernel<false, true, false, G>
+                   : (a.bias9 ? conv_img_kernel<false, false, true, G> : conv_img_kernel<false, false, false, G>);
     const int v = a.res ? 0 : (a.bias9 ? 1 : 2);
     static bool attr[3] = {false, false, false};
     if (!attr[v]) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, IMG_LDS);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         attr[v] = true;
     }
+    const dim3 grid(G::BANDS * a.B);
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, dim3(4 * a.B), dim3(256), IMG_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
+        hipExtLaunchKernelGGL(k, grid, dim3(256), G::LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
     else
-        hipLaunchKernelGGL(k, dim3(4 * a.B), dim3(256), IMG_LDS, s, a);
+        hipLaunchKernelGGL(k, grid, dim3(256), G::LDS, s, a);
     return hipGetLastError();
+}
+
+}  // namespace
+
+bool img28_supported(const ConvArgs& a) { return img_supported_t<Geo28>(a); }
+bool img56_supported(const ConvArgs& a) { return img_supported_t<Geo56>(a); }
+
+hipError_t launch_conv_img28(const ConvArgs& a, hipStream_t s) {
+    return img28_supported(a) ? launch_img_t<Geo28>(a, s) : hipErrorInvalidValue;
+}
+hipError_t launch_conv_img56(const ConvArgs& a, hipStream_t s) {
+    return img56_supported(a) ? launch_img_t<Geo56>(a, s) : hipErrorInvalidValue;
 }
 
 }  // namespace fr

@@ -1558,6 +1558,11 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         FR_HIP_CHECK(launch_conv_img28(a, (hipStream_t)stream));
         return FR_OK;
     }
+    if (d->tile == FR_TILE_IMG56 + 1) {
+        if (!img56_supported(a)) { set_error("fr_op_conv2d: img56 kernel not applicable"); return FR_ERR_ARG; }
+        FR_HIP_CHECK(launch_conv_img56(a, (hipStream_t)stream));
+        return FR_OK;
+    }
     if (d->tile > 0) {
         if (d->tile > NUM_TILE_IDS) { set_error("fr_op_conv2d: bad tile"); return FR_ERR_ARG; }
         a.tile = d->tile - 1;

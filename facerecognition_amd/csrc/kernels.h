@@ -56,6 +56,9 @@ hipError_t launch_conv_band(const ConvArgs& a, int cfg, int variant, hipStream_t
 // Image-per-workgroup direct 3x3/s1/p1 conv for 28x28, 128 -> 128 channels (conv_img.hip).
 bool img28_supported(const ConvArgs& a);
 hipError_t launch_conv_img28(const ConvArgs& a, hipStream_t s);
+// ... and for 56x56, 64 -> 64 channels (layer1), 4-row bands.
+bool img56_supported(const ConvArgs& a);
+hipError_t launch_conv_img56(const ConvArgs& a, hipStream_t s);
 // LDS-resident stage kernel (conv_stage.hip): the stride-1 IBasicBlocks of a 14x14x256 stage, one
 // workgroup per image, activation kept in LDS across all 2*nblk convs.
 struct StageConv {

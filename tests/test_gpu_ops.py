@@ -119,6 +119,21 @@ def test_conv_img28(gpu, B, dtype):
     _close(y, conv_ref(x, w, pad=(1, 1), bias=bias, act=2, slope=slope, dtype=dtype), tol=tol)
 
 
+@pytest.mark.parametrize("B", [1, 3])
+def test_conv_img56(gpu, B):
+    """Layer-1 instance of the band kernel (conv_img.hip, 56x56 64->64, 4-row bands, forced)."""
+    g = torch.Generator().manual_seed(56 + B)
+    x = torch.randn(B, 56, 56, 64, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(64, 64, 3, 3, generator=g) / np.sqrt(64 * 9)
+    bias = torch.randn(64, generator=g) * 0.1
+    slope = torch.rand(64, generator=g) * 0.5
+    res = torch.randn(B, 56, 56, 64, generator=g).to(torch.bfloat16).to(gpu)
+    y = conv_op(x, w, pad=(1, 1), bias=bias, res=res, tile=N.FR_TILE_IMG56)
+    _close(y, conv_ref(x, w, pad=(1, 1), bias=bias, res=res))
+    y = conv_op(x, w, pad=(1, 1), bias=bias, act=2, slope=slope, tile=N.FR_TILE_IMG56)
+    _close(y, conv_ref(x, w, pad=(1, 1), bias=bias, act=2, slope=slope))
+
+
 def test_conv_img28_channel_slices_and_applicability(gpu):
     """img28 reads channels [128:256) of a 256-ch buffer and writes [64:192) of another; other shapes
     are refused (fail loudly, no silent fallback)."""
@@ -333,7 +348,8 @@ def _border_class(H, W):
 
 
 BIAS9_CASES = [(2, 14, 14, 256, 256, None), (2, 14, 14, 256, 256, N.FR_TILE_BAND), (2, 28, 28, 128, 128, None),
-               (2, 56, 56, 64, 64, 2), (2, 28, 28, 128, 128, 0), (2, 28, 28, 128, 128, N.FR_TILE_IMG28)]
+               (2, 56, 56, 64, 64, 2), (2, 28, 28, 128, 128, 0), (2, 28, 28, 128, 128, N.FR_TILE_IMG28),
+               (2, 56, 56, 64, 64, N.FR_TILE_IMG56)]
 
 
 @pytest.mark.parametrize("case", BIAS9_CASES)
