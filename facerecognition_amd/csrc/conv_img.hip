@@ -9,8 +9,8 @@
 //   * per 32-input-channel chunk the 9 x 30 zero-haloed patch is DMA'd into LDS once ([4 planes of 8
 //     channels][9 rows][32 positions][16 B]) and read by all 9 taps at shifted positions; the next
 //     chunk's patch (double buffer) streams in during the current chunk's 9 K-steps;
-//   * per K-step (chunk, tap) the [128 out][32 in] weight slice (8 KiB) is gathered straight from the
-//     implicit-GEMM weight rows [Npad][Kpad] (K order (kh, kw, c)) into a 3-slot LDS ring, three steps
+//   * per K-step (chunk, tap) the [128 out][32 in] weight slice (8 KiB), pre-packed at load time in
+//     its LDS image (img_pack_weights: 1-KiB contiguous DMA pieces), streams into a 3-slot ring, three steps
 //     ahead; one mid-step s_barrier per K-step (the stage kernel's schedule, conv_stage.hip);
 //   * 2x2 waves: wave (wm, wn) computes 7 virtual-pixel frags (rows 0..6 x 32 columns, 28 valid) x
 //     64 output channels (4 n-frags): 28 v_mfma_f32_16x16x32_bf16 per K-step, 112 f32 accumulators;
@@ -85,8 +85,8 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
 
     const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * IW * IW * p.Cx * 2);
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
-    const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2);
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.wimg, 0, (uint32_t)(NSTEP * SLICE_B), 0x00020000);
 
     // patch of chunk cc (input channels 32cc..): PP pieces per wave, plane-major [4 planes][QR+2 rows]
     // [PC positions][16 B]; halo, pad and spare pieces read out of range (zeros).  Offsets recomputed
@@ -108,22 +108,17 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
             dma16s(xr, smem + buf * PATCH_B + piece * 1024, off, (uint32_t)(cc * 32 * 2));
         }
     };
-    // weight slice of K-step s (chunk cc = s / 9, tap = s % 9) gathered from the [Npad][Kpad] rows,
-    // LDS image [g][n][16 B]: WP pieces per wave = (group g, rows 64nh..); the step in soffset
-    uint32_t wv[G::WP];
-#pragma unroll
-    for (int u = 0; u < G::WP; ++u) {
-        const int piece = G::WP * wave + u, g = piece / (IC / 64), nh = piece % (IC / 64);
-        wv[u] = (uint32_t)(((size_t)(64 * nh + lane) * p.Kpad + g * 8) * 2);
-    }
+    // weight slice of K-step s: pre-packed in the LDS image [g][n][16 B] (img_pack_weights), so each
+    // of the WP pieces per wave is 1 KiB contiguous; the step in soffset
     auto issue_w = [&](int s, int slot) {
 #if FR_IMG_EXP == 1
         if (s > 2) return;
 #endif
-        const int cc = s / 9, tap = s - cc * 9;
 #pragma unroll
-        for (int u = 0; u < G::WP; ++u)
-            dma16s(wr, slots + slot * SLICE_B + (G::WP * wave + u) * 1024, wv[u], (uint32_t)((tap * IC + cc * 32) * 2));
+        for (int u = 0; u < G::WP; ++u) {
+            const int piece = G::WP * wave + u;
+            dma16s(wr, slots + slot * SLICE_B + piece * 1024, (uint32_t)(piece * 1024 + lane * 16), (uint32_t)(s * SLICE_B));
+        }
     };
 
     // fragment addresses: B (patch) virtual frag f = FM*wm + j -> positions 16f + (lane&15) (linear:
@@ -248,7 +243,7 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
 template <typename G>
 bool img_supported_t(const ConvArgs& a) {
     constexpr int IW = G::IW, IC = G::IC;
-    return a.Kh == 3 && a.Kw == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.H == IW && a.W == IW &&
+    return a.wimg && a.Kh == 3 && a.Kw == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.H == IW && a.W == IW &&
            a.Ho == IW && a.Wo == IW && a.Cin == IC && a.Cout == IC && a.Npad >= IC && a.Kpad >= 9 * IC &&
            a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.x_off + IC <= a.Cx && a.Cy % 4 == 0 && a.y_off % 4 == 0 &&
            a.y_off + IC <= a.Cy && !a.y2 && !a.partial && !a.w8 && !a.y_amax && a.B > 0 && !a.f16 &&
@@ -273,7 +268,32 @@ hipError_t launch_img_t(const ConvArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// out[s = cc*9 + tap][g][n][e] = w[n][tap*IC + 32cc + 8g + e]
+__global__ __launch_bounds__(256) void img_pack_kernel(const bf16_t* __restrict__ w, int Kpad, int ic,
+                                                       bf16_t* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x, total = (ic / 32) * 9 * 4 * ic;
+    if (i >= total) return;
+    const int n = i % ic, g = (i / ic) % 4, s = i / (4 * ic), cc = s / 9, tap = s % 9;
+    *(uint4*)(out + (size_t)i * 8) = *(const uint4*)(w + (size_t)n * Kpad + tap * ic + 32 * cc + 8 * g);
+}
+
 }  // namespace
+
+bool img_shape_ok(const ConvArgs& a, int* ic) {
+    ConvArgs t = a;
+    t.wimg = (const bf16_t*)1;
+    if (img_supported_t<Geo28>(t)) { *ic = 128; return true; }
+    if (img_supported_t<Geo56>(t)) { *ic = 64; return true; }
+    return false;
+}
+
+size_t img_packed_elems(int ic) { return (size_t)(ic / 32) * 9 * 4 * ic * 8; }
+
+hipError_t img_pack_weights(const bf16_t* w, int Kpad, int ic, bf16_t* out, hipStream_t s) {
+    const int total = (ic / 32) * 9 * 4 * ic;
+    hipLaunchKernelGGL(img_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, s, w, Kpad, ic, out);
+    return hipGetLastError();
+}
 
 bool img28_supported(const ConvArgs& a) { return img_supported_t<Geo28>(a); }
 bool img56_supported(const ConvArgs& a) { return img_supported_t<Geo56>(a); }

@@ -43,6 +43,7 @@ struct DevConvW {
     float* aff_s = nullptr;
     float* aff_b = nullptr;
     float* bias9 = nullptr;  // [9][Npad] border-class bias (input BN folded into a 3x3/s1/p1 conv)
+    bf16_t* wimg = nullptr;  // conv_img.hip K-step slice images (convs its kernels apply to)
     uint8_t* w8 = nullptr;   // FR_DTYPE_FP8: e4m3 [Npad][Kpad8] + per-channel scale
     float* wscale = nullptr;
     int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0, Kpad8 = 0;
@@ -574,6 +575,34 @@ void build_iresnet100(Builder& b) {
     b.head(x);
 }
 
+// K-step slice images for the convs the conv_img.hip kernels apply to (3x3/s1/p1 28x28x128 and
+// 56x56x64), packed on the device from the uploaded [Npad][Kpad] rows.
+int build_img_weights(fr_handle* h) {
+    for (const auto& op : h->ops) {
+        if (op.kind != OP_CONV || op.wi < 0) continue;
+        DevConvW& cw = h->convw[op.wi];
+        if (cw.wimg) continue;
+        ConvArgs a{};
+        a.B = 1; a.Cin = op.cin; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
+        a.H = h->tensors[op.in].H; a.W = h->tensors[op.in].W; a.Cx = h->tensors[op.in].C; a.x_off = op.in_off;
+        a.Ho = h->tensors[op.out].H; a.Wo = h->tensors[op.out].W; a.Cy = h->tensors[op.out].C; a.y_off = op.out_off;
+        a.Cout = cw.Cout; a.Npad = cw.Npad; a.Kpad = cw.Kpad; a.bias9 = cw.bias9;
+        a.y2 = op.out2 >= 0 ? (bf16_t*)1 : nullptr;
+        if (op.res >= 0) { a.res = (const bf16_t*)1; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
+        a.f16 = h->dtype == FR_DTYPE_F16;
+        int ic = 0;
+        if (h->dtype == FR_DTYPE_FP8 || !img_shape_ok(a, &ic)) continue;
+        void* p = nullptr;
+        int rc = dev_alloc(&p, img_packed_elems(ic) * sizeof(bf16_t));
+        if (rc) return rc;
+        h->weight_allocs.push_back(p);
+        FR_HIP_CHECK(img_pack_weights(cw.w, cw.Kpad, ic, (bf16_t*)p, nullptr));
+        cw.wimg = (bf16_t*)p;
+    }
+    FR_HIP_CHECK(hipDeviceSynchronize());
+    return FR_OK;
+}
+
 void build_resnet50(Builder& b) {
     fr_handle* h = b.h;
     h->in_size = 112;
@@ -751,11 +780,19 @@ int reserve(fr_handle* h, int maxB) {
     return fill_stage_dbg(h);
 }
 
-// The image-per-workgroup layer2 kernel (conv_img.hip) is opt-in (FR_IMG28=1): measured 94 us per
-// conv vs 86 us for the implicit GEMM (profiles/r01_img28.txt)
+// layer2 band kernel (conv_img.hip): 80 us per conv vs 86 us for the implicit GEMM
+// (profiles/r01_img28.txt); FR_NO_IMG28=1 falls back to the implicit GEMM
 bool img28_enabled() {
     static const bool on = [] {
-        const char* e = getenv("FR_IMG28");
+        const char* e = getenv("FR_NO_IMG28");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
+bool img56_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_IMG56");
         return e && e[0] == '1';
     }();
     return on;
@@ -892,9 +929,14 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
         FR_HIP_CHECK(launch_conv_fp8(a, s));
         return FR_OK;
     }
-    if (img28_enabled() && img28_supported(a)) {  // layer2 3x3 128->128 @28x28: one image per workgroup
+    if (img28_enabled() && img28_supported(a)) {  // layer2 3x3 128->128 @28x28: quarter-image bands
         ps.start("conv3x3_img W28", &a);
         FR_HIP_CHECK(launch_conv_img28(a, s));
+        return FR_OK;
+    }
+    if (img56_enabled() && img56_supported(a)) {  // layer1 3x3 64->64 @56x56: 4-row bands
+        ps.start("conv3x3_img W56", &a);
+        FR_HIP_CHECK(launch_conv_img56(a, s));
         return FR_OK;
     }
     int TH, variant;
@@ -987,7 +1029,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.w = cw.w; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
                 a.K = cw.K; a.Kpad = cw.Kpad;
                 a.Ho = to.H; a.Wo = to.W; a.M = B * to.H * to.W; a.Cout = cw.Cout; a.Npad = cw.Npad;
-                a.bias = cw.bias; a.slope = cw.slope; a.act = op.act; a.bias9 = cw.bias9;
+                a.bias = cw.bias; a.slope = cw.slope; a.act = op.act; a.bias9 = cw.bias9; a.wimg = cw.wimg;
                 if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
                 a.y = to.dev; a.Cy = to.C; a.y_off = op.out_off;
                 if (op.out2 >= 0) {
@@ -1128,6 +1170,7 @@ int fr_load_weights(fr_handle* h, const void* blob, size_t nbytes) {
     if (h->arch == FR_ARCH_IRESNET100) build_iresnet100(b);
     else if (h->arch == FR_ARCH_RESNET50_ARCFACE) build_resnet50(b);
     else build_irv1(b);
+    if (!b.rc) b.rc = build_img_weights(h);
     if (b.rc) {
         free_weights(h);
         h->tensors.clear();
@@ -1375,11 +1418,12 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
             a.Ho = h->tensors[op.out].H; a.Wo = h->tensors[op.out].W; a.ph = op.ph; a.pw = op.pw;
             a.res = op.res >= 0 ? (const bf16_t*)1 : nullptr;
             a.y2 = op.out2 >= 0 ? (bf16_t*)1 : nullptr;
-            a.Npad = cw.Npad; a.B = B;
+            a.Npad = cw.Npad; a.B = B; a.wimg = cw.wimg; a.f16 = h->dtype == FR_DTYPE_F16; a.bias9 = cw.bias9;
             a.Cx = h->tensors[op.in].C; a.x_off = op.in_off; a.Cy = h->tensors[op.out].C; a.y_off = op.out_off;
             if (op.res >= 0) { a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
             int TH, variant;
             if (img28_enabled() && img28_supported(a)) tile = FR_TILE_IMG28;
+            else if (img56_enabled() && img56_supported(a)) tile = FR_TILE_IMG56;
             else if (band_enabled() && band_plan(a, &TH, &variant) && variant >= 3) tile = FR_TILE_BAND;
             else if (sp == 1 && autotune_enabled() && !conv_tile_forced() && find_tuned(h, a) >= 0) tile = find_tuned(h, a);
         }
@@ -1553,14 +1597,21 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         FR_HIP_CHECK(launch_conv_band(a, TH, variant, (hipStream_t)stream));
         return FR_OK;
     }
-    if (d->tile == FR_TILE_IMG28 + 1) {
-        if (!img28_supported(a)) { set_error("fr_op_conv2d: img28 kernel not applicable"); return FR_ERR_ARG; }
-        FR_HIP_CHECK(launch_conv_img28(a, (hipStream_t)stream));
-        return FR_OK;
-    }
-    if (d->tile == FR_TILE_IMG56 + 1) {
-        if (!img56_supported(a)) { set_error("fr_op_conv2d: img56 kernel not applicable"); return FR_ERR_ARG; }
-        FR_HIP_CHECK(launch_conv_img56(a, (hipStream_t)stream));
+    if (d->tile == FR_TILE_IMG28 + 1 || d->tile == FR_TILE_IMG56 + 1) {
+        const bool w28 = d->tile == FR_TILE_IMG28 + 1;
+        int ic = 0;
+        if (!img_shape_ok(a, &ic) || ic != (w28 ? 128 : 64)) {
+            set_error(std::string("fr_op_conv2d: ") + (w28 ? "img28" : "img56") + " kernel not applicable");
+            return FR_ERR_ARG;
+        }
+        // the op API takes [Npad][Kpad] rows: pack the K-step slice images into stream-ordered scratch
+        hipStream_t st = (hipStream_t)stream;
+        void* tmp = nullptr;
+        FR_HIP_CHECK(hipMallocAsync(&tmp, img_packed_elems(ic) * sizeof(bf16_t), st));
+        FR_HIP_CHECK(img_pack_weights(a.w, a.Kpad, ic, (bf16_t*)tmp, st));
+        a.wimg = (const bf16_t*)tmp;
+        FR_HIP_CHECK(w28 ? launch_conv_img28(a, st) : launch_conv_img56(a, st));
+        FR_HIP_CHECK(hipFreeAsync(tmp, st));
         return FR_OK;
     }
     if (d->tile > 0) {

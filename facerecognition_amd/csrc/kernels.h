@@ -34,6 +34,7 @@ struct ConvArgs {
     const float* x_amax;
     float* y_amax;                // non-null: the epilogue atomically records max |y| (both dtypes)
     int amax_slots;               // x_amax / y_amax are arrays of this many partial maxima (block % slots)
+    const bf16_t* wimg;           // conv_img.hip: weights pre-packed as K-step slice images (img_pack_weights)
 };
 constexpr int FR_AMAX_SLOTS = 64;  // engine: spreads the producers' atomics over 64 addresses
 
@@ -59,6 +60,11 @@ hipError_t launch_conv_img28(const ConvArgs& a, hipStream_t s);
 // ... and for 56x56, 64 -> 64 channels (layer1), 4-row bands.
 bool img56_supported(const ConvArgs& a);
 hipError_t launch_conv_img56(const ConvArgs& a, hipStream_t s);
+// Shape checks without the packed weights, their size, and the device packer ([Npad][Kpad] rows ->
+// [36 or 18 K-steps][4 groups][IC rows][8 channels]).
+bool img_shape_ok(const ConvArgs& a, int* ic);
+size_t img_packed_elems(int ic);
+hipError_t img_pack_weights(const bf16_t* w, int Kpad, int ic, bf16_t* out, hipStream_t s);
 // LDS-resident stage kernel (conv_stage.hip): the stride-1 IBasicBlocks of a 14x14x256 stage, one
 // workgroup per image, activation kept in LDS across all 2*nblk convs.
 struct StageConv {

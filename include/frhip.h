@@ -170,7 +170,7 @@ typedef struct fr_conv_desc {
 #define FR_TILE_128x64_S3 8  /* 3-stage DMA ring, 2 blocks/CU */
 #define FR_TILE_64x128_S3 9  /* 3-stage DMA ring, 2 blocks/CU */
 #define FR_TILE_IMG56 11     /* the same for 56x56x64->64 (layer1), 4-row bands */
-#define FR_TILE_IMG28 10     /* image-per-workgroup direct 3x3/s1/p1 28x28x128->128 bf16 kernel (conv_img.hip); opt-in (env FR_IMG28=1) */
+#define FR_TILE_IMG28 10     /* row-band direct 3x3/s1/p1 28x28x128->128 bf16 kernel (conv_img.hip); auto-selected (env FR_NO_IMG28=1: off) */
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 
