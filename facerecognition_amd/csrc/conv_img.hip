@@ -108,6 +108,38 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
             dma16s(xr, smem + buf * PATCH_B + piece * 1024, off, (uint32_t)(cc * 32 * 2));
         }
     };
+    // chunks >= 1 go through registers instead: 4 consecutive lanes load one pixel's 64 contiguous bytes
+    // (16 segments per wave-load instead of the DMA's 64 scattered 16-B pieces), loaded at the chunk
+    // start and written plane-major into the free patch buffer three K-steps later
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+    constexpr int PH = (G::PP + 1) / 2;  // pieces per phase (two phases: register budget)
+    u32x4_t pst[PH];
+    auto load_patch = [&](int cc, int ph) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int uu = 0; uu < PH; ++uu) {
+            const int u = PH * ph + uu;
+            if (u >= G::PP) break;
+            const int sl = (4 * u + wave) * 64 + ln, pos = sl >> 2, plane = sl & 3, pr = pos / PC, pc = pos % PC;
+            const int ir = r0 - 1 + pr, ic = pc - 1;
+            const bool in = pos < G::PPOS && (unsigned)ir < (unsigned)IW && (unsigned)ic < (unsigned)IW;
+            const uint32_t off =
+                in ? (uint32_t)((((size_t)b * IW * IW + ir * IW + ic) * p.Cx + p.x_off + plane * 8) * 2) : OOB;
+            pst[uu] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, cc * 32 * 2, 0);
+        }
+    };
+    auto store_patch = [&](int buf, int ph) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int uu = 0; uu < PH; ++uu) {
+            const int u = PH * ph + uu;
+            if (u >= G::PP) break;
+            const int sl = (4 * u + wave) * 64 + ln, pos = sl >> 2, plane = sl & 3;
+            if (pos < G::PPOS) *(u32x4_t*)(smem + buf * PATCH_B + plane * PLANE_B + pos * 16) = pst[uu];
+        }
+    };
     // weight slice of K-step s: pre-packed in the LDS image [g][n][16 B] (img_pack_weights), so each
     // of the WP pieces per wave is 1 KiB contiguous; the step in soffset
     auto issue_w = [&](int s, int slot) {
@@ -154,11 +186,11 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
 
     // one K-step s (slot s % 3, chunk c = s / 9, tap t = s % 9): nxt <- patch fragments of step s+1;
     // MFMAs of the first half of the weight frags; mid-step barrier: this wave's slice s+1 landed
-    // (younger: slice s+2 and the PP patch pieces of a chunk start at step s-2 or s-1), every wave is
+    // (younger: slice s+2 and the patch loads of steps s-2, s-1), every wave is
     // past its reads of slot s % 3 and of the previous chunk's patch buffer; DMA of slice s+3 into slot
-    // s % 3 and, at t == 0, of the next chunk's patch; wf <- slice s+1 (first half now, second half in
-    // place after their MFMAs).  The next chunk's patch is read at the start of its t == 8 step: the
-    // t == 7 barrier covered it.
+    // s % 3; at t == 0 the next chunk's patch loads into registers, at t == 3 it is written to the other
+    // buffer; wf <- slice s+1 (first half now, second half in place after their MFMAs).  The next
+    // chunk's patch is read at the start of its t == 8 step: the t == 7 barrier covered it.
     auto kstep = [&](int s, frag (&cur)[FM], frag (&nxt)[FM]) {
         const int t = s % 9, c = s / 9, slot = s % NSLOT, nslot = (s + 1) % NSLOT;
         if (s + 1 < NSTEP) pread(nxt, t == 8 ? (c + 1) & 1 : c & 1, t == 8 ? 0 : t + 1);
@@ -166,10 +198,16 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
         for (int i = 0; i < FN / 2; ++i)
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
-        if (t == 1 || t == 2) wait_vm_barrier<G::WP + G::PP>();
+        // younger than slice s+1 (issued at step s-2): slice s+2 and the patch loads of steps s-2, s-1
+        if (t == 1 || t == 2) wait_vm_barrier<G::WP + PH>();
+        else if (t == 4 || t == 5) wait_vm_barrier<G::WP + (G::PP - PH)>();
         else wait_vm_barrier<G::WP>();
         issue_w(s + 3 < NSTEP ? s + 3 : NSTEP - 1, slot);  // tail: harmless re-fetch (uniform counts)
-        if (t == 0) issue_patch(c + 1 < NCH ? c + 1 : NCH - 1, (c + 1) & 1);
+        // next chunk's patch in two register phases: load at t == 0 / 3, store at t == 3 / 6 (the loads
+        // have landed by then: they precede the slices waited for), read from t == 8 on
+        const int cn = c + 1 < NCH ? c + 1 : NCH - 1;
+        if (t == 3 || t == 6) store_patch((c + 1) & 1, t == 3 ? 0 : 1);
+        if (t == 0 || t == 3) load_patch(cn, t == 0 ? 0 : 1);
 #pragma unroll
         for (int i = 0; i < FN / 2; ++i) wread(i, nslot);
 #pragma unroll
