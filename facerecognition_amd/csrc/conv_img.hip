@@ -62,9 +62,12 @@ __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* 
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, soff, 0, 0);
 }
 
-template <int N>
+// mid-step wait: vmcnt(N); LDS ops older than the step's L youngest (its next-step patch reads, which
+// no DMA of this step touches) complete -- the weight refills of the slot about to be overwritten and
+// the staged patch writes that the next barrier publishes
+template <int N, int L>
 __device__ __forceinline__ void wait_vm_barrier() {
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(%1)\n\ts_barrier" ::"n"(N), "n"(L) : "memory");
 }
 
 // RES: residual input (IBasicBlock conv2); B9: border-class bias table (conv1 with bn1 folded).  The
@@ -199,9 +202,9 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
         // younger than slice s+1 (issued at step s-2): slice s+2 and the patch loads of steps s-2, s-1
-        if (t == 1 || t == 2) wait_vm_barrier<G::WP + PH>();
-        else if (t == 4 || t == 5) wait_vm_barrier<G::WP + (G::PP - PH)>();
-        else wait_vm_barrier<G::WP>();
+        if (t == 1 || t == 2) wait_vm_barrier<G::WP + PH, FM>();
+        else if (t == 4 || t == 5) wait_vm_barrier<G::WP + (G::PP - PH), FM>();
+        else wait_vm_barrier<G::WP, FM>();
         issue_w(s + 3 < NSTEP ? s + 3 : NSTEP - 1, slot);  // tail: harmless re-fetch (uniform counts)
         // next chunk's patch in two register phases: load at t == 0 / 3, store at t == 3 / 6 (the loads
         // have landed by then: they precede the slices waited for), read from t == 8 on

@@ -47,6 +47,9 @@ constexpr int STAGE_LDS = PATCH_B + NSLOT * SLICE_B;  // 163840 = the whole 160 
 constexpr int KSTEPS = (SC / 32) * 9;        // 72 per conv
 constexpr uint32_t OOB = 0x80000000u;
 
+#ifndef FR_STAGE_LGKM7
+#define FR_STAGE_LGKM7 1  // mid-step wait leaves this step's 7 patch reads in flight (0: drain all)
+#endif
 #ifndef FR_STAGE_SCHED
 #define FR_STAGE_SCHED 0  // explicit MFMA / ds_read / DMA interleave (sched_group_barrier)
 #endif
@@ -142,7 +145,14 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
 #endif
         // slice g+1 landed (this wave); the 4 pieces of slice g+2 may stay in flight.  Branch-free: the
         // tail re-fetches the last slice into the free slot and reads clamped slots (static counts)
+#if FR_STAGE_LGKM7
+        // the 7 youngest LDS reads are this step's pread(nxt) (untouched by the DMA below: +4.5 % on the
+        // stage); the older wf refills from slot `slot` must be done before anyone overwrites it
+        // (checked in the ISA: the compiler waits for every earlier read before its MFMA use)
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(7)\n\ts_barrier" ::: "memory");
+#else
         asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
         issue_w(g + 3 < total ? g + 3 : total - 1, slot);
         const int nslot = slot == NSLOT - 1 ? 0 : slot + 1;
 #pragma unroll
