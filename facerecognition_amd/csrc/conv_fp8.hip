@@ -293,9 +293,11 @@ int conv_fp8_tile(int M, int Cout) {
 hipError_t launch_conv_fp8(const ConvArgs& a, hipStream_t s) {
     if (a.Cin % 64 != 0 || a.Kpad % KS != 0 || !a.w8 || !a.wscale) return hipErrorInvalidValue;
     switch (a.tile) {
-        case TILE_128x64: return launch_fp8_variant<128, 64, 2, 2>(a, s);
-        case TILE_64x128: return launch_fp8_variant<64, 128, 2, 2>(a, s);
-        default: return launch_fp8_variant<128, 128, 2, 2>(a, s);
+        // 4 x 1 waves: each wave converts only its own activation fragments (2 x 2 converted every
+        // fragment twice; the bf16 -> e4m3 conversion costs as much issue time as the fp8 MFMAs)
+        case TILE_128x64: return launch_fp8_variant<128, 64, 4, 1>(a, s);
+        case TILE_64x128: return launch_fp8_variant<64, 128, 4, 1>(a, s);
+        default: return launch_fp8_variant<128, 128, 4, 1>(a, s);
     }
 }
 
