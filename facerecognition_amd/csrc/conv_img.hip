@@ -196,6 +196,9 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
     // chunk's patch is read at the start of its t == 8 step: the t == 7 barrier covered it.
     auto kstep = [&](int s, frag (&cur)[FM], frag (&nxt)[FM]) {
         const int t = s % 9, c = s / 9, slot = s % NSLOT, nslot = (s + 1) % NSLOT;
+        // compiler fence: the previous step's refills and staged patch writes stay ahead of this
+        // step's reads, so "all but the FM youngest LDS ops" below means exactly those
+        asm volatile("" ::: "memory");
         if (s + 1 < NSTEP) pread(nxt, t == 8 ? (c + 1) & 1 : c & 1, t == 8 ? 0 : t + 1);
 #pragma unroll
         for (int i = 0; i < FN / 2; ++i)
@@ -204,6 +207,7 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
         // younger than slice s+1 (issued at step s-2): slice s+2 and the patch loads of steps s-2, s-1
         if (t == 1 || t == 2) wait_vm_barrier<G::WP + PH, FM>();
         else if (t == 4 || t == 5) wait_vm_barrier<G::WP + (G::PP - PH), FM>();
+        else if (t == 7) wait_vm_barrier<G::WP, 0>();  // publishes the staged patch (read from t == 8)
         else wait_vm_barrier<G::WP, FM>();
         issue_w(s + 3 < NSTEP ? s + 3 : NSTEP - 1, slot);  // tail: harmless re-fetch (uniform counts)
         // next chunk's patch in two register phases: load at t == 0 / 3, store at t == 3 / 6 (the loads

@@ -47,6 +47,9 @@ constexpr int STAGE_LDS = PATCH_B + NSLOT * SLICE_B;  // 163840 = the whole 160 
 constexpr int KSTEPS = (SC / 32) * 9;        // 72 per conv
 constexpr uint32_t OOB = 0x80000000u;
 
+#ifndef FR_STAGE_FENCE
+#define FR_STAGE_FENCE 1  // compiler fence at each K-step start (keeps the lgkmcnt(7) wait exact)
+#endif
 #ifndef FR_STAGE_LGKM7
 #define FR_STAGE_LGKM7 1  // mid-step wait leaves this step's 7 patch reads in flight (0: drain all)
 #endif
@@ -130,6 +133,9 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
     // barrier; DMA of global step g+3 into this step's slot; wf <- slice of step g+1 in place.  The
     // slot of step s is s % 3 = tap % 3 (9 and 72 are multiples of 3): compile-time after unrolling.
     auto kstep = [&](int g, int slot, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
+#if FR_STAGE_FENCE
+        asm volatile("" ::: "memory");  // the previous step's refills stay ahead of this step's reads
+#endif
         pread(nxt, cg_n, tap_n);  // (after a conv's last step: unused reads, no branch)
 #pragma unroll
         for (int i = 0; i < 4; ++i)

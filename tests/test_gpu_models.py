@@ -174,3 +174,36 @@ def test_facenet_projection_head(gpu):
     assert np.all(1 - cos <= COS_TOL)
     assert np.allclose(np.linalg.norm(raw, axis=1), np.linalg.norm(raw_ref, axis=1), rtol=2e-2)
     m.close()
+
+
+def test_full_batch_properties_bs256(gpu):
+    """BASELINE config-2 size (IResNet100 bf16, bs = 256: every production kernel at its real grid --
+    fused stem, layer2 band kernel, layer3 stage, 10k-row match).  Size-independent properties:
+    deterministic replay, finite unit-norm rows, batch independence against a 5-face call, a
+    bs=256 sample against the fp32 oracle at the 1e-3 bar, and identical top-1 on a planted gallery
+    built from the embeddings themselves."""
+    from facerecognition_amd.gallery import DeviceGallery
+    from facerecognition_amd.model import FRModel
+    m = FRModel.synthetic("iresnet100", dtype="bf16")
+    u8 = torch.from_numpy(_probes("iresnet100", 256, seed=21))
+    a = m.embed(u8).cpu()
+    b = m.embed(u8).cpu()
+    assert torch.equal(a, b), "forward is not deterministic at bs=256"
+    assert torch.isfinite(a).all()
+    assert torch.allclose(a.norm(dim=1), torch.ones(256), atol=1e-5)
+    small = m.embed(u8[100:105]).cpu()
+    cos_b = (a[100:105] * small).sum(1)
+    assert float((1 - cos_b).max()) <= COS_TOL
+    ref = _oracle_embed("iresnet100", u8[:4].numpy())
+    cos_o = (a[:4].numpy() * ref).sum(1) / np.linalg.norm(ref, axis=1)
+    assert float((1 - cos_o).max()) <= COS_TOL, 1 - cos_o
+    rng = np.random.default_rng(22)
+    G = rng.standard_normal((10000, 512)).astype(np.float32)
+    perm = rng.permutation(10000)[:256]
+    G[perm] = a.numpy() + 0.03 * rng.standard_normal((256, 512)).astype(np.float32)
+    G /= np.linalg.norm(G, axis=1, keepdims=True)
+    gal = DeviceGallery(G)
+    _, idx = gal.search(a.numpy(), 5)
+    assert np.array_equal(idx[:, 0], perm)
+    gal.close()
+    m.close()
