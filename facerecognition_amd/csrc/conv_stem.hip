@@ -9,7 +9,8 @@
 // Same operands and weights as the two-launch path: the input values 2q - 255 are exact integers in
 // bf16/f16, the weight rows are the engine's stem rows (w/255 split hi/lo over channels 0-2 / 3-5,
 // K = (tap, c) with c fastest, zero past K = 72), so only the f32 summation order differs.
-// Block = 2 output rows of one image (224 pixels = 14 m-frags) x 64 channels (4 n-frags):
+// Tile = 2 output rows of one image (224 pixels = 14 m-frags) x 64 channels (4 n-frags); 3 persistent
+// blocks per CU loop over tiles, staging the weights once and prefetching the next tile's input:
 //   * the 4 input rows (dword loads) and the 64 x 96 weight rows go to LDS once per block; the input
 //     becomes 2q - 255 in the activation dtype with a zero halo, [row][col][4];
 //   * MFMA operand B for K-step ks, k-group g is tap 4ks + g of one pixel = [v0 v1 v2 v0 v1 v2 0 0],
@@ -19,6 +20,8 @@
 #include "kernels.h"
 
 #include <hip/hip_ext.h>
+
+#include <cstdlib>
 
 namespace fr {
 namespace {
@@ -30,10 +33,10 @@ constexpr int SPIX = SROWS * SW;  // 224
 constexpr int WROW = 104;          // LDS weight row: 96 bf16 + pad (208 B: conflict-free 16-lane reads)
 
 template <bool F16>
-__global__ __launch_bounds__(256) void stem_u8_kernel(const uint8_t* __restrict__ in, const bf16_t* __restrict__ w,
-                                                      int Kpad, const float* __restrict__ bias,
-                                                      const float* __restrict__ slope, int act, bf16_t* __restrict__ y,
-                                                      int Cy, int y_off) {
+// waves_per_eu(3): the persistent loop would otherwise grow past 168 VGPRs and lose the third block per CU
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stem_u8_kernel(
+    const uint8_t* __restrict__ in, const bf16_t* __restrict__ w, int Kpad, const float* __restrict__ bias,
+    const float* __restrict__ slope, int act, bf16_t* __restrict__ y, int Cy, int y_off, int ntiles) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
     __shared__ __attribute__((aligned(16))) uint16_t sx[SROWS + 2][SW + 2][4];
@@ -42,98 +45,120 @@ __global__ __launch_bounds__(256) void stem_u8_kernel(const uint8_t* __restrict_
     __shared__ __attribute__((aligned(16))) uint16_t swt[SCO][WROW];                        // weight rows
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b = blockIdx.x / (SW / SROWS), r0 = (blockIdx.x % (SW / SROWS)) * SROWS;
 
-    // input rows r0-1 .. r0+2 (336 contiguous bytes each) as dwords, and the 64 x 96 weight rows
-    for (int e = tid; e < (SROWS + 2) * (SW * 3 / 4); e += 256) {
-        const int rr = e / (SW * 3 / 4), d = e % (SW * 3 / 4), ir = r0 - 1 + rr;
-        sraw[rr][d] = (unsigned)ir < (unsigned)SW ? *(const uint32_t*)(in + ((size_t)b * SW + ir) * SW * 3 + 4 * d) : 0u;
-    }
+    // the 64 x 96 weight rows, staged once per (persistent) block; the first tile's barrier after its
+    // sraw loads publishes them
     for (int e = tid; e < SCO * 12; e += 256) {
         const int n = e / 12, c = e % 12;
         *(uint4*)&swt[n][8 * c] = *(const uint4*)(w + (size_t)n * Kpad + 8 * c);
     }
-    __syncthreads();
-    // -> 2q - 255 in the activation dtype, zero halo columns (rows outside the image were zeroed above
-    // but must also become 0, not -255)
-    for (int e = tid; e < (SROWS + 2) * (SW + 2); e += 256) {
-        const int rr = e / (SW + 2), cc = e % (SW + 2), ir = r0 - 1 + rr, ic = cc - 1;
-        uint16_t v[3] = {0, 0, 0};
-        if ((unsigned)ir < (unsigned)SW && (unsigned)ic < (unsigned)SW) {
-            const uint8_t* q = (const uint8_t*)&sraw[rr][0] + 3 * ic;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) v[c] = T::cvt(2.0f * (float)q[c] - 255.0f);
-        }
-        *(uint2*)&sx[rr][cc][0] = make_uint2((uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2]);
-    }
-    // weight fragments: n = 16i + (lane&15), k = 32ks + 8g .. +7 (g = lane>>4)
-    frag wa[4][3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 3; ++ks)
-            wa[i][ks] = *(const frag*)&swt[16 * i + (lane & 15)][32 * ks + 8 * (lane >> 4)];
-    __syncthreads();
 
-    // wave w: m-frags w, w+4, w+8, w+12 (< 14)
-    f32x4_t acc[4][4];
+    // a tile's input rows r0-1 .. r0+2 (336 contiguous bytes each) as dwords, two per thread, loaded one
+    // tile ahead into registers so the HBM latency hides behind the previous tile's MFMA loop and stores
+    constexpr int RAWD = (SROWS + 2) * (SW * 3 / 4);
+    static_assert(RAWD <= 2 * 256, "two input dwords per thread");
+    auto load_raw = [&](int t, uint32_t (&r)[2]) {
+        const int b = t / (SW / SROWS), r0 = (t % (SW / SROWS)) * SROWS;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[u][i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int f = wave + 4 * u;
-        if (f >= SPIX / 16) break;  // wave-uniform
-        const int px = 16 * f + (lane & 15), pr = px / SW, pc = px % SW;
-#pragma unroll
-        for (int ks = 0; ks < 3; ++ks) {
-            const int tap = 4 * ks + (lane >> 4);
-            uint4 q = make_uint4(0u, 0u, 0u, 0u);
-            if (tap < 9) {
-                const uint2 v = *(const uint2*)&sx[pr + tap / 3][pc + tap % 3][0];
-                const uint32_t v0 = v.x & 0xffff, v1 = v.x >> 16, v2 = v.y & 0xffff;
-                q = make_uint4(v.x, v2 | (v0 << 16), v1 | (v2 << 16), 0u);
-            }
-            const frag bq = __builtin_bit_cast(frag, q);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[u][i] = T::mfma(wa[i][ks], bq, acc[u][i]);
+        for (int j = 0; j < 2; ++j) {
+            const int e = tid + 256 * j, rr = e / (SW * 3 / 4), d = e % (SW * 3 / 4), ir = r0 - 1 + rr;
+            r[j] = e < RAWD && (unsigned)ir < (unsigned)SW ? *(const uint32_t*)(in + ((size_t)b * SW + ir) * SW * 3 + 4 * d) : 0u;
         }
-    }
-    // epilogue: lane holds channels 16i + 4(lane>>4) .. +3 of pixel 16f + (lane&15)
+    };
+    uint32_t raw[2];
+    load_raw(blockIdx.x, raw);  // gridDim.x <= ntiles
+
+    // tiles t = blockIdx.x + j * gridDim.x; every wave runs the same trip count (block-uniform loop)
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int b = t / (SW / SROWS), r0 = (t % (SW / SROWS)) * SROWS;
+        // the previous tile's reads of sraw / sx / sy all precede a barrier every thread has passed
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int n = 16 * i + 4 * (lane >> 4);
-        const float4 bb = *(const float4*)(bias + n);
-        float4 sl = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (act == 2) sl = *(const float4*)(slope + n);
+        for (int j = 0; j < 2; ++j)
+            if (tid + 256 * j < RAWD) (&sraw[0][0])[tid + 256 * j] = raw[j];
+        __syncthreads();
+        // -> 2q - 255 in the activation dtype, zero halo columns (rows outside the image were zeroed above
+        // but must also become 0, not -255)
+        for (int e = tid; e < (SROWS + 2) * (SW + 2); e += 256) {
+            const int rr = e / (SW + 2), cc = e % (SW + 2), ir = r0 - 1 + rr, ic = cc - 1;
+            uint16_t v[3] = {0, 0, 0};
+            if ((unsigned)ir < (unsigned)SW && (unsigned)ic < (unsigned)SW) {
+                const uint8_t* q = (const uint8_t*)&sraw[rr][0] + 3 * ic;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) v[c] = T::cvt(2.0f * (float)q[c] - 255.0f);
+            }
+            *(uint2*)&sx[rr][cc][0] = make_uint2((uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2]);
+        }
+        // weight fragments from the block's LDS copy, re-read per tile (held across tiles they would add
+        // 48 live VGPRs and cost the third block per CU): n = 16i + (lane&15), k = 32ks + 8g .. +7
+        frag wa[4][3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks)
+                wa[i][ks] = *(const frag*)&swt[16 * i + (lane & 15)][32 * ks + 8 * (lane >> 4)];
+        __syncthreads();
+
+        // wave w: m-frags w, w+4, w+8, w+12 (< 14)
+        f32x4_t acc[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[u][i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int f = wave + 4 * u;
-            if (f >= SPIX / 16) break;
-            const int px = 16 * f + (lane & 15);
-            float v[8] = {acc[u][i][0] + bb.x, acc[u][i][1] + bb.y, acc[u][i][2] + bb.z, acc[u][i][3] + bb.w, 0, 0, 0, 0};
-            if (act == 2) {
-                v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
-                v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
-                v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
-                v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
-            } else if (act == 1) {
+            if (f >= SPIX / 16) break;  // wave-uniform
+            const int px = 16 * f + (lane & 15), pr = px / SW, pc = px % SW;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+            for (int ks = 0; ks < 3; ++ks) {
+                const int tap = 4 * ks + (lane >> 4);
+                uint4 q = make_uint4(0u, 0u, 0u, 0u);
+                if (tap < 9) {
+                    const uint2 v = *(const uint2*)&sx[pr + tap / 3][pc + tap % 3][0];
+                    const uint32_t v0 = v.x & 0xffff, v1 = v.x >> 16, v2 = v.y & 0xffff;
+                    q = make_uint4(v.x, v2 | (v0 << 16), v1 | (v2 << 16), 0u);
+                }
+                const frag bq = __builtin_bit_cast(frag, q);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[u][i] = T::mfma(wa[i][ks], bq, acc[u][i]);
             }
-            const uint4 pk = T::pack8(v);
-            // 16-B chunk n/8 of the pixel's 128-B row, XOR-swizzled by pixel; this lane owns half of it
-            char* dst = (char*)&sy[px * 8 + ((n >> 3) ^ (px & 7))] + (n & 4) * 2;
-            *(uint2*)dst = make_uint2(pk.x, pk.y);
         }
-    }
-    __syncthreads();
-    // coalesced stores: 224 pixels x 8 chunks of 16 B
-    const size_t row0 = ((size_t)b * SW + r0) * SW;
-    for (int e = tid; e < SPIX * 8; e += 256) {
-        const int px = e >> 3, ch = e & 7;
-        *(uint4*)(y + (row0 + px) * Cy + y_off + 8 * ch) = sy[px * 8 + (ch ^ (px & 7))];
+        if (t + (int)gridDim.x < ntiles) load_raw(t + gridDim.x, raw);  // block-uniform
+        // epilogue: lane holds channels 16i + 4(lane>>4) .. +3 of pixel 16f + (lane&15)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int n = 16 * i + 4 * (lane >> 4);
+            const float4 bb = *(const float4*)(bias + n);
+            float4 sl = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (act == 2) sl = *(const float4*)(slope + n);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int f = wave + 4 * u;
+                if (f >= SPIX / 16) break;
+                const int px = 16 * f + (lane & 15);
+                float v[8] = {acc[u][i][0] + bb.x, acc[u][i][1] + bb.y, acc[u][i][2] + bb.z, acc[u][i][3] + bb.w, 0, 0, 0, 0};
+                if (act == 2) {
+                    v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
+                    v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
+                    v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
+                    v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
+                } else if (act == 1) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                }
+                const uint4 pk = T::pack8(v);
+                // 16-B chunk n/8 of the pixel's 128-B row, XOR-swizzled by pixel; this lane owns half of it
+                char* dst = (char*)&sy[px * 8 + ((n >> 3) ^ (px & 7))] + (n & 4) * 2;
+                *(uint2*)dst = make_uint2(pk.x, pk.y);
+            }
+        }
+        __syncthreads();
+        // coalesced stores: 224 pixels x 8 chunks of 16 B
+        const size_t row0 = ((size_t)b * SW + r0) * SW;
+        for (int e = tid; e < SPIX * 8; e += 256) {
+            const int px = e >> 3, ch = e & 7;
+            *(uint4*)(y + (row0 + px) * Cy + y_off + 8 * ch) = sy[px * 8 + (ch ^ (px & 7))];
+        }
     }
 }
 
@@ -146,11 +171,23 @@ bool stem_u8_supported(int H, int W, int Cin, int K, int Kpad, int Cout, int Cy,
 
 hipError_t launch_stem_u8(const uint8_t* in, int B, const bf16_t* w, int Kpad, const float* bias, const float* slope,
                           int act, bf16_t* y, int Cy, int y_off, int f16, hipStream_t s) {
-    const dim3 grid(B * (SW / SROWS));
+    // persistent blocks: 3 per CU (the VGPR limit), trip counts balanced so no block runs an extra
+    // round; FR_STEM_PERSIST=0 launches one block per tile (weights re-staged per tile)
+    static const bool persist = [] {
+        const char* e = getenv("FR_STEM_PERSIST");
+        return !(e && e[0] == '0');
+    }();
+    const int ntiles = B * (SW / SROWS);
+    int nblk = ntiles;
+    if (persist && ntiles > 768) {
+        const int trips = (ntiles + 767) / 768;
+        nblk = (ntiles + trips - 1) / trips;
+    }
+    const dim3 grid(nblk);
     if (f16)
-        hipLaunchKernelGGL(stem_u8_kernel<true>, grid, dim3(256), 0, s, in, w, Kpad, bias, slope, act, y, Cy, y_off);
+        hipLaunchKernelGGL(stem_u8_kernel<true>, grid, dim3(256), 0, s, in, w, Kpad, bias, slope, act, y, Cy, y_off, ntiles);
     else
-        hipLaunchKernelGGL(stem_u8_kernel<false>, grid, dim3(256), 0, s, in, w, Kpad, bias, slope, act, y, Cy, y_off);
+        hipLaunchKernelGGL(stem_u8_kernel<false>, grid, dim3(256), 0, s, in, w, Kpad, bias, slope, act, y, Cy, y_off, ntiles);
     return hipGetLastError();
 }
 
