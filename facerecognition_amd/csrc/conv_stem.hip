@@ -11,10 +11,10 @@
 // K = (tap, c) with c fastest, zero past K = 72), so only the f32 summation order differs.
 // Tile = 2 output rows of one image (224 pixels = 14 m-frags) x 64 channels (4 n-frags); 3 persistent
 // blocks per CU loop over tiles, staging the weights once and prefetching the next tile's input:
-//   * the 4 input rows (dword loads) and the 64 x 96 weight rows go to LDS once per block; the input
+//   * the 64 x 96 weight rows go to LDS once per block, the 4 input rows (dword loads) once per tile; the input
 //     becomes 2q - 255 in the activation dtype with a zero halo, [row][col][4];
 //   * MFMA operand B for K-step ks, k-group g is tap 4ks + g of one pixel = [v0 v1 v2 v0 v1 v2 0 0],
-//     built from one 8-byte LDS read; operand A = 12 weight fragments per lane, read once;
+//     built from one 8-byte LDS read; operand A = 12 weight fragments per lane, read once per tile;
 //   * 3 K-steps of v_mfma_f32_16x16x32_{bf16,f16} per tile; the epilogue (bias, PReLU) stages the
 //     224 x 64 tile in LDS (16-B chunks XOR-swizzled by pixel) and writes it with 16-B coalesced stores.
 #include "kernels.h"
@@ -28,7 +28,7 @@ namespace {
 
 constexpr int SW = 112;       // image width = height
 constexpr int SCO = 64;       // output channels
-constexpr int SROWS = 2;      // output rows per block
+constexpr int SROWS = 2;      // output rows per tile
 constexpr int SPIX = SROWS * SW;  // 224
 constexpr int WROW = 104;          // LDS weight row: 96 bf16 + pad (208 B: conflict-free 16-lane reads)
 
