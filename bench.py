@@ -12,11 +12,18 @@ One step = one pass of the hot path over one batch of HBM-resident synthetic u8 
 Weak scaling: every rank embeds 256 faces; the gallery is row-sharded across ranks.
 value = faces embedded by all ranks / max-over-ranks wall time of the timed steps.
 
-Launch: python bench.py --gpus N --steps K --warmup W   (N > 1 under torch.distributed.run)
+Launch: python bench.py --gpus N --steps K --warmup W
+  N > 1 either under torch.distributed.run (RANK/WORLD_SIZE set), or directly: the parent process then
+  never touches the GPU and starts N fresh child processes, one per GPU, with RANK/LOCAL_RANK/
+  WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT set (launch_ranks).
+  Gallery default: 10k rows at N = 1 (BASELINE config 2), 1M rows at N > 1 (config 4: bs 2048 over 8
+  GPUs, 125k rows per rank).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -57,7 +64,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--gallery-rows", type=int, default=10000)
+    ap.add_argument("--gallery-rows", type=int, default=None,
+                    help="default 10000 at --gpus 1 (config 2), 1000000 at --gpus > 1 (config 4)")
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--arch", default="iresnet100")
     ap.add_argument("--dtype", default=None,
@@ -65,61 +73,147 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip the per-kernel event timing (roofline)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses cuda:0 and the collectives run on gloo "
+                         "(staged through host memory); never a measurement")
     ap.add_argument("--host-input", action="store_true",
                     help="crops start in pinned host memory and are copied H2D inside each step "
                          "(PCIe-inclusive rate, DESIGN.md; never the headline value)")
     return ap.parse_args()
 
 
+def _time_embed(model, arch, u8, M):
+    t0 = time.perf_counter()
+    e = M.embed(model, arch, u8)
+    return e, time.perf_counter() - t0
+
+
 def cpu_baseline(arch, seconds):
-    """The oracle (PyTorch fp32 CPU restatement of the path; IResNet100 has no reference code, so
-    kind='port') on a bounded sample: batches of 8 synthetic crops through embed + F.normalize, then
-    the reference's batched np.dot+argmax match against a 1k-row gallery (BASELINE configs[0])."""
+    """BASELINE configs[0] / SURVEY.md §8d config 1 on the host cores, through the oracle (PyTorch fp32
+    CPU restatement of the path; kind='port').  Two legs, each one bs=256 batch of synthetic crops:
+
+      * `arch` (the bench's model; IResNet100 by default, which has no reference code) fp32 forward +
+        F.normalize + the notebook's batched np.dot top-5 against a 1k-row gallery -> `value`;
+      * the reference's own model, ResNet-50 ArcFaceModel (oracle golden-checked against the
+        reference import, tests/test_golden.py), at bs=256, matched both ways the reference does:
+        the recognize_with_db per-row cosine_similarity loop + stable sort (recognition_engine.py:
+        267-289) for every probe, and the batched np.dot + argmax/top-5 (evaluate_arcface_kaggle.ipynb).
+
+    `seconds` bounds the IResNet100 leg: when one bs=256 forward would exceed it (estimated from a
+    32-crop probe batch), the leg times the largest multiple of 32 crops that fits and says so."""
     from facerecognition_amd.synthetic import synthetic_crops
     from facerecognition_amd.weights import INPUT_SIZE, synth_state_dict
     from oracle import models as M
-    from oracle.match import topk_dot
+    from oracle.match import recognize_with_db, topk_dot
 
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    model = M.build_model(arch, synth_state_dict(arch))
-    s = INPUT_SIZE[arch]
     gal = np.random.default_rng(1).standard_normal((1000, 512)).astype(np.float32)
     gal /= np.linalg.norm(gal, axis=1, keepdims=True)
-    bs, done = 8, 0
-    u8 = synthetic_crops(bs, s, seed=11)
+    out = {"unit": "faces/s", "cores": threads, "kind": "port"}
+
+    # leg 1: the bench's model at bs=256 (bounded)
+    s = INPUT_SIZE[arch]
+    model = M.build_model(arch, synth_state_dict(arch))
+    u8 = synthetic_crops(256, s, seed=11)
     M.embed(model, arch, u8[:2])  # warm the allocator / kernels
+    _, t32 = _time_embed(model, arch, u8[:32], M)
+    n = 256 if t32 * 8 <= seconds else max(32, int(seconds / t32) * 32)
+    e, t_emb = _time_embed(model, arch, u8[:n], M)
     t0 = time.perf_counter()
-    while True:
-        e = M.embed(model, arch, u8)
+    topk_dot(e, gal, 5)
+    t_dot = time.perf_counter() - t0
+    out["value"] = round(n / (t_emb + t_dot), 3)
+    out["sample"] = (f"{n} synthetic {s}x{s} crops in ONE batch of {n}: {arch} fp32 forward + F.normalize "
+                     f"({t_emb:.2f}s) + np.dot top-5 vs 1000x512 gallery ({t_dot * 1e3:.1f} ms), "
+                     f"torch {threads} threads")
+    del model
+
+    # leg 2: the reference's own path (ResNet-50 ArcFaceModel), bs=256, both match styles
+    if arch != "resnet50_arcface":
+        r50 = M.build_model("resnet50_arcface", synth_state_dict("resnet50_arcface"))
+        u8 = synthetic_crops(256, 112, seed=11)
+        M.embed(r50, "resnet50_arcface", u8[:2])
+        e, t_emb = _time_embed(r50, "resnet50_arcface", u8, M)
+        db = {f"id_{j}": gal[j] for j in range(len(gal))}
+        t0 = time.perf_counter()
+        for row in e:
+            recognize_with_db(row, db, 0.5)
+        t_loop = time.perf_counter() - t0
+        t0 = time.perf_counter()
         topk_dot(e, gal, 5)
-        done += bs
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(done / dt, 3), "unit": "faces/s", "cores": threads, "kind": "port",
-            "sample": f"{done} synthetic {s}x{s} crops in batches of {bs}: {arch} fp32 forward + F.normalize "
-                      f"+ np.dot top-5 vs 1000x512 gallery, torch {threads} threads, {dt:.1f}s"}
+        t_dot = time.perf_counter() - t0
+        out["reference_resnet50"] = {
+            "embed_faces_per_s": round(256 / t_emb, 2),
+            "embed_plus_recognize_with_db_loop_faces_per_s": round(256 / (t_emb + t_loop), 2),
+            "embed_plus_batched_dot_faces_per_s": round(256 / (t_emb + t_dot), 2),
+            "recognize_with_db_loop_s": round(t_loop, 3), "batched_dot_ms": round(t_dot * 1e3, 2),
+            "sample": "256 synthetic 112x112 crops, one batch of 256: ResNet-50 ArcFaceModel fp32 forward + "
+                      "F.normalize, then recognize_with_db's per-row cosine_similarity loop + sort over a "
+                      f"1000-row dict db for every probe, and np.dot + top-5; torch {threads} threads"}
+    return out
+
+
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher.  This process has not touched the GPU (importing
+    torch does not initialise HIP) and never does: it starts N fresh child processes of this same
+    command, one per GPU, with the torch.distributed.run environment, forwards their output and
+    returns the worst exit code.  If one rank fails the others are stopped by their exact PIDs."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.gallery_rows is None:
+        args.gallery_rows = 10000 if world == 1 else 1000000
+    if args.share_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.share_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from facerecognition_amd.distributed import ShardedMatcher, shard_range
     from facerecognition_amd.gallery import DeviceGallery
     from facerecognition_amd.model import FRModel
-    from facerecognition_amd.synthetic import synthetic_crops
+    from facerecognition_amd.synthetic import synthetic_crops, synthetic_gallery_rows
     from facerecognition_amd import _native as N
 
     B, K = args.batch, args.k
@@ -130,9 +224,8 @@ def main():
     # gallery: rows [r*rows/N, (r+1)*rows/N) on rank r; global indices via index_base
     rows = args.gallery_rows
     lo, hi = shard_range(rows, rank, world)
-    g = np.random.default_rng(1).standard_normal((rows, 512)).astype(np.float32)[lo:hi]
-    g /= np.linalg.norm(g, axis=1, keepdims=True)
-    gallery = DeviceGallery(g, device=local, index_base=lo)
+    gallery = DeviceGallery(device=local, index_base=lo)
+    gallery.set_device_rows(synthetic_gallery_rows(lo, hi, dev))
     emb = torch.empty((B, 512), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -191,7 +284,7 @@ def main():
         N.check(N.lib().fr_prof_only(model.handle, None), "fr_prof_only")
     embed_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))  # forward duration on its stream
     if dist:
-        t = torch.tensor([elapsed, embed_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, embed_ms], dtype=torch.float64, device="cpu" if args.share_device else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, embed_ms = float(t[0]), float(t[1])
     # sanity: top-1 indices are valid global gallery rows
@@ -209,7 +302,8 @@ def main():
         "config": {"workload": f"{args.arch} {args.dtype} embed bs={B}/GPU + top-{K} match vs "
                                f"{rows}x512 f32 gallery (row-sharded over {world} GPU(s))",
                    "batch_per_gpu": B, "global_batch": world * B, "gallery_rows": rows, "k": K,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}" + (" (shared-device gloo rehearsal, not a measurement)"
+                                                   if args.share_device else "")},
     }
     if flop_fwd:
         result["forward"] = {"embed_ms": round(embed_ms, 4),

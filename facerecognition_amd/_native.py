@@ -31,6 +31,7 @@ FR_OPT_STAGE = 1
 FR_OPT_KEEP_INTERMEDIATES = 2
 FR_OPT_MATCH_EXACT = 3
 FR_OPT_X3_MIN_ROWS = 4
+FR_OPT_STAGE_MIN_FILL = 5
 
 c_int, c_int64, c_size_t, c_void_p, c_float_p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p
 

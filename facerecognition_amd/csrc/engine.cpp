@@ -141,7 +141,9 @@ struct fr_handle {
     int proj_d = 0;
     float* emb_pre = nullptr;  // [max_batch][512] IRV1 output before the projection
     float* amax = nullptr;     // FR_DTYPE_FP8: per-tensor max |x| of the current forward [ntensors]
-    bool use_stage = true;
+    int stage_mode = 1;       // FR_OPT_STAGE: 0 off, 1 auto (stage_runs), 2 always
+    int stage_min_fill = 80;  // FR_OPT_STAGE_MIN_FILL (percent)
+    int n_cu = 256;
     bool keep_inter = false;
 };
 
@@ -976,14 +978,28 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     return FR_OK;
 }
 
+// Whether the LDS-resident stage kernel runs at batch B.  It puts one image on one CU.  Up to one image
+// per CU it beats the per-conv launches at every batch size (tools/batch_sweep.py, profiles/
+// r02_batch_sweep.jsonl: B = 1 3.76 vs 3.88 ms, B = 128 5.39 vs 5.73 ms): a small batch leaves CUs idle
+// either way, since per-conv grids of B*196 positions are a handful of tiles.  Above one round a last
+// round that is mostly empty costs a whole stage time, so auto mode then requires the rounds to be at
+// least stage_min_fill % full (B = 512: 100 %, B = 257: 50 % -> per-conv).
+static bool stage_runs(const fr_handle* h, int B) {
+    if (h->stage_mode == 0 || h->stages.empty()) return false;
+    if (h->stage_mode == 2 || B <= h->n_cu) return true;
+    const int64_t rounds = (B + h->n_cu - 1) / h->n_cu;
+    return (int64_t)B * 100 >= (int64_t)h->stage_min_fill * rounds * h->n_cu;
+}
+
 int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
     const int f16 = h->dtype == FR_DTYPE_F16;
+    const bool use_stage = stage_runs(h, B);
     if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s));
     bool skip_next = false;
     for (size_t oi = 0; oi < h->ops.size(); ++oi) {
         const Op& op = h->ops[oi];
         if (skip_next) { skip_next = false; continue; }
-        if (op.kind == OP_STAGE ? !h->use_stage : (op.stage >= 0 && h->use_stage)) continue;
+        if (op.kind == OP_STAGE ? !use_stage : (op.stage >= 0 && use_stage)) continue;
         switch (op.kind) {
             case OP_STAGE: {
                 const StageRec& r = h->stages[op.stage];
@@ -1115,9 +1131,9 @@ extern "C" {
 const char* fr_last_error(void) { return g_err.c_str(); }
 int fr_abi_version(void) { return FR_ABI_VERSION; }
 
-static bool stage_default() {
+static int stage_default() {
     const char* e = getenv("FR_NO_STAGE");
-    return !(e && e[0] == '1');
+    return (e && e[0] == '1') ? 0 : 1;
 }
 
 int fr_create(fr_handle** out, int device, int arch, int dtype) {
@@ -1137,7 +1153,10 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->arch = arch;
     h->dtype = dtype;
     h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
-    h->use_stage = stage_default();
+    h->stage_mode = stage_default();
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        h->n_cu = prop.multiProcessorCount;
     *out = h;
     return FR_OK;
 }
@@ -1352,7 +1371,10 @@ static int match_locked(fr_handle* h, const float* P, int B, int k, float* score
     hipStream_t s = (hipStream_t)stream;
     int n_split;
     int64_t rps;
-    if (h->g_hi && !h->match_exact) {  // bf16x3 candidates + exact f32 rescoring (match_x3.hip)
+    // bf16x3 candidates + exact f32 rescoring (match_x3.hip).  Its proof needs the k-th exact score to
+    // clear the 16th candidate by 2 eps, which a k close to 16 almost never does (every probe would be
+    // rescanned by one wave), so k > 8 takes the exact kernel.
+    if (h->g_hi && !h->match_exact && 2 * k <= match_x3_candidates()) {
         match_x3_plan(B, h->g_rows, &n_split, &rps);
         int rc = ensure_cand(h, (size_t)B * n_split * match_x3_candidates());
         if (rc) return rc;
@@ -1403,8 +1425,9 @@ int fr_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, i
 int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
     if (!h || !buf || n == 0 || B <= 0) { set_error("fr_debug_plan: bad argument"); return FR_ERR_ARG; }
     std::string out;
+    const bool use_stage = stage_runs(h, B);
     for (const auto& op : h->ops) {
-        if (op.kind == OP_STAGE ? !h->use_stage : (op.stage >= 0 && h->use_stage)) continue;
+        if (op.kind == OP_STAGE ? !use_stage : (op.stage >= 0 && use_stage)) continue;
         if (op.kind == OP_STAGE) {
             const StageRec& r = h->stages[op.stage];
             out += "stage " + std::to_string(B * 196) + " 256 2304 2304 " + std::to_string(2 * r.nblk) + " 1 3x3 " +
@@ -1449,7 +1472,14 @@ int fr_set_option(fr_handle* h, int option, int value) {
     if (!h) { set_error("fr_set_option: null handle"); return FR_ERR_ARG; }
     std::lock_guard<std::mutex> lk(h->mu);
     switch (option) {
-        case FR_OPT_STAGE: h->use_stage = value != 0; break;
+        case FR_OPT_STAGE:
+            if (value < 0 || value > 2) { set_error("fr_set_option: FR_OPT_STAGE is 0, 1 or 2"); return FR_ERR_ARG; }
+            h->stage_mode = value;
+            break;
+        case FR_OPT_STAGE_MIN_FILL:
+            if (value < 0 || value > 100) { set_error("fr_set_option: FR_OPT_STAGE_MIN_FILL is 0..100"); return FR_ERR_ARG; }
+            h->stage_min_fill = value;
+            break;
         case FR_OPT_KEEP_INTERMEDIATES: h->keep_inter = value != 0; break;
         case FR_OPT_MATCH_EXACT: h->match_exact = value != 0; break;
         case FR_OPT_X3_MIN_ROWS:
@@ -1465,7 +1495,8 @@ int fr_set_option(fr_handle* h, int option, int value) {
 int fr_get_option(const fr_handle* h, int option) {
     if (!h) return FR_ERR_ARG;
     switch (option) {
-        case FR_OPT_STAGE: return h->use_stage && !h->stages.empty() ? 1 : 0;
+        case FR_OPT_STAGE: return h->stages.empty() ? 0 : h->stage_mode;
+        case FR_OPT_STAGE_MIN_FILL: return h->stage_min_fill;
         case FR_OPT_KEEP_INTERMEDIATES: return h->keep_inter ? 1 : 0;
         case FR_OPT_MATCH_EXACT: return h->match_exact ? 1 : 0;
         case FR_OPT_X3_MIN_ROWS: return (int)h->x3_min_rows;

@@ -31,10 +31,14 @@ def _all_gather(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
     import torch.distributed as dist
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, inp.contiguous(), group=group)
-    else:  # gloo: list form
+    else:  # gloo (CPU tests, or several ranks sharing one GPU in the -m gpu test): list form,
+        # staged through host memory when the tensors live on the device
         world = dist.get_world_size(group)
-        parts = list(out.view(world, *inp.shape).unbind(0))
-        dist.all_gather(parts, inp.contiguous(), group=group)
+        host = out if not out.is_cuda else torch.empty(out.shape, dtype=out.dtype)
+        parts = list(host.view(world, *inp.shape).unbind(0))
+        dist.all_gather(parts, inp.contiguous().cpu(), group=group)
+        if host is not out:
+            out.copy_(host)
 
 
 def native_merge(cand_s: torch.Tensor, cand_i: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -112,7 +112,7 @@ def _load_u8(img_input, transform) -> np.ndarray:
 
 def _embed_u8(model, u8: np.ndarray) -> np.ndarray:
     import torch
-    return model.embed(torch.from_numpy(np.ascontiguousarray(u8)), normalize=True).cpu().numpy()
+    return model.embed(torch.from_numpy(np.require(u8, requirements=["C", "W"])), normalize=True).cpu().numpy()
 
 
 # ---------------------------------------------------------------------------------------- extraction

@@ -38,17 +38,20 @@ class DeviceGallery:
         self._h = handle
         if x3_min_rows is not None:  # FR_OPT_X3_MIN_ROWS: smallest gallery given the bf16x3 path
             N.check(N.lib().fr_set_option(self._h, N.FR_OPT_X3_MIN_ROWS, int(x3_min_rows)), "fr_set_option")
-        self._rows = torch.empty((0, dim), dtype=torch.float32)
+        self._rows = torch.empty((0, dim), dtype=torch.float32)  # host copy (rows added from the host)
+        self._rows_dev = None  # device rows installed by set_device_rows (no host copy is made)
+        self._n = 0
         if rows is not None:
             self.add(rows)
 
     @property
     def ntotal(self) -> int:
-        return int(self._rows.shape[0])
+        return self._n
 
     def reset(self) -> None:
         import torch
         self._rows = torch.empty((0, self.d), dtype=torch.float32)
+        self._rows_dev, self._n = None, 0
         N.check(N.lib().fr_gallery_set(self._h, None, 0, self.d, self.index_base, 0), "fr_gallery_set")
 
     def add(self, rows) -> None:
@@ -57,18 +60,21 @@ class DeviceGallery:
 
         r = torch.as_tensor(np.asarray(rows, dtype=np.float32) if not torch.is_tensor(rows) else rows)
         r = r.detach().float().cpu().reshape(-1, self.d)
+        if self._rows_dev is not None:  # rows installed from the device: bring them over once
+            self._rows, self._rows_dev = self._rows_dev.cpu(), None
         self._rows = torch.cat([self._rows, r], 0).contiguous()
+        self._n = int(self._rows.shape[0])
         self._upload()
 
     def set_device_rows(self, rows_dev) -> None:
-        """Install rows already resident on the GPU (no host round trip)."""
+        """Install rows already resident on the GPU (no host round trip; the library copies them)."""
         rows_dev = rows_dev.float().contiguous()
-        self._rows = rows_dev.detach().cpu()
         N.check(N.lib().fr_gallery_set(self._h, N.ptr(rows_dev), int(rows_dev.shape[0]), self.d, self.index_base, 1),
                 "fr_gallery_set")
+        self._rows_dev, self._n = rows_dev.detach(), int(rows_dev.shape[0])
 
     def _upload(self) -> None:
-        N.check(N.lib().fr_gallery_set(self._h, N.ptr(self._rows), self.ntotal, self.d, self.index_base, 0),
+        N.check(N.lib().fr_gallery_set(self._h, N.ptr(self._rows), self._n, self.d, self.index_base, 0),
                 "fr_gallery_set")
 
     def set_exact(self, exact: bool) -> None:

@@ -5,8 +5,9 @@ Reference → here:
   cosine_similarity :41-63            unchanged host function (a10)
   RecognitionEngine.__init__ :75-140  same arguments; dict db (.npy) and/or index + prototypes + mapping
   extract_embedding :244-265          fr_embed via extract_embedding_single (a7)
-  recognize_with_db :267-289          ONE fr_match_topk against the device copy of the db (dict order =
+  recognize_with_db :267-289          fr_match_topk against the device copy of the db (dict order =
                                        row order; (score desc, index asc) = the stable sort), top-5,
+                                       cosine_similarity's both-norms-unit rule per pair (_db_gallery),
                                        ``best < threshold`` → "Unknown"; no db → ("No database", 0.0, [])
   recognize_with_faiss :291-326       probe / (‖p‖+1e-8), exact inner-product top-k on the device
                                        index; names ``id_to_label.get(idx, f"ID_{idx}")`` (reference quirk kept)
@@ -183,15 +184,31 @@ class RecognitionEngine:
         return None
 
     def _db_gallery(self):
+        """Device copies of the dict db for cosine_similarity semantics (recognition_engine.py:41-63):
+        a pair scores dot(a, b) when BOTH norms are within 1e-3 of 1, else dot / (|a| |b|).  A row's
+        divisor therefore depends on the probe, so the rows are kept as
+          'on'  — the rows whose norm is within 1e-3 of 1, raw (scored against unit-ish probes as is);
+          'off' — the other rows divided by their norm (zero rows stay zero: score 0.0);
+          'all' — every row divided by its norm (for probes that are not unit-ish), built on first use.
+        A dict db of normalized embeddings (build_db, add_to_db) has no 'off' rows, and unit-ish probes
+        (every fr_embed output) then take one search."""
         from .gallery import DeviceGallery
         key = (id(self._db), self._db.version)
         if self._g is None or self._g[0] != key:
             names = list(self._db.keys())
             rows = np.stack([np.asarray(v, dtype=np.float32).reshape(-1) for v in self._db.values()])
+            n = np.linalg.norm(rows, axis=1)
+            on = np.abs(n - 1.0) < 1e-3
             dev = self.model.device.index if self.model is not None else _device_index(self.device)
-            self._g = (key, DeviceGallery(rows, dim=rows.shape[1], device=dev), names)
+            unit = rows / np.where(n > 0, n, 1.0)[:, None]
+            parts = {"dev": dev, "unit": unit, "dim": rows.shape[1]}
+            for tag, mask, src in (("on", on, rows), ("off", ~on, unit)):
+                idx = np.nonzero(mask)[0]
+                parts[tag] = (DeviceGallery(src[idx], dim=rows.shape[1], device=dev), idx) if len(idx) else None
+            self._g = (key, parts, names)
         return self._g[1], self._g[2]
 
+    # ------------------------------------------------------------------ embedding
     # ------------------------------------------------------------------ embedding
     def extract_embedding(self, img_input) -> Optional[np.ndarray]:
         if self.model is None:
@@ -201,22 +218,47 @@ class RecognitionEngine:
 
     # ------------------------------------------------------------------ matching
     @staticmethod
-    def _as_probes(E: np.ndarray) -> np.ndarray:
-        """Probe rows in cosine_similarity semantics: rows whose norm is not within 1e-3 of 1 are
-        divided by it (the gallery side is prepared the same way by fr_gallery_set)."""
-        E = np.asarray(E, dtype=np.float32).reshape(len(E), -1).copy()
-        n = np.linalg.norm(E, axis=1)
-        fix = (np.abs(n - 1.0) >= 1e-3) & (n > 0)
-        E[fix] /= n[fix, None]
-        return E
+    def _search_mapped(part, P, k):
+        """Top-k of host probes P against one device part; indices mapped to db rows."""
+        import torch
+        g, idx = part
+        s, i = g.search_device(torch.from_numpy(np.ascontiguousarray(P)).to(g.device), min(k, g.ntotal))
+        return s.cpu().numpy(), idx[i.cpu().numpy()]
+
+    @staticmethod
+    def _merge(lists, k):
+        """(score desc, db row asc) merge of per-part top-k lists — the stable sort's order."""
+        s = np.concatenate([a for a, _ in lists], 1)
+        i = np.concatenate([b for _, b in lists], 1)
+        order = np.lexsort((i, -s), axis=1)[:, :k]
+        return np.take_along_axis(s, order, 1), np.take_along_axis(i, order, 1)
 
     def _db_topk(self, E: np.ndarray, k: int):
-        import torch
-        g, names = self._db_gallery()
-        k = min(k, g.ntotal)
-        P = torch.from_numpy(self._as_probes(E)).to(g.device)
-        s, i = g.search_device(P, k)
-        return s.cpu().numpy(), i.cpu().numpy(), names
+        """Top-k db rows of every probe in cosine_similarity semantics (see _db_gallery)."""
+        parts, names = self._db_gallery()
+        k = min(k, len(names))
+        E = np.asarray(E, dtype=np.float32).reshape(len(E), -1)
+        npr = np.linalg.norm(E, axis=1)
+        p_on = np.abs(npr - 1.0) < 1e-3
+        E_unit = E / np.where(npr > 0, npr, 1.0)[:, None]
+        S = np.zeros((len(E), k), np.float32)
+        I = np.zeros((len(E), k), np.int64)
+        sel = np.nonzero(p_on)[0]
+        if len(sel):  # unit-ish probes: raw against 'on' rows, dot / (|p| |g|) against 'off' rows
+            lists = []
+            if parts["on"] is not None:
+                lists.append(self._search_mapped(parts["on"], E[sel], k))
+            if parts["off"] is not None:
+                lists.append(self._search_mapped(parts["off"], E_unit[sel], k))
+            S[sel], I[sel] = self._merge(lists, k) if len(lists) > 1 else lists[0]
+        sel = np.nonzero(~p_on)[0]
+        if len(sel):  # other probes (zero probes stay zero: every score 0.0): dot / (|p| |g|) everywhere
+            if "all" not in parts:
+                from .gallery import DeviceGallery
+                parts["all"] = (DeviceGallery(parts["unit"], dim=parts["dim"], device=parts["dev"]),
+                                np.arange(len(names)))
+            S[sel], I[sel] = self._search_mapped(parts["all"], E_unit[sel], k)
+        return S, I, names
 
     def _result_db(self, s_row, i_row, names):
         top = [(names[j], float(v)) for v, j in zip(s_row, i_row)]

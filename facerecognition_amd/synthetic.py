@@ -32,6 +32,27 @@ def synthetic_crops(n: int, size: int = 112, seed: int = 0, grid: int = 6, noise
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
 
 
+GALLERY_BLOCK = 1 << 16  # rows per independently seeded block of synthetic_gallery_rows
+
+
+def synthetic_gallery_rows(lo: int, hi: int, device, dim: int = 512, seed: int = 1):
+    """Rows [lo, hi) of the synthetic random unit-norm gallery (standard-normal rows,
+    L2-normalized), generated on the device in GALLERY_BLOCK-row blocks, each seeded by (seed, block).
+    Any shard of a 1M x 512 gallery is reproduced on its own rank without materialising the whole
+    2 GB matrix anywhere, and the rows do not depend on how the gallery is sharded."""
+    import torch
+
+    out = torch.empty((hi - lo, dim), dtype=torch.float32, device=device)
+    for b in range(lo // GALLERY_BLOCK, (hi + GALLERY_BLOCK - 1) // GALLERY_BLOCK):
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 1_000_003 + b)
+        blk = torch.randn((GALLERY_BLOCK, dim), generator=g, device=device)
+        s, e = max(lo, b * GALLERY_BLOCK), min(hi, (b + 1) * GALLERY_BLOCK)
+        out[s - lo:e - lo] = blk[s - b * GALLERY_BLOCK:e - b * GALLERY_BLOCK]
+    out /= out.norm(dim=1, keepdim=True)
+    return out
+
+
 def planted_gallery(probe_emb: np.ndarray, n_rows: int, seed: int = 1, jitter: float = 0.05) -> np.ndarray:
     """Unit-norm gallery [n_rows, D]: row j < len(probe_emb) = normalize(e_j + jitter*noise)
     (a planted match for probe j), the rest random directions."""

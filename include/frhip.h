@@ -194,7 +194,11 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
 /* ---- execution options (no reference counterpart: plan choices of this build) ----------------
  * FR_OPT_STAGE (default 1; env FR_NO_STAGE=1 starts at 0): run the stride-1 IResNet100 layer3 blocks
  *   as one LDS-resident stage kernel per image instead of 58 separate conv launches.  Numerically the
- *   same op sequence and bf16 rounding points (f32 accumulation in a different K order).
+ *   same op sequence and bf16 rounding points (f32 accumulation in a different K order).  0 = never,
+ *   1 = auto: at every batch of at most one image per CU (measured faster than the per-conv launches
+ *   down to B = 1), and above that only when the rounds of one image per CU are at least
+ *   FR_OPT_STAGE_MIN_FILL percent full (B = 257 on 256 CUs takes the per-conv launches), 2 = always.
+ * FR_OPT_STAGE_MIN_FILL (default 80): the auto threshold above, in percent.
  * FR_OPT_KEEP_INTERMEDIATES (default 0): the stage kernel also writes every block output and conv1
  *   output to its named tensor (per-layer drift tests; costs HBM writes).
  * Changing an option drops the captured hipGraph replays.  fr_get_option returns the value (FR_OPT_STAGE
@@ -209,6 +213,7 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
 /* FR_OPT_X3_MIN_ROWS (default 32768): smallest gallery given the bf16x3 path (its hi/lo copy is made by
  * the next fr_gallery_set); below it the f32 kernel is as fast. */
 #define FR_OPT_X3_MIN_ROWS 4
+#define FR_OPT_STAGE_MIN_FILL 5
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);
 /* Number of probes (since the gallery was first split) whose bf16x3 candidate proof failed and were

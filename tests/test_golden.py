@@ -55,16 +55,21 @@ def test_oracle_natural_image_embedding(gold, oracle_model):
 
 
 def test_host_transform_matches_reference_on_natural_image(gold):
+    """The 900x900 -> 112x112 PIL bilinear Resize + ToTensor + Normalize of the host transform equals
+    the reference transform's output (golden natural_tensor) on uploads/anh1.jpg, decoded pixels in
+    tests/golden/anh1_u8.npz (tools/gen_natural_fixture.py)."""
     from facerecognition_amd.extract_embeddings import get_transform
     from PIL import Image
-    ref_tensor = gold["natural_tensor"]
-    # the fixture holds the reference transform's output; rebuild the same PIL input from it is not
-    # possible, so check the transform on the synthetic crops (Resize is the identity at 112) and the
-    # 900->112 resize path against PIL directly
+    with np.load(os.path.join(os.path.dirname(GOLD), "anh1_u8.npz"), allow_pickle=False) as z:
+        u8 = z["u8"]
+    assert u8.shape == (900, 900, 3)
     t = get_transform()
+    x = t(Image.fromarray(u8)).numpy()
+    assert x.shape == (3, 112, 112)
+    assert np.abs(x - gold["natural_tensor"]).max() <= 1e-6
+    # and the identity-resize path on the synthetic crops
     x = t(Image.fromarray(gold["probes"][0])).numpy()
     assert np.array_equal(x, OM.preprocess_u8_nhwc(gold["probes"][:1]).numpy()[0])
-    assert ref_tensor.shape == (3, 112, 112)
 
 
 def _gallery(gold):

@@ -138,3 +138,47 @@ def test_folder_db_build_and_faiss_path(gold, r50, tmp_path):
     s_ref, i_ref = faiss_flat_ip_search(protos, gold["emb_single"][6], 3)
     assert [r[0] for r in res] == [f"ID_{i}" for i in i_ref[0]]
     assert np.allclose([r[1] for r in res], s_ref[0], atol=1e-5)
+
+
+def test_extract_embeddings_batch_vs_reference(gold, r50, tmp_path):
+    """extract_embeddings_batch (extract_embeddings.py:392-443) on image files, batch_size 3 so the
+    chunks are ragged; a bad path in the middle is skipped and left out of valid_paths."""
+    from PIL import Image
+    from facerecognition_amd import extract_embeddings as EE
+    paths = []
+    for i, p in enumerate(gold["probes"]):
+        f = str(tmp_path / f"{i}.png")
+        Image.fromarray(p).save(f)
+        paths.append(f)
+    paths.insert(4, str(tmp_path / "missing.png"))
+    emb, valid = EE.extract_embeddings_batch(paths, r50, EE.get_transform(), batch_size=3)
+    assert valid == [p for p in paths if "missing" not in p]
+    assert emb.dtype == np.float32 and emb.shape == (8, 512)
+    assert _cos_dist(emb, gold["emb_batch"]).max() <= COS_TOL
+
+
+def test_natural_image_u8_path_vs_reference(gold, r50):
+    """uploads/anh1.jpg decoded (tests/golden/anh1_u8.npz) -> host PIL resize -> fused u8 path."""
+    from PIL import Image
+    from facerecognition_amd.extract_embeddings import extract_embedding_single, get_transform
+    with np.load(os.path.join(os.path.dirname(GOLD), "anh1_u8.npz"), allow_pickle=False) as z:
+        u8 = z["u8"]
+    e = extract_embedding_single(Image.fromarray(u8), r50, get_transform())
+    assert _cos_dist(e, gold["natural_emb"]) <= COS_TOL
+
+
+def test_recognize_with_db_mixed_norm_on_device():
+    """cosine_similarity's per-pair rule (both norms within 1e-3 of 1 -> dot, else dot / |a||b|)
+    through the device galleries, including the near-tie that the old probe-only rescaling flipped."""
+    from facerecognition_amd.recognition_engine import RecognitionEngine
+    from oracle.match import recognize_with_db
+    from test_host_api import mixed_norm_case
+    db, probes = mixed_norm_case()
+    eng = RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.0)
+    eng.db = db
+    for p in probes:
+        name, score, top = eng.recognize_with_db(p)
+        rname, rscore, rtop = recognize_with_db(p, db, 0.0)
+        assert name == rname and [t[0] for t in top] == [t[0] for t in rtop]
+        assert np.allclose([t[1] for t in top], [t[1] for t in rtop], atol=1e-6)
+    assert eng.recognize_with_db(probes[0])[0] == "A"

@@ -420,8 +420,9 @@ def test_match_x3_fallback_on_ties(gpu):
 def test_match_x3_sublist_overflow_floor(gpu):
     """Twelve graded near-duplicates of the probe in rows 16*(i//4) + i%4 -- all in ONE candidate
     sub-list (rows 16j + 4*sub + r of a tile; KP = 8 entries), which overflows: its floor enters the proof.  k = 5 is provable from the candidates (no rescan);
-    k = 10 needs rows the sub-list dropped, so the proof fails and the probe is rescanned exactly.
-    Both equal the exact f32 kernel bit for bit."""
+    k = 8 needs the sub-list's own last entry, which is also its floor, so the proof fails and the
+    probe is rescanned exactly.  Both equal the exact f32 kernel bit for bit.  (k > 8 is routed to the
+    exact kernel by fr_match_topk: test_match_large_k_takes_exact_path.)"""
     from facerecognition_amd.gallery import DeviceGallery
     rng = np.random.default_rng(9)
     G = _norm(rng.standard_normal((8192, 512)))
@@ -430,7 +431,7 @@ def test_match_x3_sublist_overflow_floor(gpu):
     for i, r in enumerate(rows):
         G[r] = _norm(P[:1] + (0.1 + 0.05 * i) * _norm(rng.standard_normal((1, 512))))[0]
     gal = DeviceGallery(G, x3_min_rows=4096)
-    for k, want_fb in ((5, 0), (10, 1)):
+    for k, want_fb in ((5, 0), (8, 1)):
         gal.set_exact(False)
         fb0 = gal.fallbacks()
         s3, i3 = gal.search(P, k)
@@ -439,4 +440,20 @@ def test_match_x3_sublist_overflow_floor(gpu):
         gal.set_exact(True)
         se, ie = gal.search(P, k)
         assert np.array_equal(i3, ie) and np.array_equal(s3, se)
+    gal.close()
+
+
+def test_match_large_k_takes_exact_path(gpu):
+    """k > KC/2 = 8 goes to the exact f32 kernel on an x3-sized gallery: no candidate pass, no rescans
+    (at k = 16 the proof could never pass and every probe fell back to a one-wave rescan)."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(12)
+    G = _norm(rng.standard_normal((8192, 512)))
+    P = _norm(rng.standard_normal((64, 512)))
+    gal = DeviceGallery(G, x3_min_rows=4096)
+    fb0 = gal.fallbacks()
+    s, i = gal.search(P, 16)
+    assert gal.fallbacks() == fb0
+    rs, ri = _np_topk(P, G, 16)
+    assert np.array_equal(i[:, 0], ri[:, 0]) and np.allclose(s, rs, atol=1e-5)
     gal.close()

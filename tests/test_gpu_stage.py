@@ -41,7 +41,7 @@ def test_stage_matches_per_conv_path(gpu, dtype, B):
     x = torch.from_numpy(synthetic_crops(B, 112, seed=3))
     names = {"layer3.1.prelu", "layer3.1", "layer3.15", "layer3.29"}
     m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)
-    m.set_option(N.FR_OPT_STAGE, 1)
+    m.set_option(N.FR_OPT_STAGE, 2)  # always (auto would pick the per-conv path at these batch sizes)
     e_stage = m.embed(x).cpu().numpy()
     t_stage = _named(m, B, names)
     m.set_option(N.FR_OPT_STAGE, 0)
@@ -68,6 +68,40 @@ def test_stage_repeat_and_graph_replay(gpu):
     m.close()
     for o in outs[1:]:
         assert np.array_equal(o, outs[0])
+
+
+def test_stage_auto_rule_by_batch(gpu):
+    """Auto mode runs the stage kernel at every batch of at most one image per CU, and above that only
+    when the CU rounds are >= 80 % full; the plan dump names what runs."""
+    import ctypes
+    from facerecognition_amd.model import FRModel
+    m = FRModel.synthetic("iresnet100")
+    L = N.lib()
+    cu = torch.cuda.get_device_properties(0).multi_processor_count
+
+    def has_stage(B):
+        buf = ctypes.create_string_buffer(1 << 16)
+        N.check(L.fr_debug_plan(m.handle, B, buf, len(buf)), "fr_debug_plan")
+        return any(l.startswith("stage") for l in buf.value.decode().splitlines())
+
+    assert has_stage(1) and has_stage(cu // 2) and has_stage(cu) and has_stage(2 * cu)
+    assert not has_stage(cu + 1) and has_stage(2 * cu - cu // 8)
+    m.set_option(N.FR_OPT_STAGE_MIN_FILL, 0)
+    assert has_stage(cu + 1)
+    m.set_option(N.FR_OPT_STAGE_MIN_FILL, 80)
+    m.set_option(N.FR_OPT_STAGE, 2)
+    assert has_stage(cu + 1)
+    m.set_option(N.FR_OPT_STAGE, 0)
+    assert not has_stage(cu)
+    # B = 257: the per-conv path (auto) gives the same embeddings as the forced stage path
+    from facerecognition_amd.synthetic import synthetic_crops
+    x = torch.from_numpy(synthetic_crops(cu + 1, 112, seed=9))
+    m.set_option(N.FR_OPT_STAGE, 1)
+    a = m.embed(x).cpu().numpy()
+    m.set_option(N.FR_OPT_STAGE, 2)
+    b = m.embed(x).cpu().numpy()
+    m.close()
+    assert np.all(1 - (a * b).sum(1) <= 3e-4)
 
 
 def test_stage_absent_for_other_archs(gpu):

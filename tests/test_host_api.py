@@ -99,12 +99,62 @@ def test_result_threshold_and_names():
     assert eng._result_faiss(np.array([-np.inf]), np.array([-1])) == ("Unknown", 0.0, [])
 
 
-def test_probe_preparation_matches_cosine_branches():
-    E = np.stack([np.full(4, 0.5, np.float32), np.full(4, 2.0, np.float32), np.zeros(4, np.float32)])
-    P = RE.RecognitionEngine._as_probes(E)
-    assert np.array_equal(P[0], E[0])            # already unit: untouched (dot branch)
-    assert np.allclose(np.linalg.norm(P[1]), 1)  # rescaled (dot / |a||b| branch)
-    assert not P[2].any()                        # zero stays zero (score 0.0 branch)
+def mixed_norm_case():
+    """A db and probes that exercise every cosine_similarity branch (recognition_engine.py:41-63),
+    including a near-tie that flips if a unit-ish probe (|p| = 1.0009) is rescaled against a raw
+    unit-ish row or left unscaled against a normalized non-unit row."""
+    D = 8
+    e = np.eye(D, dtype=np.float32)
+    c_a = 0.8
+    c_b = c_a * 1.0009 * (1 - 5e-4)  # reference: A (0.80072) beats B (0.80032); wrong rule: B (0.80104) wins
+    A = c_a * e[0] + np.sqrt(1 - c_a ** 2) * e[1]
+    B = 2.0 * (c_b * e[0] + np.sqrt(1 - c_b ** 2) * e[2])
+    rng = np.random.default_rng(4)
+    db = {"A": A, "B": B, "zero": np.zeros(D, np.float32), "near": 1.0005 * e[3], "big": 3.0 * e[4]}
+    for j in range(12):
+        v = np.zeros(D, np.float32)
+        v[5:] = rng.standard_normal(D - 5)
+        v[0] = 0.3 * rng.standard_normal()
+        db[f"r{j}"] = v / np.linalg.norm(v) * (1.0 if j % 3 else 2.5)
+    probes = [1.0009 * e[0], e[0], 2.0 * e[0], np.zeros(D, np.float32), 1.0005 * e[3] + 0.01 * e[4],
+              rng.standard_normal(D).astype(np.float32)]
+    return {k: np.asarray(v, np.float32) for k, v in db.items()}, [np.asarray(p, np.float32) for p in probes]
+
+
+class _NumpyGallery:
+    """Stand-in for DeviceGallery on the CPU (host-logic test only): fr_gallery_set's row preparation
+    (rows off unit norm by >= 1e-3 are normalized, zero rows stay zero) + exact top-k."""
+
+    def __init__(self, rows, dim=512, device=0):
+        import torch
+        r = np.asarray(rows, np.float32).reshape(-1, dim).copy()
+        n = np.linalg.norm(r, axis=1)
+        fix = (np.abs(n - 1) >= 1e-3) & (n > 0)
+        r[fix] /= n[fix, None]
+        self.rows, self.device = r, torch.device("cpu")
+
+    @property
+    def ntotal(self):
+        return len(self.rows)
+
+    def search_device(self, P, k):
+        import torch
+        s, i = OMT.topk_dot(P.numpy(), self.rows, k)
+        return torch.from_numpy(s), torch.from_numpy(i.astype(np.int32))
+
+
+def test_recognize_with_db_mixed_norm_semantics(monkeypatch):
+    from facerecognition_amd import gallery
+    monkeypatch.setattr(gallery, "DeviceGallery", _NumpyGallery)
+    db, probes = mixed_norm_case()
+    eng = RE.RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.0)
+    eng.db = db
+    for p in probes:
+        name, score, top = eng.recognize_with_db(p)
+        rname, rscore, rtop = OMT.recognize_with_db(p, db, 0.0)
+        assert name == rname and [t[0] for t in top] == [t[0] for t in rtop]
+        assert np.allclose([t[1] for t in top], [t[1] for t in rtop], atol=1e-6)
+    assert eng.recognize_with_db(probes[0])[0] == "A"  # the near-tie resolves as the reference does
 
 
 def test_extract_batch_empty_and_bad_paths():
