@@ -76,11 +76,13 @@ static inline float host_bf2f(bf16_t v) {
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-// Pack two floats into two bf16 (RNE; hipcc lowers the cast to v_cvt_pk_bf16_f32 on gfx950).
+// Pack two floats into two bf16 (RNE): one v_cvt_pk_bf16_f32 on gfx950 (two scalar casts can come out
+// as two converts plus shifts and ors).
 __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
-    __bf16 x = (__bf16)a, y = (__bf16)b;
-    uint16_t xs = __builtin_bit_cast(uint16_t, x), ys = __builtin_bit_cast(uint16_t, y);
-    return (uint32_t)xs | ((uint32_t)ys << 16);
+    typedef float f32x2_v __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+    const f32x2_v v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_v));
 }
 
 __device__ __forceinline__ void unpack8_bf16(const uint4& v, float* f) {

@@ -56,6 +56,16 @@ constexpr uint32_t OOB = 0x80000000u;
 #ifndef FR_STAGE_SCHED
 #define FR_STAGE_SCHED 0  // explicit MFMA / ds_read / DMA interleave (sched_group_barrier)
 #endif
+#ifndef FR_STAGE_EXP
+#define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 1 no weight DMA in the loop, 2 no
+                        // mid-step barrier / vmcnt wait, 4 no epilogue (MFMAs dead-code eliminated too),
+                        // 8 trivial epilogue (MFMAs kept), 16 no patch reads in the loop, 32 no weight
+                        // fragment reads in the loop
+#endif
+#ifndef FR_STAGE_SB
+#define FR_STAGE_SB 1  // scheduling barrier at each K-step start: MFMAs of step s+1 cannot be hoisted
+                       // next to the refill reads of their weight fragments (exposed LDS latency)
+#endif
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -132,11 +142,57 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
     // one K-step: MFMAs on (wf, cur); nxt <- patch fragments of (cg_n, tap_n) when has_next; mid-step
     // barrier; DMA of global step g+3 into this step's slot; wf <- slice of step g+1 in place.  The
     // slot of step s is s % 3 = tap % 3 (9 and 72 are multiples of 3): compile-time after unrolling.
+#if FR_STAGE_SB == 2
+    // explicit software pipeline: the whole next slice is read into registers right after the barrier
+    // (half a step before its first use), the DMA pieces and those reads interleaved with the MFMAs
+    auto kstep = [&](int g, int slot, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
+        __builtin_amdgcn_sched_barrier(0);
+        pread(nxt, cg_n, tap_n);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(7)\n\ts_barrier" ::: "memory");
+        issue_w(g + 3 < total ? g + 3 : total - 1, slot);
+        const int nslot = slot == NSLOT - 1 ? 0 : slot + 1;
+        frag wn[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wn[i] = *(const frag*)(smem + boff + nslot * SLICE_B + i * 256);
+#pragma unroll
+        for (int i = 4; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wf[i] = wn[i];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    };
+#else
     auto kstep = [&](int g, int slot, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
 #if FR_STAGE_FENCE
         asm volatile("" ::: "memory");  // the previous step's refills stay ahead of this step's reads
 #endif
+#if FR_STAGE_SB
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+#if !(FR_STAGE_EXP & 16)
         pread(nxt, cg_n, tap_n);  // (after a conv's last step: unused reads, no branch)
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -151,7 +207,9 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
 #endif
         // slice g+1 landed (this wave); the 4 pieces of slice g+2 may stay in flight.  Branch-free: the
         // tail re-fetches the last slice into the free slot and reads clamped slots (static counts)
-#if FR_STAGE_LGKM7
+#if FR_STAGE_EXP & 2
+        asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+#elif FR_STAGE_LGKM7
         // the 7 youngest LDS reads are this step's pread(nxt) (untouched by the DMA below: +4.5 % on the
         // stage); the older wf refills from slot `slot` must be done before anyone overwrites it
         // (checked in the ISA: the compiler waits for every earlier read before its MFMA use)
@@ -159,15 +217,21 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
 #else
         asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #endif
+#if !(FR_STAGE_EXP & 1)
         issue_w(g + 3 < total ? g + 3 : total - 1, slot);
+#endif
         const int nslot = slot == NSLOT - 1 ? 0 : slot + 1;
+#if !(FR_STAGE_EXP & 32)
 #pragma unroll
         for (int i = 0; i < 4; ++i) wread(i, nslot);
+#endif
 #pragma unroll
         for (int i = 4; i < 8; ++i) {
 #pragma unroll
             for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
+#if !(FR_STAGE_EXP & 32)
             wread(i, nslot);
+#endif
         }
 #if FR_STAGE_SCHED
         // second half: refills of wf[0..3] and the 4 DMA pieces spread over the first 8 MFMAs, then
@@ -188,16 +252,46 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
 #endif
     };
+#endif
 
     const size_t img = (size_t)b * SPIX * SC;
+    // Epilogue tables (built at load time): ep[cv][9][256] = the conv's bias for each border class of the
+    // output pixel (bias9 of the folded pre-conv BN, or the plain bias in all 9 rows); slope[cv][256] =
+    // the activation's negative-side factor.  A lane's 4 channels n..n+3 of fragment i and its output
+    // column class are fixed, and its output row is interior except for fragment j = 0 of wave row 0
+    // (image row 0) and j = 6 of wave row 1 (image row 13): two float4 per fragment cover every case.
+    // The loads go through an opaque lane copy so that their ~50 addresses are not hoisted out of the K
+    // loop (LICM would keep them live across it and spill).
+    auto load_ep = [&](int cv, float4 (&bi)[8], float4 (&be)[8]) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int cc = ln & 15, ccls = cc == 0 ? 0 : (cc == SW - 1 ? 2 : 1);
+        const float* ep = p.ep + (size_t)cv * 9 * SC;
+        const float* epi = ep + (3 + ccls) * SC;              // interior rows
+        const float* epe = ep + (wm ? 6 + ccls : ccls) * SC;  // this wave's border row (0 or 13)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int n = wn * 128 + 16 * i + 4 * (ln >> 4);
+            bi[i] = *(const float4*)(epi + n);
+            be[i] = *(const float4*)(epe + n);
+        }
+    };
+    auto is_edge = [&](int j) { return (j == 0 && wm == 0) || (j == 6 && wm == 1); };
+    auto seed_bias = [&](int cv) {
+        float4 bi[8], be[8];
+        load_ep(cv, bi, be);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const float4 bb = is_edge(j) ? be[i] : bi[i];
+                acc[i][j] = (f32x4_t){bb.x, bb.y, bb.z, bb.w};
+            }
+    };
     auto run_conv = [&](int cv, auto second_tag) {
         constexpr bool second = decltype(second_tag)::value;
-        const StageConv c = p.conv[cv];
-        if (!second) {  // conv2 starts from the identity seeded by conv1's epilogue
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 7; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        if (!second) {  // conv1 starts from its bias (conv2 from x + its bias, seeded by conv1's epilogue)
+            seed_bias(cv);
         }
         pread(pA, 0, 0);
 #pragma unroll
@@ -215,63 +309,87 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
             }
         }
         // ---- epilogue: every wave is past its last patch read before the patch is overwritten.
-        // conv1: t = PReLU(acc + bias9) -> patch; the lane first reads x (the same positions and
-        //        channels it is about to overwrite -- no other lane touches them) and seeds its
-        //        accumulators with it, so conv2 accumulates onto the identity: x' = (x + conv2(t)) + b.
-        // conv2: x' -> patch (and NHWC global for the last block / intermediates).
-        // No global loads or stores between the stage's first patch load and its last block.
-        // (opaque lane copy: keeps the ~100 per-(i,j) addresses from being hoisted and spilled)
+        // The accumulators already hold the bias (seeded at conv1's start / by conv1's epilogue), so
+        // conv1: t = PReLU(acc) -> patch; the lane first reads x (the same positions and channels it is
+        //        about to overwrite -- no other lane touches them) and seeds conv2's accumulators with
+        //        x + conv2's bias, so conv2 accumulates onto the identity: x' = x + b2 + conv2(t);
+        // conv2: x' -> patch (and NHWC global for the last block / intermediates), no arithmetic.
+        // (build_stage checks that every conv1 is PReLU and every conv2 has no activation.)
+        // No global loads or stores between the stage's first patch load and its last block besides the
+        // small epilogue tables.  The barrier only needs every wave's patch reads drained (the weight
+        // DMAs in flight land in the ring slots, not in the patch, so they stay in flight).
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#if FR_STAGE_EXP & 8
+        {
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 7; ++j) sum += acc[i][j][0] + acc[i][j][3];
+            if (sum == 1.2345f) p.y[lane] = 0;
+            if (!second) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int j = 0; j < 7; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+            }
+        }
+#else
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        __syncthreads();
+        const int cc = ln & 15;
+        const bool okc = cc < SW;
+        bf16_t* dbg = nullptr;
+        if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
+        const bool store_y = second && cv == nconv - 1;
+        float4 sl[8], bi[8], be[8];
+        if (!second) {
+            load_ep(cv + 1, bi, be);  // conv2's bias: part of its accumulator seed
+            const float* slp = p.slope + (size_t)cv * SC;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sl[i] = *(const float4*)(slp + wn * 128 + 16 * i + 4 * (ln >> 4));
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_barrier(0);
             const int n = wn * 128 + 16 * i + 4 * (ln >> 4);
-            float4 sl = make_float4(0.f, 0.f, 0.f, 0.f), bb = sl;
-            if (c.slope) sl = *(const float4*)(c.slope + n);
-            if (c.bias) bb = *(const float4*)(c.bias + n);
+            char* slot0 = smem + (n >> 3) * PLANE_B + (wm * 112 + cc + 1) * 16 + (n & 7) * 2;
+            // conv1: all 7 identity reads of this n-fragment first (one LDS latency per fragment)
+            uint2 xin[7];
+            if (!second) {
+#pragma unroll
+                for (int j = 0; j < 7; ++j) xin[j] = okc ? *(const uint2*)(slot0 + j * 256) : make_uint2(0u, 0u);
+            }
 #pragma unroll
             for (int j = 0; j < 7; ++j) {
-                const int m = wm * 112 + 16 * j + (ln & 15), r = m >> 4, cc = m & 15;
-                const bool ok = r < SW && cc < SW;
-                char* slot = smem + (n >> 3) * PLANE_B + (m + 1) * 16 + (n & 7) * 2;
-                uint2 xin = make_uint2(0u, 0u);
-                if (!second && ok) xin = *(const uint2*)slot;
-                float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
-                if (c.bias9) {
-                    const float4 b9 = *(const float4*)(c.bias9 + border_class(r, cc, SW, SW) * SC + n);
-                    v[0] += b9.x; v[1] += b9.y; v[2] += b9.z; v[3] += b9.w;
-                }
-                if (c.act == 2) {
-                    v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
-                    v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
-                    v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
-                    v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
-                } else if (c.act == 1) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                char* slot = slot0 + j * 256;  // position m + 1 = wm*112 + 16j + cc + 1
+                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                if (!second) {  // PReLU: max(v, 0) + s * min(v, 0)
+                    v[0] = fmaf(sl[i].x, fminf(v[0], 0.f), fmaxf(v[0], 0.f));
+                    v[1] = fmaf(sl[i].y, fminf(v[1], 0.f), fmaxf(v[1], 0.f));
+                    v[2] = fmaf(sl[i].z, fminf(v[2], 0.f), fmaxf(v[2], 0.f));
+                    v[3] = fmaf(sl[i].w, fminf(v[3], 0.f), fmaxf(v[3], 0.f));
                 }
                 float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
                 const uint4 pk = T::pack8(o8);
                 const uint2 pk2 = make_uint2(pk.x, pk.y);
                 if (!second) {
                     float f[8];
-                    T::unpack8(make_uint4(xin.x, xin.y, 0, 0), f);
-                    acc[i][j] = (f32x4_t){f[0], f[1], f[2], f[3]};
+                    T::unpack8(make_uint4(xin[j].x, xin[j].y, 0, 0), f);
+                    const float4 bb = is_edge(j) ? be[i] : bi[i];
+                    acc[i][j] = (f32x4_t){f[0] + bb.x, f[1] + bb.y, f[2] + bb.z, f[3] + bb.w};
                 }
-                if (ok) {
+                if (okc) {
                     *(uint2*)slot = pk2;
+                    const int r = wm * 7 + j;
                     const size_t go = img + (size_t)(r * SW + cc) * SC + n;
-                    if (second && cv == nconv - 1) *(uint2*)(p.y + go) = pk2;
-                    if (p.dbg_x) {
-                        bf16_t* dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
-                        if (dbg) *(uint2*)(dbg + go) = pk2;
-                    }
+                    if (store_y) *(uint2*)(p.y + go) = pk2;
+                    if (dbg) *(uint2*)(dbg + go) = pk2;
                 }
             }
         }
-        __syncthreads();  // the new activation is visible to every wave before the next conv reads it
+#endif
+        // the new activation is visible to every wave before the next conv reads it (LDS writes only)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
 #pragma unroll 1
     for (int blk = 0; blk < p.nblk; ++blk) {

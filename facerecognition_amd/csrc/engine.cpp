@@ -78,6 +78,8 @@ struct StageRec {
     std::vector<int> t_tensors, x_tensors;  // per block: conv1 output, block output
     bf16_t* w = nullptr;                  // packed K-step weight images
     StageConv* table = nullptr;           // [2*nblk]
+    float* ep = nullptr;                  // [2*nblk][9][256] epilogue bias per border class
+    float* slope = nullptr;               // [2*nblk][256] negative-side factor (slope / 0 / 1)
     bf16_t** dbg = nullptr;               // [2*nblk] device pointer table: x outputs then t outputs
 };
 
@@ -475,12 +477,18 @@ int build_stage(fr_handle* h, StageRec& r) {
     const int nconv = 2 * r.nblk;
     std::vector<bf16_t> packed(stage_weight_bytes(nconv) / sizeof(bf16_t));
     std::vector<StageConv> tab(nconv);
+    std::vector<float> ep((size_t)nconv * 9 * 256, 0.f), sl((size_t)nconv * 256, 0.f);
     const size_t per = packed.size() / nconv;
     for (int c = 0; c < nconv; ++c) {
         const Op& op = h->ops[r.conv_ops[c]];
         const DevConvW& cw = h->convw[op.wi];
         if (cw.Cout != 256 || cw.Npad != 256 || cw.Kh != 3 || cw.Kw != 3 || cw.Cin != 256) {
             set_error("plan: stage member conv is not 3x3 256->256");
+            return FR_ERR_ARG;
+        }
+        // the stage kernel's epilogues are specialised: conv1 = bias + PReLU, conv2 = bias + identity
+        if ((c % 2 == 0 && (op.act != 2 || !cw.slope)) || (c % 2 == 1 && (op.act != 0 || op.res < 0))) {
+            set_error("plan: stage member conv has an unexpected activation / residual");
             return FR_ERR_ARG;
         }
         std::vector<bf16_t> rows((size_t)cw.Npad * cw.Kpad);
@@ -490,11 +498,27 @@ int build_stage(fr_handle* h, StageRec& r) {
         tab[c].bias9 = cw.bias9;
         tab[c].slope = cw.slope;
         tab[c].act = op.act;
+        // the epilogue's per-class bias: bias9 (which already carries the whole bias) or bias x 9
+        float* e = ep.data() + (size_t)c * 9 * 256;
+        if (cw.bias9) {
+            FR_HIP_CHECK(hipMemcpy(e, cw.bias9, 9 * 256 * sizeof(float), hipMemcpyDeviceToHost));
+        } else if (cw.bias) {
+            FR_HIP_CHECK(hipMemcpy(e, cw.bias, 256 * sizeof(float), hipMemcpyDeviceToHost));
+            for (int k = 1; k < 9; ++k) std::copy(e, e + 256, e + k * 256);
+        }
+        // negative-side factor of the activation: PReLU slope, 0 for ReLU, 1 for none
+        float* f = sl.data() + (size_t)c * 256;
+        if (op.act == 2 && cw.slope)
+            FR_HIP_CHECK(hipMemcpy(f, cw.slope, 256 * sizeof(float), hipMemcpyDeviceToHost));
+        else
+            std::fill(f, f + 256, op.act == 1 ? 0.f : 1.f);
     }
     int rc = upload(h, &r.w, packed);
     if (rc) return rc;
     rc = upload(h, &r.table, tab);
     if (rc) return rc;
+    if ((rc = upload(h, &r.ep, ep))) return rc;
+    if ((rc = upload(h, &r.slope, sl))) return rc;
     void* d = nullptr;
     if ((rc = dev_alloc(&d, (size_t)nconv * sizeof(bf16_t*)))) return rc;
     h->weight_allocs.push_back(d);
@@ -1008,6 +1032,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.y = h->tensors[r.out].dev;
                 a.w = r.w;
                 a.conv = r.table;
+                a.ep = r.ep;
+                a.slope = r.slope;
                 if (h->keep_inter) { a.dbg_x = r.dbg; a.dbg_t = r.dbg + r.nblk; }
                 a.B = B;
                 a.nblk = r.nblk;

@@ -78,6 +78,8 @@ struct StageArgs {
     bf16_t* y;                 // stage output [B][14][14][256] (written by the last block)
     const bf16_t* w;           // packed K-step images of all convs (stage_pack_weights)
     const StageConv* conv;     // [2*nblk] device table
+    const float* ep;           // [2*nblk][9][256] epilogue bias per border class (bias9, or bias broadcast)
+    const float* slope;        // [2*nblk][256] negative-side factor: PReLU slope, 0 (ReLU) or 1 (none)
     bf16_t* const* dbg_x;      // optional [nblk] per-block outputs / [nblk] conv1 outputs (device
     bf16_t* const* dbg_t;      //   pointer tables; null = do not materialise intermediates)
     int B, nblk, f16, dbg;     // dbg: timing-only experiment switches (FR_STAGE_DBG), 0 in production
