@@ -162,11 +162,35 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
     const int pbase = (lane >> 4) * PLANE_B + (16 * FM * wm + (lane & 15)) * 16;
     const int woff = (lane >> 4) * (IC * 16) + (16 * FN * wn + (lane & 15)) * 16;
 
+    // accumulator seeds, loaded while the prologue DMA is in flight: the bias (B9: of the output pixel's
+    // border class) plus (RES) the residual, so the epilogue only applies the activation and stores.
+    // Pad columns read a valid pixel (their results are never stored).
+    const size_t img = (size_t)b * IW * IW;
     f32x4_t acc[FN][FM];
+    {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));  // opaque copy: the seed addresses are not kept live in the loop
 #pragma unroll
-    for (int i = 0; i < FN; ++i)
+        for (int i = 0; i < FN; ++i) {
+            const int n = 16 * FN * wn + 16 * i + 4 * (ln >> 4);
+            float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!B9 && p.bias) bb = *(const float4*)(p.bias + n);
 #pragma unroll
-        for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < FM; ++j) {
+                const int f = FM * wm + j, v = 16 * f + (ln & 15), c = v % PC, r = r0 + v / PC;
+                const int cc = c < IW ? c : 0;
+                float4 s = bb;
+                if (B9) s = *(const float4*)(p.bias9 + border_class(r, c, IW, IW) * p.Npad + n);
+                if (RES) {
+                    const uint2 rr = *(const uint2*)(p.res + (img + r * IW + cc) * p.Cres + p.res_off + n);
+                    float f8[8];
+                    T::unpack8(make_uint4(rr.x, rr.y, 0, 0), f8);
+                    s.x += f8[0]; s.y += f8[1]; s.z += f8[2]; s.w += f8[3];
+                }
+                acc[i][j] = (f32x4_t){s.x, s.y, s.z, s.w};
+            }
+        }
+    }
     frag wf[FN], pA[FM], pB[FM];
     auto pread = [&](frag (&pf)[FM], int buf, int tap) {
         const int dh = tap / 3, dw = tap % 3;
@@ -230,56 +254,28 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
         kstep(s + 1, pB, pA);
     }
 
-    // ---- epilogue: straight from the accumulators (no LDS), 8 B per lane and (i, j).  Per channel
-    // group i the residual / bias9 loads issue together (pad columns read a valid pixel and skip only
-    // the store).  The other workgroup on the CU computes meanwhile.
-    const size_t img = (size_t)b * IW * IW;
+    // ---- epilogue: straight from the accumulators (no LDS), 8 B per lane and (i, j).  Bias and
+    // residual are already in the accumulators; the activation is v > 0 ? v : v * negf (negf = PReLU
+    // slope, 0 for ReLU, 1 for none: one branch-free form, its 4 loads issued together).
     int ln = lane;
     asm volatile("" : "+v"(ln));  // opaque copy: keeps the per-(i, j) addresses from being hoisted
+    float4 nf[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) nf[i] = *(const float4*)(p.negf + 16 * FN * wn + 16 * i + 4 * (ln >> 4));
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
         const int n = 16 * FN * wn + 16 * i + 4 * (ln >> 4);
-        float4 sl = make_float4(0.f, 0.f, 0.f, 0.f), bb = sl;
-        if (p.act == 2) sl = *(const float4*)(p.slope + n);
-        if (!B9 && p.bias) bb = *(const float4*)(p.bias + n);
-        size_t m[FM];
-        int cls[FM];
-        bool ok[FM];
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
             const int f = FM * wm + j, v = 16 * f + (ln & 15), c = v % PC, r = r0 + v / PC;
-            ok[j] = c < IW;
-            m[j] = img + r * IW + (ok[j] ? c : 0);
-            cls[j] = border_class(r, c, IW, IW);
-        }
-        uint2 rr[FM];
-        float4 b9[FM];
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-            if (RES) rr[j] = *(const uint2*)(p.res + m[j] * p.Cres + p.res_off + n);
-            if (B9) b9[j] = *(const float4*)(p.bias9 + cls[j] * p.Npad + n);
-        }
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-            float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
-            if (B9) { v[0] += b9[j].x; v[1] += b9[j].y; v[2] += b9[j].z; v[3] += b9[j].w; }
-            if (RES) {
-                float f8[8];
-                T::unpack8(make_uint4(rr[j].x, rr[j].y, 0, 0), f8);
-                v[0] += f8[0]; v[1] += f8[1]; v[2] += f8[2]; v[3] += f8[3];
-            }
-            if (p.act == 2) {
-                v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
-                v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
-                v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
-                v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
-            } else if (p.act == 1) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-            }
-            float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            o[0] = fmaf(nf[i].x, fminf(o[0], 0.f), fmaxf(o[0], 0.f));
+            o[1] = fmaf(nf[i].y, fminf(o[1], 0.f), fmaxf(o[1], 0.f));
+            o[2] = fmaf(nf[i].z, fminf(o[2], 0.f), fmaxf(o[2], 0.f));
+            o[3] = fmaf(nf[i].w, fminf(o[3], 0.f), fmaxf(o[3], 0.f));
+            float o8[8] = {o[0], o[1], o[2], o[3], 0, 0, 0, 0};
             const uint4 pk = T::pack8(o8);
-            if (ok[j]) *(uint2*)(p.y + m[j] * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
+            if (c < IW) *(uint2*)(p.y + (img + r * IW + c) * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs land before the LDS is released
@@ -292,7 +288,8 @@ bool img_supported_t(const ConvArgs& a) {
            a.Ho == IW && a.Wo == IW && a.Cin == IC && a.Cout == IC && a.Npad >= IC && a.Kpad >= 9 * IC &&
            a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.x_off + IC <= a.Cx && a.Cy % 4 == 0 && a.y_off % 4 == 0 &&
            a.y_off + IC <= a.Cy && !a.y2 && !a.partial && !a.w8 && !a.y_amax && a.B > 0 && !a.f16 &&
-           !(a.res && a.bias9) && (!a.res || (a.Cres % 4 == 0 && a.res_off % 4 == 0 && a.res_off + IC <= a.Cres));
+           !(a.res && a.bias9) && (!a.res || (a.Cres % 4 == 0 && a.res_off % 4 == 0 && a.res_off + IC <= a.Cres)) &&
+           a.negf;
 }
 
 template <typename G>
@@ -327,6 +324,7 @@ __global__ __launch_bounds__(256) void img_pack_kernel(const bf16_t* __restrict_
 bool img_shape_ok(const ConvArgs& a, int* ic) {
     ConvArgs t = a;
     t.wimg = (const bf16_t*)1;
+    t.negf = (const float*)1;
     if (img_supported_t<Geo28>(t)) { *ic = 128; return true; }
     if (img_supported_t<Geo56>(t)) { *ic = 64; return true; }
     return false;

@@ -44,6 +44,7 @@ struct DevConvW {
     float* aff_b = nullptr;
     float* bias9 = nullptr;  // [9][Npad] border-class bias (input BN folded into a 3x3/s1/p1 conv)
     bf16_t* wimg = nullptr;  // conv_img.hip K-step slice images (convs its kernels apply to)
+    float* negf = nullptr;   // conv_img.hip: [Npad] activation negative-side factor (slope / 0 / 1)
     uint8_t* w8 = nullptr;   // FR_DTYPE_FP8: e4m3 [Npad][Kpad8] + per-channel scale
     float* wscale = nullptr;
     int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0, Kpad8 = 0;
@@ -624,6 +625,10 @@ int build_img_weights(fr_handle* h) {
         h->weight_allocs.push_back(p);
         FR_HIP_CHECK(img_pack_weights(cw.w, cw.Kpad, ic, (bf16_t*)p, nullptr));
         cw.wimg = (bf16_t*)p;
+        std::vector<float> nf(cw.Npad, op.act == 1 ? 0.f : 1.f);
+        if (op.act == 2 && cw.slope)
+            FR_HIP_CHECK(hipMemcpy(nf.data(), cw.slope, cw.Cout * sizeof(float), hipMemcpyDeviceToHost));
+        if ((rc = upload(h, &cw.negf, nf))) return rc;
     }
     FR_HIP_CHECK(hipDeviceSynchronize());
     return FR_OK;
@@ -1080,6 +1085,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.K = cw.K; a.Kpad = cw.Kpad;
                 a.Ho = to.H; a.Wo = to.W; a.M = B * to.H * to.W; a.Cout = cw.Cout; a.Npad = cw.Npad;
                 a.bias = cw.bias; a.slope = cw.slope; a.act = op.act; a.bias9 = cw.bias9; a.wimg = cw.wimg;
+                a.negf = cw.negf;
                 if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
                 a.y = to.dev; a.Cy = to.C; a.y_off = op.out_off;
                 if (op.out2 >= 0) {
@@ -1675,8 +1681,22 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         FR_HIP_CHECK(hipMallocAsync(&tmp, img_packed_elems(ic) * sizeof(bf16_t), st));
         FR_HIP_CHECK(img_pack_weights(a.w, a.Kpad, ic, (bf16_t*)tmp, st));
         a.wimg = (const bf16_t*)tmp;
+        // activation negative-side factor: the PReLU slopes, 0 (ReLU) or 1 (none)
+        void* nf = nullptr;
+        FR_HIP_CHECK(hipMallocAsync(&nf, (size_t)a.Npad * sizeof(float), st));
+        if (a.act == 2) {
+            FR_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)nf, 0, a.Npad, st));
+            FR_HIP_CHECK(hipMemcpyAsync(nf, a.slope, (size_t)a.Cout * sizeof(float), hipMemcpyDeviceToDevice, st));
+        } else {
+            const float one = a.act == 1 ? 0.f : 1.f;
+            uint32_t bits;
+            std::memcpy(&bits, &one, 4);
+            FR_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)nf, (int)bits, a.Npad, st));
+        }
+        a.negf = (const float*)nf;
         FR_HIP_CHECK(w28 ? launch_conv_img28(a, st) : launch_conv_img56(a, st));
         FR_HIP_CHECK(hipFreeAsync(tmp, st));
+        FR_HIP_CHECK(hipFreeAsync(nf, st));
         return FR_OK;
     }
     if (d->tile > 0) {

@@ -35,6 +35,7 @@ struct ConvArgs {
     float* y_amax;                // non-null: the epilogue atomically records max |y| (both dtypes)
     int amax_slots;               // x_amax / y_amax are arrays of this many partial maxima (block % slots)
     const bf16_t* wimg;           // conv_img.hip: weights pre-packed as K-step slice images (img_pack_weights)
+    const float* negf;            // conv_img.hip: [Npad] activation negative-side factor (slope / 0 / 1)
 };
 constexpr int FR_AMAX_SLOTS = 64;  // engine: spreads the producers' atomics over 64 addresses
 

@@ -32,13 +32,18 @@ def analyse(trace, plan_path):
     plan = [l.split() for l in open(plan_path).read().splitlines() if l.strip()]
     rows = list(csv.DictReader(open(trace)))
     ours = [r for r in rows if "fr::" in r["Kernel_Name"]]
-    starts = [i for i, r in enumerate(ours) if "preprocess" in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(ours) if "preprocess" in r["Kernel_Name"] or "stem_u8" in r["Kernel_Name"]]
     seq = ours[starts[-1]:]
     i = 0
+    fused_stem = "stem_u8" in seq[0]["Kernel_Name"]
+    skip_next_conv = False
     tot_ns = tot_flop = 0
     agg = {}
     print(f"{'layer':34s} {'M':>8s} {'N':>5s} {'K':>5s} tile split {'us':>8s} {'TF/s':>7s}")
     for p in plan:
+        if p[0] == "pre" and fused_stem:  # one dispatch = preprocess + the stem conv
+            skip_next_conv = True
+            continue
         if p[0] in ("pre", "maxpool", "avgpool"):
             r = seq[i]; i += 1
             d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
@@ -46,13 +51,16 @@ def analyse(trace, plan_path):
             print(f"{p[0]:34s} {'':>8s} {'':>5s} {'':>5s}           {d / 1e3:8.1f}")
             continue
         M, Nn, K, Kpad, tile, split = map(int, p[1:7])
+        if skip_next_conv:
+            p = ["stem", M, Nn, K, Kpad, tile, split, "stem(u8 fused)"]
+            skip_next_conv = False
         d = 0
         r = seq[i]; i += 1
         d += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         if split > 1 or p[0] == "head":
             r = seq[i]; i += 1  # split-K epilogue / head finalize
             d += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        flop = 2.0 * M * Nn * K
+        flop = 2.0 * M * Nn * K * (tile if p[0] == "stage" else 1)  # stage line: tile = its conv count
         tot_ns += d
         tot_flop += flop
         key = (M, Nn, K, p[7])
