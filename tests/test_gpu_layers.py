@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 REL_TOL = 0.08  # per-stage relative L2 error bound (bf16 storage of every activation)
 
 
-def stage_report(arch, B=2, seed=0):
+def stage_report(arch, B=2, seed=0, dtype=None):
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.weights import INPUT_SIZE, synth_state_dict
     from oracle import models as M
@@ -24,7 +24,7 @@ def stage_report(arch, B=2, seed=0):
     from facerecognition_amd.synthetic import synthetic_crops
     u8 = synthetic_crops(B, INPUT_SIZE[arch], seed=seed)
     sd = synth_state_dict(arch)
-    m = FRModel(arch, sd)
+    m = FRModel(arch, sd, dtype=dtype)
     m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)  # the layer3 stage kernel materialises its blocks too
     dt = torch.float16 if m.dtype == "f16" else torch.bfloat16
     m.embed(torch.from_numpy(u8))

@@ -34,8 +34,8 @@ def _oracle_embed(arch, u8):
     return _cache[key]
 
 
-# (arch, dtype): every backbone at the 1e-3 bar in its default dtype, plus f16 for all.
-# bf16 InceptionResnetV1 is measured (test_irv1_bf16_drift_report) — DESIGN.md §5.
+# (arch, dtype): IResNet100 / ResNet-50 at the 1e-3 bar in bf16 and f16, InceptionResnetV1 in f16;
+# bf16 InceptionResnetV1 (its default) is test_irv1_bf16_parity (xfail) — DESIGN.md §5.
 CASES = [("iresnet100", "bf16"), ("resnet50_arcface", "bf16"), ("irv1_facenet", "f16"),
          ("iresnet100", "f16"), ("resnet50_arcface", "f16")]
 
@@ -109,18 +109,51 @@ def test_top1_planted_gallery(arch_model):
     assert np.array_equal(ri[:, 0], np.arange(6))
 
 
-def test_irv1_bf16_drift_report(gpu):
-    """bf16 InceptionResnetV1 on the synthetic weights: the stem's rounding is amplified by the
-    random network to ~2e-3 cosine (CPU bf16 emulation of the oracle gives the same number), so
-    its bar here is 5e-3; the f16 path meets 1e-3 (CASES above)."""
+@pytest.mark.xfail(reason="bf16 InceptionResnetV1 misses the 1e-3 bar on the synthetic weights (~2e-3: "
+                          "bf16 rounding of the stem layers, amplified by the calibrated last_bn; f16 meets it, "
+                          "test_embedding_cosine[irv1_facenet-f16]); DESIGN.md §5", strict=False)
+def test_irv1_bf16_parity(gpu):
+    """BASELINE config 3's dtype (bf16) at the north-star bar, 1e-3 cosine vs the fp32 oracle.  Known to
+    fail (xfail) on the synthetic weights; the measured 1-cos is printed."""
     from facerecognition_amd.model import FRModel
     m = FRModel.synthetic("irv1_facenet", dtype="bf16")
     u8 = _probes("irv1_facenet", 6)
     ref = _oracle_embed("irv1_facenet", u8)
     got = m.embed(torch.from_numpy(u8)).cpu().numpy()
+    m.close()
     cos = np.sum(got * ref, axis=1)
     print("irv1 bf16 1-cos", 1 - cos)
-    assert np.all(1 - cos <= 5e-3)
+    assert np.all(1 - cos <= COS_TOL), f"irv1 bf16: 1-cos = {1 - cos}"
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_irv1_full_batch_bs256(gpu, dtype):
+    """BASELINE config-3 size (InceptionResnetV1 @160, bs = 256): deterministic replay, finite unit-norm
+    rows, batch independence against a 5-face call, an oracle sample (f16: the 1e-3 bar; bf16: its
+    measured ~2e-3 level, 3e-3, see test_irv1_bf16_parity), and identical top-1 against the oracle's
+    ranking on a planted 10k gallery."""
+    from facerecognition_amd.gallery import DeviceGallery
+    from facerecognition_amd.model import FRModel
+    m = FRModel.synthetic("irv1_facenet", dtype=dtype)
+    u8 = torch.from_numpy(_probes("irv1_facenet", 256, seed=31))
+    a = m.embed(u8).cpu()
+    b = m.embed(u8).cpu()
+    assert torch.equal(a, b), "forward is not deterministic at bs=256"
+    assert torch.isfinite(a).all() and torch.allclose(a.norm(dim=1), torch.ones(256), atol=1e-5)
+    small = m.embed(u8[60:65]).cpu()
+    assert float((1 - (a[60:65] * small).sum(1)).max()) <= COS_TOL
+    ref = _oracle_embed("irv1_facenet", u8[:4].numpy())
+    cos_o = (a[:4].numpy() * ref).sum(1) / np.linalg.norm(ref, axis=1)
+    assert float((1 - cos_o).max()) <= (COS_TOL if dtype == "f16" else 3e-3), 1 - cos_o
+    rng = np.random.default_rng(32)
+    G = rng.standard_normal((10000, 512)).astype(np.float32)
+    perm = rng.permutation(10000)[:256]
+    G[perm] = a.numpy() + 0.03 * rng.standard_normal((256, 512)).astype(np.float32)
+    G /= np.linalg.norm(G, axis=1, keepdims=True)
+    gal = DeviceGallery(G)
+    _, idx = gal.search(a.numpy(), 5)
+    assert np.array_equal(idx[:, 0], perm)
+    gal.close()
     m.close()
 
 
@@ -156,7 +189,7 @@ def test_facenet_projection_head(gpu):
     from facerecognition_amd.weights import synth_state_dict
     from oracle import models as M
     sd = synth_state_dict("irv1_facenet", embedding_size=128)
-    m = FRModel("irv1_facenet", sd)
+    m = FRModel("irv1_facenet", sd, dtype="f16")  # the 1e-3 bar: f16 (bf16: test_irv1_bf16_parity)
     assert m.embedding_size == 128
     u8 = _probes("irv1_facenet", 4, seed=2)
     got = m.embed(torch.from_numpy(u8)).cpu().numpy()
