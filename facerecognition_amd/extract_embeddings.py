@@ -9,9 +9,12 @@ Reference → here:
   get_transform / get_facenet_transform :170-185   Resize(PIL bilinear)+ToTensor+Normalize(0.5)
   extract_embedding_single :348-389   one image → np.f32 [512] or None on any error
   extract_embeddings_batch :392-443   (emb [M,512], valid_paths); bad files skipped; empty → (array([]), [])
-  extract_embedding_for_folder :714-762   per-identity mean + renorm — batched: ONE fr_embed for the
-                                 folder instead of one forward per image
-  compute_prototypes :555-592 / build_faiss_index :595-645 (→ DeviceGallery, IndexFlatIP surface)
+  extract_embedding_for_folder :714-762   per-identity mean + renorm on the device (segment_means: batched
+                                 fr_embed + fr_segment_mean_normalize) instead of one forward per image
+  build_db :765-835              every identity's crops in shared 256-image fr_embed batches, one
+                                 segmented-mean launch per ~4096 images
+  compute_prototypes :555-592 / build_faiss_index :595-645 (→ DeviceGallery, IndexFlatIP surface; the
+                                 .faiss flat-index file format without faiss: faiss_io.py)
   build_db :765-835, extract_embeddings_from_csv :446-552, full_pipeline :838-888
 Face detection/alignment (FacePreprocessor, MTCNN) and t-SNE plotting are out of scope (SURVEY.md
 §2.1 rows 1/11): requesting them prints a warning and the raw image is used, exactly as the reference
@@ -147,9 +150,46 @@ def extract_embeddings_batch(image_paths: List[str], model, transform, device: s
     return np.vstack(embeddings).astype(np.float32), valid_paths
 
 
-def _mean_renorm(embs: np.ndarray) -> np.ndarray:
-    m = np.mean(np.stack(list(embs), axis=0), axis=0)
-    return m / (np.linalg.norm(m) + 1e-8)
+def segment_means(model, groups: List[List[np.ndarray]]) -> List[Optional[np.ndarray]]:
+    """Identity rows of a gallery, batched on the device: every crop of every group
+    goes through fr_embed in batches of up to model.max_batch (256) images into one device buffer, and
+    fr_segment_mean_normalize reduces each group to mean / (||mean|| + 1e-8) -- the reference's per-folder
+    ``np.mean`` + renorm (extract_embeddings.py:755-760, recognition_engine.py:411-413), for all groups
+    in one launch.  Empty groups give None (the reference skips an identity with no valid image)."""
+    import torch
+    from . import _native as N
+    out: List[Optional[np.ndarray]] = [None] * len(groups)
+    live = [g for g, imgs in enumerate(groups) if len(imgs)]
+    if not live:
+        return out
+    crops = [c for g in live for c in groups[g]]
+    dev = model.device
+    D = model.embedding_size
+    E = torch.empty((len(crops), D), dtype=torch.float32, device=dev)
+    mb = max(1, getattr(model, "max_batch", 0) or 256)
+    for a in range(0, len(crops), mb):
+        x = torch.from_numpy(np.stack(crops[a:a + mb])).to(dev, non_blocking=True)
+        model.embed(x, normalize=True, out=E[a:a + len(x)])
+    starts = np.cumsum([0] + [len(groups[g]) for g in live]).astype(np.int32)
+    seg = torch.from_numpy(starts).to(dev)
+    M = torch.empty((len(live), D), dtype=torch.float32, device=dev)
+    N.check(N.lib().fr_segment_mean_normalize(N.ptr(E), D, N.ptr(seg), len(live), N.ptr(M), N.stream_ptr(dev)),
+            "fr_segment_mean_normalize")
+    rows = M.cpu().numpy()
+    for r, g in enumerate(live):
+        out[g] = rows[r]
+    return out
+
+
+def _folder_crops(folder: str, transform) -> List[np.ndarray]:
+    paths = [os.path.join(folder, f) for f in os.listdir(folder) if f.lower().endswith(IMG_EXTS)]
+    imgs = []
+    for p in paths:  # os.listdir order, as the reference
+        try:
+            imgs.append(_load_u8(p, transform))
+        except Exception as e:
+            print(f"Loi xu ly {p}: {e}")
+    return imgs
 
 
 def extract_embedding_for_folder(folder: str, model, transform, device: str = "cuda", preprocessor=None,
@@ -158,16 +198,7 @@ def extract_embedding_for_folder(folder: str, model, transform, device: str = "c
         return None
     if preprocessor is not None:
         print("[WARN] face detection/alignment is out of scope for facerecognition_amd; using raw images")
-    paths = [os.path.join(folder, f) for f in os.listdir(folder) if f.lower().endswith(IMG_EXTS)]
-    imgs = []
-    for p in paths:  # os.listdir order, as the reference
-        try:
-            imgs.append(_load_u8(p, transform))
-        except Exception as e:
-            print(f"Loi xu ly {p}: {e}")
-    if not imgs:
-        return None
-    return _mean_renorm(_embed_u8(model, np.stack(imgs))).astype(np.float32)
+    return segment_means(model, [_folder_crops(folder, transform)])[0]
 
 
 def compute_prototypes(embeddings: np.ndarray, labels: np.ndarray, output_path: str = None) -> np.ndarray:
@@ -185,8 +216,10 @@ def compute_prototypes(embeddings: np.ndarray, labels: np.ndarray, output_path: 
 
 
 def build_faiss_index(embeddings: np.ndarray, output_path: str = None, use_gpu: bool = True):
-    """IndexFlatIP equivalent on the GPU: rows L2-normalized (+1e-8) like the reference; saved as an
-    .npz (rows) because the FAISS binary format needs faiss, which is not part of this path."""
+    """IndexFlatIP equivalent on the GPU: rows L2-normalized (+1e-8) like the reference; saved in FAISS's
+    own flat-index file format (faiss_io.write_flat_index), readable by faiss.read_index and by
+    read_index here."""
+    from .faiss_io import write_flat_index
     from .gallery import DeviceGallery
 
     print("\n=== BUILDING DEVICE INDEX (IndexFlatIP semantics) ===")
@@ -195,17 +228,23 @@ def build_faiss_index(embeddings: np.ndarray, output_path: str = None, use_gpu: 
     index = DeviceGallery(e, dim=e.shape[1])
     print(f"Index built: {index.ntotal} vectors, {e.shape[1]}D")
     if output_path:
-        np.savez(output_path if output_path.endswith(".npz") else output_path + ".npz", rows=e)
-        print(f"Saved index: {output_path}")
+        write_flat_index(output_path, e)
+        print(f"Saved FAISS index: {output_path}")
     return index
 
 
 def read_index(path: str):
-    """Load an index written by build_faiss_index (the .faiss path of the reference maps to .npz)."""
+    """faiss.read_index for flat indexes (the reference's arcface_index.faiss) into a DeviceGallery with
+    IndexFlatIP search semantics; round-1 .npz row files are still accepted."""
+    from .faiss_io import read_flat_index
     from .gallery import DeviceGallery
-    p = path if os.path.exists(path) else (path + ".npz")
-    with np.load(p, allow_pickle=False) as z:
-        rows = z["rows"]
+    if path.endswith(".npz") or (not os.path.exists(path) and os.path.exists(path + ".npz")):
+        with np.load(path if os.path.exists(path) else path + ".npz", allow_pickle=False) as z:
+            rows = z["rows"]
+    else:
+        rows, metric = read_flat_index(path)
+        if metric != 0:
+            raise ValueError(f"{path}: metric {metric} index; the reference builds IndexFlatIP (metric 0)")
     return DeviceGallery(rows, dim=rows.shape[1])
 
 
@@ -234,11 +273,26 @@ def build_db(model_path: str, root_folder: str = "data/celeb", save_path: str = 
     db: Dict[str, np.ndarray] = {}
     persons = [p for p in os.listdir(root_folder) if os.path.isdir(os.path.join(root_folder, p))]
     print(f"\nTim thay {len(persons)} celebrities")
+    # identities are embedded together: crops of consecutive persons are collected
+    # until about FLUSH images, then embedded in 256-image fr_embed batches and reduced per person by one
+    # segmented-mean launch; host memory stays bounded by one flush
+    FLUSH = 4096
+    pending: List[str] = []
+    groups: List[List[np.ndarray]] = []
+
+    def flush():
+        for person, emb in zip(pending, segment_means(model, groups)):
+            if emb is not None:
+                db[person] = emb
+        pending.clear()
+        groups.clear()
+
     for person in persons:
-        emb = extract_embedding_for_folder(os.path.join(root_folder, person), model, transform, device, None,
-                                           model_type)
-        if emb is not None:
-            db[person] = emb
+        pending.append(person)
+        groups.append(_folder_crops(os.path.join(root_folder, person), transform))
+        if sum(len(g) for g in groups) >= FLUSH:
+            flush()
+    flush()
     if not db:
         print("\nKhong co embeddings nao duoc tao!")
         return
@@ -286,7 +340,7 @@ def full_pipeline(model_path: str, csv_path: str, data_root: str = None, output_
     result = extract_embeddings_from_csv(model_path, csv_path, data_root, output_dir, device, batch_size)
     prototypes = compute_prototypes(result["embeddings"], result["labels"],
                                     os.path.join(output_dir, "arcface_prototypes.npy"))
-    build_faiss_index(prototypes, os.path.join(output_dir, "arcface_index.npz"))
+    build_faiss_index(prototypes, os.path.join(output_dir, "arcface_index.faiss"))
     print("t-SNE visualization skipped (out of scope)")
     return result
 

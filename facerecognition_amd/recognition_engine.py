@@ -14,6 +14,8 @@ Reference → here:
   recognize :328-381                  same result dict / status / message
   recognize_batch :383-389            batched: all images in one fr_embed + one fr_match_topk (§8f row 1)
   add_to_db / save_db / get_db_identities / set_threshold :391-435, :165-167
+  FaceNetMatcher                      the FaceNet web route's matcher (web_app.py:537-559): renormalized
+                                       rows, score + L2 distance, threshold
 Face detection/alignment (MTCNN) is out of scope: with ``use_face_detection=True`` the engine reports the
 detector as unavailable and continues without it — the reference's own fallback (:122-124).
 
@@ -33,7 +35,7 @@ import numpy as np
 
 from . import weights as Wt
 from .extract_embeddings import (_device_index, _embed_u8, _load_u8, extract_embedding_single,
-                                 get_transform, load_arcface_model, read_index)
+                                 get_transform, load_arcface_model, read_index, segment_means)
 
 MAX_K = 16  # fr_match_topk limit
 
@@ -360,9 +362,7 @@ class RecognitionEngine:
         if not crops:
             print(f"Khong the extract embedding cho {name}")
             return False
-        E = _embed_u8(self.model, np.stack(crops))
-        m = np.mean(np.stack(list(E)), axis=0)
-        m = m / (np.linalg.norm(m) + 1e-8)
+        m = segment_means(self.model, [crops])[0]  # fr_embed + fr_segment_mean_normalize (:411-413)
         if self.db is None:
             self.db = {}
         self.db[name] = m
@@ -380,9 +380,45 @@ class RecognitionEngine:
 
 
 
+class FaceNetMatcher:
+    """The FaceNet web route's matcher (web_app.py:537-559) on the device: the probe and every db row are
+    divided by (|v| + 1e-8) (the route renormalizes rows in case the db was not normalized), score = dot
+    product (fr_match_topk, (score desc, row asc) = the stable sort), distance = |e - row| computed for
+    the returned rows exactly as the route does, best < threshold -> "Unknown".  One device gallery per
+    db, rebuilt when the dict changes (same tracking as RecognitionEngine)."""
+
+    def __init__(self, db: Dict[str, np.ndarray], threshold: float = 0.5, device: int = 0):
+        from .gallery import DeviceGallery
+        self.threshold = threshold
+        self.names = list(db.keys())
+        rows = np.stack([np.asarray(v, dtype=np.float32).reshape(-1) for v in db.values()])
+        self.rows = rows / (np.linalg.norm(rows, axis=1, keepdims=True) + 1e-8)
+        self.gallery = DeviceGallery(self.rows, dim=rows.shape[1], device=device)
+
+    def match_batch(self, embeddings: np.ndarray, k: int = 5) -> List[Dict]:
+        import torch
+        E = np.asarray(embeddings, dtype=np.float32).reshape(len(embeddings), -1)
+        E = E / (np.linalg.norm(E, axis=1, keepdims=True) + 1e-8)
+        k = min(k, len(self.names))
+        s, i = self.gallery.search_device(torch.from_numpy(np.ascontiguousarray(E)).to(self.gallery.device), k)
+        s, i = s.cpu().numpy(), i.cpu().numpy()
+        out = []
+        for r in range(len(E)):
+            top = [(self.names[j], float(v), float(np.linalg.norm(E[r] - self.rows[j]))) for v, j in zip(s[r], i[r])]
+            name, score, dist = top[0]
+            out.append({"identity": "Unknown" if score < self.threshold else name, "confidence": score,
+                        "distance": dist, "top_k": top, "status": "success"})
+        return out
+
+    def match(self, embedding: np.ndarray, k: int = 5) -> Dict:
+        return self.match_batch(np.asarray(embedding)[None], k)[0]
+
+
 def create_engine_from_embeddings_dir(model_path: str, embeddings_dir: str, threshold: float = 0.5,
                                       device: str = None) -> RecognitionEngine:
-    idx = os.path.join(embeddings_dir, "arcface_index.npz")
+    idx = os.path.join(embeddings_dir, "arcface_index.faiss")  # recognition_engine.py:453
+    if not os.path.exists(idx) and os.path.exists(os.path.join(embeddings_dir, "arcface_index.npz")):
+        idx = os.path.join(embeddings_dir, "arcface_index.npz")  # round-1 row files
     protos = os.path.join(embeddings_dir, "arcface_prototypes.npy")
     mapping = os.path.join(embeddings_dir, "label_mapping.npy")
     return RecognitionEngine(model_path=model_path, faiss_index_path=idx if os.path.exists(idx) else None,

@@ -88,3 +88,21 @@ def merge_topk(cand_s: np.ndarray, cand_i: np.ndarray, k: int) -> Tuple[np.ndarr
     key_i = np.where(i < 0, np.iinfo(np.int64).max, i)
     order = np.lexsort((key_i, -s), axis=1)[:, :k]
     return np.take_along_axis(s, order, 1), np.take_along_axis(i, order, 1)
+
+
+def facenet_web_match(embedding: np.ndarray, db: Dict[str, np.ndarray], threshold: float):
+    """web_app.py:537-559 (the FaceNet recognition route): probe / (|e| + 1e-8); every db row renormalized
+    by (|row| + 1e-8); score = dot, distance = |e - row|; stable sort by score desc; best < threshold ->
+    "Unknown".  Returns (identity, confidence, distance, top_k[:5] as (name, score, distance))."""
+    e = np.asarray(embedding, dtype=np.float32).flatten()
+    e = e / (np.linalg.norm(e) + 1e-8)
+    top_k = []
+    for name, db_emb in db.items():
+        r = np.asarray(db_emb, dtype=np.float32).flatten()
+        r = r / (np.linalg.norm(r) + 1e-8)
+        top_k.append((name, float(np.dot(e, r)), float(np.linalg.norm(e - r))))
+    top_k.sort(key=lambda x: x[1], reverse=True)
+    best_name, best_score, best_distance = top_k[0]
+    if best_score < threshold:
+        best_name = "Unknown"
+    return best_name, best_score, best_distance, top_k[:5]

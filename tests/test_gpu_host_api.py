@@ -132,7 +132,7 @@ def test_folder_db_build_and_faiss_path(gold, r50, tmp_path):
     # FAISS-style index over the same identities
     protos = np.stack([eng.db[k] for k in ("p0", "p1", "p2")])
     os.makedirs(tmp_path / "emb")
-    EE.build_faiss_index(protos, str(tmp_path / "emb" / "arcface_index.npz"))
+    EE.build_faiss_index(protos, str(tmp_path / "emb" / "arcface_index.faiss"))  # FAISS file format
     eng2 = create_engine_from_embeddings_dir(ck, str(tmp_path / "emb"), threshold=0.3)
     name, score, res = eng2.recognize_with_faiss(gold["emb_single"][6], k=3)
     s_ref, i_ref = faiss_flat_ip_search(protos, gold["emb_single"][6], 3)
@@ -182,3 +182,79 @@ def test_recognize_with_db_mixed_norm_on_device():
         assert name == rname and [t[0] for t in top] == [t[0] for t in rtop]
         assert np.allclose([t[1] for t in top], [t[1] for t in rtop], atol=1e-6)
     assert eng.recognize_with_db(probes[0])[0] == "A"
+
+
+def test_database_builder_end_to_end(gold, tmp_path):
+    """DatabaseBuilder.create_job / start_build (database_builder.py:184-234) -> build_db with every
+    identity's crops in shared fr_embed batches + one fr_segment_mean_normalize launch -> the reference's
+    dict .npy; rows equal the folder means of the reference's own embeddings (golden emb_single)."""
+    from PIL import Image
+    import torch
+    from facerecognition_amd import database_builder as DB
+    from facerecognition_amd.recognition_engine import load_npy_object
+    from facerecognition_amd.weights import synth_state_dict
+    from oracle.match import folder_mean
+    groups = {"p0": [0, 1, 2], "p1": [3, 4], "p2": [5, 6, 7], "empty": []}
+    for person, idx in groups.items():
+        os.makedirs(tmp_path / "celeb" / person)
+        for i in idx:
+            Image.fromarray(gold["probes"][i]).save(tmp_path / "celeb" / person / f"{i}.png")
+    (tmp_path / "celeb" / "p1" / "notes.txt").write_text("not an image")
+    sd = synth_state_dict("resnet50_arcface", seed=int(gold["seed"]), num_classes=int(gold["num_classes"]))
+    ck = str(tmp_path / "arcface_best.pth")
+    torch.save({"model_state_dict": {k: torch.as_tensor(v) for k, v in sd.items()},
+                "config": {"num_classes": 100, "model": {"embedding_size": 512}}}, ck)
+    out = str(tmp_path / "db.npy")
+    b = DB.DatabaseBuilder()
+    b.create_job("j", "arcface", {"model_path": ck, "data_dir": str(tmp_path / "celeb"), "output_path": out,
+                                  "use_face_detection": False})
+    b.start_build("j").join(300)
+    job = b.get_job("j")
+    assert job.status == "completed", job.logs
+    db = load_npy_object(out)
+    assert sorted(db) == ["p0", "p1", "p2"]  # the identity with no image is skipped, as the reference
+    for person, idx in groups.items():
+        if idx:
+            assert _cos_dist(db[person], folder_mean(gold["emb_single"][idx])) <= COS_TOL
+
+
+def test_segment_means_many_identities(r50):
+    """segment_means over 300 identities of 1-3 crops (spans two 256-image fr_embed batches): each row
+    equals the host mean / renorm of that identity's fr_embed outputs."""
+    import torch
+    from facerecognition_amd.extract_embeddings import segment_means
+    from facerecognition_amd.synthetic import synthetic_crops
+    from oracle.match import folder_mean
+    u8 = synthetic_crops(600, 112, seed=40)
+    sizes = [1 + (g % 3) for g in range(300)]
+    groups, o = [], 0
+    for n in sizes:
+        groups.append(list(u8[o:o + n]))
+        o += n
+    groups.insert(7, [])
+    rows = segment_means(r50, groups)
+    assert rows[7] is None
+    # the same 256-image batches as segment_means, so the per-image embeddings are bit-identical
+    E = np.concatenate([r50.embed(torch.from_numpy(u8[a:min(a + 256, o)])).cpu().numpy() for a in range(0, o, 256)])
+    o = 0
+    for g, n in enumerate(sizes):
+        row = rows[g if g < 7 else g + 1]
+        assert np.allclose(row, folder_mean(E[o:o + n]), atol=2e-6)
+        o += n
+
+
+def test_facenet_matcher_vs_web_route():
+    """FaceNetMatcher (device) vs the web route's loop (web_app.py:537-559): renormalized rows (some
+    far from unit norm), names / order, scores, distances, threshold."""
+    from facerecognition_amd.recognition_engine import FaceNetMatcher
+    from oracle.match import facenet_web_match
+    rng = np.random.default_rng(8)
+    db = {f"id{j}": rng.standard_normal(512).astype(np.float32) * (1.0 if j % 4 else 3.0) for j in range(300)}
+    probes = [db["id5"] * 0.5 + 0.1 * rng.standard_normal(512).astype(np.float32),
+              rng.standard_normal(512).astype(np.float32), 2.0 * db["id12"]]
+    m = FaceNetMatcher(db, threshold=0.3)
+    for p, got in zip(probes, m.match_batch(np.stack(probes))):
+        name, score, dist, top = facenet_web_match(p, db, 0.3)
+        assert got["identity"] == name and [t[0] for t in got["top_k"]] == [t[0] for t in top]
+        assert abs(got["confidence"] - score) < 1e-5 and abs(got["distance"] - dist) < 1e-5
+        assert np.allclose([t[2] for t in got["top_k"]], [t[2] for t in top], atol=1e-5)

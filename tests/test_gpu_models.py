@@ -240,3 +240,34 @@ def test_full_batch_properties_bs256(gpu):
     assert np.array_equal(idx[:, 0], perm)
     gal.close()
     m.close()
+
+
+def test_top1_agreement_random_gallery(gpu):
+    """Non-planted top-1 agreement (SURVEY.md §7 'Hard parts'): 64 IResNet100 bf16 embeddings vs the fp32
+    oracle's against a random 10k unit gallery.  Reports the agreement rate and the oracle's top-1/top-2
+    gap; a disagreement is only allowed where the oracle's own gap is below the score perturbation that
+    the embedding error can cause (|dg| <= |e - e_ref| * 2, rows being unit)."""
+    from facerecognition_amd.gallery import DeviceGallery
+    from facerecognition_amd.model import FRModel
+    from oracle.match import topk_dot
+    m = FRModel.synthetic("iresnet100", dtype="bf16")
+    u8 = _probes("iresnet100", 64, seed=51)
+    ref = _oracle_embed("iresnet100", u8)
+    got = m.embed(torch.from_numpy(u8)).cpu().numpy()
+    m.close()
+    rng = np.random.default_rng(52)
+    G = rng.standard_normal((10000, 512)).astype(np.float32)
+    G /= np.linalg.norm(G, axis=1, keepdims=True)
+    gal = DeviceGallery(G)
+    _, gi = gal.search(got, 2)
+    gal.close()
+    rs, ri = topk_dot(ref, G, 2)
+    agree = gi[:, 0] == ri[:, 0]
+    gap = rs[:, 0] - rs[:, 1]
+    err = np.linalg.norm(got - ref / np.linalg.norm(ref, axis=1, keepdims=True), axis=1)
+    print(f"top-1 agreement {agree.mean():.4f} on 64 probes x 10k random rows; oracle gap median "
+          f"{np.median(gap):.2e} min {gap.min():.2e}; embedding error max {err.max():.2e}")
+    # measured 0.94 (4 flips in 64, all inside the bound): a random 10k gallery has top-1/top-2 gaps down
+    # to ~3e-4, below what bf16 storage through 100 layers (|e - e_ref| ~ 1e-2) can resolve
+    assert agree.mean() >= 0.85
+    assert np.all(agree | (gap <= 2 * err)), "a top-1 flip where the oracle's gap exceeds the error bound"
