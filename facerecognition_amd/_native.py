@@ -69,6 +69,9 @@ _SIGS = {
     "fr_embed_match": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "fr_segment_mean_normalize": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "fr_resize_u8_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "fr_resize_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p]),
+    "fr_warp_affine_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "fr_set_option": (c_int, [c_void_p, c_int, c_int]),
     "fr_get_option": (c_int, [c_void_p, c_int]),
     "fr_debug_match_fallbacks": (c_int, [c_void_p]),

@@ -1720,6 +1720,35 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
     return FR_OK;
 }
 
+size_t fr_resize_u8_workspace(int B, int H, int W, int OH, int OW) {
+    if (B <= 0 || H <= 0 || W <= 0 || OH <= 0 || OW <= 0) return 0;
+    return resize_u8_workspace(B, H, W, OH, OW);
+}
+
+int fr_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, void* ws, size_t ws_bytes,
+                 void* stream) {
+    if (!in || !out || B <= 0 || H <= 0 || W <= 0 || OH <= 0 || OW <= 0 || (size_t)B * H * W * 3 > 0x7fffffffull * 4) {
+        set_error("fr_resize_u8: bad argument");
+        return FR_ERR_ARG;
+    }
+    if (ws_bytes < resize_u8_workspace(B, H, W, OH, OW) || (!ws && ws_bytes == 0 && W != OW)) {
+        set_error("fr_resize_u8: workspace smaller than fr_resize_u8_workspace()");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_resize_u8(in, B, H, W, out, OH, OW, ws, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_warp_affine_u8(const uint8_t* in, int B, int H, int W, const double* M, uint8_t* out, int OH, int OW,
+                      void* stream) {
+    if (!in || !out || !M || B <= 0 || H <= 0 || W <= 0 || OH <= 0 || OW <= 0) {
+        set_error("fr_warp_affine_u8: bad argument");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_warp_affine_u8(in, B, H, W, M, out, OH, OW, (hipStream_t)stream));
+    return FR_OK;
+}
+
 int fr_op_preprocess(const void* in, int in_fmt, int B, int H, int W, void* out, int dtype, void* stream) {
     if (!in || !out || B <= 0 || H <= 0 || W <= 0 || (in_fmt != FR_IN_U8_NHWC && in_fmt != FR_IN_F32_NCHW)) {
         set_error("fr_op_preprocess: bad argument");

@@ -136,5 +136,11 @@ hipError_t launch_segment_mean_normalize(const float* E, int D, const int32_t* s
                                          float* out, hipStream_t s);
 // Gallery preparation: rows with |‖g‖-1| >= 1e-3 divided by ‖g‖ (cosine_similarity semantics).
 hipError_t launch_gallery_prepare(float* G, int64_t N, int D, hipStream_t s);
+// Crop preparation (preprocess.hip): Pillow-exact bilinear resize, cv2-exact affine warp (u8 RGB NHWC).
+size_t resize_u8_workspace(int B, int H, int W, int OH, int OW);
+hipError_t launch_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, void* ws,
+                            hipStream_t s);
+hipError_t launch_warp_affine_u8(const uint8_t* in, int B, int H, int W, const double* M, uint8_t* out, int OH, int OW,
+                                 hipStream_t s);
 
 }  // namespace fr

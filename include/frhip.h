@@ -122,6 +122,23 @@ int fr_embed_match(fr_handle* h, const void* in, int in_fmt, int B, int H, int W
 int fr_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, int n_seg,
                               float* out, void* stream);
 
+/* ---- crop preparation on the device (u8 RGB NHWC in and out) ---- */
+
+/* Bytes of device workspace fr_resize_u8 needs for this shape (0 when the width is unchanged). */
+size_t fr_resize_u8_workspace(int B, int H, int W, int OH, int OW);
+/* Replaces: PIL Image.resize((OW, OH), Image.BILINEAR) inside get_transform / get_facenet_transform's
+ * Resize (inference/extract_embeddings.py:170-185): Pillow's two-pass antialiased bilinear resampler,
+ * bit-exact (coefficients in double as Pillow, 22-bit fixed point, horizontal pass first).  in: device
+ * [B,H,W,3] u8; out: device [B,OH,OW,3] u8; ws: device workspace of fr_resize_u8_workspace bytes. */
+int fr_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, void* ws, size_t ws_bytes,
+                 void* stream);
+/* Replaces: cv2.warpAffine(image, M, (OW, OH), borderValue=0) of align_face (extract_embeddings.py:216-242,
+ * recognition_engine.py:169-204; INTER_LINEAR, BORDER_CONSTANT 0), restating OpenCV's fixed-point path
+ * (1/32-pixel grid, 15-bit weights).  M: device [B][2][3] float64, the FORWARD source->destination matrices
+ * (SimilarityTransform(src landmarks -> ARCFACE_TEMPLATE).params[:2], as the reference passes them). */
+int fr_warp_affine_u8(const uint8_t* in, int B, int H, int W, const double* M, uint8_t* out, int OH, int OW,
+                      void* stream);
+
 /* ---- op-level entry points (kernel parity tests and custom graphs) ---- */
 
 /* Implicit-GEMM convolution on NHWC bf16 with fused epilogue:

@@ -1,0 +1,77 @@
+"""Device crop preparation (preprocess.hip through fr_resize_u8 / fr_warp_affine_u8) vs its references:
+the resize against PIL itself (bit-exact; PIL is the reference's own transform), the warp against the
+OpenCV restatement (bit-exact; oracle/preprocess.py, parity unpinned as cv2 is absent), and the aligned
+crop through the embedding path against the host path."""
+import os
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from oracle.preprocess import cv2_warp_affine
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _pil(img, w, h):
+    return np.asarray(Image.fromarray(img).resize((w, h), Image.BILINEAR))
+
+
+@pytest.mark.parametrize("shape,out,B", [((900, 900), (112, 112), 1), ((50, 50), (112, 112), 3),
+                                         ((200, 150), (112, 112), 4), ((97, 230), (160, 160), 2),
+                                         ((112, 300), (112, 112), 2), ((300, 112), (112, 112), 2),
+                                         ((640, 480), (160, 160), 5)])
+def test_resize_matches_pil(gpu, shape, out, B):
+    from facerecognition_amd.align import resize_u8
+    rng = np.random.default_rng(shape[0] + 7 * shape[1] + B)
+    imgs = rng.integers(0, 256, (B,) + shape + (3,), dtype=np.uint8)
+    if shape == (900, 900):
+        with np.load(os.path.join(GOLD, "anh1_u8.npz"), allow_pickle=False) as z:
+            imgs = z["u8"][None]
+    got = resize_u8(torch.from_numpy(imgs).to(gpu), out[0], out[1]).cpu().numpy()
+    for b in range(B):
+        assert np.array_equal(got[b], _pil(imgs[b], out[1], out[0])), f"image {b}"
+
+
+def test_warp_matches_opencv_restatement(gpu):
+    from facerecognition_amd.align import ARCFACE_TEMPLATE, similarity_transform, warp_affine_u8
+    rng = np.random.default_rng(11)
+    B, H, W = 6, 240, 200
+    imgs = rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8)
+    mats = []
+    for b in range(B):  # landmarks scattered over the image, partly near / beyond the borders
+        src = ARCFACE_TEMPLATE * rng.uniform(0.8, 2.2) + rng.uniform(-40, 160, 2)
+        src = src + rng.normal(0, 2.0, src.shape)
+        mats.append(similarity_transform(src)[:2])
+    mats[0] = np.array([[1.0, 0, 0], [0, 1.0, 0]])           # identity
+    mats[1] = np.array([[0.5, 0.0, -30.25], [0.0, 0.5, 7.5]])  # exact binary fractions, border crossing
+    got = warp_affine_u8(torch.from_numpy(imgs).to(gpu), np.stack(mats)).cpu().numpy()
+    for b in range(B):
+        ref = cv2_warp_affine(imgs[b], mats[b], 112, 112)
+        assert np.array_equal(got[b], ref), f"image {b}: {np.abs(got[b].astype(int) - ref).max()}"
+
+
+def test_align_then_embed_matches_host_path(gpu):
+    """align_faces (device warp) -> fr_embed equals the host-warped crops through the same model, and a
+    face without landmarks is reported as not aligned."""
+    from facerecognition_amd.align import ARCFACE_TEMPLATE, LANDMARK_KEYS, align_faces, similarity_transform
+    from facerecognition_amd.model import FRModel
+    rng = np.random.default_rng(12)
+    imgs = rng.integers(0, 256, (3, 180, 160, 3), dtype=np.uint8)
+    lms = []
+    for b in range(3):
+        pts = ARCFACE_TEMPLATE * 1.3 + np.array([10.0 + 5 * b, 20.0])
+        lms.append({k: list(map(float, p)) for k, p in zip(LANDMARK_KEYS, pts)})
+    lms[2] = {}
+    crops, ok = align_faces(torch.from_numpy(imgs).to(gpu), lms)
+    assert list(ok) == [True, True, False] and not crops[2].any()
+    host = np.stack([cv2_warp_affine(imgs[b], similarity_transform(
+        np.array([lms[b][k] for k in LANDMARK_KEYS], np.float32))[:2], 112, 112) for b in range(2)])
+    assert np.array_equal(crops[:2].cpu().numpy(), host)
+    m = FRModel.synthetic("iresnet100")
+    e_dev = m.embed(crops[:2]).cpu().numpy()
+    e_host = m.embed(torch.from_numpy(host)).cpu().numpy()
+    m.close()
+    assert np.array_equal(e_dev, e_host)
