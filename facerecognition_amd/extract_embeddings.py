@@ -105,17 +105,44 @@ def get_facenet_transform(image_size: int = 160):
 
 
 def _load_u8(img_input, transform) -> np.ndarray:
-    """PIL/path → resized RGB u8 HWC (the fused u8 path of fr_embed does ToTensor+Normalize exactly)."""
+    """PIL/path -> decoded RGB u8 HWC at its own size (the Resize of the transform runs on the device:
+    _device_crops; ToTensor + Normalize are fused into fr_embed's u8 path)."""
     from PIL import Image
+    if not isinstance(transform, _Transform):
+        raise TypeError("transform must come from get_transform()/get_facenet_transform()")
     img = Image.open(img_input) if isinstance(img_input, str) else img_input
-    if isinstance(transform, _Transform):
-        return np.asarray(transform.resize(img), dtype=np.uint8)
-    raise TypeError("transform must come from get_transform()/get_facenet_transform()")
+    return np.asarray(img.convert("RGB"), dtype=np.uint8)
 
 
-def _embed_u8(model, u8: np.ndarray) -> np.ndarray:
+def _device_crops(arrays: List[np.ndarray], size: int, device):
+    """Decoded RGB u8 images of any sizes -> device u8 [n, size, size, 3]: images already size x size are
+    copied, the others go through fr_resize_u8 (Pillow's BILINEAR resize, bit-exact) one launch per
+    distinct input size."""
     import torch
-    return model.embed(torch.from_numpy(np.require(u8, requirements=["C", "W"])), normalize=True).cpu().numpy()
+    from .align import resize_u8
+    out = torch.empty((len(arrays), size, size, 3), dtype=torch.uint8, device=device)
+    by_shape: Dict[tuple, List[int]] = {}
+    for i, a in enumerate(arrays):
+        by_shape.setdefault(a.shape, []).append(i)
+    for shape, idx in by_shape.items():
+        x = torch.from_numpy(np.ascontiguousarray(np.stack([arrays[i] for i in idx]))).to(device, non_blocking=True)
+        if shape[:2] != (size, size):
+            x = resize_u8(x, size, size)
+        out[torch.as_tensor(idx, device=device)] = x
+    return out
+
+
+def _embed_u8(model, arrays) -> np.ndarray:
+    """Normalized embeddings (host f32 [n, D]) of decoded images of any sizes, in batches of up to
+    model.max_batch (256), resized on the device."""
+    import torch
+    mb = max(1, getattr(model, "max_batch", 0) or 256)
+    arrays = list(arrays)
+    outs = []
+    for a in range(0, len(arrays), mb):
+        x = _device_crops(arrays[a:a + mb], model.input_size, model.device)
+        outs.append(model.embed(x, normalize=True).cpu().numpy())
+    return np.concatenate(outs) if outs else np.zeros((0, model.embedding_size), np.float32)
 
 
 # ---------------------------------------------------------------------------------------- extraction
@@ -123,7 +150,7 @@ def extract_embedding_single(img_input, model, transform, device: str = "cuda",
                              model_type: str = "arcface") -> Optional[np.ndarray]:
     try:
         u8 = _load_u8(img_input, transform)
-        return _embed_u8(model, u8[None])[0].astype(np.float32).flatten()
+        return _embed_u8(model, [u8])[0].astype(np.float32).flatten()
     except Exception as e:  # reference: any failure → None (extract_embeddings.py:386-389)
         if isinstance(img_input, str):
             print(f"Loi xu ly {img_input}: {e}")
@@ -143,7 +170,7 @@ def extract_embeddings_batch(image_paths: List[str], model, transform, device: s
                 print(f"Skip {path}: {e}")
         if not imgs:
             continue
-        embeddings.append(_embed_u8(model, np.stack(imgs)))
+        embeddings.append(_embed_u8(model, imgs))
         valid_paths.extend(paths)
     if not embeddings:
         return np.array([]), []
@@ -151,8 +178,8 @@ def extract_embeddings_batch(image_paths: List[str], model, transform, device: s
 
 
 def segment_means(model, groups: List[List[np.ndarray]]) -> List[Optional[np.ndarray]]:
-    """Identity rows of a gallery, batched on the device: every crop of every group
-    goes through fr_embed in batches of up to model.max_batch (256) images into one device buffer, and
+    """Identity rows of a gallery, batched on the device: every decoded image of every
+    group (any size: resized on the device) goes through fr_embed in batches of up to model.max_batch (256) images into one device buffer, and
     fr_segment_mean_normalize reduces each group to mean / (||mean|| + 1e-8) -- the reference's per-folder
     ``np.mean`` + renorm (extract_embeddings.py:755-760, recognition_engine.py:411-413), for all groups
     in one launch.  Empty groups give None (the reference skips an identity with no valid image)."""
@@ -168,7 +195,7 @@ def segment_means(model, groups: List[List[np.ndarray]]) -> List[Optional[np.nda
     E = torch.empty((len(crops), D), dtype=torch.float32, device=dev)
     mb = max(1, getattr(model, "max_batch", 0) or 256)
     for a in range(0, len(crops), mb):
-        x = torch.from_numpy(np.stack(crops[a:a + mb])).to(dev, non_blocking=True)
+        x = _device_crops(crops[a:a + mb], model.input_size, dev)
         model.embed(x, normalize=True, out=E[a:a + len(x)])
     starts = np.cumsum([0] + [len(groups[g]) for g in live]).astype(np.int32)
     seg = torch.from_numpy(starts).to(dev)

@@ -329,8 +329,7 @@ class RecognitionEngine:
                 results[n]["message"] = "Cannot extract embedding (no face or invalid image)"
         if not ok:
             return results
-        mb = max(1, getattr(self.model, "max_batch", 256) or 256)
-        E = np.concatenate([_embed_u8(self.model, np.stack(crops[j:j + mb])) for j in range(0, len(crops), mb)])
+        E = _embed_u8(self.model, crops)  # device resize + fr_embed in 256-image batches
         if use_faiss is None:
             use_faiss = self.faiss_index is not None
         if use_faiss and self.faiss_index is not None:
