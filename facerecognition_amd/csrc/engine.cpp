@@ -44,7 +44,9 @@ struct DevConvW {
     float* aff_b = nullptr;
     float* bias9 = nullptr;  // [9][Npad] border-class bias (input BN folded into a 3x3/s1/p1 conv)
     bf16_t* wimg = nullptr;  // conv_img.hip K-step slice images (convs its kernels apply to)
-    float* negf = nullptr;   // conv_img.hip: [Npad] activation negative-side factor (slope / 0 / 1)
+    float* negf = nullptr;   // conv_img / conv_rows: [Npad] activation negative-side factor (slope / 0 / 1)
+    bf16_t* wrows = nullptr; // conv_rows.hip weight image (rows_pack_weights)
+    float* ep = nullptr;     // conv_rows.hip: [9][Npad] bias per border class
     uint8_t* w8 = nullptr;   // FR_DTYPE_FP8: e4m3 [Npad][Kpad8] + per-channel scale
     float* wscale = nullptr;
     int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0, Kpad8 = 0;
@@ -608,7 +610,7 @@ int build_img_weights(fr_handle* h) {
     for (const auto& op : h->ops) {
         if (op.kind != OP_CONV || op.wi < 0) continue;
         DevConvW& cw = h->convw[op.wi];
-        if (cw.wimg) continue;
+        if (cw.wimg || cw.wrows) continue;
         ConvArgs a{};
         a.B = 1; a.Cin = op.cin; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
         a.H = h->tensors[op.in].H; a.W = h->tensors[op.in].W; a.Cx = h->tensors[op.in].C; a.x_off = op.in_off;
@@ -618,17 +620,44 @@ int build_img_weights(fr_handle* h) {
         if (op.res >= 0) { a.res = (const bf16_t*)1; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
         a.f16 = h->dtype == FR_DTYPE_F16;
         int ic = 0;
-        if (h->dtype == FR_DTYPE_FP8 || !img_shape_ok(a, &ic)) continue;
+        if (h->dtype == FR_DTYPE_FP8) continue;
+        // the activation's negative-side factor (conv_img and conv_rows epilogues)
+        auto make_negf = [&]() -> int {
+            if (cw.negf) return FR_OK;
+            std::vector<float> nf(cw.Npad, op.act == 1 ? 0.f : 1.f);
+            if (op.act == 2 && cw.slope)
+                FR_HIP_CHECK(hipMemcpy(nf.data(), cw.slope, cw.Cout * sizeof(float), hipMemcpyDeviceToHost));
+            return upload(h, &cw.negf, nf);
+        };
+        {
+            ConvArgs r = a;
+            r.wimg = (const bf16_t*)1;
+            if (rows_supported(r) && !cw.wrows) {
+                void* q = nullptr;
+                int rc = dev_alloc(&q, rows_packed_elems(cw.Cout) * sizeof(bf16_t));
+                if (rc) return rc;
+                h->weight_allocs.push_back(q);
+                FR_HIP_CHECK(rows_pack_weights(cw.w, cw.Kpad, cw.Cout, (bf16_t*)q, nullptr));
+                cw.wrows = (bf16_t*)q;
+                std::vector<float> ep((size_t)9 * cw.Npad, 0.f);
+                if (cw.bias9) {
+                    FR_HIP_CHECK(hipMemcpy(ep.data(), cw.bias9, ep.size() * sizeof(float), hipMemcpyDeviceToHost));
+                } else if (cw.bias) {
+                    FR_HIP_CHECK(hipMemcpy(ep.data(), cw.bias, cw.Npad * sizeof(float), hipMemcpyDeviceToHost));
+                    for (int k = 1; k < 9; ++k) std::copy(ep.begin(), ep.begin() + cw.Npad, ep.begin() + k * cw.Npad);
+                }
+                if ((rc = upload(h, &cw.ep, ep))) return rc;
+                if ((rc = make_negf())) return rc;
+            }
+        }
+        if (!img_shape_ok(a, &ic)) continue;
         void* p = nullptr;
         int rc = dev_alloc(&p, img_packed_elems(ic) * sizeof(bf16_t));
         if (rc) return rc;
         h->weight_allocs.push_back(p);
         FR_HIP_CHECK(img_pack_weights(cw.w, cw.Kpad, ic, (bf16_t*)p, nullptr));
         cw.wimg = (bf16_t*)p;
-        std::vector<float> nf(cw.Npad, op.act == 1 ? 0.f : 1.f);
-        if (op.act == 2 && cw.slope)
-            FR_HIP_CHECK(hipMemcpy(nf.data(), cw.slope, cw.Cout * sizeof(float), hipMemcpyDeviceToHost));
-        if ((rc = upload(h, &cw.negf, nf))) return rc;
+        if ((rc = make_negf())) return rc;
     }
     FR_HIP_CHECK(hipDeviceSynchronize());
     return FR_OK;
@@ -821,6 +850,14 @@ bool img28_enabled() {
     return on;
 }
 
+bool rows_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_ROWS");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 bool img56_enabled() {
     static const bool on = [] {
         const char* e = getenv("FR_IMG56");
@@ -968,6 +1005,15 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
         FR_HIP_CHECK(launch_conv_fp8(a, s));
         return FR_OK;
     }
+    if (rows_enabled() && a.wrows_ && a.ep && a.negf) {  // 64-channel 3x3/s1 convs: weight-resident rows
+        ConvArgs r = a;
+        r.wimg = a.wrows_;
+        if (rows_supported(r)) {
+            ps.start("conv3x3_rows W" + std::to_string(a.W) + " N" + std::to_string(a.Cout), &r);
+            FR_HIP_CHECK(launch_conv_rows(r, h->n_cu, s));
+            return FR_OK;
+        }
+    }
     if (img28_enabled() && img28_supported(a)) {  // layer2 3x3 128->128 @28x28: quarter-image bands
         ps.start("conv3x3_img W28", &a);
         FR_HIP_CHECK(launch_conv_img28(a, s));
@@ -1085,7 +1131,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.K = cw.K; a.Kpad = cw.Kpad;
                 a.Ho = to.H; a.Wo = to.W; a.M = B * to.H * to.W; a.Cout = cw.Cout; a.Npad = cw.Npad;
                 a.bias = cw.bias; a.slope = cw.slope; a.act = op.act; a.bias9 = cw.bias9; a.wimg = cw.wimg;
-                a.negf = cw.negf;
+                a.negf = cw.negf; a.ep = cw.ep;
+                a.wrows_ = cw.wrows;
                 if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
                 a.y = to.dev; a.Cy = to.C; a.y_off = op.out_off;
                 if (op.out2 >= 0) {
@@ -1485,7 +1532,11 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
             a.Cx = h->tensors[op.in].C; a.x_off = op.in_off; a.Cy = h->tensors[op.out].C; a.y_off = op.out_off;
             if (op.res >= 0) { a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
             int TH, variant;
-            if (img28_enabled() && img28_supported(a)) tile = FR_TILE_IMG28;
+            ConvArgs rr = a;
+            rr.wimg = cw.wrows;
+            rr.y2 = a.y2; rr.partial = nullptr;
+            if (rows_enabled() && cw.wrows && rows_supported(rr)) tile = FR_TILE_ROWS;
+            else if (img28_enabled() && img28_supported(a)) tile = FR_TILE_IMG28;
             else if (img56_enabled() && img56_supported(a)) tile = FR_TILE_IMG56;
             else if (band_enabled() && band_plan(a, &TH, &variant) && variant >= 3) tile = FR_TILE_BAND;
             else if (sp == 1 && autotune_enabled() && !conv_tile_forced() && find_tuned(h, a) >= 0) tile = find_tuned(h, a);
@@ -1666,6 +1717,41 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         int TH, variant;
         if (!band_plan(a, &TH, &variant)) { set_error("fr_op_conv2d: band kernel not applicable"); return FR_ERR_ARG; }
         FR_HIP_CHECK(launch_conv_band(a, TH, variant, (hipStream_t)stream));
+        return FR_OK;
+    }
+    if (d->tile == FR_TILE_ROWS + 1) {
+        // the op API takes [Npad][Kpad] rows: pack the weight image, the class-bias and negf tables into
+        // stream-ordered scratch (the tables built on the host from the caller's device vectors)
+        a.wimg = (const bf16_t*)1;
+        a.ep = a.negf = (const float*)1;
+        if (!rows_supported(a)) { set_error("fr_op_conv2d: rows kernel not applicable"); return FR_ERR_ARG; }
+        hipStream_t st = (hipStream_t)stream;
+        FR_HIP_CHECK(hipStreamSynchronize(st));
+        std::vector<float> ep((size_t)9 * a.Npad, 0.f), nf(a.Npad, a.act == 1 ? 0.f : 1.f);
+        if (a.bias9) FR_HIP_CHECK(hipMemcpy(ep.data(), a.bias9, ep.size() * sizeof(float), hipMemcpyDeviceToHost));
+        else if (a.bias) {
+            FR_HIP_CHECK(hipMemcpy(ep.data(), a.bias, a.Cout * sizeof(float), hipMemcpyDeviceToHost));
+            for (int k = 1; k < 9; ++k) std::copy(ep.begin(), ep.begin() + a.Npad, ep.begin() + k * a.Npad);
+        }
+        if (a.act == 2) FR_HIP_CHECK(hipMemcpy(nf.data(), a.slope, a.Cout * sizeof(float), hipMemcpyDeviceToHost));
+        void *tw = nullptr, *te = nullptr, *tn = nullptr;
+        FR_HIP_CHECK(hipMalloc(&tw, rows_packed_elems(a.Cout) * sizeof(bf16_t)));
+        FR_HIP_CHECK(hipMalloc(&te, ep.size() * sizeof(float)));
+        FR_HIP_CHECK(hipMalloc(&tn, nf.size() * sizeof(float)));
+        FR_HIP_CHECK(hipMemcpy(te, ep.data(), ep.size() * sizeof(float), hipMemcpyHostToDevice));
+        FR_HIP_CHECK(hipMemcpy(tn, nf.data(), nf.size() * sizeof(float), hipMemcpyHostToDevice));
+        FR_HIP_CHECK(rows_pack_weights(a.w, a.Kpad, a.Cout, (bf16_t*)tw, st));
+        a.wimg = (const bf16_t*)tw;
+        a.ep = (const float*)te;
+        a.negf = (const float*)tn;
+        int dev = 0, ncu = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) ncu = prop.multiProcessorCount;
+        FR_HIP_CHECK(launch_conv_rows(a, ncu, st));
+        FR_HIP_CHECK(hipStreamSynchronize(st));
+        (void)hipFree(tw);
+        (void)hipFree(te);
+        (void)hipFree(tn);
         return FR_OK;
     }
     if (d->tile == FR_TILE_IMG28 + 1 || d->tile == FR_TILE_IMG56 + 1) {

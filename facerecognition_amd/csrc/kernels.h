@@ -35,8 +35,16 @@ struct ConvArgs {
     float* y_amax;                // non-null: the epilogue atomically records max |y| (both dtypes)
     int amax_slots;               // x_amax / y_amax are arrays of this many partial maxima (block % slots)
     const bf16_t* wimg;           // conv_img.hip: weights pre-packed as K-step slice images (img_pack_weights)
-    const float* negf;            // conv_img.hip: [Npad] activation negative-side factor (slope / 0 / 1)
+    const float* negf;            // conv_img / conv_rows: [Npad] activation negative-side factor (slope / 0 / 1)
+    const float* ep;              // conv_rows.hip: [9][Npad] bias per border class (bias9, or bias x 9)
+    const bf16_t* wrows_;         // engine: the conv's conv_rows weight image when it has one (else null)
 };
+// Persistent weight-resident 3x3/s1/p1 conv with 64 input channels (conv_rows.hip); a.wimg = the
+// rows_pack_weights image, a.ep / a.negf set.
+bool rows_supported(const ConvArgs& a);
+size_t rows_packed_elems(int Cout);
+hipError_t rows_pack_weights(const bf16_t* w, int Kpad, int Cout, bf16_t* out, hipStream_t s);
+hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s);
 constexpr int FR_AMAX_SLOTS = 64;  // engine: spreads the producers' atomics over 64 addresses
 
 // FP8 (e4m3 x e4m3, v_mfma_scale_f32_16x16x128_f8f6f4) implicit GEMM; Cin % 64 == 0.

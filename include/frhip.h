@@ -188,6 +188,8 @@ typedef struct fr_conv_desc {
 #define FR_TILE_64x128_S3 9  /* 3-stage DMA ring, 2 blocks/CU */
 #define FR_TILE_IMG56 11     /* the same for 56x56x64->64 (layer1), 4-row bands */
 #define FR_TILE_IMG28 10     /* row-band direct 3x3/s1/p1 28x28x128->128 bf16 kernel (conv_img.hip); auto-selected (env FR_NO_IMG28=1: off) */
+#define FR_TILE_ROWS 12      /* persistent weight-resident 3x3/s1/p1 kernel for Cin = 64, Cout % 64 == 0, W % 56 == 0,
+                              * H % 4 == 0, bf16 (conv_rows.hip); auto-selected (env FR_NO_ROWS=1: off) */
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 

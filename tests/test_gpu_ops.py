@@ -134,6 +134,32 @@ def test_conv_img56(gpu, B):
     _close(y, conv_ref(x, w, pad=(1, 1), bias=bias, act=2, slope=slope))
 
 
+ROWS_CASES = [(1, 56, 56, 64), (3, 56, 56, 64), (1, 112, 112, 64), (2, 56, 56, 128), (2, 112, 56, 64),
+              (5, 56, 112, 128)]
+
+
+@pytest.mark.parametrize("case", ROWS_CASES)
+def test_conv_rows(gpu, case):
+    """Persistent weight-resident 64-input-channel kernel (conv_rows.hip, forced): the IResNet conv2
+    epilogue (bias + residual) and the conv1 one (PReLU), Cout 64 and 128 (two n-groups), 56- and
+    112-wide images (column halves), non-square images, batches whose unit count does not divide the
+    grid."""
+    B, H, W, Cout = case
+    g = torch.Generator().manual_seed(H + W + Cout + B)
+    x = torch.randn(B, H, W, 64, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(Cout, 64, 3, 3, generator=g) / np.sqrt(64 * 9)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    slope = torch.rand(Cout, generator=g) * 0.5
+    res = torch.randn(B, H, W, Cout, generator=g).to(torch.bfloat16).to(gpu)
+    y = conv_op(x, w, pad=(1, 1), bias=bias, res=res, tile=N.FR_TILE_ROWS)
+    _close(y, conv_ref(x, w, pad=(1, 1), bias=bias, res=res))
+    y = conv_op(x, w, pad=(1, 1), bias=bias, act=2, slope=slope, tile=N.FR_TILE_ROWS)
+    _close(y, conv_ref(x, w, pad=(1, 1), bias=bias, act=2, slope=slope))
+    # same bits as the implicit GEMM up to f32 summation order: compare against tile 0 tightly
+    y0 = conv_op(x, w, pad=(1, 1), bias=bias, act=2, slope=slope, tile=0)
+    _close(y, y0.float().cpu(), tol=1e-2)
+
+
 def test_conv_img28_channel_slices_and_applicability(gpu):
     """img28 reads channels [128:256) of a 256-ch buffer and writes [64:192) of another; other shapes
     are refused (fail loudly, no silent fallback)."""
@@ -349,7 +375,8 @@ def _border_class(H, W):
 
 BIAS9_CASES = [(2, 14, 14, 256, 256, None), (2, 14, 14, 256, 256, N.FR_TILE_BAND), (2, 28, 28, 128, 128, None),
                (2, 56, 56, 64, 64, 2), (2, 28, 28, 128, 128, 0), (2, 28, 28, 128, 128, N.FR_TILE_IMG28),
-               (2, 56, 56, 64, 64, N.FR_TILE_IMG56)]
+               (2, 56, 56, 64, 64, N.FR_TILE_IMG56), (2, 56, 56, 64, 64, N.FR_TILE_ROWS),
+               (1, 112, 112, 64, 64, N.FR_TILE_ROWS), (2, 56, 56, 64, 128, N.FR_TILE_ROWS)]
 
 
 @pytest.mark.parametrize("case", BIAS9_CASES)
