@@ -60,12 +60,21 @@ constexpr uint32_t OOB = 0x80000000u;
 #define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 1 no weight DMA in the loop, 2 no
                         // mid-step barrier / vmcnt wait, 4 no epilogue (MFMAs dead-code eliminated too),
                         // 8 trivial epilogue (MFMAs kept), 16 no patch reads in the loop, 32 no weight
-                        // fragment reads in the loop
+                        // fragment reads in the loop, 64 weight DMA from the first 3 slices only (L2-hot),
+                        // 128 epilogue tables replaced by constants (no global loads)
 #endif
 #ifndef FR_STAGE_SB
 #define FR_STAGE_SB 1  // scheduling barrier at each K-step start: MFMAs of step s+1 cannot be hoisted
                        // next to the refill reads of their weight fragments (exposed LDS latency)
 #endif
+#ifndef FR_STAGE_WAVES
+#define FR_STAGE_WAVES 8  // 8: two waves per SIMD, 64 output channels per wave (4: one per SIMD, 128 each;
+                          // 2.55 -> 2.44 ms on the 14x14 stage at bs=256: the second wave hides LDS and barrier waits)
+#endif
+constexpr int SNW = FR_STAGE_WAVES;          // waves per workgroup (2 pixel halves x SNW/2 channel groups)
+constexpr int FN = 16 / (SNW / 2);           // 16-channel fragments per wave (8 or 4)
+constexpr int NPW = 16 * FN;                 // output channels per wave
+constexpr int WPW = 16 / SNW;                // 1-KiB weight DMA pieces per wave per K-step
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -74,7 +83,7 @@ __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* 
 }
 
 template <bool F16>
-__global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
+__global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
     extern __shared__ __attribute__((aligned(16))) char smem[];  // [patch][slot0][slot1][slot2]
@@ -93,19 +102,19 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
     {
         const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * SPIX * SC * 2);
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
-        for (int u = 0; u < PATCH_B / 1024 / 4; ++u) {
-            const int piece = wave + 4 * u, q = piece * 64 + lane;
+        for (int u = 0; u < PATCH_B / 1024 / SNW; ++u) {
+            const int piece = wave + SNW * u, q = piece * 64 + lane;
             const int plane = q / PPOS, pos = q - plane * PPOS, r = pos / SWP, c = pos % SWP - 1;
             const uint32_t src = (unsigned)c < (unsigned)SW ? (uint32_t)((((b * SPIX + r * SW + c) * SC) + plane * 8) * 2) : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(smem + piece * 1024), 16, src, 0, 0, 0);
         }
     }
-    // weight slices of global K-steps 0..2 (4 pieces per wave each)
+    // weight slices of global K-steps 0..2 (WPW pieces per wave each)
     auto issue_w = [&](int g, int slot) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            dma16s(wr, smem + PATCH_B + slot * SLICE_B + (wave * 4 + u) * 1024, (uint32_t)((wave * 4 + u) * 1024 + lane * 16),
-                   (uint32_t)g * SLICE_B);
+        for (int u = 0; u < WPW; ++u)
+            dma16s(wr, smem + PATCH_B + slot * SLICE_B + (wave * WPW + u) * 1024,
+                   (uint32_t)((wave * WPW + u) * 1024 + lane * 16), (uint32_t)g * SLICE_B);
     };
     issue_w(0, 0);
     issue_w(1, 1);
@@ -119,10 +128,10 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
 #pragma unroll
     for (int j = 0; j < 7; ++j) aoff[j] = (lane >> 4) * PLANE_B + ((wm * 7 + j) * SWP + (lane & 15)) * 16;
     const int zoff = (lane >> 4) * PLANE_B;  // position 0 = left halo of row 0: a zero slot in every plane
-    const int boff = PATCH_B + (lane >> 4) * 4096 + (wn * 128 + (lane & 15)) * 16;
+    const int boff = PATCH_B + (lane >> 4) * 4096 + (wn * NPW + (lane & 15)) * 16;
 
-    f32x4_t acc[8][7];
-    frag wf[8], pA[7], pB[7];
+    f32x4_t acc[FN][7];
+    frag wf[FN], pA[7], pB[7];
     // patch fragments of (cg, tap): output row r = wm*7 + j reads source row r + dh - 1; rows -1 and 14
     // (wave 0 frag 0 at dh = 0, wave 1 frag 6 at dh = 2) are halo -> the zero slot
     auto pread = [&](frag (&pf)[7], int cg, int tap) {
@@ -142,47 +151,6 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
     // one K-step: MFMAs on (wf, cur); nxt <- patch fragments of (cg_n, tap_n) when has_next; mid-step
     // barrier; DMA of global step g+3 into this step's slot; wf <- slice of step g+1 in place.  The
     // slot of step s is s % 3 = tap % 3 (9 and 72 are multiples of 3): compile-time after unrolling.
-#if FR_STAGE_SB == 2
-    // explicit software pipeline: the whole next slice is read into registers right after the barrier
-    // (half a step before its first use), the DMA pieces and those reads interleaved with the MFMAs
-    auto kstep = [&](int g, int slot, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
-        __builtin_amdgcn_sched_barrier(0);
-        pread(nxt, cg_n, tap_n);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(7)\n\ts_barrier" ::: "memory");
-        issue_w(g + 3 < total ? g + 3 : total - 1, slot);
-        const int nslot = slot == NSLOT - 1 ? 0 : slot + 1;
-        frag wn[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wn[i] = *(const frag*)(smem + boff + nslot * SLICE_B + i * 256);
-#pragma unroll
-        for (int i = 4; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wf[i] = wn[i];
-#pragma unroll
-        for (int q = 0; q < 7; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    };
-#else
     auto kstep = [&](int g, int slot, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
 #if FR_STAGE_FENCE
         asm volatile("" ::: "memory");  // the previous step's refills stay ahead of this step's reads
@@ -194,7 +162,7 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
         pread(nxt, cg_n, tap_n);  // (after a conv's last step: unused reads, no branch)
 #endif
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FN / 2; ++i)
 #pragma unroll
             for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
 #if FR_STAGE_SCHED
@@ -213,20 +181,24 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
         // the 7 youngest LDS reads are this step's pread(nxt) (untouched by the DMA below: +4.5 % on the
         // stage); the older wf refills from slot `slot` must be done before anyone overwrites it
         // (checked in the ISA: the compiler waits for every earlier read before its MFMA use)
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(7)\n\ts_barrier" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(7)\n\ts_barrier" ::"n"(WPW) : "memory");
 #else
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(WPW) : "memory");
 #endif
 #if !(FR_STAGE_EXP & 1)
+#if FR_STAGE_EXP & 64
+        issue_w(slot, slot);
+#else
         issue_w(g + 3 < total ? g + 3 : total - 1, slot);
+#endif
 #endif
         const int nslot = slot == NSLOT - 1 ? 0 : slot + 1;
 #if !(FR_STAGE_EXP & 32)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) wread(i, nslot);
+        for (int i = 0; i < FN / 2; ++i) wread(i, nslot);
 #endif
 #pragma unroll
-        for (int i = 4; i < 8; ++i) {
+        for (int i = FN / 2; i < FN; ++i) {
 #pragma unroll
             for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
 #if !(FR_STAGE_EXP & 32)
@@ -252,7 +224,6 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
 #endif
     };
-#endif
 
     const size_t img = (size_t)b * SPIX * SC;
     // Epilogue tables (built at load time): ep[cv][9][256] = the conv's bias for each border class of the
@@ -262,7 +233,7 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
     // (image row 0) and j = 6 of wave row 1 (image row 13): two float4 per fragment cover every case.
     // The loads go through an opaque lane copy so that their ~50 addresses are not hoisted out of the K
     // loop (LICM would keep them live across it and spill).
-    auto load_ep = [&](int cv, float4 (&bi)[8], float4 (&be)[8]) {
+    auto load_ep = [&](int cv, float4 (&bi)[FN], float4 (&be)[FN]) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int cc = ln & 15, ccls = cc == 0 ? 0 : (cc == SW - 1 ? 2 : 1);
@@ -270,18 +241,23 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
         const float* epi = ep + (3 + ccls) * SC;              // interior rows
         const float* epe = ep + (wm ? 6 + ccls : ccls) * SC;  // this wave's border row (0 or 13)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int n = wn * 128 + 16 * i + 4 * (ln >> 4);
+        for (int i = 0; i < FN; ++i) {
+            const int n = wn * NPW + 16 * i + 4 * (ln >> 4);
+#if FR_STAGE_EXP & 128
+            bi[i] = make_float4(epi - ep + n, 0.f, 1.f, 2.f);
+            be[i] = make_float4(epe - ep + n, 0.f, 1.f, 2.f);
+#else
             bi[i] = *(const float4*)(epi + n);
             be[i] = *(const float4*)(epe + n);
+#endif
         }
     };
     auto is_edge = [&](int j) { return (j == 0 && wm == 0) || (j == 6 && wm == 1); };
     auto seed_bias = [&](int cv) {
-        float4 bi[8], be[8];
+        float4 bi[FN], be[FN];
         load_ep(cv, bi, be);
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < FN; ++i)
 #pragma unroll
             for (int j = 0; j < 7; ++j) {
                 const float4 bb = is_edge(j) ? be[i] : bi[i];
@@ -295,7 +271,7 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
         }
         pread(pA, 0, 0);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) wread(i, 0);  // step 0 of every conv sits in slot 0 (72 % 3 == 0)
+        for (int i = 0; i < FN; ++i) wread(i, 0);  // step 0 of every conv sits in slot 0 (72 % 3 == 0)
         const int g0 = cv * KSTEPS;
 #pragma unroll 1
         for (int cg = 0; cg < SC / 32; cg += 2) {
@@ -323,13 +299,13 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
         {
             float sum = 0.f;
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < FN; ++i)
 #pragma unroll
                 for (int j = 0; j < 7; ++j) sum += acc[i][j][0] + acc[i][j][3];
             if (sum == 1.2345f) p.y[lane] = 0;
             if (!second) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i)
+                for (int i = 0; i < FN; ++i)
 #pragma unroll
                     for (int j = 0; j < 7; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
             }
@@ -342,16 +318,21 @@ __global__ __launch_bounds__(256, 1) void stage_kernel(StageArgs p) {
         bf16_t* dbg = nullptr;
         if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
         const bool store_y = second && cv == nconv - 1;
-        float4 sl[8], bi[8], be[8];
+        float4 sl[FN], bi[FN], be[FN];
         if (!second) {
             load_ep(cv + 1, bi, be);  // conv2's bias: part of its accumulator seed
             const float* slp = p.slope + (size_t)cv * SC;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) sl[i] = *(const float4*)(slp + wn * 128 + 16 * i + 4 * (ln >> 4));
+            for (int i = 0; i < FN; ++i)
+#if FR_STAGE_EXP & 128
+                sl[i] = make_float4(0.25f, (float)i, 0.f, 0.f);
+#else
+                sl[i] = *(const float4*)(slp + wn * NPW + 16 * i + 4 * (ln >> 4));
+#endif
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int n = wn * 128 + 16 * i + 4 * (ln >> 4);
+        for (int i = 0; i < FN; ++i) {
+            const int n = wn * NPW + 16 * i + 4 * (ln >> 4);
             char* slot0 = smem + (n >> 3) * PLANE_B + (wm * 112 + cc + 1) * 16 + (n & 7) * 2;
             // conv1: all 7 identity reads of this n-fragment first (one LDS latency per fragment)
             uint2 xin[7];
@@ -426,9 +407,9 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t s) {
         attr[a.f16 ? 1 : 0] = true;
     }
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, dim3(a.B), dim3(256), STAGE_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
+        hipExtLaunchKernelGGL(k, dim3(a.B), dim3(64 * SNW), STAGE_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
     else
-        hipLaunchKernelGGL(k, dim3(a.B), dim3(256), STAGE_LDS, s, a);
+        hipLaunchKernelGGL(k, dim3(a.B), dim3(64 * SNW), STAGE_LDS, s, a);
     return hipGetLastError();
 }
 
