@@ -386,16 +386,17 @@ bool stage_supported(int B, int H, int W, int C) { return B > 0 && H == SW && W 
 
 size_t stage_weight_bytes(int nconv) { return (size_t)nconv * KSTEPS * SLICE_B; }
 
-// Packs one conv's [256][Kpad] row-major weights (K order (kh, kw, c)) into the stage's K-step
-// image: step s = cg*9 + tap, [4 groups g][256 rows n][8 channels] with channel 32cg + 8g + e.
-void stage_pack_weights(const bf16_t* rows, int Kpad, bf16_t* out) {
-    for (int cg = 0; cg < SC / 32; ++cg)
+// Packs one conv's [C][Kpad] row-major weights (K order (kh, kw, c)) into a stage's K-step image:
+// step s = cg*9 + tap, [4 groups g][C rows n][8 channels] with channel 32cg + 8g + e (C = 256 here,
+// 128 for the layer2 stage, conv_stage28.hip).
+void stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out) {
+    for (int cg = 0; cg < C / 32; ++cg)
         for (int tap = 0; tap < 9; ++tap) {
-            bf16_t* s = out + (size_t)(cg * 9 + tap) * (SLICE_B / 2);
+            bf16_t* s = out + (size_t)(cg * 9 + tap) * 4 * C * 8;
             for (int g = 0; g < 4; ++g)
-                for (int n = 0; n < SC; ++n)
+                for (int n = 0; n < C; ++n)
                     for (int e = 0; e < 8; ++e)
-                        s[(g * 256 + n) * 8 + e] = rows[(size_t)n * Kpad + tap * SC + cg * 32 + g * 8 + e];
+                        s[(g * C + n) * 8 + e] = rows[(size_t)n * Kpad + tap * C + cg * 32 + g * 8 + e];
         }
 }
 

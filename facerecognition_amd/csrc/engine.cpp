@@ -74,9 +74,11 @@ struct Op {
     bool fuse_stem = false;  // OP_PRE of IResNet100: u8 input runs preprocess + the next (stem) conv fused
 };
 
-// One LDS-resident stage (conv_stage.hip): blocks [first, first+nblk) of a 14x14x256 layer.
+// One LDS-resident stage: the stride-1 blocks of a 14x14x256 layer (conv_stage.hip, geo 0: one
+// workgroup per image) or of a 28x28x128 layer (conv_stage28.hip, geo 1: two workgroups per image).
 struct StageRec {
     int in = -1, out = -1, nblk = 0;
+    int geo = 0, H = 14, C = 256;
     std::vector<int> conv_ops;            // member OP_CONV indices, conv1/conv2 alternating
     std::vector<int> t_tensors, x_tensors;  // per block: conv1 output, block output
     bf16_t* w = nullptr;                  // packed K-step weight images
@@ -146,6 +148,9 @@ struct fr_handle {
     int proj_d = 0;
     float* emb_pre = nullptr;  // [max_batch][512] IRV1 output before the projection
     float* amax = nullptr;     // FR_DTYPE_FP8: per-tensor max |x| of the current forward [ntensors]
+    bf16_t* stage_xchg = nullptr;  // split-stage boundary rows [max_batch][2][2][28][128] (reserve)
+    int* stage_flags = nullptr;    // split-stage per-half progress counters [max_batch][2]
+    int* stage_spin = nullptr;     // split-stage bounded-wait overruns (fr_debug_stage_timeouts)
     int stage_mode = 1;       // FR_OPT_STAGE: 0 off, 1 auto (stage_runs), 2 always
     int stage_min_fill = 80;  // FR_OPT_STAGE_MIN_FILL (percent)
     int n_cu = 256;
@@ -188,6 +193,8 @@ void free_acts(fr_handle* h) {
     drop_graphs(h);
     for (void* p : h->act_allocs) (void)hipFree(p);
     h->act_allocs.clear();
+    h->stage_xchg = nullptr;
+    h->stage_flags = nullptr;
     for (auto& t : h->tensors) t.dev = nullptr;
     h->partial = nullptr;
     h->partial_floats = 0;
@@ -477,16 +484,17 @@ struct Builder {
 
 // Packs a stage's weights (from the member convs' [Npad][Kpad] device images) and its epilogue table.
 int build_stage(fr_handle* h, StageRec& r) {
-    const int nconv = 2 * r.nblk;
-    std::vector<bf16_t> packed(stage_weight_bytes(nconv) / sizeof(bf16_t));
+    const int nconv = 2 * r.nblk, C = r.C;
+    const size_t wbytes = r.geo ? stage28_weight_bytes(nconv) : stage_weight_bytes(nconv);
+    std::vector<bf16_t> packed(wbytes / sizeof(bf16_t));
     std::vector<StageConv> tab(nconv);
-    std::vector<float> ep((size_t)nconv * 9 * 256, 0.f), sl((size_t)nconv * 256, 0.f);
+    std::vector<float> ep((size_t)nconv * 9 * C, 0.f), sl((size_t)nconv * C, 0.f);
     const size_t per = packed.size() / nconv;
     for (int c = 0; c < nconv; ++c) {
         const Op& op = h->ops[r.conv_ops[c]];
         const DevConvW& cw = h->convw[op.wi];
-        if (cw.Cout != 256 || cw.Npad != 256 || cw.Kh != 3 || cw.Kw != 3 || cw.Cin != 256) {
-            set_error("plan: stage member conv is not 3x3 256->256");
+        if (cw.Cout != C || cw.Npad < C || cw.Kh != 3 || cw.Kw != 3 || cw.Cin != C) {
+            set_error("plan: stage member conv is not 3x3 " + std::to_string(C) + "->" + std::to_string(C));
             return FR_ERR_ARG;
         }
         // the stage kernel's epilogues are specialised: conv1 = bias + PReLU, conv2 = bias + identity
@@ -496,25 +504,27 @@ int build_stage(fr_handle* h, StageRec& r) {
         }
         std::vector<bf16_t> rows((size_t)cw.Npad * cw.Kpad);
         FR_HIP_CHECK(hipMemcpy(rows.data(), cw.w, rows.size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
-        stage_pack_weights(rows.data(), cw.Kpad, packed.data() + c * per);
+        stage_pack_weights(rows.data(), cw.Kpad, C, packed.data() + c * per);
         tab[c].bias = cw.bias9 ? nullptr : cw.bias;
         tab[c].bias9 = cw.bias9;
         tab[c].slope = cw.slope;
         tab[c].act = op.act;
         // the epilogue's per-class bias: bias9 (which already carries the whole bias) or bias x 9
-        float* e = ep.data() + (size_t)c * 9 * 256;
+        // (bias9 rows are Npad apart)
+        float* e = ep.data() + (size_t)c * 9 * C;
         if (cw.bias9) {
-            FR_HIP_CHECK(hipMemcpy(e, cw.bias9, 9 * 256 * sizeof(float), hipMemcpyDeviceToHost));
+            for (int k = 0; k < 9; ++k)
+                FR_HIP_CHECK(hipMemcpy(e + k * C, cw.bias9 + (size_t)k * cw.Npad, C * sizeof(float), hipMemcpyDeviceToHost));
         } else if (cw.bias) {
-            FR_HIP_CHECK(hipMemcpy(e, cw.bias, 256 * sizeof(float), hipMemcpyDeviceToHost));
-            for (int k = 1; k < 9; ++k) std::copy(e, e + 256, e + k * 256);
+            FR_HIP_CHECK(hipMemcpy(e, cw.bias, C * sizeof(float), hipMemcpyDeviceToHost));
+            for (int k = 1; k < 9; ++k) std::copy(e, e + C, e + k * C);
         }
         // negative-side factor of the activation: PReLU slope, 0 for ReLU, 1 for none
-        float* f = sl.data() + (size_t)c * 256;
+        float* f = sl.data() + (size_t)c * C;
         if (op.act == 2 && cw.slope)
-            FR_HIP_CHECK(hipMemcpy(f, cw.slope, 256 * sizeof(float), hipMemcpyDeviceToHost));
+            FR_HIP_CHECK(hipMemcpy(f, cw.slope, C * sizeof(float), hipMemcpyDeviceToHost));
         else
-            std::fill(f, f + 256, op.act == 1 ? 0.f : 1.f);
+            std::fill(f, f + C, op.act == 1 ? 0.f : 1.f);
     }
     int rc = upload(h, &r.w, packed);
     if (rc) return rc;
@@ -526,6 +536,12 @@ int build_stage(fr_handle* h, StageRec& r) {
     if ((rc = dev_alloc(&d, (size_t)nconv * sizeof(bf16_t*)))) return rc;
     h->weight_allocs.push_back(d);
     r.dbg = (bf16_t**)d;
+    if (r.geo == 1 && !h->stage_spin) {
+        if ((rc = dev_alloc(&d, sizeof(int)))) return rc;
+        h->weight_allocs.push_back(d);
+        h->stage_spin = (int*)d;
+        FR_HIP_CHECK(hipMemset(h->stage_spin, 0, sizeof(int)));
+    }
     return FR_OK;
 }
 
@@ -560,13 +576,18 @@ void build_iresnet100(Builder& b) {
     int H = 112, C = 64;
     for (int l = 0; l < 4; ++l) {
         const int P = planes[l], Ho = H / 2;
-        // layer3 blocks 1.. (stride 1, 14x14x256): also emitted as one LDS-resident stage op
+        // layer3 blocks 1.. (stride 1, 14x14x256) and layer2 blocks 1.. (28x28x128): also emitted as one
+        // LDS-resident stage op each
         int st_op = -1;
         StageRec rec;
         for (int i = 0; i < nblk[l]; ++i) {
-            if (i == 1 && h->dtype != FR_DTYPE_FP8 && stage_supported(1, Ho, Ho, P) && P == C) {
+            const bool s14 = stage_supported(1, Ho, Ho, P), s28 = stage28_supported(Ho, Ho, P);
+            if (i == 1 && h->dtype != FR_DTYPE_FP8 && (s14 || s28) && P == C) {
                 st_op = (int)h->ops.size();
                 rec.in = x;
+                rec.geo = s28 ? 1 : 0;
+                rec.H = Ho;
+                rec.C = P;
                 Op op;
                 op.kind = OP_STAGE;
                 op.stage = (int)h->stages.size();
@@ -837,6 +858,17 @@ int reserve(fr_handle* h, int maxB) {
         h->act_allocs.push_back(q);
         h->emb_pre = (float*)q;
     }
+    if (std::any_of(h->stages.begin(), h->stages.end(), [](const StageRec& r) { return r.geo == 1; })) {
+        void* q = nullptr;
+        rc = dev_alloc(&q, stage28_xchg_elems(maxB) * sizeof(bf16_t));
+        if (rc) { free_acts(h); return rc; }
+        h->act_allocs.push_back(q);
+        h->stage_xchg = (bf16_t*)q;
+        rc = dev_alloc(&q, (size_t)maxB * 2 * sizeof(int));
+        if (rc) { free_acts(h); return rc; }
+        h->act_allocs.push_back(q);
+        h->stage_flags = (int*)q;
+    }
     return fill_stage_dbg(h);
 }
 
@@ -1059,22 +1091,45 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
 // either way, since per-conv grids of B*196 positions are a handful of tiles.  Above one round a last
 // round that is mostly empty costs a whole stage time, so auto mode then requires the rounds to be at
 // least stage_min_fill % full (B = 512: 100 %, B = 257: 50 % -> per-conv).
-static bool stage_runs(const fr_handle* h, int B) {
-    if (h->stage_mode == 0 || h->stages.empty()) return false;
-    if (h->stage_mode == 2 || B <= h->n_cu) return true;
-    const int64_t rounds = (B + h->n_cu - 1) / h->n_cu;
-    return (int64_t)B * 100 >= (int64_t)h->stage_min_fill * rounds * h->n_cu;
+// The layer2 split stage puts one image on two CUs: a round is n_cu / 2 images.
+static bool stage28_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_STAGE28");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
+static bool stage_runs(const fr_handle* h, int B, const StageRec& r) {
+    if (h->stage_mode == 0) return false;
+    if (r.geo == 1 && !stage28_enabled()) return false;
+    const int cap = std::max(1, r.geo == 1 ? h->n_cu / 2 : h->n_cu);
+    if (h->stage_mode == 2 || B <= cap) return true;
+    const int64_t rounds = (B + cap - 1) / cap;
+    return (int64_t)B * 100 >= (int64_t)h->stage_min_fill * rounds * cap;
+}
+
+// Per-op skip rule: a stage op runs when its stage runs; its member convs run when it does not.
+static std::vector<char> stage_plan(const fr_handle* h, int B) {
+    std::vector<char> run(h->stages.size());
+    for (size_t i = 0; i < run.size(); ++i) run[i] = stage_runs(h, B, h->stages[i]);
+    return run;
+}
+
+static bool op_skipped(const Op& op, const std::vector<char>& run) {
+    if (op.kind == OP_STAGE) return !run[op.stage];
+    return op.stage >= 0 && run[op.stage];
 }
 
 int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
     const int f16 = h->dtype == FR_DTYPE_F16;
-    const bool use_stage = stage_runs(h, B);
+    const std::vector<char> stage_run = stage_plan(h, B);
     if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s));
     bool skip_next = false;
     for (size_t oi = 0; oi < h->ops.size(); ++oi) {
         const Op& op = h->ops[oi];
         if (skip_next) { skip_next = false; continue; }
-        if (op.kind == OP_STAGE ? !use_stage : (op.stage >= 0 && use_stage)) continue;
+        if (op_skipped(op, stage_run)) continue;
         switch (op.kind) {
             case OP_STAGE: {
                 const StageRec& r = h->stages[op.stage];
@@ -1090,10 +1145,13 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.nblk = r.nblk;
                 a.f16 = f16;
                 a.dbg = stage_dbg();
+                a.xchg = h->stage_xchg;
+                a.flags = h->stage_flags;
+                a.spin_timeouts = h->stage_spin;
                 ProfScope ps(h, s);
-                ps.flops = 2.0 * r.nblk * 2.0 * B * 196.0 * 256.0 * 2304.0;
-                ps.start("stage layer3");
-                FR_HIP_CHECK(launch_stage(a, s));
+                ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
+                ps.start(r.geo == 1 ? "stage layer2" : "stage layer3");
+                FR_HIP_CHECK(r.geo == 1 ? launch_stage28(a, s) : launch_stage(a, s));
                 break;
             }
             case OP_PRE: {
@@ -1504,13 +1562,14 @@ int fr_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, i
 int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
     if (!h || !buf || n == 0 || B <= 0) { set_error("fr_debug_plan: bad argument"); return FR_ERR_ARG; }
     std::string out;
-    const bool use_stage = stage_runs(h, B);
+    const std::vector<char> stage_run = stage_plan(h, B);
     for (const auto& op : h->ops) {
-        if (op.kind == OP_STAGE ? !use_stage : (op.stage >= 0 && use_stage)) continue;
+        if (op_skipped(op, stage_run)) continue;
         if (op.kind == OP_STAGE) {
             const StageRec& r = h->stages[op.stage];
-            out += "stage " + std::to_string(B * 196) + " 256 2304 2304 " + std::to_string(2 * r.nblk) + " 1 3x3 " +
-                   h->tensors[r.out].name + "\n";
+            const std::string K = std::to_string(9 * r.C);
+            out += "stage " + std::to_string(B * r.H * r.H) + " " + std::to_string(r.C) + " " + K + " " + K + " " +
+                   std::to_string(2 * r.nblk) + " 1 3x3 " + h->tensors[r.out].name + "\n";
             continue;
         }
         if (op.kind != OP_CONV && op.kind != OP_HEAD) {
@@ -1595,6 +1654,17 @@ int fr_debug_match_fallbacks(fr_handle* h) {
     FR_HIP_CHECK(hipSetDevice(h->device));
     FR_HIP_CHECK(hipDeviceSynchronize());
     FR_HIP_CHECK(hipMemcpy(&v, h->match_fb, sizeof(int), hipMemcpyDeviceToHost));
+    return v;
+}
+
+int fr_debug_stage_timeouts(fr_handle* h) {
+    if (!h) return FR_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!h->stage_spin) return 0;
+    int v = 0;
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    FR_HIP_CHECK(hipDeviceSynchronize());
+    FR_HIP_CHECK(hipMemcpy(&v, h->stage_spin, sizeof(int), hipMemcpyDeviceToHost));
     return v;
 }
 

@@ -238,6 +238,10 @@ int fr_get_option(const fr_handle* h, int option);
 /* Number of probes (since the gallery was first split) whose bf16x3 candidate proof failed and were
  * rescanned exactly (synchronizes the device). */
 int fr_debug_match_fallbacks(fr_handle* h);
+/* Number of bounded waits of the layer2 split stage kernel (two workgroups per image exchanging a
+ * boundary row per conv) that ran out before the partner published; 0 on a healthy device.  Each one
+ * means that image's embedding is wrong (synchronizes the device). */
+int fr_debug_stage_timeouts(fr_handle* h);
 
 /* ---- debug: named intermediate tensors of the forward plan (per-layer drift tests) ----
  * Tensor names are the reference/oracle module whose output the tensor equals

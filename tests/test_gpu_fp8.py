@@ -18,8 +18,11 @@ from facerecognition_amd import _native as N
 
 pytestmark = pytest.mark.gpu
 
-COS_VS_BF16 = 2e-2     # 1 - cos(fp8, bf16) per face (e4m3 has 3 mantissa bits; stated in DESIGN.md)
-COS_VS_ORACLE = 2e-2   # 1 - cos(fp8, fp32 oracle)
+COS_VS_BF16 = 1e-3     # cosine(fp8, bf16) >= 0.999 per face -- NOT met (xfail below)
+# Regression guard only, not a parity claim: e4m3 activations and weights with per-tensor / per-channel
+# scales measure 1 - cos = 0.008 .. 0.011 against bf16 and the fp32 oracle; a broken
+# fp8 path (wrong scale, lost K-block) lands at 0.1 .. 1.
+FP8_GUARD = 2e-2
 
 
 def _fp8(t):
@@ -120,24 +123,43 @@ def test_conv_fp8_large_activations_no_nan(gpu):
     assert ((y - ref).abs() <= 1e-2 * (ref.abs() + ref.abs().max() / 8)).all()
 
 
-def test_iresnet100_fp8_vs_bf16_and_oracle(gpu):
+def _fp8_vs_bf16(u8):
     from facerecognition_amd.model import FRModel
-    from facerecognition_amd.synthetic import synthetic_crops
     from facerecognition_amd.weights import synth_state_dict
-    from oracle import models as M
     sd = synth_state_dict("iresnet100")
-    u8 = synthetic_crops(6, 112, seed=4)
     m8 = FRModel("iresnet100", sd, dtype="fp8")
     mb = FRModel("iresnet100", sd, dtype="bf16")
     e8 = m8.embed(torch.from_numpy(u8)).cpu().numpy()
     eb = mb.embed(torch.from_numpy(u8)).cpu().numpy()
+    m8.close()
+    mb.close()
+    return sd, e8, eb
+
+
+@pytest.mark.xfail(strict=False, reason="fp8 (e4m3 activations + weights, per-tensor activation scale) measures "
+                   "1-cos 0.008-0.011 vs bf16; the config-5 bar is 1e-3 (DESIGN.md §5)")
+def test_iresnet100_fp8_meets_config5_bar(gpu):
+    from facerecognition_amd.synthetic import synthetic_crops
+    _, e8, eb = _fp8_vs_bf16(synthetic_crops(6, 112, seed=4))
+    c_b = np.sum(e8 * eb, axis=1)
+    print(f"\nfp8 vs bf16 1-cos: {1 - c_b}")
+    assert np.all(1 - c_b <= COS_VS_BF16), f"fp8 vs bf16: 1-cos = {1 - c_b}"
+
+
+def test_iresnet100_fp8_guard_and_top1(gpu):
+    """Regression guard (FP8_GUARD, see above) against bf16 and the fp32 oracle, and identical top-1 on a
+    planted gallery."""
+    from facerecognition_amd.synthetic import synthetic_crops
+    from oracle import models as M
+    u8 = synthetic_crops(6, 112, seed=4)
+    sd, e8, eb = _fp8_vs_bf16(u8)
     ref = M.embed(M.build_model("iresnet100", sd), "iresnet100", u8)
     c_b = np.sum(e8 * eb, axis=1)
     c_o = np.sum(e8 * ref, axis=1) / np.linalg.norm(ref, axis=1)
     print(f"\nfp8 vs bf16 1-cos: {1 - c_b}\nfp8 vs oracle 1-cos: {1 - c_o}")
     assert np.all(np.isfinite(e8))
-    assert np.all(1 - c_b <= COS_VS_BF16), f"fp8 vs bf16: 1-cos = {1 - c_b}"
-    assert np.all(1 - c_o <= COS_VS_ORACLE), f"fp8 vs oracle: 1-cos = {1 - c_o}"
+    assert np.all(1 - c_b <= FP8_GUARD), f"fp8 vs bf16: 1-cos = {1 - c_b}"
+    assert np.all(1 - c_o <= FP8_GUARD), f"fp8 vs oracle: 1-cos = {1 - c_o}"
     # identical top-1 on a planted gallery (rows = normalize(ref + 0.05 noise) + distractors)
     rng = np.random.default_rng(11)
     G = rng.standard_normal((1000, 512)).astype(np.float32)
@@ -149,5 +171,41 @@ def test_iresnet100_fp8_vs_bf16_and_oracle(gpu):
     _, ib = gal.search(eb, 1)
     assert np.array_equal(i8[:, 0], np.arange(6)) and np.array_equal(ib[:, 0], np.arange(6))
     gal.close()
+
+
+def test_iresnet100_fp8_bs256(gpu):
+    """BASELINE config-5 size (IResNet100 fp8, bs = 256, the autotuner's bs=256 tiles): deterministic replay,
+    finite unit-norm rows, the distribution of 1-cos against bf16 at the same batch (guard bar; the spec
+    bar is the xfail above), an oracle sample, and identical top-1 on a planted 10k gallery."""
+    from facerecognition_amd.gallery import DeviceGallery
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    from facerecognition_amd.weights import synth_state_dict
+    from oracle import models as M
+    sd = synth_state_dict("iresnet100")
+    u8 = synthetic_crops(256, 112, seed=41)
+    m8 = FRModel("iresnet100", sd, dtype="fp8")
+    a = m8.embed(torch.from_numpy(u8)).cpu()
+    b = m8.embed(torch.from_numpy(u8)).cpu()
+    assert torch.equal(a, b), "fp8 forward is not deterministic at bs=256"
+    assert torch.isfinite(a).all() and torch.allclose(a.norm(dim=1), torch.ones(256), atol=1e-5)
     m8.close()
+    mb = FRModel("iresnet100", sd, dtype="bf16")
+    eb = mb.embed(torch.from_numpy(u8)).cpu().numpy()
     mb.close()
+    d = 1 - np.sum(a.numpy() * eb, axis=1)
+    print(f"\nfp8 vs bf16 at bs=256: 1-cos median {np.median(d):.4g}, p99 {np.quantile(d, 0.99):.4g}, max {d.max():.4g}, "
+          f"share <= 1e-3: {np.mean(d <= COS_VS_BF16):.3f}")
+    assert d.max() <= FP8_GUARD
+    ref = M.embed(M.build_model("iresnet100", sd), "iresnet100", u8[:3])
+    c_o = (a[:3].numpy() * ref).sum(1) / np.linalg.norm(ref, axis=1)
+    assert float((1 - c_o).max()) <= FP8_GUARD, 1 - c_o
+    rng = np.random.default_rng(42)
+    G = rng.standard_normal((10000, 512)).astype(np.float32)
+    perm = rng.permutation(10000)[:256]
+    G[perm] = a.numpy() + 0.03 * rng.standard_normal((256, 512)).astype(np.float32)
+    G /= np.linalg.norm(G, axis=1, keepdims=True)
+    gal = DeviceGallery(G)
+    _, idx = gal.search(a.numpy(), 5)
+    assert np.array_equal(idx[:, 0], perm)
+    gal.close()
