@@ -14,17 +14,17 @@
 //     PReLU(conv1(x)) straight into it, after reading x from the same positions to seed conv2's
 //     accumulators (the identity), and conv2's epilogue writes x' = (x + conv2(t)) + bias back: no
 //     global traffic at all between the first patch load and the last block's NHWC store;
-//   * the weights stream through a 3-slot LDS ring of 16 KiB K-steps (32 input channels x one tap x 256
-//     output channels), pre-packed in exactly the LDS image so each DMA piece is a contiguous 1 KiB;
-//     the DMA stream runs three K-steps ahead across conv boundaries (two steps of latency cover), so a
-//     new conv never waits for its first weights;
-//   * one s_barrier per K-step, mid-step: after it the slice of step s+1 has landed everywhere and the
-//     slot of step s is free for step s+3; the weight fragments of step s+1 are refilled in place as
-//     each one retires, the patch fragments of step s+1 are read during step s.
-// MFMA geometry = conv3x3_bandp_kernel<14,14,2,2,7,8>: 2x2 waves, each 112 patch positions (7 m-frags,
-// columns 14/15 computed and discarded) x 128 channels (8 n-frags), v_mfma_f32_16x16x32_{bf16,f16};
-// operand A = weight rows, operand B = patch positions, so a lane ends with 4 consecutive channels of
-// one pixel.
+//   * the weights of one K-step (32 input channels x one tap x 256 output channels, 16 KiB, pre-packed
+//     as [4 channel groups][256 rows][16 B]) go straight from L2 into registers: each wave loads the
+//     four 16-channel A fragments of its 64 output channels (4 x 16 B per lane) into a 3-step register
+//     ring, two steps ahead and across conv boundaries.  Every CU runs the same K-step of the same
+//     weights at about the same time, so the stream is L2-resident.  The patch is the only LDS data and
+//     it is read-only inside a conv: the K loop has no barrier at all (a 3-slot LDS-DMA ring with one
+//     mid-step barrier per K-step ran 2.50 ms vs 2.38 ms for this at bs = 256, same box);
+//   * 8 waves = 2 pixel halves (7 rows = 7 m-frags of 16 positions, columns 14/15 computed and
+//     discarded) x 4 channel groups (64 channels = 4 n-frags): 28 v_mfma_f32_16x16x32_{bf16,f16} per wave
+//     per K-step, two waves per SIMD (the second hides the first's LDS and L2 waits); operand A =
+//     weight rows, operand B = patch positions, so a lane ends with 4 consecutive channels of one pixel.
 #include "kernels.h"
 
 #include <hip/hip_ext.h>
@@ -41,52 +41,26 @@ constexpr int SPIX = SW * SW;                // 196
 constexpr int PPOS = SW * SWP;               // 224 stored positions per plane (rows 0..13)
 constexpr int PLANE_B = PPOS * 16;           // 3584: one 8-channel plane
 constexpr int PATCH_B = (SC / 8) * PLANE_B;  // 114688
-constexpr int SLICE_B = 4 * 256 * 16;        // 16384: [4 groups of 8 ch][256 rows][16 B]
-constexpr int NSLOT = 3;
-constexpr int STAGE_LDS = PATCH_B + NSLOT * SLICE_B;  // 163840 = the whole 160 KiB
+constexpr int SLICE_B = 4 * 256 * 16;        // 16384: one K-step of packed weights [4 groups of 8 ch][256 rows][16 B]
+constexpr int STAGE_LDS = PATCH_B;
 constexpr int KSTEPS = (SC / 32) * 9;        // 72 per conv
 constexpr uint32_t OOB = 0x80000000u;
-
-#ifndef FR_STAGE_FENCE
-#define FR_STAGE_FENCE 1  // compiler fence at each K-step start (keeps the lgkmcnt(7) wait exact)
-#endif
-#ifndef FR_STAGE_LGKM7
-#define FR_STAGE_LGKM7 1  // mid-step wait leaves this step's 7 patch reads in flight (0: drain all)
-#endif
-#ifndef FR_STAGE_SCHED
-#define FR_STAGE_SCHED 0  // explicit MFMA / ds_read / DMA interleave (sched_group_barrier)
-#endif
-#ifndef FR_STAGE_EXP
-#define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 1 no weight DMA in the loop, 2 no
-                        // mid-step barrier / vmcnt wait, 4 no epilogue (MFMAs dead-code eliminated too),
-                        // 8 trivial epilogue (MFMAs kept), 16 no patch reads in the loop, 32 no weight
-                        // fragment reads in the loop, 64 weight DMA from the first 3 slices only (L2-hot),
-                        // 128 epilogue tables replaced by constants (no global loads)
-#endif
-#ifndef FR_STAGE_SB
-#define FR_STAGE_SB 1  // scheduling barrier at each K-step start: MFMAs of step s+1 cannot be hoisted
-                       // next to the refill reads of their weight fragments (exposed LDS latency)
-#endif
-#ifndef FR_STAGE_WAVES
-#define FR_STAGE_WAVES 8  // 8: two waves per SIMD, 64 output channels per wave (4: one per SIMD, 128 each;
-                          // 2.55 -> 2.44 ms on the 14x14 stage at bs=256: the second wave hides LDS and barrier waits)
-#endif
-constexpr int SNW = FR_STAGE_WAVES;          // waves per workgroup (2 pixel halves x SNW/2 channel groups)
-constexpr int FN = 16 / (SNW / 2);           // 16-channel fragments per wave (8 or 4)
+constexpr int SNW = 8;                       // waves per workgroup: 2 pixel halves x 4 channel groups
+constexpr int FN = 4;                        // 16-channel fragments per wave
 constexpr int NPW = 16 * FN;                 // output channels per wave
-constexpr int WPW = 16 / SNW;                // 1-KiB weight DMA pieces per wave per K-step
+
+#ifndef FR_STAGE_EXP
+#define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 8 trivial epilogue (MFMAs kept), 16 no
+                        // patch reads in the loop, 128 epilogue tables replaced by constants (no loads)
+#endif
 
 typedef __attribute__((address_space(3))) void lds_void;
-
-__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff, uint32_t soff) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, soff, 0, 0);
-}
 
 template <bool F16>
 __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
-    extern __shared__ __attribute__((aligned(16))) char smem[];  // [patch][slot0][slot1][slot2]
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // the patch
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -109,29 +83,19 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(smem + piece * 1024), 16, src, 0, 0, 0);
         }
     }
-    // weight slices of global K-steps 0..2 (WPW pieces per wave each)
-    auto issue_w = [&](int g, int slot) {
-#pragma unroll
-        for (int u = 0; u < WPW; ++u)
-            dma16s(wr, smem + PATCH_B + slot * SLICE_B + (wave * WPW + u) * 1024,
-                   (uint32_t)((wave * WPW + u) * 1024 + lane * 16), (uint32_t)g * SLICE_B);
-    };
-    issue_w(0, 0);
-    issue_w(1, 1);
-    issue_w(2, 2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
     // fragment addresses: B (patch) rows m = wm*112 + 16j + (lane&15) at plane (lane>>4) of the group;
-    // A (weights) rows n = wn*128 + 16i + (lane&15) in group (lane>>4)
+    // A (weights) rows n = wn*64 + 16i + (lane&15) in group (lane>>4) of the K-step's packed image
     int aoff[7];
 #pragma unroll
     for (int j = 0; j < 7; ++j) aoff[j] = (lane >> 4) * PLANE_B + ((wm * 7 + j) * SWP + (lane & 15)) * 16;
     const int zoff = (lane >> 4) * PLANE_B;  // position 0 = left halo of row 0: a zero slot in every plane
-    const int boff = PATCH_B + (lane >> 4) * 4096 + (wn * NPW + (lane & 15)) * 16;
+    const uint32_t wvo = (uint32_t)((lane >> 4) * 4096 + (wn * NPW + (lane & 15)) * 16);
 
     f32x4_t acc[FN][7];
-    frag wf[FN], pA[7], pB[7];
+    frag pA[7], pB[7];
     // patch fragments of (cg, tap): output row r = wm*7 + j reads source row r + dh - 1; rows -1 and 14
     // (wave 0 frag 0 at dh = 0, wave 1 frag 6 at dh = 2) are halo -> the zero slot
     auto pread = [&](frag (&pf)[7], int cg, int tap) {
@@ -146,83 +110,29 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
             pf[j] = *(const frag*)a;
         }
     };
-    auto wread = [&](int i, int slot) { wf[i] = *(const frag*)(smem + boff + slot * SLICE_B + i * 256); };
-
-    // one K-step: MFMAs on (wf, cur); nxt <- patch fragments of (cg_n, tap_n) when has_next; mid-step
-    // barrier; DMA of global step g+3 into this step's slot; wf <- slice of step g+1 in place.  The
-    // slot of step s is s % 3 = tap % 3 (9 and 72 are multiples of 3): compile-time after unrolling.
-    auto kstep = [&](int g, int slot, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
-#if FR_STAGE_FENCE
-        asm volatile("" ::: "memory");  // the previous step's refills stay ahead of this step's reads
-#endif
-#if FR_STAGE_SB
+    // weight fragments of global K-step g: a 3-step register ring, loads two steps ahead.  The ring slot
+    // of step g is g % 3 = tap % 3 (9 and 72 are multiples of 3): compile-time after unrolling
+    frag wq[3][FN];
+    auto wload = [&](frag (&w)[FN], int g) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+            w[i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wvo + i * 256, (uint32_t)g * SLICE_B, 0));
+    };
+    wload(wq[0], 0);
+    wload(wq[1], 1);
+    // one K-step: nxt <- patch fragments of (cg_n, tap_n) (after a conv's last step: unused reads, no
+    // branch); weights of step g+2 (clamped: the tail re-fetches the last step); 28 MFMAs on (wq[r], cur)
+    auto kstep = [&](int g, int r, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-#endif
 #if !(FR_STAGE_EXP & 16)
-        pread(nxt, cg_n, tap_n);  // (after a conv's last step: unused reads, no branch)
+        pread(nxt, cg_n, tap_n);
 #endif
+        wload(wq[(r + 2) % 3], g + 2 < total ? g + 2 : total - 1);
 #pragma unroll
-        for (int i = 0; i < FN / 2; ++i)
+        for (int i = 0; i < FN; ++i)
 #pragma unroll
-            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
-#if FR_STAGE_SCHED
-        // first half: one patch read after every 4 MFMAs
-#pragma unroll
-        for (int q = 0; q < 7; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-#endif
-        // slice g+1 landed (this wave); the 4 pieces of slice g+2 may stay in flight.  Branch-free: the
-        // tail re-fetches the last slice into the free slot and reads clamped slots (static counts)
-#if FR_STAGE_EXP & 2
-        asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
-#elif FR_STAGE_LGKM7
-        // the 7 youngest LDS reads are this step's pread(nxt) (untouched by the DMA below: +4.5 % on the
-        // stage); the older wf refills from slot `slot` must be done before anyone overwrites it
-        // (checked in the ISA: the compiler waits for every earlier read before its MFMA use)
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(7)\n\ts_barrier" ::"n"(WPW) : "memory");
-#else
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(WPW) : "memory");
-#endif
-#if !(FR_STAGE_EXP & 1)
-#if FR_STAGE_EXP & 64
-        issue_w(slot, slot);
-#else
-        issue_w(g + 3 < total ? g + 3 : total - 1, slot);
-#endif
-#endif
-        const int nslot = slot == NSLOT - 1 ? 0 : slot + 1;
-#if !(FR_STAGE_EXP & 32)
-#pragma unroll
-        for (int i = 0; i < FN / 2; ++i) wread(i, nslot);
-#endif
-#pragma unroll
-        for (int i = FN / 2; i < FN; ++i) {
-#pragma unroll
-            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
-#if !(FR_STAGE_EXP & 32)
-            wread(i, nslot);
-#endif
-        }
-#if FR_STAGE_SCHED
-        // second half: refills of wf[0..3] and the 4 DMA pieces spread over the first 8 MFMAs, then
-        // each wf[4..7] refill right after its 7th MFMA
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-#endif
+            for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(wq[r][i], cur[j], acc[i][j]);
     };
 
     const size_t img = (size_t)b * SPIX * SC;
@@ -270,8 +180,6 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
             seed_bias(cv);
         }
         pread(pA, 0, 0);
-#pragma unroll
-        for (int i = 0; i < FN; ++i) wread(i, 0);  // step 0 of every conv sits in slot 0 (72 % 3 == 0)
         const int g0 = cv * KSTEPS;
 #pragma unroll 1
         for (int cg = 0; cg < SC / 32; cg += 2) {
@@ -291,9 +199,9 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
         //        x + conv2's bias, so conv2 accumulates onto the identity: x' = x + b2 + conv2(t);
         // conv2: x' -> patch (and NHWC global for the last block / intermediates), no arithmetic.
         // (build_stage checks that every conv1 is PReLU and every conv2 has no activation.)
-        // No global loads or stores between the stage's first patch load and its last block besides the
-        // small epilogue tables.  The barrier only needs every wave's patch reads drained (the weight
-        // DMAs in flight land in the ring slots, not in the patch, so they stay in flight).
+        // No activation traffic between the stage's first patch load and its last block (global loads:
+        // the weight stream and the small epilogue tables).  The barrier only needs every wave's patch
+        // reads drained (the weight loads in flight go to registers).
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #if FR_STAGE_EXP & 8
         {
@@ -377,7 +285,7 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
         run_conv(2 * blk, std::false_type{});
         run_conv(2 * blk + 1, std::true_type{});
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs land before the LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's weight loads retire before the wave ends
 }
 
 }  // namespace
