@@ -74,11 +74,12 @@ struct Op {
     bool fuse_stem = false;  // OP_PRE of IResNet100: u8 input runs preprocess + the next (stem) conv fused
 };
 
-// One LDS-resident stage: the stride-1 blocks of a 14x14x256 layer (conv_stage.hip, geo 0: one
-// workgroup per image) or of a 28x28x128 layer (conv_stage28.hip, geo 1: two workgroups per image).
+// One LDS-resident stage: the stride-1 blocks of a 14x14x256 layer (conv_stage.hip: one workgroup per
+// image, parts = 1) or of a 28x28x128 / 56x56x64 layer (conv_split_stage.hip: parts = 2 / 4 workgroups
+// per image).
 struct StageRec {
     int in = -1, out = -1, nblk = 0;
-    int geo = 0, H = 14, C = 256;
+    int parts = 1, H = 14, C = 256;
     std::vector<int> conv_ops;            // member OP_CONV indices, conv1/conv2 alternating
     std::vector<int> t_tensors, x_tensors;  // per block: conv1 output, block output
     bf16_t* w = nullptr;                  // packed K-step weight images
@@ -148,8 +149,8 @@ struct fr_handle {
     int proj_d = 0;
     float* emb_pre = nullptr;  // [max_batch][512] IRV1 output before the projection
     float* amax = nullptr;     // FR_DTYPE_FP8: per-tensor max |x| of the current forward [ntensors]
-    bf16_t* stage_xchg = nullptr;  // split-stage boundary rows [max_batch][2][2][28][128] (reserve)
-    int* stage_flags = nullptr;    // split-stage per-half progress counters [max_batch][2]
+    bf16_t* stage_xchg = nullptr;  // split-stage boundary rows (split_stage_xchg_elems(max_batch), reserve)
+    int* stage_flags = nullptr;    // split-stage per-part progress counters [max_batch][4]
     int* stage_spin = nullptr;     // split-stage bounded-wait overruns (fr_debug_stage_timeouts)
     int stage_mode = 1;       // FR_OPT_STAGE: 0 off, 1 auto (stage_runs), 2 always
     int stage_min_fill = 80;  // FR_OPT_STAGE_MIN_FILL (percent)
@@ -485,7 +486,7 @@ struct Builder {
 // Packs a stage's weights (from the member convs' [Npad][Kpad] device images) and its epilogue table.
 int build_stage(fr_handle* h, StageRec& r) {
     const int nconv = 2 * r.nblk, C = r.C;
-    const size_t wbytes = r.geo ? stage28_weight_bytes(nconv) : stage_weight_bytes(nconv);
+    const size_t wbytes = r.parts > 1 ? split_stage_weight_bytes(C, nconv) : stage_weight_bytes(nconv);
     std::vector<bf16_t> packed(wbytes / sizeof(bf16_t));
     std::vector<StageConv> tab(nconv);
     std::vector<float> ep((size_t)nconv * 9 * C, 0.f), sl((size_t)nconv * C, 0.f);
@@ -536,7 +537,7 @@ int build_stage(fr_handle* h, StageRec& r) {
     if ((rc = dev_alloc(&d, (size_t)nconv * sizeof(bf16_t*)))) return rc;
     h->weight_allocs.push_back(d);
     r.dbg = (bf16_t**)d;
-    if (r.geo == 1 && !h->stage_spin) {
+    if (r.parts > 1 && !h->stage_spin) {
         if ((rc = dev_alloc(&d, sizeof(int)))) return rc;
         h->weight_allocs.push_back(d);
         h->stage_spin = (int*)d;
@@ -581,11 +582,12 @@ void build_iresnet100(Builder& b) {
         int st_op = -1;
         StageRec rec;
         for (int i = 0; i < nblk[l]; ++i) {
-            const bool s14 = stage_supported(1, Ho, Ho, P), s28 = stage28_supported(Ho, Ho, P);
-            if (i == 1 && h->dtype != FR_DTYPE_FP8 && (s14 || s28) && P == C) {
+            const bool s14 = stage_supported(1, Ho, Ho, P);
+            const int parts = split_stage_parts(Ho, Ho, P);
+            if (i == 1 && h->dtype != FR_DTYPE_FP8 && (s14 || parts) && P == C) {
                 st_op = (int)h->ops.size();
                 rec.in = x;
-                rec.geo = s28 ? 1 : 0;
+                rec.parts = s14 ? 1 : parts;
                 rec.H = Ho;
                 rec.C = P;
                 Op op;
@@ -858,13 +860,13 @@ int reserve(fr_handle* h, int maxB) {
         h->act_allocs.push_back(q);
         h->emb_pre = (float*)q;
     }
-    if (std::any_of(h->stages.begin(), h->stages.end(), [](const StageRec& r) { return r.geo == 1; })) {
+    if (std::any_of(h->stages.begin(), h->stages.end(), [](const StageRec& r) { return r.parts > 1; })) {
         void* q = nullptr;
-        rc = dev_alloc(&q, stage28_xchg_elems(maxB) * sizeof(bf16_t));
+        rc = dev_alloc(&q, split_stage_xchg_elems(maxB) * sizeof(bf16_t));
         if (rc) { free_acts(h); return rc; }
         h->act_allocs.push_back(q);
         h->stage_xchg = (bf16_t*)q;
-        rc = dev_alloc(&q, (size_t)maxB * 2 * sizeof(int));
+        rc = dev_alloc(&q, (size_t)maxB * 4 * sizeof(int));
         if (rc) { free_acts(h); return rc; }
         h->act_allocs.push_back(q);
         h->stage_flags = (int*)q;
@@ -1091,19 +1093,20 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
 // either way, since per-conv grids of B*196 positions are a handful of tiles.  Above one round a last
 // round that is mostly empty costs a whole stage time, so auto mode then requires the rounds to be at
 // least stage_min_fill % full (B = 512: 100 %, B = 257: 50 % -> per-conv).
-// The layer2 split stage puts one image on two CUs: a round is n_cu / 2 images.
-static bool stage28_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_STAGE28");
-        return !(e && e[0] == '1');
+// A split stage puts one image on `parts` CUs: a round is n_cu / parts images.  FR_NO_SPLIT_STAGE=1 /
+// =28 / =56 turns the split stages off (all / layer2 / layer1) for A/B timing.
+static bool split_stage_enabled(int H) {
+    static const int off = [] {
+        const char* e = getenv("FR_NO_SPLIT_STAGE");
+        return e ? atoi(e) : 0;
     }();
-    return on;
+    return !(off == 1 || off == H);
 }
 
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r) {
     if (h->stage_mode == 0) return false;
-    if (r.geo == 1 && !stage28_enabled()) return false;
-    const int cap = std::max(1, r.geo == 1 ? h->n_cu / 2 : h->n_cu);
+    if (r.parts > 1 && !split_stage_enabled(r.H)) return false;
+    const int cap = std::max(1, h->n_cu / r.parts);
     if (h->stage_mode == 2 || B <= cap) return true;
     const int64_t rounds = (B + cap - 1) / cap;
     return (int64_t)B * 100 >= (int64_t)h->stage_min_fill * rounds * cap;
@@ -1150,8 +1153,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.spin_timeouts = h->stage_spin;
                 ProfScope ps(h, s);
                 ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
-                ps.start(r.geo == 1 ? "stage layer2" : "stage layer3");
-                FR_HIP_CHECK(r.geo == 1 ? launch_stage28(a, s) : launch_stage(a, s));
+                ps.start(r.H == 14 ? "stage layer3" : (r.H == 28 ? "stage layer2" : "stage layer1"));
+                FR_HIP_CHECK(r.parts > 1 ? launch_split_stage(a, r.H, r.C, s) : launch_stage(a, s));
                 break;
             }
             case OP_PRE: {

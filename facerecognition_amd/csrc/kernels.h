@@ -91,9 +91,9 @@ struct StageArgs {
     const float* slope;        // [2*nblk][256] negative-side factor: PReLU slope, 0 (ReLU) or 1 (none)
     bf16_t* const* dbg_x;      // optional [nblk] per-block outputs / [nblk] conv1 outputs (device
     bf16_t* const* dbg_t;      //   pointer tables; null = do not materialise intermediates)
-    // split stage (conv_stage28.hip) only: boundary-row exchange between an image's two workgroups
-    bf16_t* xchg;              // [B][2 halves][2 parities][28][128]
-    int* flags;                // [B][2] per-half progress (convs published), zeroed by the launcher
+    // split stages (conv_split_stage.hip) only: boundary-row exchange between an image's workgroups
+    bf16_t* xchg;              // [B][parts][2 rows][2 parities][W][C]
+    int* flags;                // [B][parts] per-part progress (convs published), zeroed by the launcher
     int* spin_timeouts;        // bounded-wait overruns (fr_debug_stage_timeouts); 0 when healthy
     int B, nblk, f16, dbg;     // dbg: timing-only experiment switches (FR_STAGE_DBG), 0 in production
     void* ev0;
@@ -103,12 +103,13 @@ bool stage_supported(int B, int H, int W, int C);
 size_t stage_weight_bytes(int nconv);
 void stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out);
 hipError_t launch_stage(const StageArgs& a, hipStream_t s);
-// Split LDS-resident stage for 28x28x128 (IResNet100 layer2.1 .. layer2.12): two workgroups per image
-// (14 output rows each) that exchange one boundary row per conv through xchg / flags.
-bool stage28_supported(int H, int W, int C);
-size_t stage28_weight_bytes(int nconv);
-size_t stage28_xchg_elems(int B);
-hipError_t launch_stage28(const StageArgs& a, hipStream_t s);
+// Split LDS-resident stages (conv_split_stage.hip): 28x28x128 (IResNet100 layer2.1 .. layer2.12) in two
+// workgroups per image, 56x56x64 (layer1.1 .. layer1.2) in four, 14 output rows each, exchanging their
+// boundary rows per conv through xchg / flags.  split_stage_parts: workgroups per image, 0 = unsupported.
+int split_stage_parts(int H, int W, int C);
+size_t split_stage_weight_bytes(int C, int nconv);
+size_t split_stage_xchg_elems(int B);  // enough for either geometry
+hipError_t launch_split_stage(const StageArgs& a, int H, int C, hipStream_t s);
 // Split-K reduction + the same fused epilogue as the conv kernel.
 hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
 // Number of K-tiles of 64 (for split-k planning).

@@ -1,6 +1,6 @@
-"""LDS-resident stage kernels -- layer3 (conv_stage.hip, one workgroup per image) and the layer2 split
-stage (conv_stage28.hip, two workgroups per image exchanging a boundary row per conv) -- vs the
-per-conv launch path of the same plan.
+"""LDS-resident stage kernels -- layer3 (conv_stage.hip, one workgroup per image) and the layer2 / layer1
+split stages (conv_split_stage.hip, two / four workgroups per image exchanging boundary rows per conv) --
+vs the per-conv launch path of the same plan.
 
 Both paths run the same folded ops with the same bf16/f16 rounding points; only the f32
 accumulation order inside each conv differs, so the stage output must agree with the per-conv
@@ -42,7 +42,7 @@ def test_stage_matches_per_conv_path(gpu, dtype, B):
     assert m.get_option(N.FR_OPT_STAGE) == 1
     x = torch.from_numpy(synthetic_crops(B, 112, seed=3))
     names = {"layer3.1.prelu", "layer3.1", "layer3.15", "layer3.29", "layer2.1.prelu", "layer2.1", "layer2.6",
-             "layer2.12"}
+             "layer2.12", "layer1.1.prelu", "layer1.1", "layer1.2"}
     m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)
     m.set_option(N.FR_OPT_STAGE, 2)  # always (auto would pick the per-conv path at these batch sizes)
     e_stage = m.embed(x).cpu().numpy()
@@ -82,14 +82,22 @@ def test_stage_auto_rule_by_batch(gpu):
     L = N.lib()
     cu = torch.cuda.get_device_properties(0).multi_processor_count
 
-    def has_stage(B):
+    def has_stage(B, last="layer3.29"):
         buf = ctypes.create_string_buffer(1 << 16)
         N.check(L.fr_debug_plan(m.handle, B, buf, len(buf)), "fr_debug_plan")
-        return any(l.startswith("stage") for l in buf.value.decode().splitlines())
+        return any(l.startswith("stage") and l.endswith(last) for l in buf.value.decode().splitlines())
 
     assert has_stage(1) and has_stage(cu // 2) and has_stage(cu) and has_stage(2 * cu)
-    # (the layer2 split stage's rounds are cu / 2 images: the same decisions at these sizes)
     assert not has_stage(cu + 1) and has_stage(2 * cu - cu // 8)
+    # split stages: the same rule over rounds of cu / parts images (layer2: 2 parts, layer1: 4)
+    def rule(B, parts):
+        cap = cu // parts
+        rounds = -(-B // cap)
+        return B <= cap or B * 100 >= 80 * rounds * cap
+
+    for B in (1, cu // 4, cu // 4 + 1, cu // 2 + 1, cu, cu + 1, 2 * cu - cu // 8):
+        assert has_stage(B, "layer2.12") == rule(B, 2), B
+        assert has_stage(B, "layer1.2") == rule(B, 4), B
     m.set_option(N.FR_OPT_STAGE_MIN_FILL, 0)
     assert has_stage(cu + 1)
     m.set_option(N.FR_OPT_STAGE_MIN_FILL, 80)
@@ -115,12 +123,16 @@ def test_stage_absent_for_other_archs(gpu):
     m.close()
 
 
-@pytest.mark.parametrize("B", [1, 3, 17, 130])
-def test_stage28_batches_and_exchange(gpu, B):
-    """Layer2 split stage at batch sizes that leave padded workgroup pairs (B = 1, 3, 17) and that span
-    two rounds of CUs (B = 130 > 128 = 256 CUs / 2): the stage's layer2 output agrees with the per-conv
-    path image by image (a lost or stale boundary row shows up as a localized error in its image), and
-    no bounded wait of the row exchange ran out."""
+SPLIT_CASES = [("layer2.12", "layer2.1.prelu", 2, B) for B in (1, 3, 17, 130)] + \
+              [("layer1.2", "layer1.1.prelu", 4, B) for B in (1, 5, 70)]
+
+
+@pytest.mark.parametrize("last,first_t,parts,B", SPLIT_CASES)
+def test_split_stage_batches_and_exchange(gpu, last, first_t, parts, B):
+    """Split stages at batch sizes that leave padded workgroup groups (B = 1, 3, 5, 17) and that span two
+    rounds of CUs (B = 130 > 256 CUs / 2 for layer2, B = 70 > 256 / 4 for layer1): the stage's output
+    agrees with the per-conv path image by image and part by part (a lost or stale boundary row shows up
+    as a localized error in its part), and no bounded wait of the row exchange ran out."""
     import ctypes
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
@@ -131,18 +143,19 @@ def test_stage28_batches_and_exchange(gpu, B):
     m.set_option(N.FR_OPT_STAGE, 2)
     buf = ctypes.create_string_buffer(1 << 16)
     N.check(L.fr_debug_plan(m.handle, B, buf, len(buf)), "fr_debug_plan")
-    assert any(l.startswith("stage") and l.endswith("layer2.12") for l in buf.value.decode().splitlines())
+    assert any(l.startswith("stage") and l.endswith(last) for l in buf.value.decode().splitlines())
     e_stage = m.embed(x).cpu().numpy()
-    t_stage = _named(m, B, {"layer2.12", "layer2.1.prelu"})
+    t_stage = _named(m, B, {last, first_t})
     assert L.fr_debug_stage_timeouts(m.handle) == 0
     m.set_option(N.FR_OPT_STAGE, 0)
     e_conv = m.embed(x).cpu().numpy()
-    t_conv = _named(m, B, {"layer2.12", "layer2.1.prelu"})
+    t_conv = _named(m, B, {last, first_t})
     m.close()
     for n in t_stage:
         a, b = t_stage[n], t_conv[n]
-        for i in range(B):  # per image and per half (rows 0..13 / 14..27)
-            for r in (slice(0, 14), slice(14, 28)):
+        for i in range(B):  # per image and per part (14 rows each)
+            for p in range(parts):
+                r = slice(14 * p, 14 * p + 14)
                 d = (a[i, r] - b[i, r]).norm() / (b[i, r].norm() + 1e-12)
                 assert d < 2e-2, f"{n} image {i} rows {r}: rel err {d:.3e}"
     assert np.all(1 - np.sum(e_stage * e_conv, axis=1) <= 3e-4)

@@ -39,6 +39,7 @@ def analyse(trace, plan_path):
     skip_next_conv = False
     tot_ns = tot_flop = 0
     agg = {}
+    per = []
     print(f"{'layer':34s} {'M':>8s} {'N':>5s} {'K':>5s} tile split {'us':>8s} {'TF/s':>7s}")
     for p in plan:
         if p[0] == "pre" and fused_stem:  # one dispatch = preprocess + the stem conv
@@ -64,6 +65,7 @@ def analyse(trace, plan_path):
         tot_ns += d
         tot_flop += flop
         key = (M, Nn, K, p[7])
+        per.append((p[8] if len(p) > 8 else "-", p[0], M, Nn, K, tile, split, d, flop))
         agg.setdefault(key, [0, 0, 0.0, tile, split])
         agg[key][0] += 1
         agg[key][1] += d
@@ -71,6 +73,9 @@ def analyse(trace, plan_path):
     for (M, Nn, K, kk), (cnt, d, flop, tile, split) in sorted(agg.items(), key=lambda t: -t[1][1]):
         print(f"{kk + ' x' + str(cnt):34s} {M:8d} {Nn:5d} {K:5d} {tile:4d} {split:5d} {d / 1e3:8.1f} {flop / d / 1e3:7.1f}")
     print(f"forward: {tot_ns / 1e3:.1f} us, {tot_flop / tot_ns / 1e3:.1f} TFLOP/s over conv+head FLOPs")
+    print("\nper launch (slowest first):")
+    for name, kind, M, Nn, K, tile, split, d, flop in sorted(per, key=lambda t: -t[7]):
+        print(f"  {name:24s} {kind:5s} {M:8d} {Nn:5d} {K:5d} {tile:4d} {split:5d} {d / 1e3:8.1f} {flop / d / 1e3:7.1f}")
 
 
 if __name__ == "__main__":
