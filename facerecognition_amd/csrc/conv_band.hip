@@ -717,7 +717,7 @@ static bool band_legacy() {
 
 bool band_plan(const ConvArgs& a, int* cfg, int* variant) {
     if (a.Kh != 3 || a.Kw != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1) return false;
-    if (a.Cin % 64 != 0 || a.Ho != a.H || a.Wo != a.W || a.partial) return false;
+    if (a.Cin % 64 != 0 || a.Ho != a.H || a.Wo != a.W || a.partial || a.x2) return false;
     int v;
     if (a.Cout % 256 == 0) v = 0;
     else if (a.Cout % 128 == 0) v = 1;

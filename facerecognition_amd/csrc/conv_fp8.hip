@@ -291,7 +291,7 @@ int conv_fp8_tile(int M, int Cout) {
 }
 
 hipError_t launch_conv_fp8(const ConvArgs& a, hipStream_t s) {
-    if (a.Cin % 64 != 0 || a.Kpad % KS != 0 || !a.w8 || !a.wscale) return hipErrorInvalidValue;
+    if (a.Cin % 64 != 0 || a.Kpad % KS != 0 || !a.w8 || !a.wscale || a.x2) return hipErrorInvalidValue;
     switch (a.tile) {
         // 4 x 1 waves: each wave converts only its own activation fragments (2 x 2 converted every
         // fragment twice; the bf16 -> e4m3 conversion costs as much issue time as the fp8 MFMAs)

@@ -136,6 +136,7 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
     const int HoWo = p.Ho * p.Wo;
     int a_ih[NA], a_iw[NA];
     uint32_t a_base[NA];  // byte offset of (b, ih0, iw0, x_off [+ 8*cl]) — wraps if ih0/iw0 < 0, only used when valid
+    uint32_t a_base2[NA];  // FASTK + x2: byte offset of (b, oh*st2, ow*st2, x2_off + 8*cl) in x2, OOB past M
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
         const int m = m0 + 8 * (wave + NW * i) + lrow;
@@ -147,12 +148,21 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
             // FASTK: c_cur is the K-step's channel base, the lane adds its chunk here;
             // generic: c_cur already is the lane's own channel.
             a_base[i] = (uint32_t)((((b * p.H + a_ih[i]) * p.W + a_iw[i]) * p.Cx + p.x_off + (FASTK ? 8 * cl : 0)) * 2);
+            a_base2[i] = FASTK && p.x2
+                             ? (uint32_t)((((b * p.H2 + oh * p.st2) * p.W2 + ow * p.st2) * p.Cx2 + p.x2_off + 8 * cl) * 2)
+                             : OOB;
         } else {
             a_ih[i] = -(1 << 28);
             a_iw[i] = 0;
             a_base[i] = 0;
+            a_base2[i] = OOB;
         }
     }
+    // K-steps from kt_x2 on read x2 (the K-concatenated 1x1 projection)
+    const int kt_x2 = FASTK && p.x2 ? p.K1 / BK : nkt;
+    const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.x2 ? p.x2 : p.x), 0,
+        (uint32_t)min((size_t)0x7fffffff, p.x2 ? (size_t)p.B * p.H2 * p.W2 * p.Cx2 * 2 : (size_t)0), 0x00020000);
     uint32_t b_base[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) b_base[j] = (uint32_t)(((n0 + 8 * (wave + NW * j) + lrow) * p.Kpad + 8 * cl) * 2);
@@ -173,14 +183,21 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
         const char* sA = smem + buf * STAGE;
         const char* sB = sA + STAGE_A;
         const bool skipA = (dbg & 32) && kt > kt0 + 1, skipB = (dbg & 64) && kt > kt0 + 1;
-        const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
+        if (FASTK && kt >= kt_x2) {  // projection K-steps: x2 at the output's stride-st2 position
+            const uint32_t c2 = (uint32_t)((kt - kt_x2) * BK * 2);
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
-            const int ih = a_ih[i] + r_cur, iw = a_iw[i] + s_cur;
-            bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-            if (!FASTK) ok = ok && k_cur < p.K;
-            const uint32_t off = ok ? a_base[i] + (uint32_t)soff : OOB;
-            if (!skipA) dma16(xr, sA + (wave + NW * i) * 1024, off);
+            for (int i = 0; i < NA; ++i)
+                if (!skipA) dma16(x2r, sA + (wave + NW * i) * 1024, a_base2[i] == OOB ? OOB : a_base2[i] + c2);
+        } else {
+            const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
+#pragma unroll
+            for (int i = 0; i < NA; ++i) {
+                const int ih = a_ih[i] + r_cur, iw = a_iw[i] + s_cur;
+                bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+                if (!FASTK) ok = ok && k_cur < p.K;
+                const uint32_t off = ok ? a_base[i] + (uint32_t)soff : OOB;
+                if (!skipA) dma16(xr, sA + (wave + NW * i) * 1024, off);
+            }
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j)
@@ -418,6 +435,8 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(ConvArgs p) {
 
 template <bool F16, int BM, int BN, int WM, int WN, int STAGES>
 hipError_t launch_variant(const ConvArgs& a, hipStream_t s) {
+    if (a.x2 && (a.Cin % 64 != 0 || a.K1 != a.Kh * a.Kw * a.Cin || a.C2 % 64 != 0 || a.K1 + a.C2 > a.Kpad))
+        return hipErrorInvalidValue;  // the projection K-steps need the FASTK path
     const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.Cout + BN - 1) / BN;
     const int nkt = a.Kpad / BK;
     const int split = a.split_k > 1 ? a.split_k : 1;

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
 template <typename G>
 bool img_supported_t(const ConvArgs& a) {
     constexpr int IW = G::IW, IC = G::IC;
-    return a.wimg && a.Kh == 3 && a.Kw == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.H == IW && a.W == IW &&
+    return a.wimg && !a.x2 && a.Kh == 3 && a.Kw == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.H == IW && a.W == IW &&
            a.Ho == IW && a.Wo == IW && a.Cin == IC && a.Cout == IC && a.Npad >= IC && a.Kpad >= 9 * IC &&
            a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.x_off + IC <= a.Cx && a.Cy % 4 == 0 && a.y_off % 4 == 0 &&
            a.y_off + IC <= a.Cy && !a.y2 && !a.partial && !a.w8 && !a.y_amax && a.B > 0 && !a.f16 &&

@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void rows_pack_kernel(const bf16_t* __restrict
 }  // namespace
 
 bool rows_supported(const ConvArgs& a) {
-    return a.Kh == 3 && a.Kw == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.Cin == 64 &&
+    return !a.x2 && a.Kh == 3 && a.Kw == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 && a.Cin == 64 &&
            a.Cout % 64 == 0 && a.Npad >= a.Cout && a.H == a.Ho && a.W == a.Wo && a.H % RROWS == 0 &&
            a.W % RCOLS == 0 && a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.x_off + 64 <= a.Cx && a.Cy % 8 == 0 &&
            a.y_off % 8 == 0 && a.y_off + a.Cout <= a.Cy && !a.y2 && !a.partial && !a.w8 && !a.y_amax && !a.f16 &&

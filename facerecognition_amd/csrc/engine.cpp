@@ -50,6 +50,7 @@ struct DevConvW {
     uint8_t* w8 = nullptr;   // FR_DTYPE_FP8: e4m3 [Npad][Kpad8] + per-channel scale
     float* wscale = nullptr;
     int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0, Kpad8 = 0;
+    int K1 = 0, C2 = 0;  // K-concatenated 1x1 projection: K = K1 + C2 (ConvArgs::x2), else K1 = K, C2 = 0
 };
 
 struct TensorDesc {
@@ -71,6 +72,7 @@ struct Op {
     int wi = -1;
     int pk = 0, ps = 0, pp = 0;
     int stage = -1;  // OP_STAGE: its StageRec; OP_CONV: the stage that covers it (skipped when stages run)
+    int x2 = -1, x2_off = 0, st2 = 1;  // OP_CONV with a K-concatenated downsample: its input tensor, stride
     bool fuse_stem = false;  // OP_PRE of IResNet100: u8 input runs preprocess + the next (stem) conv fused
 };
 
@@ -282,7 +284,10 @@ struct Builder {
     }
 
     // Build one (possibly N-concatenated) conv weight: names[i].w is [Cout_i, kh, kw, Cin_w] f32.
-    int make_convw(const std::vector<std::string>& names, int kh, int kw, int cin, int act, const std::string& aff) {
+    // kcat (single name only): a 1x1 conv [Cout, 1, 1, c2] whose weights are appended to every row
+    // (K = kh*kw*cin + c2) and whose bias is added: a residual block's downsample folded into its last conv.
+    int make_convw(const std::vector<std::string>& names, int kh, int kw, int cin, int act, const std::string& aff,
+                   const std::string& kcat = "", int c2 = 0) {
         const bool stem_split = stem;
         stem = false;
         DevConvW cw;
@@ -332,6 +337,29 @@ struct Builder {
             cout += co;
         }
         cw.Cout = cout;
+        cw.K1 = cw.K;
+        if (!kcat.empty()) {
+            const HostT* w2 = find(kcat + ".w");
+            if (names.size() != 1 || !w2 || w2->dims.size() != 4 || w2->dims[0] != cout || w2->dims[1] != 1 ||
+                w2->dims[2] != 1 || w2->dims[3] != c2) {
+                set_error("weights: missing or mis-shaped tensor " + kcat + ".w");
+                rc = FR_ERR_WEIGHTS;
+                return -1;
+            }
+            std::vector<float> cat((size_t)cout * (cw.K + c2));
+            for (int o = 0; o < cout; ++o) {
+                std::copy(wrows.begin() + (size_t)o * cw.K, wrows.begin() + (size_t)(o + 1) * cw.K,
+                          cat.begin() + (size_t)o * (cw.K + c2));
+                std::copy(w2->v.begin() + (size_t)o * c2, w2->v.begin() + (size_t)(o + 1) * c2,
+                          cat.begin() + (size_t)o * (cw.K + c2) + cw.K);
+            }
+            wrows.swap(cat);
+            const HostT* b2 = find(kcat + ".b");
+            if (b2)
+                for (int o = 0; o < cout; ++o) bias[o] += b2->v[o];
+            cw.C2 = c2;
+            cw.K += c2;
+        }
         cw.Npad = round_up(cout, 128);
         cw.Kpad = round_up(cw.K, 64);
         std::vector<bf16_t> packed((size_t)cw.Npad * cw.Kpad, 0);
@@ -343,7 +371,7 @@ struct Builder {
             }
         bias.resize(cw.Npad, 0.f);
         if ((rc = upload(h, &cw.w, packed))) return -1;
-        if (h->dtype == FR_DTYPE_FP8 && names.size() == 1 && !stem_split && cin % 64 == 0) {
+        if (h->dtype == FR_DTYPE_FP8 && names.size() == 1 && !stem_split && cin % 64 == 0 && kcat.empty()) {
             const HostT* ws = find(names[0] + ".wscale");
             if (ws) {  // e4m3 weights: the blob carries e4m3-representable values w/s and the scales s
                 if ((int)ws->v.size() != cout) {
@@ -411,6 +439,14 @@ struct Builder {
     void conv(const std::vector<std::string>& names, int in, int in_off, int cin, int out, int out_off, int kh, int kw,
               int sh, int sw, int ph, int pw, int act, int res = -1, int res_off = 0, int out2 = -1,
               const std::string& aff = "") {
+        conv_ds(names, in, in_off, cin, out, out_off, kh, kw, sh, sw, ph, pw, act, res, res_off, out2, aff, "", -1, 0, 1);
+    }
+
+    // conv whose residual is a downsample (1x1 conv `ds` of tensor x2 at stride st2) folded into its K
+    // (ds empty: a plain conv)
+    void conv_ds(const std::vector<std::string>& names, int in, int in_off, int cin, int out, int out_off, int kh,
+                 int kw, int sh, int sw, int ph, int pw, int act, int res, int res_off, int out2, const std::string& aff,
+                 const std::string& ds, int x2, int c2, int st2) {
         if (rc) return;
         Op op;
         op.kind = OP_CONV;
@@ -418,19 +454,34 @@ struct Builder {
         op.out = out; op.out_off = out_off;
         op.res = res; op.res_off = res_off; op.out2 = out2;
         op.kh = kh; op.kw = kw; op.sh = sh; op.sw = sw; op.ph = ph; op.pw = pw; op.act = act;
-        op.wi = make_convw(names, kh, kw, cin, act, aff);
+        op.x2 = ds.empty() ? -1 : x2;
+        op.st2 = st2;
+        op.wi = make_convw(names, kh, kw, cin, act, aff, ds, c2);
         if (op.wi < 0) return;
         const auto& ti = h->tensors[in];
         const auto& to = h->tensors[out];
         const int Ho = (ti.H + 2 * ph - kh) / sh + 1, Wo = (ti.W + 2 * pw - kw) / sw + 1;
         const int cout = h->convw[op.wi].Cout;
         if (Ho != to.H || Wo != to.W || out_off + cout > to.C || in_off + cin > ti.C ||
-            (res >= 0 && (h->tensors[res].H != Ho || res_off + cout > h->tensors[res].C))) {
+            (res >= 0 && (h->tensors[res].H != Ho || res_off + cout > h->tensors[res].C)) ||
+            (op.x2 >= 0 && (h->tensors[x2].C != c2 || (Ho - 1) * st2 >= h->tensors[x2].H ||
+                            (Wo - 1) * st2 >= h->tensors[x2].W || cin % 64 != 0 || c2 % 64 != 0))) {
             set_error("plan: shape mismatch at conv " + names[0]);
             rc = FR_ERR_ARG;
             return;
         }
         h->ops.push_back(op);
+    }
+
+    // whether a residual block's downsample folds into its last conv (igemm K-concatenation): not for
+    // fp8 (its conv kernel has no projection source) and only on the 64-channel fast-K path;
+    // FR_NO_DS_FUSE=1 keeps the separate downsample conv (A/B)
+    bool fuse_ds(int cin, int c2) const {
+        static const bool off = [] {
+            const char* e = getenv("FR_NO_DS_FUSE");
+            return e && e[0] == '1';
+        }();
+        return !off && h->dtype != FR_DTYPE_FP8 && cin % 64 == 0 && c2 % 64 == 0;
     }
     void maxpool(int in, int out, int out_off, int k, int s, int p) {
         Op op;
@@ -600,12 +651,17 @@ void build_iresnet100(Builder& b) {
             const int hmid = b.tensor(Hin, Hin, P, pre + ".prelu");
             b.conv({pre + ".conv1"}, x, 0, C, hmid, 0, 3, 3, 1, 1, 1, 1, 2);
             int res = x;
-            if (i == 0) {
+            const bool fuse = i == 0 && b.fuse_ds(P, C);
+            if (i == 0 && !fuse) {
                 res = b.tensor(Ho, Ho, P, pre + ".downsample");
                 b.conv({pre + ".downsample"}, x, 0, C, res, 0, 1, 1, 2, 2, 0, 0, 0);
             }
             const int y = b.tensor(Ho, Ho, P, pre);
-            b.conv({pre + ".conv2"}, hmid, 0, P, y, 0, 3, 3, st, st, 1, 1, 0, res, 0);
+            if (fuse)  // y = conv2(t) + downsample(x) in one K loop (no downsample tensor)
+                b.conv_ds({pre + ".conv2"}, hmid, 0, P, y, 0, 3, 3, st, st, 1, 1, 0, -1, 0, -1, "", pre + ".downsample",
+                          x, C, 2);
+            else
+                b.conv({pre + ".conv2"}, hmid, 0, P, y, 0, 3, 3, st, st, 1, 1, 0, res, 0);
             if (st_op >= 0 && !b.rc) {
                 rec.conv_ops.push_back((int)h->ops.size() - 2);
                 rec.conv_ops.push_back((int)h->ops.size() - 1);
@@ -709,12 +765,16 @@ void build_resnet50(Builder& b) {
             const int h2 = b.tensor(Ho, Ho, P);
             b.conv({pre + ".conv2"}, h1, 0, P, h2, 0, 3, 3, s, s, 1, 1, 1);
             int id = x;
-            if (i == 0) {
+            const bool fuse = i == 0 && b.fuse_ds(P, C);
+            if (i == 0 && !fuse) {
                 id = b.tensor(Ho, Ho, 4 * P, pre + ".downsample");
                 b.conv({pre + ".downsample"}, x, 0, C, id, 0, 1, 1, s, s, 0, 0, 0);
             }
             const int y = b.tensor(Ho, Ho, 4 * P, pre);
-            b.conv({pre + ".conv3"}, h2, 0, P, y, 0, 1, 1, 1, 1, 0, 0, 1, id, 0);
+            if (fuse)  // y = relu(conv3(h2) + downsample(x)) in one K loop
+                b.conv_ds({pre + ".conv3"}, h2, 0, P, y, 0, 1, 1, 1, 1, 0, 0, 1, -1, 0, -1, "", pre + ".downsample", x, C, s);
+            else
+                b.conv({pre + ".conv3"}, h2, 0, P, y, 0, 1, 1, 1, 1, 0, 0, 1, id, 0);
             x = y;
             C = 4 * P;
             H = Ho;
@@ -965,7 +1025,7 @@ struct ProfScope {
     }
 };
 
-double conv_flops(const ConvArgs& a) { return 2.0 * (double)a.M * a.Cout * ((double)a.Cin * a.Kh * a.Kw); }
+double conv_flops(const ConvArgs& a) { return 2.0 * (double)a.M * a.Cout * ((double)a.Cin * a.Kh * a.Kw + (a.x2 ? a.C2 : 0)); }
 
 bool autotune_enabled() {
     static const bool on = [] {
@@ -1195,6 +1255,11 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.negf = cw.negf; a.ep = cw.ep;
                 a.wrows_ = cw.wrows;
                 if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
+                if (op.x2 >= 0) {
+                    const auto& t2 = h->tensors[op.x2];
+                    a.x2 = t2.dev; a.H2 = t2.H; a.W2 = t2.W; a.Cx2 = t2.C; a.x2_off = op.x2_off;
+                    a.C2 = cw.C2; a.st2 = op.st2; a.K1 = cw.K1;
+                }
                 a.y = to.dev; a.Cy = to.C; a.y_off = op.out_off;
                 if (op.out2 >= 0) {
                     a.y2 = h->tensors[op.out2].dev; a.Cy2 = h->tensors[op.out2].C; a.y2_off = 0;

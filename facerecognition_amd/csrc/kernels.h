@@ -38,6 +38,11 @@ struct ConvArgs {
     const float* negf;            // conv_img / conv_rows: [Npad] activation negative-side factor (slope / 0 / 1)
     const float* ep;              // conv_rows.hip: [9][Npad] bias per border class (bias9, or bias x 9)
     const bf16_t* wrows_;         // engine: the conv's conv_rows weight image when it has one (else null)
+    // K-concatenated 1x1 projection (a residual block's downsample folded into its last conv; igemm with
+    // Cin % 64 == 0 only): K steps [K1, K1 + C2) read x2 [B][H2][W2][Cx2] at (oh * st2, ow * st2),
+    // channels x2_off.., and the weight rows hold [W_conv | W_downsample] (bias = the sum)
+    const bf16_t* x2;
+    int H2, W2, Cx2, x2_off, C2, st2, K1;
 };
 // Persistent weight-resident 3x3/s1/p1 conv with 64 input channels (conv_rows.hip); a.wimg = the
 // rows_pack_weights image, a.ep / a.negf set.
