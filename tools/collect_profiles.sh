@@ -5,7 +5,7 @@ T=${1:?tag}; R=${2:?round prefix}; O=gpurun_out/$T
 set -e
 cp $O/bench.json profiles/${R}_bench.json
 : > profiles/${R}_bench_runs.jsonl
-for b in bench bench_noprof bench_host bench_irv1 bench_r50 bench_fp8 bench_1m; do tail -1 $O/$b.log >> profiles/${R}_bench_runs.jsonl; done
+for b in bench bench_noprof bench_host bench_irv1 bench_irv1_f16 bench_r50 bench_fp8 bench_1m bench_bs1 bench_r50_bs1 bench_2share; do tail -1 $O/$b.log >> profiles/${R}_bench_runs.jsonl; done
 cp "$(find $O/prof -name '*kernel_stats.csv' | head -1)" profiles/${R}_bench_kernel_stats.csv
 grep '^{' $O/match_bench.log > profiles/${R}_match_bench.jsonl
 cp $O/pmc_traffic.json profiles/${R}_pmc_traffic.json

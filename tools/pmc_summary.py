@@ -14,7 +14,7 @@ def main(root, filt=""):
             k = r["Kernel_Name"]
             if filt not in k:
                 continue
-            key = k.split("(")[0][-70:]
+            key = k.replace("(anonymous namespace)::", "").rsplit("(", 1)[0][-90:]
             agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
             cnt[key][r["Counter_Name"]] += 1
     for k, d in agg.items():
@@ -22,6 +22,11 @@ def main(root, filt=""):
         n = max(cnt[k].values())
         for c in sorted(d):
             print(f"   {c:28s} total {d[c]:.4g}   per-dispatch {d[c] / cnt[k][c]:.4g}   (n={cnt[k][c]})")
+        if d.get("SQ_WAVE_CYCLES"):  # quad-cycle counters over the same waves (MI355X_MICROARCH.md)
+            w = d["SQ_WAVE_CYCLES"]
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"):
+                if c in d:
+                    print(f"   {c + ' / SQ_WAVE_CYCLES':44s} {d[c] / w:.3f}")
 
 
 if __name__ == "__main__":
