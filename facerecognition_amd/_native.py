@@ -78,6 +78,7 @@ _SIGS = {
     "fr_debug_match_fallbacks": (c_int, [c_void_p]),
     "fr_debug_stage_timeouts": (c_int, [c_void_p]),
     "fr_debug_tensor_count": (c_int, [c_void_p]),
+    "fr_debug_tensor_dtype": (c_int, [c_void_p, c_int]),
     "fr_debug_plan": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t]),
     "fr_prof_enable": (c_int, [c_void_p, c_int]),
     "fr_prof_collect": (c_int, [c_void_p]),

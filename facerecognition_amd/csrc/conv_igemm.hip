@@ -75,7 +75,7 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, float* v, int m, in
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sl[e];
     }
-    *(uint4*)(p.y + (size_t)m * p.Cy + p.y_off + n) = T::pack8(v);
+    *(uint4*)(p.y + (size_t)m * p.Cy + p.y_off + n) = F16 && p.y_bf16 ? Num<false>::pack8(v) : T::pack8(v);
     if (p.y2) {
         const float4 a0 = *(const float4*)(p.aff_s + n), a1 = *(const float4*)(p.aff_s + n + 4);
         const float4 c0 = *(const float4*)(p.aff_b + n), c1 = *(const float4*)(p.aff_b + n + 4);
@@ -398,7 +398,7 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
         if (m < p.M && nv) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
-            *(uint4*)(p.y + (size_t)m * p.Cy + p.y_off + n) = T::pack8(v);
+            *(uint4*)(p.y + (size_t)m * p.Cy + p.y_off + n) = F16 && p.y_bf16 ? Num<false>::pack8(v) : T::pack8(v);
             if (p.y2) {
                 float u[8];
 #pragma unroll
@@ -437,6 +437,7 @@ template <bool F16, int BM, int BN, int WM, int WN, int STAGES>
 hipError_t launch_variant(const ConvArgs& a, hipStream_t s) {
     if (a.x2 && (a.Cin % 64 != 0 || a.K1 != a.Kh * a.Kw * a.Cin || a.C2 % 64 != 0 || a.K1 + a.C2 > a.Kpad))
         return hipErrorInvalidValue;  // the projection K-steps need the FASTK path
+    if (a.y_bf16 && (!a.f16 || a.res || a.y2)) return hipErrorInvalidValue;  // bf16 output of an f16 conv only
     const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.Cout + BN - 1) / BN;
     const int nkt = a.Kpad / BK;
     const int split = a.split_k > 1 ? a.split_k : 1;

@@ -57,6 +57,7 @@ struct TensorDesc {
     int H, W, C;
     bf16_t* dev = nullptr;
     std::string name;  // oracle module whose output this tensor equals ("" = internal)
+    bool f16 = false;  // stored as f16 in a bf16 plan (IRV1's high-resolution stem, build_irv1)
 };
 
 enum OpKind { OP_PRE, OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_STAGE };
@@ -279,8 +280,10 @@ struct Builder {
 
     bool stem = false;  // next conv is the network stem: fold 1/255 + hi/lo split (see launch_preprocess)
 
+    bool pack_f16 = false;  // the conv being built reads an f16 tensor: f16 weights (set by conv_ds)
+
     float round16(float v) const {  // stem hi/lo split in the activation dtype (bf16 for FR_DTYPE_FP8)
-        return h->dtype == FR_DTYPE_F16 ? host_h2f(host_f2h(v)) : host_bf2f(host_f2bf(v));
+        return pack_f16 ? host_h2f(host_f2h(v)) : host_bf2f(host_f2bf(v));
     }
 
     // Build one (possibly N-concatenated) conv weight: names[i].w is [Cout_i, kh, kw, Cin_w] f32.
@@ -363,7 +366,7 @@ struct Builder {
         cw.Npad = round_up(cout, 128);
         cw.Kpad = round_up(cw.K, 64);
         std::vector<bf16_t> packed((size_t)cw.Npad * cw.Kpad, 0);
-        const bool f16 = h->dtype == FR_DTYPE_F16;
+        const bool f16 = pack_f16;
         for (int o = 0; o < cout; ++o)
             for (int k = 0; k < cw.K; ++k) {
                 const float v = wrows[(size_t)o * cw.K + k];
@@ -456,6 +459,12 @@ struct Builder {
         op.kh = kh; op.kw = kw; op.sh = sh; op.sw = sw; op.ph = ph; op.pw = pw; op.act = act;
         op.x2 = ds.empty() ? -1 : x2;
         op.st2 = st2;
+        pack_f16 = h->dtype == FR_DTYPE_F16 || h->tensors[in].f16;
+        if (h->tensors[in].f16 && (res >= 0 || out2 >= 0 || !ds.empty() || h->dtype != FR_DTYPE_BF16)) {
+            set_error("plan: f16 section conv " + names[0] + " with a residual / second output / projection");
+            rc = FR_ERR_ARG;
+            return;
+        }
         op.wi = make_convw(names, kh, kw, cin, act, aff, ds, c2);
         if (op.wi < 0) return;
         const auto& ti = h->tensors[in];
@@ -792,19 +801,29 @@ void build_irv1(Builder& b) {
     const int in = b.tensor(160, 160, 8);
     h->ops.push_back(Op{OP_PRE, -1, 0, 0, in});
     const int a = b.tensor(79, 79, 32, m + "conv2d_1a");
+    const int bb = b.tensor(77, 77, 32, m + "conv2d_2a");
+    const int c = b.tensor(77, 77, 64, m + "conv2d_2b");
+    const int d = b.tensor(38, 38, 64, m + "maxpool_3a");
+    const int e = b.tensor(38, 38, 80, m + "conv2d_3b");
+    const int f = b.tensor(36, 36, 192, m + "conv2d_4a");
+    int x = b.tensor(17, 17, 256, m + "conv2d_4b");
+    // bf16 plan: the high-resolution stem (input .. conv2d_4a) is stored and multiplied in f16.  Its
+    // activations are ~90 % of the forward's bf16 rounding drift (profiles/r02_irv1_drift_bf16_vs_f16.txt:
+    // 1.28e-2 of 1.61e-2 relative error is in place at conv2d_4b); f16 MFMAs run at the bf16 rate, and
+    // conv2d_4b writes bf16 for the rest of the network.  FR_IRV1_BF16_STEM=1 keeps it bf16 (A/B).
+    static const bool bf16_stem = [] {
+        const char* e = getenv("FR_IRV1_BF16_STEM");
+        return e && e[0] == '1';
+    }();
+    if (h->dtype == FR_DTYPE_BF16 && !bf16_stem)
+        for (int t : {in, a, bb, c, d, e, f}) h->tensors[t].f16 = true;
     b.stem = true;
     b.conv({m + "conv2d_1a"}, in, 0, 8, a, 0, 3, 3, 2, 2, 0, 0, 1);
-    const int bb = b.tensor(77, 77, 32, m + "conv2d_2a");
     b.conv({m + "conv2d_2a"}, a, 0, 32, bb, 0, 3, 3, 1, 1, 0, 0, 1);
-    const int c = b.tensor(77, 77, 64, m + "conv2d_2b");
     b.conv({m + "conv2d_2b"}, bb, 0, 32, c, 0, 3, 3, 1, 1, 1, 1, 1);
-    const int d = b.tensor(38, 38, 64, m + "maxpool_3a");
     b.maxpool(c, d, 0, 3, 2, 0);
-    const int e = b.tensor(38, 38, 80, m + "conv2d_3b");
     b.conv({m + "conv2d_3b"}, d, 0, 64, e, 0, 1, 1, 1, 1, 0, 0, 1);
-    const int f = b.tensor(36, 36, 192, m + "conv2d_4a");
     b.conv({m + "conv2d_4a"}, e, 0, 80, f, 0, 3, 3, 1, 1, 0, 0, 1);
-    int x = b.tensor(17, 17, 256, m + "conv2d_4b");
     b.conv({m + "conv2d_4b"}, f, 0, 192, x, 0, 3, 3, 2, 2, 0, 0, 1);
     // repeat_1: Block35 x5 @17x17. cat layout [t1 | t2 | b0 | b1 | b2]; conv2d reads [64:160].
     for (int i = 0; i < 5; ++i) {
@@ -1238,7 +1257,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 }
                 ps.start("preprocess");
                 const auto& t = h->tensors[op.out];
-                FR_HIP_CHECK(launch_preprocess(in, in_fmt, B, t.H, t.W, t.dev, f16, s));
+                FR_HIP_CHECK(launch_preprocess(in, in_fmt, B, t.H, t.W, t.dev, f16 || t.f16, s));
                 break;
             }
             case OP_CONV: {
@@ -1246,7 +1265,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 const auto& ti = h->tensors[op.in];
                 const auto& to = h->tensors[op.out];
                 ConvArgs a{};
-                a.f16 = f16;
+                a.f16 = f16 || ti.f16;
+                a.y_bf16 = ti.f16 && !to.f16;  // f16 section -> bf16 plan boundary
                 a.x = ti.dev; a.B = B; a.H = ti.H; a.W = ti.W; a.Cx = ti.C; a.x_off = op.in_off; a.Cin = op.cin;
                 a.w = cw.w; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
                 a.K = cw.K; a.Kpad = cw.Kpad;
@@ -1282,8 +1302,12 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 ps.start("maxpool");
                 const auto& ti = h->tensors[op.in];
                 const auto& to = h->tensors[op.out];
+                if (ti.f16 != to.f16) {
+                    set_error("plan: maxpool across the f16 section boundary");
+                    return FR_ERR_ARG;
+                }
                 FR_HIP_CHECK(launch_maxpool(ti.dev, B, ti.H, ti.W, ti.C, 0, ti.C, op.pk, op.ps, op.pp, to.dev, to.C,
-                                            op.out_off, to.H, to.W, f16, s));
+                                            op.out_off, to.H, to.W, f16 || ti.f16, s));
                 break;
             }
             case OP_AVGPOOL: {
@@ -1804,6 +1828,11 @@ int fr_debug_tensor_shape(const fr_handle* h, int t, int* H, int* W, int* C) {
     if (!h || t < 0 || t >= (int)h->tensors.size() || !H || !W || !C) { set_error("fr_debug_tensor_shape: bad argument"); return FR_ERR_ARG; }
     *H = h->tensors[t].H; *W = h->tensors[t].W; *C = h->tensors[t].C;
     return FR_OK;
+}
+
+int fr_debug_tensor_dtype(const fr_handle* h, int t) {
+    if (!h || t < 0 || t >= (int)h->tensors.size()) { set_error("fr_debug_tensor_dtype: bad argument"); return FR_ERR_ARG; }
+    return h->tensors[t].f16 ? FR_DTYPE_F16 : (h->dtype == FR_DTYPE_FP8 ? FR_DTYPE_BF16 : h->dtype);
 }
 
 int fr_debug_copy_tensor(fr_handle* h, int t, int B, void* dst, void* stream) {

@@ -43,6 +43,7 @@ struct ConvArgs {
     // channels x2_off.., and the weight rows hold [W_conv | W_downsample] (bias = the sum)
     const bf16_t* x2;
     int H2, W2, Cx2, x2_off, C2, st2, K1;
+    int y_bf16;                   // f16 input / MFMA, bf16 output (igemm; the end of an f16 plan section)
 };
 // Persistent weight-resident 3x3/s1/p1 conv with 64 input channels (conv_rows.hip); a.wimg = the
 // rows_pack_weights image, a.ep / a.negf set.

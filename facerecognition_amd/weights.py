@@ -28,11 +28,9 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 ARCHS = ("resnet50_arcface", "iresnet100", "irv1_facenet")
-# Default compute dtype per backbone: bf16 as BASELINE.json names it; the synthetic
-# Every backbone defaults to bf16 (BASELINE configs 2-3).  InceptionResnetV1 in bf16 misses the 1e-3
-# cosine bar on the synthetic weights (~2e-3: the stem layers' bf16 output rounding, 8x the f16 error at
-# every stage, amplified by the calibrated last_bn; tools/drift_compare.py); dtype="f16"
-# (same MFMA rate, 3 more mantissa bits) meets it.
+# Default compute dtype per backbone: bf16 as BASELINE.json names it (configs 2-3).  The
+# bf16 InceptionResnetV1 plan stores and multiplies its high-resolution stem (conv2d_1a .. conv2d_4a) in
+# f16: all-bf16 missed the 1e-3 cosine bar (~2e-3, the stem's rounding dominates; tools/drift_compare.py).
 DEFAULT_DTYPE = {"resnet50_arcface": "bf16", "iresnet100": "bf16", "irv1_facenet": "bf16"}
 ARCH_IDS = {"resnet50_arcface": 0, "iresnet100": 1, "irv1_facenet": 2}
 INPUT_SIZE = {"resnet50_arcface": 112, "iresnet100": 112, "irv1_facenet": 160}

@@ -270,6 +270,9 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n);
 const char* fr_debug_tensor_name(const fr_handle* h, int t);
 int fr_debug_tensor_shape(const fr_handle* h, int t, int* H, int* W, int* C);
 /* Copy the first B samples of tensor t (bf16 NHWC) to dst (device) after an fr_embed. */
+/* Storage dtype of tensor t (FR_DTYPE_BF16 / FR_DTYPE_F16): a bf16 IRV1 plan keeps its high-resolution stem
+ * tensors in f16, so fr_debug_copy_tensor's 16-bit elements are to be read in this dtype. */
+int fr_debug_tensor_dtype(const fr_handle* h, int t);
 int fr_debug_copy_tensor(fr_handle* h, int t, int B, void* dst, void* stream);
 
 #ifdef __cplusplus

@@ -26,7 +26,6 @@ def stage_report(arch, B=2, seed=0, dtype=None):
     sd = synth_state_dict(arch)
     m = FRModel(arch, sd, dtype=dtype)
     m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)  # the layer3 stage kernel materialises its blocks too
-    dt = torch.float16 if m.dtype == "f16" else torch.bfloat16
     m.embed(torch.from_numpy(u8))
     torch.cuda.synchronize()
     L = N.lib()
@@ -37,6 +36,8 @@ def stage_report(arch, B=2, seed=0, dtype=None):
             continue
         H, W, C = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         N.check(L.fr_debug_tensor_shape(m.handle, t, ctypes.byref(H), ctypes.byref(W), ctypes.byref(C)))
+        # storage dtype per tensor (a bf16 IRV1 plan keeps its stem in f16)
+        dt = torch.float16 if L.fr_debug_tensor_dtype(m.handle, t) == N.FR_DTYPE_F16 else torch.bfloat16
         buf = torch.empty((B, H.value, W.value, C.value), dtype=dt, device="cuda")
         N.check(L.fr_debug_copy_tensor(m.handle, t, B, buf.data_ptr(), N.stream_ptr()))
         torch.cuda.synchronize()

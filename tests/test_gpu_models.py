@@ -34,9 +34,9 @@ def _oracle_embed(arch, u8):
     return _cache[key]
 
 
-# (arch, dtype): IResNet100 / ResNet-50 at the 1e-3 bar in bf16 and f16, InceptionResnetV1 in f16;
-# bf16 InceptionResnetV1 (its default) is test_irv1_bf16_parity (xfail) — DESIGN.md §5.
-CASES = [("iresnet100", "bf16"), ("resnet50_arcface", "bf16"), ("irv1_facenet", "f16"),
+# (arch, dtype): every model at the 1e-3 bar in bf16 and f16 (a bf16 InceptionResnetV1 plan keeps its
+# high-resolution stem in f16).
+CASES = [("iresnet100", "bf16"), ("resnet50_arcface", "bf16"), ("irv1_facenet", "bf16"), ("irv1_facenet", "f16"),
          ("iresnet100", "f16"), ("resnet50_arcface", "f16")]
 
 
@@ -109,12 +109,10 @@ def test_top1_planted_gallery(arch_model):
     assert np.array_equal(ri[:, 0], np.arange(6))
 
 
-@pytest.mark.xfail(reason="bf16 InceptionResnetV1 misses the 1e-3 bar on the synthetic weights (~2e-3: "
-                          "bf16 rounding of the stem layers, amplified by the calibrated last_bn; f16 meets it, "
-                          "test_embedding_cosine[irv1_facenet-f16]); DESIGN.md §5", strict=False)
 def test_irv1_bf16_parity(gpu):
-    """BASELINE config 3's dtype (bf16) at the north-star bar, 1e-3 cosine vs the fp32 oracle.  Known to
-    fail (xfail) on the synthetic weights; the measured 1-cos is printed."""
+    """BASELINE config 3's dtype (bf16) at the north-star bar, 1e-3 cosine vs the fp32 oracle.  An all-bf16
+    plan measured ~2e-3 (profiles/r02_irv1_drift_bf16_vs_f16.txt: the stem's rounding dominates); the
+    plan keeps conv2d_1a .. conv2d_4a in f16 storage and MFMA, conv2d_4b writes bf16 (4e-4 .. 8e-4)."""
     from facerecognition_amd.model import FRModel
     m = FRModel.synthetic("irv1_facenet", dtype="bf16")
     u8 = _probes("irv1_facenet", 6)
@@ -129,9 +127,8 @@ def test_irv1_bf16_parity(gpu):
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_irv1_full_batch_bs256(gpu, dtype):
     """BASELINE config-3 size (InceptionResnetV1 @160, bs = 256): deterministic replay, finite unit-norm
-    rows, batch independence against a 5-face call, an oracle sample (f16: the 1e-3 bar; bf16: its
-    measured ~2e-3 level, 3e-3, see test_irv1_bf16_parity), and identical top-1 against the oracle's
-    ranking on a planted 10k gallery."""
+    rows, batch independence against a 5-face call, an oracle sample at the 1e-3 bar, and identical top-1
+    against the oracle's ranking on a planted 10k gallery."""
     from facerecognition_amd.gallery import DeviceGallery
     from facerecognition_amd.model import FRModel
     m = FRModel.synthetic("irv1_facenet", dtype=dtype)
@@ -144,7 +141,7 @@ def test_irv1_full_batch_bs256(gpu, dtype):
     assert float((1 - (a[60:65] * small).sum(1)).max()) <= COS_TOL
     ref = _oracle_embed("irv1_facenet", u8[:4].numpy())
     cos_o = (a[:4].numpy() * ref).sum(1) / np.linalg.norm(ref, axis=1)
-    assert float((1 - cos_o).max()) <= (COS_TOL if dtype == "f16" else 3e-3), 1 - cos_o
+    assert float((1 - cos_o).max()) <= COS_TOL, 1 - cos_o
     rng = np.random.default_rng(32)
     G = rng.standard_normal((10000, 512)).astype(np.float32)
     perm = rng.permutation(10000)[:256]
@@ -189,7 +186,7 @@ def test_facenet_projection_head(gpu):
     from facerecognition_amd.weights import synth_state_dict
     from oracle import models as M
     sd = synth_state_dict("irv1_facenet", embedding_size=128)
-    m = FRModel("irv1_facenet", sd, dtype="f16")  # the 1e-3 bar: f16 (bf16: test_irv1_bf16_parity)
+    m = FRModel("irv1_facenet", sd, dtype="bf16")
     assert m.embedding_size == 128
     u8 = _probes("irv1_facenet", 4, seed=2)
     got = m.embed(torch.from_numpy(u8)).cpu().numpy()

@@ -18,12 +18,12 @@ pytestmark = pytest.mark.gpu
 def _named(m, B, names):
     import ctypes
     L = N.lib()
-    dt = torch.float16 if m.dtype == "f16" else torch.bfloat16
     out = {}
     for t in range(L.fr_debug_tensor_count(m.handle)):
         name = L.fr_debug_tensor_name(m.handle, t).decode()
         if name not in names:
             continue
+        dt = torch.float16 if L.fr_debug_tensor_dtype(m.handle, t) == N.FR_DTYPE_F16 else torch.bfloat16
         H, W, C = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         N.check(L.fr_debug_tensor_shape(m.handle, t, ctypes.byref(H), ctypes.byref(W), ctypes.byref(C)))
         buf = torch.empty((B, H.value, W.value, C.value), dtype=dt, device="cuda")
