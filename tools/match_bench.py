@@ -16,13 +16,13 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(rows, probes, k, iters, exact=False):
+def run(rows, probes, k, iters, exact=False, x3_min_rows=None):
     from facerecognition_amd.gallery import DeviceGallery
     g = torch.randn(rows, 512, device="cuda")
     g = g / g.norm(dim=1, keepdim=True)
     p = torch.randn(probes, 512, device="cuda")
     p = p / p.norm(dim=1, keepdim=True)
-    gal = DeviceGallery(handle=None)
+    gal = DeviceGallery(handle=None, x3_min_rows=x3_min_rows)
     gal.set_device_rows(g)
     gal.set_exact(exact)
     for _ in range(3):
@@ -40,7 +40,8 @@ def run(rows, probes, k, iters, exact=False):
     agree = float((i[:64, 0] == ref).float().mean())
     flop = 2.0 * probes * rows * 512
     gbytes = rows * 512 * 4 / 1e9
-    return {"rows": rows, "probes": probes, "k": k, "path": "exact-f32" if exact or rows < 32768 else "bf16x3", "ms": round(ms, 4), "tflops_f32": round(flop / ms / 1e9, 2),
+    x3 = not exact and rows >= (x3_min_rows or 32768)
+    return {"rows": rows, "probes": probes, "k": k, "path": "bf16x3" if x3 else "exact-f32", "ms": round(ms, 4), "tflops_f32": round(flop / ms / 1e9, 2),
             "gallery_GBps": round(gbytes / ms * 1e3, 1), "top1_agree_torch": agree}
 
 
@@ -49,6 +50,9 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--exact", action="store_true", help="force the f32-MFMA kernel (FR_OPT_MATCH_EXACT)")
+    ap.add_argument("--x3-min-rows", type=int, default=None, help="FR_OPT_X3_MIN_ROWS for the galleries")
+    ap.add_argument("--only-rows", type=int, default=None, help="run only the shape with this many rows")
     a = ap.parse_args()
     for rows, probes in ((10000, 256), (125000, 2048), (1000000, 256)):
-        print(json.dumps(run(rows, probes, a.k, a.iters, a.exact)), flush=True)
+        if a.only_rows is None or rows == a.only_rows:
+            print(json.dumps(run(rows, probes, a.k, a.iters, a.exact, a.x3_min_rows)), flush=True)
