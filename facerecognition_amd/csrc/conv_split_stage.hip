@@ -91,6 +91,16 @@ __device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {
     return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
+// K-step order within a pair of 32-channel groups (18 positions): the 3 dh = 1 taps of both groups first
+// (they read own rows only), then dh = 0 and dh = 2 (which also read the halo rows).  The halo rows of a
+// conv are imported while positions 2 .. 4 of its first pair run (run_conv).  The weights are packed in
+// this order (split_stage_pack_weights).
+__host__ __device__ constexpr int pos_cg(int q) { return q < 3 ? 0 : (q < 6 ? 1 : (q < 12 ? 0 : 1)); }
+__host__ __device__ constexpr int pos_tap(int q) {
+    return q < 6 ? 3 + q % 3 : ((q - 6) % 6 < 3 ? (q - 6) % 6 : 3 + (q - 6) % 6);
+}
+constexpr int HALO_POS = 2;  // the import is issued between positions 1 and 2 and lands by position 4
+
 // xchg layout: [B][PARTS][which: 0 = first row, 1 = last row][parity][IW][C]
 template <typename G>
 __host__ __device__ constexpr size_t xchg_elems(int B) { return (size_t)B * G::PARTS * 2 * 2 * G::XROW; }
@@ -159,7 +169,9 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     // one K-step (the layer3 stage's former schedule): MFMAs of the first half of the weight fragments on
     // `cur` while `nxt` is read; mid-step barrier (the issuing waves' slice g+1 landed, every wave is
     // past its reads of slot g % 3); DMA of slice g+3 into that slot; refills of wf with slice g+1
-    auto kstep = [&](int g, int slot, frag (&cur)[FM], frag (&nxt)[FM], int cg_n, int tap_n) {
+    // halo: vector-memory ops younger than this step's weight slice that may stay in flight (the halo-row
+    // DMAs issued between positions 1 and 2 of a conv's first pair: 0, 1, 2 or 4 per wave)
+    auto kstep = [&](int g, int slot, frag (&cur)[FM], frag (&nxt)[FM], int cg_n, int tap_n, int halo) {
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         pread(nxt, cg_n, tap_n);
@@ -168,7 +180,10 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wf[i], cur[j], acc[i][j]);
         // the FM youngest LDS reads are this step's pread(nxt); older refills of slot `slot` must be done
-        asm volatile("s_waitcnt vmcnt(1) lgkmcnt(7)\n\ts_barrier" ::: "memory");
+        if (halo == 0) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(7)\n\ts_barrier" ::: "memory");
+        else if (halo == 1) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(7)\n\ts_barrier" ::: "memory");
+        else if (halo == 2) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(7)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(5) lgkmcnt(7)\n\ts_barrier" ::: "memory");
         issue_w(g + 3 < total ? g + 3 : total - 1, slot);
         const int nslot = slot == NSLOT - 1 ? 0 : slot + 1;
 #pragma unroll
@@ -234,23 +249,70 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     // element offset of row `which` of part `pt`, parity `par`
     auto xrow_off = [&](int pt, int which, int par) { return (((size_t)(b * PARTS + pt) * 2 + which) * 2 + par) * XROW; };
 
+    // Halo import of conv cv's boundary rows (published by the neighbours at the end of conv cv), issued
+    // inside conv cv+1 between positions 1 and 2: wave 0 polls the neighbours' counters, the other waves
+    // join it at a barrier, then every wave LDS-DMAs its planes' halo rows (sc1, straight into the patch:
+    // one instruction per (plane, row), 512 B on 32 lanes for PC = 32) and returns the count it issued.
+    // Positions 2 and 3 leave those DMAs in flight (kstep's halo slack); position 4's wait and barrier
+    // complete them before position 5 reads position 6, the first halo tap.
+    auto import_halo = [&](int cv) {
+        if (wave == 0 && lane < 2 && !(FR_SPLIT_EXP & 1) && (lane == 0 ? has_up : has_dn)) {
+            const int* nf = my_flag + (lane == 0 ? -1 : 1);
+            int it = 0;
+            while (__hip_atomic_load(nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cv + 1) {
+                if (++it == SPIN_LIMIT) {
+                    __hip_atomic_fetch_add(p.spin_timeouts, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        // raw barrier: __syncthreads() would first drain every wave's in-flight weight DMAs
+        asm volatile("s_barrier" ::: "memory");
+        int n = 0;
+        const int pos = lane, px = pos - 1;  // patch column pos <- image column pos - 1 (halo columns: zeros)
+        const bool lane_on = pos < PC;
+#pragma unroll
+        for (int u = 0; u < NPL / NW; ++u) {
+            const int pl = wave + NW * u;
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                if (side == 0 ? !has_up : !has_dn) continue;
+                const size_t row = side == 0 ? xrow_off(part - 1, 1, cv & 1) : xrow_off(part + 1, 0, cv & 1);
+                const uint32_t off = (unsigned)px < (unsigned)IW ? (uint32_t)((row + px * C + pl * 8) * 2) : OOB;
+                char* dst = smem + pl * PLANE_B + (side == 0 ? 0 : (PR - 1) * PC * 16);
+                if (lane_on)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr_x, (lds_void*)dst, 16, off, 0, 0, SC1);
+                ++n;
+            }
+        }
+        return n;
+    };
+    int pending = -1;  // conv whose boundary rows are still to be imported (-1: none)
+
     auto run_conv = [&](int cv, auto second_tag) {
         constexpr bool second = decltype(second_tag)::value;
         if (!second) seed_bias(cv);  // conv2's seed (x + its bias) comes from conv1's epilogue
-        pread(pA, 0, 0);
+        pread(pA, pos_cg(0), pos_tap(0));
 #pragma unroll
         for (int i = 0; i < FN; ++i) wread(i, 0);  // step 0 of every conv sits in slot 0 (KSTEPS % 3 == 0)
         const int g0 = cv * KSTEPS;
+        int halo = 0;
 #pragma unroll 1
         for (int cg = 0; cg < C / 32; cg += 2) {
 #pragma unroll
             for (int t = 0; t < 18; ++t) {
-                const int cgl = cg + t / 9, tap = t % 9;
-                const int cgn = t == 8 ? cg + 1 : (t == 17 ? (cg + 2 < C / 32 ? cg + 2 : 0) : cgl);
-                const int tapn = t == 8 || t == 17 ? 0 : tap + 1;
-                if (t & 1) kstep(g0 + cgl * 9 + tap, tap % 3, pB, pA, cgn, tapn);
-                else kstep(g0 + cgl * 9 + tap, tap % 3, pA, pB, cgn, tapn);
+                if (t == HALO_POS && cg == 0 && pending >= 0 && !(FR_SPLIT_EXP & 2)) {
+                    halo = import_halo(pending);
+                    pending = -1;
+                }
+                const int cgn = t == 17 ? (cg + 2 < C / 32 ? cg + 2 : 0) : cg + pos_cg(t + 1);
+                const int tapn = t == 17 ? pos_tap(0) : pos_tap(t + 1);
+                const int hs = t == HALO_POS || t == HALO_POS + 1 ? halo : 0;
+                if (t & 1) kstep(g0 + cg * 9 + t, t % 3, pB, pA, cgn, tapn, hs);
+                else kstep(g0 + cg * 9 + t, t % 3, pA, pB, cgn, tapn, hs);
             }
+            halo = 0;
         }
         // ---- epilogue (every wave is past its last patch read)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -313,42 +375,15 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
             }
         }
         if (exch && !(FR_SPLIT_EXP & 2)) {
-            // publish: every storing wave's rows are complete, a barrier, one sc1 counter store
+            // publish: every storing wave's rows are complete, a barrier, one sc1 counter store; the
+            // neighbours' rows are imported during the next conv (import_halo)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (threadIdx.x == 0 && !(FR_SPLIT_EXP & 1))
                 __hip_atomic_store(my_flag, cv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // wait for the neighbours' conv cv (wave 0 polls, the others join it at the barrier)
-            if (wave == 0 && lane < 2 && !(FR_SPLIT_EXP & 1) && (lane == 0 ? has_up : has_dn)) {
-                const int* nf = my_flag + (lane == 0 ? -1 : 1);
-                int it = 0;
-                while (__hip_atomic_load(nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cv + 1) {
-                    if (++it == SPIN_LIMIT) {
-                        __hip_atomic_fetch_add(p.spin_timeouts, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            __syncthreads();
-            // the neighbours' rows into the halo rows: IW x NPL slots of 16 B per row (pixel-major, NPL
-            // threads per pixel), sc1 loads
-            const int t = threadIdx.x;
-            if (t < IW * NPL) {
-                const int px = t / NPL, pl = t % NPL;
-                if (has_up) {
-                    const uint32_t off = (uint32_t)((xrow_off(part - 1, 1, cv & 1) + px * C + pl * 8) * 2);
-                    const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr_x, off, 0, SC1));
-                    *(uint4*)(smem + pl * PLANE_B + (px + 1) * 16) = v;
-                }
-                if (has_dn) {
-                    const uint32_t off = (uint32_t)((xrow_off(part + 1, 0, cv & 1) + px * C + pl * 8) * 2);
-                    const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr_x, off, 0, SC1));
-                    *(uint4*)(smem + pl * PLANE_B + ((PR - 1) * PC + px + 1) * 16) = v;
-                }
-            }
+            pending = cv;
         }
-        // the new activation (and halo rows) is visible to every wave before the next conv reads it
+        // the new activation is visible to every wave before the next conv reads it
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
 #pragma unroll 1
@@ -378,6 +413,20 @@ hipError_t launch_split_t(const StageArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+// Per conv: pairs of 32-channel groups, 18 positions each in the pos_cg / pos_tap order, each position the
+// K-step image [4 groups g][C rows n][8 channels] of channels 32 (2 pair + pos_cg) + 8 g + e at tap pos_tap.
+void split_stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out) {
+    for (int pair = 0; pair < C / 64; ++pair)
+        for (int q = 0; q < 18; ++q) {
+            const int cg = 2 * pair + pos_cg(q), tap = pos_tap(q);
+            bf16_t* s = out + (size_t)(pair * 18 + q) * 4 * C * 8;
+            for (int g = 0; g < 4; ++g)
+                for (int n = 0; n < C; ++n)
+                    for (int e = 0; e < 8; ++e)
+                        s[(g * C + n) * 8 + e] = rows[(size_t)n * Kpad + tap * C + cg * 32 + g * 8 + e];
+        }
+}
 
 int split_stage_parts(int H, int W, int C) {
     if (H == Split28::IW && W == Split28::IW && C == Split28::C) return Split28::PARTS;

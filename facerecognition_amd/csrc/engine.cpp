@@ -565,7 +565,8 @@ int build_stage(fr_handle* h, StageRec& r) {
         }
         std::vector<bf16_t> rows((size_t)cw.Npad * cw.Kpad);
         FR_HIP_CHECK(hipMemcpy(rows.data(), cw.w, rows.size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
-        stage_pack_weights(rows.data(), cw.Kpad, C, packed.data() + c * per);
+        if (r.parts > 1) split_stage_pack_weights(rows.data(), cw.Kpad, C, packed.data() + c * per);
+        else stage_pack_weights(rows.data(), cw.Kpad, C, packed.data() + c * per);
         tab[c].bias = cw.bias9 ? nullptr : cw.bias;
         tab[c].bias9 = cw.bias9;
         tab[c].slope = cw.slope;

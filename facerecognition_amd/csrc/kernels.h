@@ -114,6 +114,7 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t s);
 // boundary rows per conv through xchg / flags.  split_stage_parts: workgroups per image, 0 = unsupported.
 int split_stage_parts(int H, int W, int C);
 size_t split_stage_weight_bytes(int C, int nconv);
+void split_stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out);  // the split stages' K order
 size_t split_stage_xchg_elems(int B);  // enough for either geometry
 hipError_t launch_split_stage(const StageArgs& a, int H, int C, hipStream_t s);
 // Split-K reduction + the same fused epilogue as the conv kernel.
