@@ -46,6 +46,12 @@ constexpr uint32_t OOB = 0x80000000u;
 #ifndef FR_ROWS_SEED_EARLY
 #define FR_ROWS_SEED_EARLY 0  // issue the next unit's seed loads before the K loop instead of after it
 #endif
+#ifndef FR_ROWS_SCHED
+#define FR_ROWS_SCHED 1  // K-step instruction order pinned with sched_group_barrier (A/B: 0 = compiler's)
+#endif
+#ifndef FR_ROWS_DRAIN
+#define FR_ROWS_DRAIN 0  // A/B: 1 = drain the unit's output stores before the next unit starts
+#endif
 #ifndef FR_ROWS_EXP
 #define FR_ROWS_EXP 0  // timing-only experiments (WRONG results): 1 trivial epilogue, 2 no K-loop MFMAs,
                        // 4 no next-patch DMA, 8 no fragment reads in the K loop
@@ -204,12 +210,27 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
         read_step(0, buf, 0);
 #pragma unroll
         for (int s = 0; s < NKS; ++s) {
+#if FR_ROWS_SCHED
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             if (s + 1 < NKS && !(FR_ROWS_EXP & 8)) read_step(s + 1, buf, (s + 1) & 1);
 #if !(FR_ROWS_EXP & 2)
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(fa[s & 1][i], fb[s & 1][j], acc[i][j]);
+#if FR_ROWS_SCHED
+            // pinned order: one next-step fragment read behind each of the first 9 MFMAs (left to
+            // itself the scheduler sinks each read to just before its use and waits on it there)
+            if (s + 1 < NKS && !(FR_ROWS_EXP & 8)) {
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
+            }
+#endif
 #else
             acc[s & 1][s % 7][0] += (float)fa[s & 1][0][0] + (float)fb[s & 1][s % 7][0];
 #endif
@@ -257,7 +278,10 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
                     if (has_next) seed(i, j);
                 }
             }
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            // every load of this unit (the next patch's DMA, then the seeds) has landed before the
+            // copy-out stores issue, so the unit's end need not drain them (vmcnt would: gfx950 counts
+            // stores in vmcnt, and a load/store mix may retire out of order)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             // copy-out: 224 x 8 chunks of 16 B, 8 consecutive lanes per pixel row
 #pragma unroll
             for (int q = 0; q < 7; ++q) {
@@ -267,10 +291,14 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
                 *(uint4*)(p.y + (base + rr * W + c) * p.Cy + p.y_off + 64 * ng + cl * 8) = v;
             }
         }
-        // next patch (and seeds) landed for every wave; every wave is past its reads of `buf`, which
-        // the next iteration's DMA overwrites
+        // every wave is past its copy-out reads of `buf`, which the next iteration's DMA overwrites (the
+        // next patch landed before the copy-out; its stores stay in flight)
+#if FR_ROWS_DRAIN || (FR_ROWS_EXP & 1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#else
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
         cur = nxt;
         buf ^= 1;
     }
