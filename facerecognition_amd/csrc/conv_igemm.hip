@@ -29,6 +29,9 @@ namespace fr {
 namespace {
 
 constexpr int BK = 64;
+#ifndef FR_IGEMM_SCHED
+#define FR_IGEMM_SCHED 1  // K-step fragment reads pinned between MFMAs (A/B: 0 = the compiler's order)
+#endif
 constexpr uint32_t OOB = 0x80000000u;  // buffer offset past num_records → the DMA writes zeros
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -228,25 +231,54 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
     auto compute = [&](int buf) {
         const bf16_t* sA = (const bf16_t*)(smem + buf * STAGE);
         const bf16_t* sW = (const bf16_t*)(smem + buf * STAGE + STAGE_A);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            frag af[FN], bfr[FM];
+        frag af[2][FN], bfr[2][FM];
+        auto rd = [&](int kk) {
             const int ch = kk * 4 + (lane >> 4);
 #pragma unroll
             for (int i = 0; i < FN; ++i) {
                 const int row = wn * TWN + i * 16 + (lane & 15);
-                af[i] = *(const frag*)(sW + row * BK + swz(row, ch) * 8);
+                af[kk][i] = *(const frag*)(sW + row * BK + swz(row, ch) * 8);
             }
 #pragma unroll
             for (int j = 0; j < FM; ++j) {
                 const int row = wm * TWM + j * 16 + (lane & 15);
-                bfr[j] = *(const frag*)(sA + row * BK + swz(row, ch) * 8);
+                bfr[kk][j] = *(const frag*)(sA + row * BK + swz(row, ch) * 8);
             }
+        };
+#if FR_IGEMM_SCHED
+        // pinned order: the first half-step's fragments, then its MFMAs with the second half-step's
+        // fragment reads spread between them (left to itself the scheduler issues each read just before
+        // its use and waits on it there)
+        __builtin_amdgcn_sched_barrier(0);
+        rd(0);
+        __builtin_amdgcn_sched_barrier(0);
+        rd(1);
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[0][i], bfr[0][j], acc[i][j]);
+        constexpr int R = FN + FM, MF = FN * FM, PER = MF / R > 0 ? MF / R : 1;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if constexpr (MF > PER * R) __builtin_amdgcn_sched_group_barrier(0x008, MF - PER * R, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[1][i], bfr[1][j], acc[i][j]);
+#else
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            rd(kk);
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
-                for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
+                for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[kk][i], bfr[kk][j], acc[i][j]);
         }
+#endif
     };
 
     constexpr int G = BN / 8;            // 8-channel groups per tile row
