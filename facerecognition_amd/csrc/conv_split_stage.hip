@@ -55,7 +55,10 @@ struct SplitGeo {
     static constexpr int PATCH_B = NPL * PLANE_B;
     static constexpr int SLICE_B = 4 * C * 16;       // one K-step: [4 groups of 8 ch][C rows][16 B]
     static constexpr int NSLOT = 3;
-    static constexpr int LDS = PATCH_B + NSLOT * SLICE_B;
+    static constexpr int TAB_ROWS_B = 6 * C * 4;     // the 6 border classes a part can meet, [6][C] f32
+    static constexpr int TS = TAB_ROWS_B + C * 4;      // + one row: the PReLU slope of the conv before
+    static constexpr int TAB = PATCH_B + NSLOT * SLICE_B;
+    static constexpr int LDS = TAB + 2 * TS;
     static constexpr int KSTEPS = (C / 32) * 9;
     static constexpr int NG = C / 64;                // channel groups of 64
     static constexpr int MG = 8 / NG;                // pixel groups
@@ -78,17 +81,13 @@ constexpr int SC1 = 16;                   // buffer-load cache policy: sc1 (L1 b
 
 #ifndef FR_SPLIT_EXP
 #define FR_SPLIT_EXP 0  // timing-only experiments (WRONG results): 1 exchange rows without the counter
-                        // synchronisation, 2 no exchange at all
+                        // synchronisation, 2 no exchange at all, 4 trivial epilogue (MFMAs kept)
 #endif
 
 typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, soff, 0, 0);
-}
-
-__device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {
-    return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
 // K-step order within a pair of 32-channel groups (18 positions): the 3 dh = 1 taps of both groups first
@@ -101,7 +100,7 @@ __host__ __device__ constexpr int pos_tap(int q) {
 }
 constexpr int HALO_POS = 2;  // the import is issued between positions 1 and 2 and lands by position 4
 
-// xchg layout: [B][PARTS][which: 0 = first row, 1 = last row][parity][IW][C]
+// xchg layout: [B][PARTS][which: 0 = first row, 1 = last row][parity][C / 8 planes][IW][8]
 template <typename G>
 __host__ __device__ constexpr size_t xchg_elems(int B) { return (size_t)B * G::PARTS * 2 * 2 * G::XROW; }
 
@@ -146,11 +145,6 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         if (WB == 1024 || lane < WB / 16)
             dma16s(wr, smem + PATCH_B + slot * SLICE_B + wave * WB, (uint32_t)(wave * WB + lane * 16), (uint32_t)g * SLICE_B);
     };
-    issue_w(0, 0);
-    issue_w(1, 1);
-    issue_w(2, 2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
 
     // fragment addresses: B (patch) fragment f = FM wm + j covers virtual pixels 16f + (lane & 15) at plane
     // (lane >> 4) of the K-step's 4-plane group; A (weights) rows n = 64 wn + 16 i + (lane & 15)
@@ -196,58 +190,61 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         }
     };
 
-    // Epilogue tables ep[cv][9][C] (bias per border class) / slope[cv][C], as in the layer3 stage.
-    // Fragment f = FM wm + j lies in row f / QPR, columns 16 (f % QPR) + (lane & 15): its column class
-    // is left for f % QPR == 0 and lane column 0, right for f % QPR == QPR - 1 at column IW - 1, else
-    // interior; its row class is the image border only for the first row of part 0 and the last row of
-    // the last part.  Per channel fragment i a lane needs 6 biases: {interior, border row} x {first,
-    // middle, last fragment of a row}.
-    auto load_ep = [&](int cv, int i, float4 (&e)[6]) {
+    // Epilogue tables ep[cv][9][C] (bias per border class, class = 3 row class + column class) and
+    // slope[cv][C], staged in LDS per conv: slot 0 holds the conv1 biases of the current block (its
+    // accumulator seeds), slot 1 the conv2 biases (seeded in conv1's epilogue) plus conv1's slopes.  A part
+    // meets 6 classes at most (row classes tbase, tbase + 1: top + interior for part 0, interior + bottom
+    // for the others), so a slot holds those 6 rows.  Slot 1 is DMA'd at conv1's start, slot 0 (the next
+    // block's) at conv2's start; the K loop's per-step vmcnt waits and barriers complete them.
+    const int tbase = part == 0 ? 0 : 1;
+    const __amdgpu_buffer_rsrc_t epr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.ep, 0, (uint32_t)((size_t)nconv * 9 * C * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t slr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv * C * 4), 0x00020000);
+    auto issue_tab = [&](int cv, int cv_slope, int slot) {
+        char* dst = smem + G::TAB + slot * G::TS;
+        if (wave * 1024 < G::TAB_ROWS_B && wave * 1024 + lane * 16 < G::TAB_ROWS_B)
+            dma16s(epr, dst + wave * 1024, (uint32_t)(wave * 1024 + lane * 16), (uint32_t)((cv * 9 + 3 * tbase) * C * 4));
+        if (cv_slope >= 0 && wave == NW - 1 && lane * 16 < C * 4)
+            dma16s(slr, dst + G::TAB_ROWS_B, (uint32_t)(lane * 16), (uint32_t)(cv_slope * C * 4));
+    };
+    // table-row byte offset of fragment j's output pixel for this lane: row class (wave-uniform) and
+    // column class (the lane's column: left edge, interior, right edge)
+    auto tab_row = [&](int j, int ln) {  // ln: an opaque lane copy (keeps LICM from hoisting + spilling)
+        const int f = FM * wm + j, q = f % QPR, cl = ln & 15;
+        const int rc = (part == 0 && f < QPR) ? 0 : ((part == PARTS - 1 && f >= (HR - 1) * QPR) ? 2 : 1);
+        const int cc = (q == 0 && cl == 0) ? 0 : ((q == QPR - 1 && cl == (IW - 1) % 16) ? 2 : 1);
+        return ((rc - tbase) * 3 + cc) * C * 4;
+    };
+    auto seed_bias = [&]() {
         int ln = lane;
-        asm volatile("" : "+v"(ln));  // opaque copy: the addresses are not hoisted into the K loop
-        const int cl = ln & 15, ccf = cl == 0 ? 0 : 1, ccl = cl == (IW - 1) % 16 ? 2 : 1;
-        const int br = part == 0 ? 0 : 6;  // border-row class of this part (used by part 0 / the last part)
-        const float* ep = p.ep + (size_t)cv * 9 * C + 64 * wn + 16 * i + 4 * (ln >> 4);
-        e[0] = *(const float4*)(ep + (3 + ccf) * C);
-        e[2] = *(const float4*)(ep + (3 + ccl) * C);
-        e[3] = *(const float4*)(ep + (br + ccf) * C);
-        e[5] = *(const float4*)(ep + (br + ccl) * C);
-        if (QPR > 2) {  // rows with interior-only fragments
-            e[1] = *(const float4*)(ep + 4 * C);
-            e[4] = *(const float4*)(ep + (br + 1) * C);
-        } else {
-            e[1] = e[4] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    auto pick = [&](const float4 (&e)[6], int j) {
-        const int f = FM * wm + j, q = f % QPR;
-        const bool border = (part == 0 && f < QPR) || (part == PARTS - 1 && f >= (HR - 1) * QPR);
-        // component selects on values: a dynamic index, or a select of element addresses, would keep
-        // e in scratch memory
-        const float4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4], e5 = e[5];
-        const float4 in = sel4(q == 0, e0, QPR > 2 ? sel4(q == QPR - 1, e2, e1) : e2);
-        const float4 bo = sel4(q == 0, e3, QPR > 2 ? sel4(q == QPR - 1, e5, e4) : e5);
-        return sel4(border, bo, in);
-    };
-    auto seed_bias = [&](int cv) {
+        asm volatile("" : "+v"(ln));
+        const char* t = smem + G::TAB;
+        const int nl4 = (64 * wn + 4 * (ln >> 4)) * 4;  // + 64 i: the lane's channel bytes in a table row
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-            float4 e[6];
-            load_ep(cv, i, e);
+        for (int j = 0; j < FM; ++j) {
+            const int tr = tab_row(j, ln);
 #pragma unroll
-            for (int j = 0; j < FM; ++j) {
-                const float4 bb = pick(e, j);
+            for (int i = 0; i < FN; ++i) {
+                const float4 bb = *(const float4*)(t + tr + nl4 + 64 * i);
                 acc[i][j] = (f32x4_t){bb.x, bb.y, bb.z, bb.w};
             }
         }
     };
+
+    issue_w(0, 0);
+    issue_w(1, 1);
+    issue_w(2, 2);
+    issue_tab(0, -1, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 
     const bool has_up = part > 0, has_dn = part < PARTS - 1;
     int* const my_flag = p.flags + b * PARTS + part;
     const __amdgpu_buffer_rsrc_t xr_x = __builtin_amdgcn_make_buffer_rsrc(
         (void*)p.xchg, 0, (uint32_t)min((size_t)0x7fffffff, xchg_elems<G>(p.B) * 2), 0x00020000);
     // element offset of row `which` of part `pt`, parity `par`
-    auto xrow_off = [&](int pt, int which, int par) { return (((size_t)(b * PARTS + pt) * 2 + which) * 2 + par) * XROW; };
+    auto xrow_off = [&](int pt, int which, int par) { return (((b * PARTS + pt) * 2 + which) * 2 + par) * XROW; };
 
     // Halo import of conv cv's boundary rows (published by the neighbours at the end of conv cv), issued
     // inside conv cv+1 between positions 1 and 2: wave 0 polls the neighbours' counters, the other waves
@@ -270,7 +267,9 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         // raw barrier: __syncthreads() would first drain every wave's in-flight weight DMAs
         asm volatile("s_barrier" ::: "memory");
         int n = 0;
-        const int pos = lane, px = pos - 1;  // patch column pos <- image column pos - 1 (halo columns: zeros)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));  // opaque: the offsets are recomputed per import, not kept live (spills)
+        const int pos = ln, px = pos - 1;  // patch column pos <- image column pos - 1 (halo columns: zeros)
         const bool lane_on = pos < PC;
 #pragma unroll
         for (int u = 0; u < NPL / NW; ++u) {
@@ -278,8 +277,8 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
 #pragma unroll
             for (int side = 0; side < 2; ++side) {
                 if (side == 0 ? !has_up : !has_dn) continue;
-                const size_t row = side == 0 ? xrow_off(part - 1, 1, cv & 1) : xrow_off(part + 1, 0, cv & 1);
-                const uint32_t off = (unsigned)px < (unsigned)IW ? (uint32_t)((row + px * C + pl * 8) * 2) : OOB;
+                const int row = side == 0 ? xrow_off(part - 1, 1, cv & 1) : xrow_off(part + 1, 0, cv & 1);
+                const uint32_t off = (unsigned)px < (unsigned)IW ? (uint32_t)((row + (pl * IW + px) * 8) * 2) : OOB;
                 char* dst = smem + pl * PLANE_B + (side == 0 ? 0 : (PR - 1) * PC * 16);
                 if (lane_on)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr_x, (lds_void*)dst, 16, off, 0, 0, SC1);
@@ -292,7 +291,12 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
 
     auto run_conv = [&](int cv, auto second_tag) {
         constexpr bool second = decltype(second_tag)::value;
-        if (!second) seed_bias(cv);  // conv2's seed (x + its bias) comes from conv1's epilogue
+        if (!second) {
+            seed_bias();  // conv2's seed (x + its bias) comes from conv1's epilogue
+            if (cv + 1 < nconv) issue_tab(cv + 1, cv, 1);
+        } else if (cv + 1 < nconv) {
+            issue_tab(cv + 1, -1, 0);  // the next block's conv1 biases
+        }
         pread(pA, pos_cg(0), pos_tap(0));
 #pragma unroll
         for (int i = 0; i < FN; ++i) wread(i, 0);  // step 0 of every conv sits in slot 0 (KSTEPS % 3 == 0)
@@ -314,63 +318,101 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
             }
             halo = 0;
         }
-        // ---- epilogue (every wave is past its last patch read)
+        // ---- epilogue (every wave is past its last patch read): accumulators -> patch only; the global
+        // copies (boundary rows, stage output, intermediates) are read back from the patch afterwards
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const int cl = ln & 15;
-        bf16_t* dbg = nullptr;
-        if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
-        const bool store_y = second && cv == nconv - 1;
-        const bool exch = cv < nconv - 1;
-        bf16_t* const xo_up = p.xchg + xrow_off(part, 0, cv & 1);  // first row, for the part above
-        bf16_t* const xo_dn = p.xchg + xrow_off(part, 1, cv & 1);  // last row, for the part below
+#if FR_SPLIT_EXP & 4
+        {  // timing-only: trivial epilogue (the accumulators stay live, nothing is written)
+            float sum = 0.f;
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-            const int n = 64 * wn + 16 * i + 4 * (ln >> 4);
-            uint2 xin[FM];
-            float4 sl, e[6];  // conv1: this fragment's slope and conv2's biases (its accumulator seed)
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j) sum += acc[i][j][0] + acc[i][j][3];
+            if (sum == 1.2345f) p.y[lane] = 0;
+        }
+        if (false)
+#endif
+        {
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            const int cl = ln & 15;
+            const char* t2 = smem + G::TAB + G::TS;  // conv2's biases, conv1's slopes
+            int tr[FM];
             if (!second) {
-                load_ep(cv + 1, i, e);
-                sl = *(const float4*)(p.slope + (size_t)cv * C + n);
 #pragma unroll
-                for (int j = 0; j < FM; ++j) {
-                    const int f = FM * wm + j, col = 16 * (f % QPR) + cl;
-                    const char* slot = smem + (n >> 3) * PLANE_B + ((f / QPR + 1) * PC + col + 1) * 16 + (n & 7) * 2;
-                    xin[j] = col < IW ? *(const uint2*)slot : make_uint2(0u, 0u);
-                }
+                for (int j = 0; j < FM; ++j) tr[j] = tab_row(j, ln);
             }
 #pragma unroll
-            for (int j = 0; j < FM; ++j) {
-                const int f = FM * wm + j, row = f / QPR, col = 16 * (f % QPR) + cl;
-                char* slot = smem + (n >> 3) * PLANE_B + ((row + 1) * PC + col + 1) * 16 + (n & 7) * 2;
-                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-                if (!second) {  // PReLU: max(v, 0) + s * min(v, 0)
-                    v[0] = fmaf(sl.x, fminf(v[0], 0.f), fmaxf(v[0], 0.f));
-                    v[1] = fmaf(sl.y, fminf(v[1], 0.f), fmaxf(v[1], 0.f));
-                    v[2] = fmaf(sl.z, fminf(v[2], 0.f), fmaxf(v[2], 0.f));
-                    v[3] = fmaf(sl.w, fminf(v[3], 0.f), fmaxf(v[3], 0.f));
-                }
-                float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
-                const uint4 pk = T::pack8(o8);
-                const uint2 pk2 = make_uint2(pk.x, pk.y);
+            for (int i = 0; i < FN; ++i) {
+                const int n = 64 * wn + 16 * i + 4 * (ln >> 4);
+                char* const slot0 = smem + (n >> 3) * PLANE_B + (PC + cl + 1) * 16 + (n & 7) * 2;
+                uint2 xin[FM];
+                float4 s1;  // conv1: slope - 1, PReLU(v) = v + (s - 1) min(v, 0)
                 if (!second) {
-                    float fx[8];
-                    T::unpack8(make_uint4(xin[j].x, xin[j].y, 0, 0), fx);
-                    const float4 bb = pick(e, j);
-                    acc[i][j] = (f32x4_t){fx[0] + bb.x, fx[1] + bb.y, fx[2] + bb.z, fx[3] + bb.w};
+                    const float4 sl = *(const float4*)(t2 + G::TAB_ROWS_B + n * 4);
+                    s1 = make_float4(sl.x - 1.f, sl.y - 1.f, sl.z - 1.f, sl.w - 1.f);
+#pragma unroll
+                    for (int j = 0; j < FM; ++j) {
+                        const int f = FM * wm + j;
+                        xin[j] = *(const uint2*)(slot0 + ((f / QPR) * PC + 16 * (f % QPR)) * 16);
+                    }
                 }
-                if (col < IW) {
+#pragma unroll
+                for (int j = 0; j < FM; ++j) {
+                    const int f = FM * wm + j, q = f % QPR;
+                    char* slot = slot0 + ((f / QPR) * PC + 16 * q) * 16;
+                    float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                    if (!second) {
+                        v[0] = fmaf(s1.x, fminf(v[0], 0.f), v[0]);
+                        v[1] = fmaf(s1.y, fminf(v[1], 0.f), v[1]);
+                        v[2] = fmaf(s1.z, fminf(v[2], 0.f), v[2]);
+                        v[3] = fmaf(s1.w, fminf(v[3], 0.f), v[3]);
+                    }
+                    float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+                    const uint4 pk = T::pack8(o8);
+                    uint2 pk2 = make_uint2(pk.x, pk.y);
+                    // lanes past the image's last column write the zero right halo / spare positions
+                    if (IW % 16 != 0 && q == QPR - 1 && cl >= IW % 16) pk2 = make_uint2(0u, 0u);
+                    if (!second) {
+                        float fx[8];
+                        T::unpack8(make_uint4(xin[j].x, xin[j].y, 0, 0), fx);
+                        const float4 bb = *(const float4*)(t2 + tr[j] + n * 4);
+                        acc[i][j] = (f32x4_t){fx[0] + bb.x, fx[1] + bb.y, fx[2] + bb.z, fx[3] + bb.w};
+                    }
                     *(uint2*)slot = pk2;
-                    const size_t go = ((size_t)(b * IW + r0 + row) * IW + col) * C + n;
-                    if (store_y) *(uint2*)(p.y + go) = pk2;
-                    if (dbg) *(uint2*)(dbg + go) = pk2;
-                    // boundary rows for the neighbours: sc1 stores (the hand-off rule, header)
-                    const uint64_t pk64 = (uint64_t)pk2.x | ((uint64_t)pk2.y << 32);
-                    if (exch && has_up && row == 0)
-                        __hip_atomic_store((uint64_t*)(xo_up + col * C + n), pk64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (exch && has_dn && row == HR - 1)
-                        __hip_atomic_store((uint64_t*)(xo_dn + col * C + n), pk64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        // the conv's output is in the patch for every wave (the next conv's reads, the copies below)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const bool exch = cv < nconv - 1;
+        if (exch && !(FR_SPLIT_EXP & 2)) {
+            // boundary rows for the neighbours, plane-major [NPL][IW][8] per row (16-B chunks, positions
+            // fastest: conflict-free LDS reads, contiguous stores), sc1 stores (the hand-off rule, header)
+            for (int c = threadIdx.x; c < 2 * NPL * IW; c += 64 * NW) {
+                const int side = c / (NPL * IW), rem = c - side * (NPL * IW), pl = rem / IW, pos = rem - pl * IW;
+                if (side == 0 ? has_up : has_dn) {
+                    const uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((side == 0 ? 1 : HR) * PC + pos + 1) * 16);
+                    const uint32_t off = (uint32_t)((xrow_off(part, side, cv & 1) + (pl * IW + pos) * 8) * 2);
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    __builtin_amdgcn_raw_buffer_store_b128((u32x4){v.x, v.y, v.z, v.w}, xr_x, off, 0, SC1);
+                }
+            }
+        }
+        bf16_t* dbg = nullptr;
+        if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
+        bf16_t* const yo = second && cv == nconv - 1 ? p.y : dbg;
+        if (yo) {  // the part's rows, NHWC (once per stage; every conv for intermediates)
+            for (int c = threadIdx.x; c < HR * IW * NPL; c += 64 * NW) {
+                const int pix = c / NPL, pl = c - pix * NPL, row = pix / IW, pos = pix - row * IW;
+                const uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((row + 1) * PC + pos + 1) * 16);
+                *(uint4*)(yo + ((size_t)(b * IW + r0 + row) * IW + pos) * C + pl * 8) = v;
+            }
+            if (dbg && yo != dbg) {
+                for (int c = threadIdx.x; c < HR * IW * NPL; c += 64 * NW) {
+                    const int pix = c / NPL, pl = c - pix * NPL, row = pix / IW, pos = pix - row * IW;
+                    const uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((row + 1) * PC + pos + 1) * 16);
+                    *(uint4*)(dbg + ((size_t)(b * IW + r0 + row) * IW + pos) * C + pl * 8) = v;
                 }
             }
         }
@@ -383,8 +425,6 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
                 __hip_atomic_store(my_flag, cv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             pending = cv;
         }
-        // the new activation is visible to every wave before the next conv reads it
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
 #pragma unroll 1
     for (int blkc = 0; blkc < p.nblk; ++blkc) {
