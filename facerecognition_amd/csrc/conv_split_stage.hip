@@ -86,6 +86,14 @@ constexpr int SC1 = 16;                   // buffer-load cache policy: sc1 (L1 b
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// threadIdx.x through an empty asm: loop-invariant copy-out addresses are recomputed where they are used
+// instead of being hoisted to the kernel's start and spilled across the K loops
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, soff, 0, 0);
 }
@@ -203,6 +211,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv * C * 4), 0x00020000);
     auto issue_tab = [&](int cv, int cv_slope, int slot) {
         char* dst = smem + G::TAB + slot * G::TS;
+        int lane = opaque_tid() & 63;  // opaque: the DMA offsets are not hoisted out of the block loop
         if (wave * 1024 < G::TAB_ROWS_B && wave * 1024 + lane * 16 < G::TAB_ROWS_B)
             dma16s(epr, dst + wave * 1024, (uint32_t)(wave * 1024 + lane * 16), (uint32_t)((cv * 9 + 3 * tbase) * C * 4));
         if (cv_slope >= 0 && wave == NW - 1 && lane * 16 < C * 4)
@@ -389,7 +398,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         if (exch && !(FR_SPLIT_EXP & 2)) {
             // boundary rows for the neighbours, plane-major [NPL][IW][8] per row (16-B chunks, positions
             // fastest: conflict-free LDS reads, contiguous stores), sc1 stores (the hand-off rule, header)
-            for (int c = threadIdx.x; c < 2 * NPL * IW; c += 64 * NW) {
+            for (int c = opaque_tid(); c < 2 * NPL * IW; c += 64 * NW) {
                 const int side = c / (NPL * IW), rem = c - side * (NPL * IW), pl = rem / IW, pos = rem - pl * IW;
                 if (side == 0 ? has_up : has_dn) {
                     const uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((side == 0 ? 1 : HR) * PC + pos + 1) * 16);
@@ -403,13 +412,13 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
         bf16_t* const yo = second && cv == nconv - 1 ? p.y : dbg;
         if (yo) {  // the part's rows, NHWC (once per stage; every conv for intermediates)
-            for (int c = threadIdx.x; c < HR * IW * NPL; c += 64 * NW) {
+            for (int c = opaque_tid(); c < HR * IW * NPL; c += 64 * NW) {
                 const int pix = c / NPL, pl = c - pix * NPL, row = pix / IW, pos = pix - row * IW;
                 const uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((row + 1) * PC + pos + 1) * 16);
                 *(uint4*)(yo + ((size_t)(b * IW + r0 + row) * IW + pos) * C + pl * 8) = v;
             }
             if (dbg && yo != dbg) {
-                for (int c = threadIdx.x; c < HR * IW * NPL; c += 64 * NW) {
+                for (int c = opaque_tid(); c < HR * IW * NPL; c += 64 * NW) {
                     const int pix = c / NPL, pl = c - pix * NPL, row = pix / IW, pos = pix - row * IW;
                     const uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((row + 1) * PC + pos + 1) * 16);
                     *(uint4*)(dbg + ((size_t)(b * IW + r0 + row) * IW + pos) * C + pl * 8) = v;

@@ -42,7 +42,11 @@ constexpr int PPOS = SW * SWP;               // 224 stored positions per plane (
 constexpr int PLANE_B = PPOS * 16;           // 3584: one 8-channel plane
 constexpr int PATCH_B = (SC / 8) * PLANE_B;  // 114688
 constexpr int SLICE_B = 4 * 256 * 16;        // 16384: one K-step of packed weights [4 groups of 8 ch][256 rows][16 B]
-constexpr int STAGE_LDS = PATCH_B;
+constexpr int PAD_B = 256;                   // zeros written by the epilogue's discarded lanes past the patch
+constexpr int TAB_ROWS_B = 9 * SC * 4;       // epilogue table: bias per border class [9][256] f32
+constexpr int TS = TAB_ROWS_B + SC * 4;      // + the PReLU slopes of the conv before [256]
+constexpr int TAB = PATCH_B + PAD_B;
+constexpr int STAGE_LDS = TAB + 2 * TS;      // 134400
 constexpr int KSTEPS = (SC / 32) * 9;        // 72 per conv
 constexpr uint32_t OOB = 0x80000000u;
 constexpr int SNW = 8;                       // waves per workgroup: 2 pixel halves x 4 channel groups
@@ -55,6 +59,14 @@ constexpr int NPW = 16 * FN;                 // output channels per wave
 #endif
 
 typedef __attribute__((address_space(3))) void lds_void;
+
+// threadIdx.x through an empty asm: loop-invariant copy-out addresses are recomputed where they are used
+// instead of being hoisted to the kernel's start and spilled across the K loops
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
 
 template <bool F16>
 __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
@@ -83,9 +95,7 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(smem + piece * 1024), 16, src, 0, 0, 0);
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
+    // ---- the pad after the patch (written by discarded lanes) needs no init; first conv1 table below
     // fragment addresses: B (patch) rows m = wm*112 + 16j + (lane&15) at plane (lane>>4) of the group;
     // A (weights) rows n = wn*64 + 16i + (lane&15) in group (lane>>4) of the K-step's packed image
     int aoff[7];
@@ -118,8 +128,6 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
         for (int i = 0; i < FN; ++i)
             w[i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wvo + i * 256, (uint32_t)g * SLICE_B, 0));
     };
-    wload(wq[0], 0);
-    wload(wq[1], 1);
     // one K-step: nxt <- patch fragments of (cg_n, tap_n) (after a conv's last step: unused reads, no
     // branch); weights of step g+2 (clamped: the tail re-fetches the last step); 28 MFMAs on (wq[r], cur)
     auto kstep = [&](int g, int r, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
@@ -138,46 +146,67 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
     const size_t img = (size_t)b * SPIX * SC;
     // Epilogue tables (built at load time): ep[cv][9][256] = the conv's bias for each border class of the
     // output pixel (bias9 of the folded pre-conv BN, or the plain bias in all 9 rows); slope[cv][256] =
-    // the activation's negative-side factor.  A lane's 4 channels n..n+3 of fragment i and its output
-    // column class are fixed, and its output row is interior except for fragment j = 0 of wave row 0
-    // (image row 0) and j = 6 of wave row 1 (image row 13): two float4 per fragment cover every case.
-    // The loads go through an opaque lane copy so that their ~50 addresses are not hoisted out of the K
-    // loop (LICM would keep them live across it and spill).
-    auto load_ep = [&](int cv, float4 (&bi)[FN], float4 (&be)[FN]) {
+    // the activation's negative-side factor.  Staged in LDS per conv: slot 0 = the conv1 biases of the
+    // current block (its accumulator seeds), slot 1 = the conv2 biases (seeded in conv1's epilogue) and
+    // conv1's slopes; slot 1 is DMA'd at conv1's start, slot 0 (the next block's) at conv2's start, and
+    // both land long before use (loads retire in order; the weight loads behind them are waited on).
+    // A lane's 4 channels n..n+3 of fragment i and its column class are fixed, and its output row is
+    // interior except for fragment j = 0 of wave row 0 (image row 0) and j = 6 of wave row 1 (row 13).
+    const __amdgpu_buffer_rsrc_t epr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.ep, 0, (uint32_t)((size_t)nconv * TAB_ROWS_B), 0x00020000);
+    const __amdgpu_buffer_rsrc_t slr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv * SC * 4), 0x00020000);
+    auto issue_tab = [&](int cv, int cv_slope, int slot) {
+        char* dst = smem + TAB + slot * TS;
+        int lane = opaque_tid() & 63;  // opaque: the DMA offsets are not hoisted out of the block loop
+#pragma unroll
+        for (int u = 0; u < (TAB_ROWS_B / 1024 + SNW - 1) / SNW; ++u) {
+            const int piece = wave + SNW * u;
+            if (piece < TAB_ROWS_B / 1024)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(epr, (lds_void*)(dst + piece * 1024), 16,
+                                                         (uint32_t)(piece * 1024 + lane * 16), (uint32_t)(cv * TAB_ROWS_B), 0, 0);
+        }
+        if (cv_slope >= 0 && wave == SNW - 1)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(slr, (lds_void*)(dst + TAB_ROWS_B), 16, (uint32_t)(lane * 16),
+                                                     (uint32_t)(cv_slope * SC * 4), 0, 0);
+    };
+    // table-row byte offsets of the lane's output pixels: interior rows, and this wave's border row (the
+    // fragment j = 0 / 6 of wave row 0 / 1); ln: an opaque lane copy, keeps LICM from hoisting them
+    auto is_edge = [&](int j) { return (j == 0 && wm == 0) || (j == 6 && wm == 1); };
+    auto tab_rows = [&](int ln, int& tri, int& tre) {
+        const int cc = ln & 15, ccls = cc == 0 ? 0 : (cc == SW - 1 ? 2 : 1);
+        tri = (3 + ccls) * SC * 4;
+        tre = ((wm ? 6 : 0) + ccls) * SC * 4;
+    };
+    auto seed_bias = [&]() {
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        const int cc = ln & 15, ccls = cc == 0 ? 0 : (cc == SW - 1 ? 2 : 1);
-        const float* ep = p.ep + (size_t)cv * 9 * SC;
-        const float* epi = ep + (3 + ccls) * SC;              // interior rows
-        const float* epe = ep + (wm ? 6 + ccls : ccls) * SC;  // this wave's border row (0 or 13)
+        const char* t = smem + TAB + (wn * NPW + 4 * (ln >> 4)) * 4;
+        int tri, tre;
+        tab_rows(ln, tri, tre);
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-            const int n = wn * NPW + 16 * i + 4 * (ln >> 4);
-#if FR_STAGE_EXP & 128
-            bi[i] = make_float4(epi - ep + n, 0.f, 1.f, 2.f);
-            be[i] = make_float4(epe - ep + n, 0.f, 1.f, 2.f);
-#else
-            bi[i] = *(const float4*)(epi + n);
-            be[i] = *(const float4*)(epe + n);
-#endif
-        }
-    };
-    auto is_edge = [&](int j) { return (j == 0 && wm == 0) || (j == 6 && wm == 1); };
-    auto seed_bias = [&](int cv) {
-        float4 bi[FN], be[FN];
-        load_ep(cv, bi, be);
+        for (int j = 0; j < 7; ++j) {
+            const int tr = is_edge(j) ? tre : tri;
 #pragma unroll
-        for (int i = 0; i < FN; ++i)
-#pragma unroll
-            for (int j = 0; j < 7; ++j) {
-                const float4 bb = is_edge(j) ? be[i] : bi[i];
+            for (int i = 0; i < FN; ++i) {
+                const float4 bb = *(const float4*)(t + tr + 64 * i);
                 acc[i][j] = (f32x4_t){bb.x, bb.y, bb.z, bb.w};
             }
+        }
     };
+    issue_tab(0, -1, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    wload(wq[0], 0);
+    wload(wq[1], 1);
+
     auto run_conv = [&](int cv, auto second_tag) {
         constexpr bool second = decltype(second_tag)::value;
         if (!second) {  // conv1 starts from its bias (conv2 from x + its bias, seeded by conv1's epilogue)
-            seed_bias(cv);
+            seed_bias();
+            if (cv + 1 < nconv) issue_tab(cv + 1, cv, 1);
+        } else if (cv + 1 < nconv) {
+            issue_tab(cv + 1, -1, 0);  // the next block's conv1 biases
         }
         pread(pA, 0, 0);
         const int g0 = cv * KSTEPS;
@@ -223,62 +252,67 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
         asm volatile("" : "+v"(ln));
         const int cc = ln & 15;
         const bool okc = cc < SW;
-        bf16_t* dbg = nullptr;
-        if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
-        const bool store_y = second && cv == nconv - 1;
-        float4 sl[FN], bi[FN], be[FN];
-        if (!second) {
-            load_ep(cv + 1, bi, be);  // conv2's bias: part of its accumulator seed
-            const float* slp = p.slope + (size_t)cv * SC;
-#pragma unroll
-            for (int i = 0; i < FN; ++i)
-#if FR_STAGE_EXP & 128
-                sl[i] = make_float4(0.25f, (float)i, 0.f, 0.f);
-#else
-                sl[i] = *(const float4*)(slp + wn * NPW + 16 * i + 4 * (ln >> 4));
-#endif
-        }
+        const char* t2 = smem + TAB + TS;  // conv2's biases, conv1's slopes
+        int tri = 0, tre = 0;
+        if (!second) tab_rows(ln, tri, tre);
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
             const int n = wn * NPW + 16 * i + 4 * (ln >> 4);
             char* slot0 = smem + (n >> 3) * PLANE_B + (wm * 112 + cc + 1) * 16 + (n & 7) * 2;
-            // conv1: all 7 identity reads of this n-fragment first (one LDS latency per fragment)
+            // conv1: all 7 identity reads of this n-fragment first (one LDS latency per fragment); lanes of
+            // the discarded columns 14/15 read (and later zero) the halo slots
             uint2 xin[7];
+            float4 s1;  // conv1: slope - 1, PReLU(v) = v + (s - 1) min(v, 0)
             if (!second) {
+                const float4 sl = *(const float4*)(t2 + TAB_ROWS_B + n * 4);
+                s1 = make_float4(sl.x - 1.f, sl.y - 1.f, sl.z - 1.f, sl.w - 1.f);
 #pragma unroll
-                for (int j = 0; j < 7; ++j) xin[j] = okc ? *(const uint2*)(slot0 + j * 256) : make_uint2(0u, 0u);
+                for (int j = 0; j < 7; ++j) xin[j] = *(const uint2*)(slot0 + j * 256);
             }
 #pragma unroll
             for (int j = 0; j < 7; ++j) {
                 char* slot = slot0 + j * 256;  // position m + 1 = wm*112 + 16j + cc + 1
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-                if (!second) {  // PReLU: max(v, 0) + s * min(v, 0)
-                    v[0] = fmaf(sl[i].x, fminf(v[0], 0.f), fmaxf(v[0], 0.f));
-                    v[1] = fmaf(sl[i].y, fminf(v[1], 0.f), fmaxf(v[1], 0.f));
-                    v[2] = fmaf(sl[i].z, fminf(v[2], 0.f), fmaxf(v[2], 0.f));
-                    v[3] = fmaf(sl[i].w, fminf(v[3], 0.f), fmaxf(v[3], 0.f));
+                if (!second) {
+                    v[0] = fmaf(s1.x, fminf(v[0], 0.f), v[0]);
+                    v[1] = fmaf(s1.y, fminf(v[1], 0.f), v[1]);
+                    v[2] = fmaf(s1.z, fminf(v[2], 0.f), v[2]);
+                    v[3] = fmaf(s1.w, fminf(v[3], 0.f), v[3]);
                 }
                 float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
                 const uint4 pk = T::pack8(o8);
-                const uint2 pk2 = make_uint2(pk.x, pk.y);
+                // columns 14/15 write zeros: the right halo, the next row's left halo (past the last row:
+                // the pad after the patch)
+                const uint2 pk2 = okc ? make_uint2(pk.x, pk.y) : make_uint2(0u, 0u);
                 if (!second) {
                     float f[8];
                     T::unpack8(make_uint4(xin[j].x, xin[j].y, 0, 0), f);
-                    const float4 bb = is_edge(j) ? be[i] : bi[i];
+                    const float4 bb = *(const float4*)(t2 + (is_edge(j) ? tre : tri) + n * 4);
                     acc[i][j] = (f32x4_t){f[0] + bb.x, f[1] + bb.y, f[2] + bb.z, f[3] + bb.w};
                 }
-                if (okc) {
-                    *(uint2*)slot = pk2;
-                    const int r = wm * 7 + j;
-                    const size_t go = img + (size_t)(r * SW + cc) * SC + n;
-                    if (store_y) *(uint2*)(p.y + go) = pk2;
-                    if (dbg) *(uint2*)(dbg + go) = pk2;
-                }
+                *(uint2*)slot = pk2;
             }
         }
 #endif
-        // the new activation is visible to every wave before the next conv reads it (LDS writes only)
+        // the new activation is visible to every wave before the next conv reads it (and the copies below)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        bf16_t* dbg = nullptr;
+        if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
+        bf16_t* const yo = second && cv == nconv - 1 ? p.y : dbg;
+        if (yo) {  // NHWC copies from the patch (the stage output once; intermediates every conv)
+            for (int c = opaque_tid(); c < SPIX * (SC / 8); c += 64 * SNW) {
+                const int pix = c / (SC / 8), pl = c - pix * (SC / 8), r = pix / SW, col = pix - r * SW;
+                const uint4 v = *(const uint4*)(smem + pl * PLANE_B + (r * SWP + col + 1) * 16);
+                *(uint4*)(yo + img + (size_t)pix * SC + pl * 8) = v;
+            }
+            if (dbg && yo != dbg) {
+                for (int c = opaque_tid(); c < SPIX * (SC / 8); c += 64 * SNW) {
+                    const int pix = c / (SC / 8), pl = c - pix * (SC / 8), r = pix / SW, col = pix - r * SW;
+                    const uint4 v = *(const uint4*)(smem + pl * PLANE_B + (r * SWP + col + 1) * 16);
+                    *(uint4*)(dbg + img + (size_t)pix * SC + pl * 8) = v;
+                }
+            }
+        }
     };
 #pragma unroll 1
     for (int blk = 0; blk < p.nblk; ++blk) {
