@@ -584,6 +584,11 @@ void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
 }
 
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
+    if (a.tile == TILE_WRING) {  // conv_wring.hip (an autotuner pick)
+        ConvArgs w = a;
+        w.wimg = a.wring_;
+        return launch_conv_wring(w, s);
+    }
     return a.f16 ? launch_dtype<true>(a, s) : launch_dtype<false>(a, s);
 }
 

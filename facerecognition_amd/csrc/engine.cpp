@@ -47,6 +47,7 @@ struct DevConvW {
     float* negf = nullptr;   // conv_img / conv_rows: [Npad] activation negative-side factor (slope / 0 / 1)
     bf16_t* wrows = nullptr; // conv_rows.hip weight image (rows_pack_weights)
     float* ep = nullptr;     // conv_rows.hip: [9][Npad] bias per border class
+    bf16_t* wring = nullptr; // conv_wring.hip substep images (wring_pack_weights)
     uint8_t* w8 = nullptr;   // FR_DTYPE_FP8: e4m3 [Npad][Kpad8] + per-channel scale
     float* wscale = nullptr;
     int Cout = 0, Kh = 1, Kw = 1, Cin = 0, K = 0, Npad = 0, Kpad = 0, Kpad8 = 0;
@@ -699,7 +700,7 @@ int build_img_weights(fr_handle* h) {
     for (const auto& op : h->ops) {
         if (op.kind != OP_CONV || op.wi < 0) continue;
         DevConvW& cw = h->convw[op.wi];
-        if (cw.wimg || cw.wrows) continue;
+        if ((cw.wimg || cw.wrows) && cw.wring) continue;
         ConvArgs a{};
         a.B = 1; a.Cin = op.cin; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
         a.H = h->tensors[op.in].H; a.W = h->tensors[op.in].W; a.Cx = h->tensors[op.in].C; a.x_off = op.in_off;
@@ -710,6 +711,20 @@ int build_img_weights(fr_handle* h) {
         a.f16 = h->dtype == FR_DTYPE_F16;
         int ic = 0;
         if (h->dtype == FR_DTYPE_FP8) continue;
+        if (!cw.wring) {  // conv_wring.hip substep images (the autotuner decides per shape whether they run)
+            ConvArgs w = a;
+            w.K = cw.K;
+            w.x2 = nullptr;
+            if (op.x2 >= 0) { w.x2 = (const bf16_t*)1; w.C2 = cw.C2; w.K1 = cw.K1; }
+            if (wring_supported(w)) {
+                void* q = nullptr;
+                int rc = dev_alloc(&q, wring_packed_elems(cw.Kpad, cw.Npad) * sizeof(bf16_t));
+                if (rc) return rc;
+                h->weight_allocs.push_back(q);
+                FR_HIP_CHECK(wring_pack_weights(cw.w, cw.Kpad, cw.Npad, (bf16_t*)q, nullptr));
+                cw.wring = (bf16_t*)q;
+            }
+        }
         // the activation's negative-side factor (conv_img and conv_rows epilogues)
         auto make_negf = [&]() -> int {
             if (cw.negf) return FR_OK;
@@ -739,7 +754,7 @@ int build_img_weights(fr_handle* h) {
                 if ((rc = make_negf())) return rc;
             }
         }
-        if (!img_shape_ok(a, &ic)) continue;
+        if (cw.wimg || !img_shape_ok(a, &ic)) continue;
         void* p = nullptr;
         int rc = dev_alloc(&p, img_packed_elems(ic) * sizeof(bf16_t));
         if (rc) return rc;
@@ -1070,9 +1085,23 @@ int find_tuned(const fr_handle* h, const ConvArgs& a) {
 
 // Time every applicable tile on this conv (1 warm + 3 timed launches each, HIP events on `s`) and
 // remember the fastest for the shape.  Runs only inside the eager tuning pass of embed_locked.
+static bool wring_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_WRING");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     int cand[16];
-    const int nc = conv_tile_candidates(a.Cout, cand);
+    int nc = conv_tile_candidates(a.Cout, cand);
+    if (wring_enabled() && a.wring_) {  // the register-weight-ring kernel competes per shape
+        ConvArgs w = a;
+        w.wimg = a.wring_;
+        w.partial = nullptr;
+        if (wring_supported(w)) cand[nc++] = TILE_WRING;
+    }
     hipEvent_t e0, e1;
     FR_HIP_CHECK(hipEventCreate(&e0));
     FR_HIP_CHECK(hipEventCreate(&e1));
@@ -1161,7 +1190,7 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) split /= 2;
     if (split > 1) a.partial = h->partial;
     a.split_k = split;
-    ps.start("conv_igemm tile" + std::to_string(tile) + (split > 1 ? " splitk" : ""), &a);
+    ps.start(tile == TILE_WRING ? std::string("conv_wring") : "conv_igemm tile" + std::to_string(tile) + (split > 1 ? " splitk" : ""), &a);
     FR_HIP_CHECK(launch_conv(a, s));
     if (split > 1 && a.y) FR_HIP_CHECK(launch_splitk_epilogue(a, s));
     return FR_OK;
@@ -1275,6 +1304,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.bias = cw.bias; a.slope = cw.slope; a.act = op.act; a.bias9 = cw.bias9; a.wimg = cw.wimg;
                 a.negf = cw.negf; a.ep = cw.ep;
                 a.wrows_ = cw.wrows;
+                a.wring_ = cw.wring;
                 if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
                 if (op.x2 >= 0) {
                     const auto& t2 = h->tensors[op.x2];
@@ -1885,6 +1915,30 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         int TH, variant;
         if (!band_plan(a, &TH, &variant)) { set_error("fr_op_conv2d: band kernel not applicable"); return FR_ERR_ARG; }
         FR_HIP_CHECK(launch_conv_band(a, TH, variant, (hipStream_t)stream));
+        return FR_OK;
+    }
+    if (d->tile == FR_TILE_WRING + 1) {
+        // the substep images, packed on the stream into a scratch buffer kept for the next call with the
+        // same weight pointer and shape (repeated launches, tools/conv_bench.py, pay the packing once)
+        a.wimg = (const bf16_t*)1;
+        if (!wring_supported(a)) { set_error("fr_op_conv2d: wring kernel not applicable"); return FR_ERR_ARG; }
+        static std::mutex mu;
+        static void* tw = nullptr;
+        static const void* tw_src = nullptr;
+        static int tw_kpad = 0, tw_npad = 0;
+        std::lock_guard<std::mutex> lk(mu);
+        hipStream_t st = (hipStream_t)stream;
+        if (tw_src != d->w || tw_kpad != a.Kpad || tw_npad != a.Npad) {
+            FR_HIP_CHECK(hipStreamSynchronize(st));
+            if (tw) (void)hipFree(tw);
+            tw = nullptr;
+            tw_src = nullptr;
+            FR_HIP_CHECK(hipMalloc(&tw, wring_packed_elems(a.Kpad, a.Npad) * sizeof(bf16_t)));
+            FR_HIP_CHECK(wring_pack_weights(a.w, a.Kpad, a.Npad, (bf16_t*)tw, st));
+            tw_src = d->w; tw_kpad = a.Kpad; tw_npad = a.Npad;
+        }
+        a.wimg = (const bf16_t*)tw;
+        FR_HIP_CHECK(launch_conv_wring(a, st));
         return FR_OK;
     }
     if (d->tile == FR_TILE_ROWS + 1) {

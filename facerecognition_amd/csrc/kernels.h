@@ -8,7 +8,8 @@ namespace fr {
 // Conv tile variants (BM pixels x BN channels, 4 waves each).
 enum { TILE_128x128 = 0, TILE_256x64 = 1, TILE_128x64 = 2, TILE_64x128 = 3,
        TILE_128x128_S3 = 4, TILE_256x128 = 5, TILE_128x256 = 6,  // *_S3 / 8-wave tiles: 3-stage DMA ring
-       TILE_128x64_S3 = 8, TILE_64x128_S3 = 9, NUM_TILE_IDS = 10 };   // (7 = the band kernel's id in the ABI)
+       TILE_128x64_S3 = 8, TILE_64x128_S3 = 9, NUM_TILE_IDS = 10,     // (7 = the band kernel's id in the ABI)
+       TILE_WRING = 13 };  // conv_wring.hip (= FR_TILE_WRING), an autotuner candidate beside the igemm tiles
 
 // Implicit-GEMM convolution, NHWC bf16 in/out, f32 accumulate, fused epilogue.
 // GEMM view: M = B*Ho*Wo output pixels, N = Cout, K = Kh*Kw*Cin (c fastest).
@@ -44,7 +45,14 @@ struct ConvArgs {
     const bf16_t* x2;
     int H2, W2, Cx2, x2_off, C2, st2, K1;
     int y_bf16;                   // f16 input / MFMA, bf16 output (igemm; the end of an f16 plan section)
+    const bf16_t* wring_;         // engine: the conv's conv_wring weight image when it has one (else null)
 };
+// Implicit GEMM with the weights streamed from L2 into a register ring (conv_wring.hip): Cin % 64 == 0,
+// Cout % 256 == 0, Kpad = K (+ the K-concatenated projection) % 128 == 0; a.wimg = the packed image.
+bool wring_supported(const ConvArgs& a);
+size_t wring_packed_elems(int Kpad, int Npad);
+hipError_t wring_pack_weights(const bf16_t* w, int Kpad, int Npad, bf16_t* out, hipStream_t s);
+hipError_t launch_conv_wring(const ConvArgs& a, hipStream_t s);
 // Persistent weight-resident 3x3/s1/p1 conv with 64 input channels (conv_rows.hip); a.wimg = the
 // rows_pack_weights image, a.ep / a.negf set.
 bool rows_supported(const ConvArgs& a);

@@ -190,6 +190,8 @@ typedef struct fr_conv_desc {
 #define FR_TILE_IMG28 10     /* row-band direct 3x3/s1/p1 28x28x128->128 bf16 kernel (conv_img.hip); auto-selected (env FR_NO_IMG28=1: off) */
 #define FR_TILE_ROWS 12      /* persistent weight-resident 3x3/s1/p1 kernel for Cin = 64, Cout % 64 == 0, W % 56 == 0,
                               * H % 4 == 0, bf16 (conv_rows.hip); auto-selected (env FR_NO_ROWS=1: off) */
+#define FR_TILE_WRING 13     /* implicit GEMM with a register weight ring (conv_wring.hip): Cin % 64 == 0, Cout % 256 == 0;
+                                autotuned per shape against the igemm tiles (env FR_NO_WRING=1: off) */
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 

@@ -160,6 +160,34 @@ def test_conv_rows(gpu, case):
     _close(y, y0.float().cpu(), tol=1e-2)
 
 
+WRING_CASES = [  # (B, H, W, Cin, Cout, stride): layer4 (two 7x7 images per block, M not a multiple of
+    # 112 at B = 3), layer3.0.conv1, the layer4.0 stride-2 conv, a 28x28 stride-2 one
+    (3, 7, 7, 512, 512, 1), (1, 28, 28, 128, 256, 1), (2, 14, 14, 256, 512, 2), (2, 28, 28, 128, 256, 2)]
+
+
+@pytest.mark.parametrize("case", WRING_CASES)
+def test_conv_wring(gpu, case):
+    """Register-weight-ring implicit GEMM (conv_wring.hip, forced): bias + residual, PReLU and the
+    border-class bias epilogues; it sums K in the igemm's order, so it must equal tile 0 bit for bit."""
+    B, H, W, Cin, Cout, st = case
+    g = torch.Generator().manual_seed(B + H + Cin + Cout + st)
+    x = torch.randn(B, H, W, Cin, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    slope = torch.rand(Cout, generator=g) * 0.5
+    Ho = (H + 2 - 3) // st + 1
+    res = torch.randn(B, Ho, Ho, Cout, generator=g).to(torch.bfloat16).to(gpu)
+    kw = dict(stride=(st, st), pad=(1, 1))
+    y = conv_op(x, w, bias=bias, res=res, tile=N.FR_TILE_WRING, **kw)
+    _close(y, conv_ref(x, w, bias=bias, res=res, **kw))
+    assert torch.equal(y, conv_op(x, w, bias=bias, res=res, tile=0, **kw))
+    b9 = torch.randn(9, Cout, generator=g) * 0.1
+    y = conv_op(x, w, act=2, slope=slope, bias9=b9, tile=N.FR_TILE_WRING, **kw)
+    assert torch.equal(y, conv_op(x, w, act=2, slope=slope, bias9=b9, tile=0, **kw))
+    with pytest.raises(RuntimeError, match="wring"):  # Cout % 256 != 0: refused, no silent fallback
+        conv_op(x, torch.randn(128, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_WRING)
+
+
 def test_conv_img28_channel_slices_and_applicability(gpu):
     """img28 reads channels [128:256) of a 256-ch buffer and writes [64:192) of another; other shapes
     are refused (fail loudly, no silent fallback)."""
