@@ -33,12 +33,19 @@ constexpr int NW = 8;                       // waves
 constexpr int BN = 256;                     // output channels per block (32 per wave)
 constexpr int FM = 7;                       // pixel fragments
 constexpr int BM = 16 * FM;                 // 112 pixels per block
-constexpr int SROWS = 128;                  // LDS rows per stage
-constexpr int STAGE_B = SROWS * 128;        // 16 KiB: 128 rows x 64 channels
+constexpr int SROWS = 128;                  // LDS rows per stage (112 used)
 constexpr int NST = 4;                      // LDS stages
 constexpr int EPI_LD = BN + 4;              // f32 epilogue row (floats)
 constexpr int EPI_B = BM * EPI_LD * 4;      // 116480
-constexpr int WR_LDS = EPI_B > NST * STAGE_B ? EPI_B : NST * STAGE_B;
+// KSS = 32-deep substeps per LDS stage (2: 128-B rows, 16 KiB stages; 4: 256-B rows, 32 KiB stages, half
+// the barriers, needs Cin % 128 == 0)
+template <int KSS>
+struct WGeo {
+    static constexpr int CH = 32 * KSS, ROWB = 2 * CH, NCH = ROWB / 16, RPP = 1024 / ROWB;
+    static constexpr int STAGE_B = SROWS * ROWB;
+    static constexpr int LDS = EPI_B > NST * STAGE_B ? EPI_B : NST * STAGE_B;
+    __device__ static int swz(int row) { return KSS == 2 ? (row >> 1) & 7 : row & 15; }
+};
 constexpr uint32_t OOB = 0x80000000u;
 
 #ifndef FR_WRING_EXP
@@ -55,10 +62,12 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const char* l
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
 }
 
-template <bool F16>
+template <bool F16, int KSS>
 __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int tiles_m) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
+    typedef WGeo<KSS> Gm;
+    constexpr int CH = Gm::CH, ROWB = Gm::ROWB, NCH = Gm::NCH, RPP = Gm::RPP, STAGE_B = Gm::STAGE_B;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -68,20 +77,21 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
     const int m0 = tm * BM, n0 = tn * BN;
     const int nks = p.Kpad / 32;  // 32-deep substeps (a multiple of 4, host-checked)
 
-    // ---- operand B: this lane's two DMA rows 8 (wave + 8 i) + (lane >> 3) and its swizzled chunk
-    const int lrow = lane >> 3;
-    const int cl = (lane & 7) ^ ((4 * wave + (lane >> 4)) & 7);
+    // ---- operand B: piece q = wave + 8 i (i < KSS) of a stage holds rows RPP q .. RPP q + RPP - 1; the
+    // lane's row and its source chunk (the logical chunk stored at its linear destination position)
+    const int lrow = lane / NCH;
+    const int cl = (lane % NCH) ^ Gm::swz(RPP * wave + lrow);  // the same for every i
     const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * p.H * p.W * p.Cx * 2);
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.x2 ? p.x2 : p.x), 0,
         (uint32_t)min((size_t)0x7fffffff, p.x2 ? (size_t)p.B * p.H2 * p.W2 * p.Cx2 * 2 : (size_t)0), 0x00020000);
     const int HoWo = p.Ho * p.Wo;
-    int a_ih[2], a_iw[2];
-    uint32_t a_base[2], a_base2[2];
+    int a_ih[KSS], a_iw[KSS];
+    uint32_t a_base[KSS], a_base2[KSS];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int row = 8 * (wave + NW * i) + lrow, m = m0 + row;
+    for (int i = 0; i < KSS; ++i) {
+        const int row = RPP * (wave + NW * i) + lrow, m = m0 + row;
         if (row < BM && m < p.M) {
             const int b = m / HoWo, r = m - b * HoWo, oh = r / p.Wo, ow = r - oh * p.Wo;
             a_ih[i] = oh * p.sh - p.ph;
@@ -103,19 +113,20 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
         if (k_cur >= K1) {  // projection K-steps: x2 at the output's stride-st2 position
             const uint32_t c2 = (uint32_t)((k_cur - K1) * 2);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) dma16(x2r, dst + (wave + NW * i) * 1024, a_base2[i] == OOB ? OOB : a_base2[i] + c2);
+            for (int i = 0; i < KSS; ++i)
+                dma16(x2r, dst + (wave + NW * i) * 1024, a_base2[i] == OOB ? OOB : a_base2[i] + c2);
         } else {
             const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < KSS; ++i) {
                 const int ih = a_ih[i] + r_cur, iw = a_iw[i] + s_cur;
                 const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
                 dma16(xr, dst + (wave + NW * i) * 1024, ok ? a_base[i] + (uint32_t)soff : OOB);
             }
         }
         if (FR_WRING_EXP & 2) return;
-        k_cur += 64;
-        c_cur += 64;
+        k_cur += CH;
+        c_cur += CH;
         if (c_cur == p.Cin) {
             c_cur = 0;
             if (++s_cur == p.Kw) { s_cur = 0; ++r_cur; }
@@ -135,14 +146,16 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
                                                                                   (FR_WRING_EXP & 1) ? 0u : (uint32_t)s * wstep, 0));
     };
 
-    // B fragment j, k-half kk of a stage: row 16 j + (lane & 15), chunk (4 kk + (lane >> 4)) ^ ((row >> 1) & 7)
-    const int boff0 = (lane & 15) * 128 + ((0 + (lane >> 4)) ^ ((lane >> 1) & 7)) * 16;
-    const int boff1 = (lane & 15) * 128 + ((4 + (lane >> 4)) ^ ((lane >> 1) & 7)) * 16;
+    // B fragment j, substep kk of a stage: row 16 j + (lane & 15), logical chunk 4 kk + (lane >> 4)
+    int boff[KSS];
+#pragma unroll
+    for (int kk = 0; kk < KSS; ++kk)
+        boff[kk] = (lane & 15) * ROWB + ((4 * kk + (lane >> 4)) ^ Gm::swz(lane & 15)) * 16;
     frag bq[2][FM];
     auto bread = [&](frag (&b)[FM], int slot, int kk) {
-        const char* a = smem + slot * STAGE_B + (kk ? boff1 : boff0);
+        const char* a = smem + slot * STAGE_B + boff[kk];
 #pragma unroll
-        for (int j = 0; j < FM; ++j) b[j] = *(const frag*)(a + j * 2048);
+        for (int j = 0; j < FM; ++j) b[j] = *(const frag*)(a + j * 16 * ROWB);
     };
 
     f32x4_t acc[2][FM];
@@ -151,7 +164,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-    // ---- prologue: stages 0..2, weight substeps 0..2 (vmcnt order: DMA0 DMA1 DMA2 W0 W1 W2, 2 ops each)
+    // ---- prologue: stages 0..2, weight substeps 0..2 (vmcnt order: DMA0 DMA1 DMA2 (KSS ops each),
+    // W0 W1 W2 (2 each))
     issue(0);
     issue(1);
     issue(2);
@@ -159,11 +173,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
     wload(wq[1], 1);
     wload(wq[2], 2);
 
-    // Stage t issues (after its barrier) DMA(t + 3), then the weight loads of substeps 2t + 3 and 2t + 4:
-    // 6 VMEM ops per stage, so 16 ops are younger than DMA(t) when stage t waits for it (t >= 2; t = 0 / 1:
-    // 10 / 14).  Every stage issues all 6, unconditionally (a branch around them makes the compiler's
-    // own waits for the weight registers drain everything): past the end the DMAs re-fill slots nobody
-    // reads again (zeros, or in-bounds bytes of x2) and the weight loads repeat the last substep.
+    // Stage t issues (after its barrier) DMA(t + 3), then the weight loads of the substeps 3 ahead of its
+    // own: 3 KSS VMEM ops per stage, so 8 KSS ops are younger than DMA(t) when stage t waits for it
+    // (t >= 3; t = 0, 1, 2: 2 KSS + 6, 4 KSS + 6, 6 KSS + 6).  Every stage issues all of them,
+    // unconditionally (a branch around them makes the compiler's own waits for the weight registers drain
+    // everything): past the end the DMAs re-fill slots nobody reads again (zeros, or in-bounds bytes of
+    // x2) and the weight loads repeat the last substep.
     auto mfmas = [&](int slot_w, frag (&b)[FM]) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -173,33 +188,41 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
 #pragma unroll 1
     for (int s4 = 0; s4 < nks; s4 += 4) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int t = s4 / 2 + u, slot = t & (NST - 1);
-            if (t >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            else if (t == 1) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        for (int u = 0; u < 4 / KSS; ++u) {
+            const int t = s4 / KSS + u, slot = t & (NST - 1);
+            if constexpr (KSS == 2) {
+                if (t >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                else if (t == 1) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+            } else {
+                if (t >= 3) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                else if (t == 2) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+                else if (t == 1) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+            }
             // every wave's DMA of stage t landed; every wave is past its reads of stage t - 1, whose slot
             // stage t + 3 refills
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             issue((t + 3) & (NST - 1));
-            // substep 2t: fragments of k-half 0, then its MFMAs with k-half 1's reads between them
             bread(bq[0], slot, 0);
-            const int sa = 2 * t, wa = (2 * u) & 3, wb = (2 * u + 1) & 3;  // s4 % 4 == 0: compile-time ring slots
-            wload(wq[(wa + 3) & 3], sa + 3 < nks ? sa + 3 : nks - 1);
-            __builtin_amdgcn_sched_barrier(0);
-            bread(bq[1], slot, 1);
-            mfmas(wa, bq[0]);
-#if FR_WRING_SCHED
 #pragma unroll
-            for (int q = 0; q < FM; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
+            for (int kk = 0; kk < KSS; ++kk) {
+                const int s = t * KSS + kk, w = (u * KSS + kk) & 3;  // s4 % 4 == 0: compile-time ring slots
+                __builtin_amdgcn_sched_barrier(0);
+                wload(wq[(w + 3) & 3], s + 3 < nks ? s + 3 : nks - 1);
+                if (kk + 1 < KSS) bread(bq[(kk + 1) & 1], slot, kk + 1);
+                mfmas(w, bq[kk & 1]);
+#if FR_WRING_SCHED
+                if (kk + 1 < KSS) {
+#pragma unroll
+                    for (int q = 0; q < FM; ++q) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                }
 #endif
-            __builtin_amdgcn_sched_barrier(0);
-            wload(wq[(wb + 3) & 3], sa + 4 < nks ? sa + 4 : nks - 1);
-            mfmas(wb, bq[1]);
+            }
         }
     }
 
@@ -297,21 +320,37 @@ hipError_t wring_pack_weights(const bf16_t* w, int Kpad, int Npad, bf16_t* out, 
     return hipGetLastError();
 }
 
-hipError_t launch_conv_wring(const ConvArgs& a, hipStream_t s) {
-    if (!wring_supported(a) || !a.wimg) return hipErrorInvalidValue;
+template <int KSS>
+hipError_t launch_kss(const ConvArgs& a, hipStream_t s) {
     const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.Cout / BN;
-    auto k = a.f16 ? conv_wring_kernel<true> : conv_wring_kernel<false>;
+    auto k = a.f16 ? conv_wring_kernel<true, KSS> : conv_wring_kernel<false, KSS>;
     static bool attr[2] = {false, false};
     if (!attr[a.f16 ? 1 : 0]) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, WR_LDS);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, WGeo<KSS>::LDS);
         attr[a.f16 ? 1 : 0] = true;
     }
     const dim3 grid((unsigned)(tiles_m * tiles_n));
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, grid, dim3(64 * NW), WR_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, tiles_m);
+        hipExtLaunchKernelGGL(k, grid, dim3(64 * NW), WGeo<KSS>::LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a,
+                              tiles_m);
     else
-        hipLaunchKernelGGL(k, grid, dim3(64 * NW), WR_LDS, s, a, tiles_m);
+        hipLaunchKernelGGL(k, grid, dim3(64 * NW), WGeo<KSS>::LDS, s, a, tiles_m);
     return hipGetLastError();
+}
+
+// 128-channel stages where the channel counts allow (FR_WRING_KSS=2 forces 64-channel stages)
+static bool use_kss4(const ConvArgs& a) {
+    static const int force = [] {
+        const char* e = getenv("FR_WRING_KSS");
+        return e ? atoi(e) : 0;
+    }();
+    const bool ok = a.Cin % 128 == 0 && (!a.x2 || a.C2 % 128 == 0) && a.Kpad / 128 >= 3;
+    return ok && force != 2;
+}
+
+hipError_t launch_conv_wring(const ConvArgs& a, hipStream_t s) {
+    if (!wring_supported(a) || !a.wimg) return hipErrorInvalidValue;
+    return use_kss4(a) ? launch_kss<4>(a, s) : launch_kss<2>(a, s);
 }
 
 }  // namespace fr
