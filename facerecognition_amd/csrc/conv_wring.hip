@@ -29,23 +29,31 @@
 namespace fr {
 namespace {
 
-constexpr int NW = 8;                       // waves
-constexpr int BN = 256;                     // output channels per block (32 per wave)
 constexpr int FM = 7;                       // pixel fragments
 constexpr int BM = 16 * FM;                 // 112 pixels per block
 constexpr int SROWS = 128;                  // LDS rows per stage (112 used)
 constexpr int NST = 4;                      // LDS stages
-constexpr int EPI_LD = BN + 4;              // f32 epilogue row (floats)
-constexpr int EPI_B = BM * EPI_LD * 4;      // 116480
 // KSS = 32-deep substeps per LDS stage (2: 128-B rows, 16 KiB stages; 4: 256-B rows, 32 KiB stages, half
-// the barriers, needs Cin % 128 == 0)
-template <int KSS>
+// the barriers, needs Cin % 128 == 0); NW = waves = output channels / 32 (8: 256 channels, one block per
+// CU; 4: 128 channels, two blocks per CU)
+template <int KSS, int NW>
 struct WGeo {
+    static constexpr int BN = 32 * NW, EPI_LD = BN + 4, EPI_B = BM * EPI_LD * 4;
     static constexpr int CH = 32 * KSS, ROWB = 2 * CH, NCH = ROWB / 16, RPP = 1024 / ROWB;
     static constexpr int STAGE_B = SROWS * ROWB;
+    static constexpr int PPW = SROWS * ROWB / 1024 / NW;  // DMA pieces per wave per stage
+    static constexpr int P = PPW + 2 * KSS;               // VMEM ops per stage (DMA + weight loads)
     static constexpr int LDS = EPI_B > NST * STAGE_B ? EPI_B : NST * STAGE_B;
+    // vmcnt when stage t waits for its DMA: ops younger than it (prologue DMA0..2, W0..2, then P a stage)
+    static constexpr int Y3 = 2 * KSS + 2 * P, Y0 = 2 * PPW + 6, Y1 = PPW + 6 + P;
+    static constexpr int Y2 = 6 + 2 * P < Y3 ? 6 + 2 * P : Y3;
     __device__ static int swz(int row) { return KSS == 2 ? (row >> 1) & 7 : row & 15; }
 };
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 constexpr uint32_t OOB = 0x80000000u;
 
 #ifndef FR_WRING_EXP
@@ -62,12 +70,13 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const char* l
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
 }
 
-template <bool F16, int KSS>
-__global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int tiles_m) {
+template <bool F16, int KSS, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p, int tiles_m) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
-    typedef WGeo<KSS> Gm;
+    typedef WGeo<KSS, NW> Gm;
     constexpr int CH = Gm::CH, ROWB = Gm::ROWB, NCH = Gm::NCH, RPP = Gm::RPP, STAGE_B = Gm::STAGE_B;
+    constexpr int BN = Gm::BN, EPI_LD = Gm::EPI_LD, PPW = Gm::PPW;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -75,9 +84,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
     const int lid = xcd_remap(blockIdx.x, gridDim.x);
     const int tn = lid / tiles_m, tm = lid - tn * tiles_m;  // pixels fastest: an XCD keeps one weight half
     const int m0 = tm * BM, n0 = tn * BN;
-    const int nks = p.Kpad / 32;  // 32-deep substeps (a multiple of 4, host-checked)
+    const int nks = p.Kpad / 32;  // 32-deep substeps (a multiple of KSS, host-checked)
 
-    // ---- operand B: piece q = wave + 8 i (i < KSS) of a stage holds rows RPP q .. RPP q + RPP - 1; the
+    // ---- operand B: piece q = wave + NW i (i < PPW) of a stage holds rows RPP q .. RPP q + RPP - 1; the
     // lane's row and its source chunk (the logical chunk stored at its linear destination position)
     const int lrow = lane / NCH;
     const int cl = (lane % NCH) ^ Gm::swz(RPP * wave + lrow);  // the same for every i
@@ -87,10 +96,10 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
         (void*)(p.x2 ? p.x2 : p.x), 0,
         (uint32_t)min((size_t)0x7fffffff, p.x2 ? (size_t)p.B * p.H2 * p.W2 * p.Cx2 * 2 : (size_t)0), 0x00020000);
     const int HoWo = p.Ho * p.Wo;
-    int a_ih[KSS], a_iw[KSS];
-    uint32_t a_base[KSS], a_base2[KSS];
+    int a_ih[PPW], a_iw[PPW];
+    uint32_t a_base[PPW], a_base2[PPW];
 #pragma unroll
-    for (int i = 0; i < KSS; ++i) {
+    for (int i = 0; i < PPW; ++i) {
         const int row = RPP * (wave + NW * i) + lrow, m = m0 + row;
         if (row < BM && m < p.M) {
             const int b = m / HoWo, r = m - b * HoWo, oh = r / p.Wo, ow = r - oh * p.Wo;
@@ -113,12 +122,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
         if (k_cur >= K1) {  // projection K-steps: x2 at the output's stride-st2 position
             const uint32_t c2 = (uint32_t)((k_cur - K1) * 2);
 #pragma unroll
-            for (int i = 0; i < KSS; ++i)
+            for (int i = 0; i < PPW; ++i)
                 dma16(x2r, dst + (wave + NW * i) * 1024, a_base2[i] == OOB ? OOB : a_base2[i] + c2);
         } else {
             const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
 #pragma unroll
-            for (int i = 0; i < KSS; ++i) {
+            for (int i = 0; i < PPW; ++i) {
                 const int ih = a_ih[i] + r_cur, iw = a_iw[i] + s_cur;
                 const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
                 dma16(xr, dst + (wave + NW * i) * 1024, ok ? a_base[i] + (uint32_t)soff : OOB);
@@ -174,8 +183,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
     wload(wq[2], 2);
 
     // Stage t issues (after its barrier) DMA(t + 3), then the weight loads of the substeps 3 ahead of its
-    // own: 3 KSS VMEM ops per stage, so 8 KSS ops are younger than DMA(t) when stage t waits for it
-    // (t >= 3; t = 0, 1, 2: 2 KSS + 6, 4 KSS + 6, 6 KSS + 6).  Every stage issues all of them,
+    // own: P = PPW + 2 KSS VMEM ops per stage, so WGeo::Y3 ops are younger than DMA(t) when stage t waits
+    // for it (t >= 3; Y0..Y2 before the ring is full).  Every stage issues all of them,
     // unconditionally (a branch around them makes the compiler's own waits for the weight registers drain
     // everything): past the end the DMAs re-fill slots nobody reads again (zeros, or in-bounds bytes of
     // x2) and the weight loads repeat the last substep.
@@ -190,16 +199,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_wring_kernel(ConvArgs p, int 
 #pragma unroll
         for (int u = 0; u < 4 / KSS; ++u) {
             const int t = s4 / KSS + u, slot = t & (NST - 1);
-            if constexpr (KSS == 2) {
-                if (t >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                else if (t == 1) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-            } else {
-                if (t >= 3) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-                else if (t == 2) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
-                else if (t == 1) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-            }
+            if (KSS == 2 && u == 1 && 2 * t >= nks) break;  // Kpad % 128 == 64: a last half iteration
+            if (t >= 3) wait_vm<Gm::Y3>();
+            else if (t == 2) wait_vm<Gm::Y2>();
+            else if (t == 1) wait_vm<Gm::Y1>();
+            else wait_vm<Gm::Y0>();
             // every wave's DMA of stage t landed; every wave is past its reads of stage t - 1, whose slot
             // stage t + 3 refills
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -302,10 +306,14 @@ __global__ __launch_bounds__(256) void wring_pack_kernel(const bf16_t* __restric
 
 }  // namespace
 
+// waves per block for a conv: 8 (256-channel blocks) when Cout % 256 == 0, else 4 (128-channel blocks)
+static int wring_nw(const ConvArgs& a) { return a.Cout % 256 == 0 ? 8 : 4; }
+
 bool wring_supported(const ConvArgs& a) {
     const bool kcat = a.x2 != nullptr;
-    return a.B > 0 && a.Cin % 64 == 0 && a.Cout % BN == 0 && a.Npad % BN == 0 && a.Npad >= a.Cout &&
-           a.Kpad % 128 == 0 && a.Kpad / 64 >= 3 &&
+    const int bn = 32 * wring_nw(a);
+    return a.B > 0 && a.Cin % 64 == 0 && a.Cout % 128 == 0 && a.Cout % bn == 0 && a.Npad % bn == 0 &&
+           a.Npad >= a.Cout && a.Kpad % 64 == 0 && a.Kpad / 64 >= 3 &&
            (kcat ? (a.C2 % 64 == 0 && a.K1 == a.Kh * a.Kw * a.Cin && a.K1 + a.C2 == a.Kpad) : a.K == a.Kpad) &&
            a.K == a.Kh * a.Kw * a.Cin + (kcat ? a.C2 : 0) && a.Cx % 8 == 0 && a.x_off % 8 == 0 &&
            a.Cy % 8 == 0 && a.y_off % 8 == 0 && !a.y2 && !a.partial && !a.w8 && !a.y_amax &&
@@ -320,21 +328,21 @@ hipError_t wring_pack_weights(const bf16_t* w, int Kpad, int Npad, bf16_t* out, 
     return hipGetLastError();
 }
 
-template <int KSS>
+template <int KSS, int NW>
 hipError_t launch_kss(const ConvArgs& a, hipStream_t s) {
-    const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.Cout / BN;
-    auto k = a.f16 ? conv_wring_kernel<true, KSS> : conv_wring_kernel<false, KSS>;
+    typedef WGeo<KSS, NW> Gm;
+    const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.Cout / Gm::BN;
+    auto k = a.f16 ? conv_wring_kernel<true, KSS, NW> : conv_wring_kernel<false, KSS, NW>;
     static bool attr[2] = {false, false};
     if (!attr[a.f16 ? 1 : 0]) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, WGeo<KSS>::LDS);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, Gm::LDS);
         attr[a.f16 ? 1 : 0] = true;
     }
     const dim3 grid((unsigned)(tiles_m * tiles_n));
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, grid, dim3(64 * NW), WGeo<KSS>::LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a,
-                              tiles_m);
+        hipExtLaunchKernelGGL(k, grid, dim3(64 * NW), Gm::LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, tiles_m);
     else
-        hipLaunchKernelGGL(k, grid, dim3(64 * NW), WGeo<KSS>::LDS, s, a, tiles_m);
+        hipLaunchKernelGGL(k, grid, dim3(64 * NW), Gm::LDS, s, a, tiles_m);
     return hipGetLastError();
 }
 
@@ -344,13 +352,14 @@ static bool use_kss4(const ConvArgs& a) {
         const char* e = getenv("FR_WRING_KSS");
         return e ? atoi(e) : 0;
     }();
-    const bool ok = a.Cin % 128 == 0 && (!a.x2 || a.C2 % 128 == 0) && a.Kpad / 128 >= 3;
+    const bool ok = a.Cin % 128 == 0 && (!a.x2 || a.C2 % 128 == 0) && a.Kpad % 128 == 0 && a.Kpad / 128 >= 3;
     return ok && force != 2;
 }
 
 hipError_t launch_conv_wring(const ConvArgs& a, hipStream_t s) {
     if (!wring_supported(a) || !a.wimg) return hipErrorInvalidValue;
-    return use_kss4(a) ? launch_kss<4>(a, s) : launch_kss<2>(a, s);
+    if (wring_nw(a) == 4) return launch_kss<2, 4>(a, s);  // 128-channel blocks: two per CU (64 KiB stages)
+    return use_kss4(a) ? launch_kss<4, 8>(a, s) : launch_kss<2, 8>(a, s);
 }
 
 }  // namespace fr

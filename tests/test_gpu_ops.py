@@ -162,7 +162,8 @@ def test_conv_rows(gpu, case):
 
 WRING_CASES = [  # (B, H, W, Cin, Cout, stride): layer4 (two 7x7 images per block, M not a multiple of
     # 112 at B = 3), layer3.0.conv1, the layer4.0 stride-2 conv, a 28x28 stride-2 one
-    (3, 7, 7, 512, 512, 1), (1, 28, 28, 128, 256, 1), (2, 14, 14, 256, 512, 2), (2, 28, 28, 128, 256, 2)]
+    (3, 7, 7, 512, 512, 1), (1, 28, 28, 128, 256, 1), (2, 14, 14, 256, 512, 2), (2, 28, 28, 128, 256, 2),
+    (2, 28, 28, 128, 128, 1), (1, 56, 56, 64, 128, 2)]  # 128-channel blocks (4 waves); Kpad % 128 == 64
 
 
 @pytest.mark.parametrize("case", WRING_CASES)
@@ -184,8 +185,8 @@ def test_conv_wring(gpu, case):
     b9 = torch.randn(9, Cout, generator=g) * 0.1
     y = conv_op(x, w, act=2, slope=slope, bias9=b9, tile=N.FR_TILE_WRING, **kw)
     assert torch.equal(y, conv_op(x, w, act=2, slope=slope, bias9=b9, tile=0, **kw))
-    with pytest.raises(RuntimeError, match="wring"):  # Cout % 256 != 0: refused, no silent fallback
-        conv_op(x, torch.randn(128, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_WRING)
+    with pytest.raises(RuntimeError, match="wring"):  # Cout % 128 != 0: refused, no silent fallback
+        conv_op(x, torch.randn(64, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_WRING)
 
 
 def test_conv_img28_channel_slices_and_applicability(gpu):
