@@ -119,19 +119,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
     int r_cur = 0, s_cur = 0, c_cur = 0, k_cur = 0;  // the next stage to issue: tap (r, s), channel base
     auto issue = [&](int slot) {
         const char* dst = smem + slot * STAGE_B;
-        if (k_cur >= K1) {  // projection K-steps: x2 at the output's stride-st2 position
-            const uint32_t c2 = (uint32_t)((k_cur - K1) * 2);
+        // branch-free (x or the projection input x2 by selects): a branch around the DMAs made the
+        // compiler's counted waits for the weight registers conservative
+        const bool kx2 = k_cur >= K1;  // projection K-steps: x2 at the output's stride-st2 position
+        const __amdgpu_buffer_rsrc_t rs = kx2 ? x2r : xr;
+        const uint32_t c2 = (uint32_t)((k_cur - K1) * 2);
+        const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
 #pragma unroll
-            for (int i = 0; i < PPW; ++i)
-                dma16(x2r, dst + (wave + NW * i) * 1024, a_base2[i] == OOB ? OOB : a_base2[i] + c2);
-        } else {
-            const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
-#pragma unroll
-            for (int i = 0; i < PPW; ++i) {
-                const int ih = a_ih[i] + r_cur, iw = a_iw[i] + s_cur;
-                const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-                dma16(xr, dst + (wave + NW * i) * 1024, ok ? a_base[i] + (uint32_t)soff : OOB);
-            }
+        for (int i = 0; i < PPW; ++i) {
+            const int ih = a_ih[i] + r_cur, iw = a_iw[i] + s_cur;
+            const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            const uint32_t o1 = ok ? a_base[i] + (uint32_t)soff : OOB;
+            const uint32_t o2 = a_base2[i] == OOB ? OOB : a_base2[i] + c2;
+            dma16(rs, dst + (wave + NW * i) * 1024, kx2 ? o2 : o1);
         }
         if (FR_WRING_EXP & 2) return;
         k_cur += CH;
@@ -194,12 +194,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wq[slot_w][i], b[j], acc[i][j]);
     };
+    // 16 substeps per loop iteration: at the loop head the compiler cannot track the register ring
+    // carried around the back edge and waits for every outstanding load (the stage DMAs issued just
+    // before included), so the head should come rarely; a partial last iteration breaks out
 #pragma unroll 1
-    for (int s4 = 0; s4 < nks; s4 += 4) {
+    for (int s4 = 0; s4 < nks; s4 += 16) {
 #pragma unroll
-        for (int u = 0; u < 4 / KSS; ++u) {
+        for (int u = 0; u < 16 / KSS; ++u) {
             const int t = s4 / KSS + u, slot = t & (NST - 1);
-            if (KSS == 2 && u == 1 && 2 * t >= nks) break;  // Kpad % 128 == 64: a last half iteration
+            if (u > 0 && KSS * t >= nks) break;
             if (t >= 3) wait_vm<Gm::Y3>();
             else if (t == 2) wait_vm<Gm::Y2>();
             else if (t == 1) wait_vm<Gm::Y1>();
