@@ -32,6 +32,34 @@ constexpr int SROWS = 2;      // output rows per tile
 constexpr int SPIX = SROWS * SW;  // 224
 constexpr int WROW = 104;          // LDS weight row: 96 bf16 + pad (208 B: conflict-free 16-lane reads)
 
+// Workgroup barrier that waits for LDS only: __syncthreads()'s fence also drains vmcnt, i.e. every 16-B
+// output store of the previous tile (gfx950 counts stores in vmcnt) and the next tile's prefetched input
+// rows, so each tile's 28 KiB of stores would run exposed instead of behind the next tile's work.
+constexpr int OFF_SY = 0;                                     // 28672
+constexpr int OFF_SWT = OFF_SY + SPIX * 8 * 16;               // 13312
+constexpr int OFF_SX = OFF_SWT + SCO * WROW * 2;              // 3648
+constexpr int OFF_SBS = OFF_SX + (SROWS + 2) * (SW + 2) * 8;  // 512
+constexpr int OFF_RAW = OFF_SBS + 2 * SCO * 4;                // 2048
+constexpr int STEM_LDS = OFF_RAW + 2 * 256 * 4;
+static_assert(OFF_SX % 16 == 0 && OFF_SBS % 16 == 0 && OFF_RAW % 16 == 0, "16-B aligned LDS arrays");
+
+// 4-byte LDS-DMA (buffer_load_dword ... lds; lane l lands at lds_addr + 4 l) issued from inline asm: the
+// compiler then does not know about the LDS write, and its waitcnt pass does not guard every later LDS
+// access with a vmcnt(0) (which would also drain the output stores); the kernel's own waits cover the DMA
+// (m0 is reserved to the compiler, hence the pragma; nothing else in this kernel uses m0)
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma_dword(const v4i32& rsrc, uint32_t lds_addr, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds"
+                 :
+                 : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <bool F16>
 // waves_per_eu(3): the persistent loop would otherwise grow past 168 VGPRs and lose the third block per CU
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stem_u8_kernel(
@@ -39,11 +67,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
     const float* __restrict__ slope, int act, bf16_t* __restrict__ y, int Cy, int y_off, int ntiles) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
-    __shared__ __attribute__((aligned(16))) uint16_t sx[SROWS + 2][SW + 2][4];
-    __shared__ __attribute__((aligned(16))) uint4 sy[SPIX * 8];
-    __shared__ __attribute__((aligned(16))) uint32_t sraw[SROWS + 2][SW * 3 / 4];          // u8 rows as dwords
-    __shared__ __attribute__((aligned(16))) uint16_t swt[SCO][WROW];                        // weight rows
-
+    // one dynamic LDS block (STEM_LDS bytes): with static __shared__ arrays the compiler cannot tell the
+    // input DMA's target from the other arrays and puts a vmcnt(0) (which drains the output stores) before
+    // every LDS access after the DMA issue
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint16_t(*sx)[SW + 2][4] = (uint16_t(*)[SW + 2][4])(smem + OFF_SX);  // [SROWS + 2][SW + 2][4]
+    uint4* sy = (uint4*)(smem + OFF_SY);                                  // [SPIX * 8]
+    uint16_t(*swt)[WROW] = (uint16_t(*)[WROW])(smem + OFF_SWT);          // [SCO][WROW] weight rows
+    float(*sbs)[SCO] = (float(*)[SCO])(smem + OFF_SBS);                   // [2][SCO] bias, PReLU slope
+    uint32_t* sraw = (uint32_t*)(smem + OFF_RAW);                         // [2 * 256] u8 rows as dwords + pad
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
     // the 64 x 96 weight rows, staged once per (persistent) block; the first tile's barrier after its
@@ -52,37 +84,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
         const int n = e / 12, c = e % 12;
         *(uint4*)&swt[n][8 * c] = *(const uint4*)(w + (size_t)n * Kpad + 8 * c);
     }
+    // bias and slope in LDS too: global loads in the epilogue would make its vmcnt waits also wait for the
+    // next tile's input prefetch (issued just before) and for nothing else
+    if (tid < SCO) {
+        sbs[0][tid] = bias[tid];
+        sbs[1][tid] = act == 2 ? slope[tid] : 0.f;
+    }
 
     // a tile's input rows r0-1 .. r0+2 (336 contiguous bytes each) as dwords, two per thread, loaded one
     // tile ahead into registers so the HBM latency hides behind the previous tile's MFMA loop and stores
     constexpr int RAWD = (SROWS + 2) * (SW * 3 / 4);
     static_assert(RAWD <= 2 * 256, "two input dwords per thread");
-    auto load_raw = [&](int t, uint32_t (&r)[2]) {
+    // The rows go straight to LDS by LDS-DMA (4 B per lane, linear: dword e = tid + 256 j of sraw), branch
+    // free: rows outside the image and the pad dwords get an out-of-range offset, which reads 0.  The waits
+    // are explicit: at a tile's top the only VMEM operations issued after its DMA are the previous tile's
+    // 7 output stores, which stay in flight (vmcnt(7)).
+    const uint64_t inp = (uint64_t)in;
+    const v4i32 inr = {(int)(uint32_t)inp, (int)((inp >> 32) & 0xffff), (int)((ntiles / (SW / SROWS)) * (SW * SW * 3)),
+                       0x00020000};
+    auto dma_raw = [&](int t) {
         const int b = t / (SW / SROWS), r0 = (t % (SW / SROWS)) * SROWS;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int e = tid + 256 * j, rr = e / (SW * 3 / 4), d = e % (SW * 3 / 4), ir = r0 - 1 + rr;
-            r[j] = e < RAWD && (unsigned)ir < (unsigned)SW ? *(const uint32_t*)(in + ((size_t)b * SW + ir) * SW * 3 + 4 * d) : 0u;
+            const bool ok = e < RAWD && (unsigned)ir < (unsigned)SW;
+            const uint32_t off = ok ? (uint32_t)(((b * SW + ir) * SW * 3) + 4 * d) : 0x80000000u;
+            dma_dword(inr, (uint32_t)(uintptr_t)&sraw[256 * j + 64 * wave], off);
         }
     };
-    uint32_t raw[2];
-    load_raw(blockIdx.x, raw);  // gridDim.x <= ntiles
+    dma_raw(blockIdx.x);  // gridDim.x <= ntiles
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // tiles t = blockIdx.x + j * gridDim.x; every wave runs the same trip count (block-uniform loop)
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int b = t / (SW / SROWS), r0 = (t % (SW / SROWS)) * SROWS;
         // the previous tile's reads of sraw / sx / sy all precede a barrier every thread has passed
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if (tid + 256 * j < RAWD) (&sraw[0][0])[tid + 256 * j] = raw[j];
-        __syncthreads();
+        if (t != (int)blockIdx.x) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // this tile's DMA landed
+        lds_barrier();
         // -> 2q - 255 in the activation dtype, zero halo columns (rows outside the image were zeroed above
         // but must also become 0, not -255)
         for (int e = tid; e < (SROWS + 2) * (SW + 2); e += 256) {
             const int rr = e / (SW + 2), cc = e % (SW + 2), ir = r0 - 1 + rr, ic = cc - 1;
             uint16_t v[3] = {0, 0, 0};
             if ((unsigned)ir < (unsigned)SW && (unsigned)ic < (unsigned)SW) {
-                const uint8_t* q = (const uint8_t*)&sraw[rr][0] + 3 * ic;
+                const uint8_t* q = (const uint8_t*)&sraw[rr * (SW * 3 / 4)] + 3 * ic;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) v[c] = T::cvt(2.0f * (float)q[c] - 255.0f);
             }
@@ -96,7 +141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
 #pragma unroll
             for (int ks = 0; ks < 3; ++ks)
                 wa[i][ks] = *(const frag*)&swt[16 * i + (lane & 15)][32 * ks + 8 * (lane >> 4)];
-        __syncthreads();
+        lds_barrier();
 
         // wave w: m-frags w, w+4, w+8, w+12 (< 14)
         f32x4_t acc[4][4];
@@ -123,14 +168,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
                 for (int i = 0; i < 4; ++i) acc[u][i] = T::mfma(wa[i][ks], bq, acc[u][i]);
             }
         }
-        if (t + (int)gridDim.x < ntiles) load_raw(t + gridDim.x, raw);  // block-uniform
+        if (t + (int)gridDim.x < ntiles) dma_raw(t + gridDim.x);  // block-uniform; sraw's reads are behind barrier 2
         // epilogue: lane holds channels 16i + 4(lane>>4) .. +3 of pixel 16f + (lane&15)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int n = 16 * i + 4 * (lane >> 4);
-            const float4 bb = *(const float4*)(bias + n);
-            float4 sl = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (act == 2) sl = *(const float4*)(slope + n);
+            const float4 bb = *(const float4*)&sbs[0][n];
+            const float4 sl = *(const float4*)&sbs[1][n];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int f = wave + 4 * u;
@@ -152,11 +196,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
                 *(uint2*)dst = make_uint2(pk.x, pk.y);
             }
         }
-        __syncthreads();
+        lds_barrier();
         // coalesced stores: 224 pixels x 8 chunks of 16 B
         const size_t row0 = ((size_t)b * SW + r0) * SW;
-        for (int e = tid; e < SPIX * 8; e += 256) {
-            const int px = e >> 3, ch = e & 7;
+        static_assert(SPIX * 8 % 256 == 0, "whole store rounds");
+#pragma unroll
+        for (int q = 0; q < SPIX * 8 / 256; ++q) {
+            const int e = tid + 256 * q, px = e >> 3, ch = e & 7;
             *(uint4*)(y + (row0 + px) * Cy + y_off + 8 * ch) = sy[px * 8 + (ch ^ (px & 7))];
         }
     }
@@ -177,6 +223,7 @@ hipError_t launch_stem_u8(const uint8_t* in, int B, const bf16_t* w, int Kpad, c
         const char* e = getenv("FR_STEM_PERSIST");
         return !(e && e[0] == '0');
     }();
+    if ((size_t)B * SW * SW * 3 >= 0x80000000ull) return hipErrorInvalidValue;  // buffer offsets are 31-bit
     const int ntiles = B * (SW / SROWS);
     int nblk = ntiles;
     if (persist && ntiles > 768) {
@@ -185,9 +232,9 @@ hipError_t launch_stem_u8(const uint8_t* in, int B, const bf16_t* w, int Kpad, c
     }
     const dim3 grid(nblk);
     if (f16)
-        hipLaunchKernelGGL(stem_u8_kernel<true>, grid, dim3(256), 0, s, in, w, Kpad, bias, slope, act, y, Cy, y_off, ntiles);
+        hipLaunchKernelGGL(stem_u8_kernel<true>, grid, dim3(256), STEM_LDS, s, in, w, Kpad, bias, slope, act, y, Cy, y_off, ntiles);
     else
-        hipLaunchKernelGGL(stem_u8_kernel<false>, grid, dim3(256), 0, s, in, w, Kpad, bias, slope, act, y, Cy, y_off, ntiles);
+        hipLaunchKernelGGL(stem_u8_kernel<false>, grid, dim3(256), STEM_LDS, s, in, w, Kpad, bias, slope, act, y, Cy, y_off, ntiles);
     return hipGetLastError();
 }
 
