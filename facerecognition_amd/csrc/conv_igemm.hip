@@ -22,6 +22,7 @@
 
 #include <hip/hip_ext.h>
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace fr {
@@ -581,6 +582,42 @@ void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
     }
     *tile = bt;
     *split = bs;
+}
+
+// The embedding head (M = batch, N = 512, K = 25,088 at 7x7x512): a few output tiles over a very long K, so
+// split-K wide enough to give every CU two blocks (conv_plan stops at 16 splits: 256 blocks of 24 K-steps
+// at bs = 256, 43 us); splits that divide the K-steps evenly, >= 4 K-steps each.  FR_HEAD_PLAN=tile,split
+// overrides (experiments).
+void head_plan(int M, int Cout, int Kpad, int* tile, int* split) {
+    static const int env[2] = {-1, -1};
+    static const bool has_env = [] {
+        const char* e = getenv("FR_HEAD_PLAN");
+        if (!e) return false;
+        int t = -1, sp = -1;
+        if (sscanf(e, "%d,%d", &t, &sp) != 2 || t < 0 || sp < 1) return false;
+        const_cast<int*>(env)[0] = t;
+        const_cast<int*>(env)[1] = sp;
+        return true;
+    }();
+    if (has_env) {
+        *tile = env[0];
+        *split = env[1];
+        return;
+    }
+    const int nkt = Kpad / BK;
+    const long tiles = (long)((M + 127) / 128) * ((Cout + 63) / 64);
+    int best = 1;
+    for (int sp = 1; sp <= nkt / 4; ++sp) {
+        if (nkt % sp) continue;
+        if (tiles * sp > 512) break;
+        best = sp;
+    }
+    if (best == 1) {  // no even split: fall back to the generic plan
+        conv_plan(M, Cout, Kpad, tile, split);
+        return;
+    }
+    *tile = TILE_128x64;
+    *split = best;
 }
 
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {

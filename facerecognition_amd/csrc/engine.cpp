@@ -916,7 +916,8 @@ size_t partial_need(fr_handle* h, int B) {
         const auto& cw = h->convw[op.wi];
         const int M = op.kind == OP_HEAD ? B : B * h->tensors[op.out].H * h->tensors[op.out].W;
         int tile, sp;
-        conv_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
+        if (op.kind == OP_HEAD) head_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
+        else conv_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
         if (sp > 1 || op.kind == OP_HEAD) need = std::max(need, (size_t)sp * M * cw.Npad);
     }
     return need;
@@ -1360,7 +1361,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.w = cw.w; a.Kh = 1; a.Kw = 1; a.sh = 1; a.sw = 1; a.K = cw.K; a.Kpad = cw.Kpad;
                 a.Ho = 1; a.Wo = 1; a.M = B; a.Cout = cw.Cout; a.Npad = cw.Npad;
                 int tile, split;
-                conv_plan(B, cw.Cout, cw.Kpad, &tile, &split);
+                head_plan(B, cw.Cout, cw.Kpad, &tile, &split);
                 while (split > 1 && (size_t)split * B * cw.Npad > h->partial_floats) split /= 2;
                 a.tile = tile;
                 a.split_k = split;
@@ -1702,7 +1703,8 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
         const auto& cw = h->convw[op.wi];
         const int M = op.kind == OP_HEAD ? B : B * h->tensors[op.out].H * h->tensors[op.out].W;
         int tile, sp;
-        conv_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
+        if (op.kind == OP_HEAD) head_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
+        else conv_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
         if (op.kind == OP_CONV) {
             ConvArgs a{};
             a.M = M; a.Cout = cw.Cout; a.Kpad = cw.Kpad; a.Cin = op.cin; a.Kh = op.kh; a.Kw = op.kw;

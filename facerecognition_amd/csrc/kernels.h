@@ -69,6 +69,7 @@ hipError_t launch_conv_fp8(const ConvArgs& a, hipStream_t s);
 bool conv_tile_forced();
 int conv_tile_candidates(int Cout, int* out);
 void conv_plan(int M, int Cout, int Kpad, int* tile, int* split);
+void head_plan(int M, int Cout, int Kpad, int* tile, int* split);  // the embedding head's split-K
 int conv_tile_bm(int tile);
 int conv_tile_bn(int tile);
 

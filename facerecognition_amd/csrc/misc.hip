@@ -103,23 +103,39 @@ __device__ __forceinline__ float block_sum_256(float v, float* red) {
     return red[0] + red[1] + red[2] + red[3];
 }
 
-// One block per row: out[b][n] = sum_s partial[s][b][n] + bias[n]; optional L2 normalize.
+// One block per row: out[b][n] = sum_s partial[s][b][n] + bias[n]; optional L2 normalize.  N % 4 == 0 and
+// N <= 1024 (the launcher checks): a thread owns 4 consecutive columns, float4 loads, the split loop
+// unrolled so its loads are in flight together.
 __global__ __launch_bounds__(256) void head_finalize_kernel(const float* __restrict__ partial, int split, int B,
                                                             int N, int Npad, const float* __restrict__ bias,
                                                             int normalize, float* __restrict__ out) {
     __shared__ float red[4];
-    const int b = blockIdx.x;
-    float ss = 0.f;
-    for (int n = threadIdx.x; n < N; n += 256) {
-        float v = bias ? bias[n] : 0.f;
-        for (int s = 0; s < split; ++s) v += partial[((size_t)s * B + b) * Npad + n];
-        out[(size_t)b * N + n] = v;
-        ss += v * v;
+    const int b = blockIdx.x, n = 4 * threadIdx.x;
+    const bool own = n < N;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (own) {
+        if (bias) v = *(const float4*)(bias + n);
+        const float* src = partial + (size_t)b * Npad + n;
+        const size_t stride = (size_t)B * Npad;
+        int s = 0;
+        for (; s + 4 <= split; s += 4) {
+            float4 q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) q[u] = *(const float4*)(src + (s + u) * stride);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { v.x += q[u].x; v.y += q[u].y; v.z += q[u].z; v.w += q[u].w; }
+        }
+        for (; s < split; ++s) {
+            const float4 q = *(const float4*)(src + s * stride);
+            v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+        }
     }
-    if (!normalize) return;
-    const float tot = block_sum_256(ss, red);
-    const float inv = 1.0f / fmaxf(sqrtf(tot), 1e-12f);
-    for (int n = threadIdx.x; n < N; n += 256) out[(size_t)b * N + n] *= inv;
+    if (normalize) {
+        const float tot = block_sum_256(own ? v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w : 0.f, red);
+        const float inv = 1.0f / fmaxf(sqrtf(tot), 1e-12f);
+        v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+    }
+    if (own) *(float4*)(out + (size_t)b * N + n) = v;
 }
 
 __global__ __launch_bounds__(256) void l2norm_rows_kernel(float* __restrict__ x, int D) {
@@ -236,6 +252,7 @@ hipError_t launch_avgpool(const bf16_t* x, int B, int H, int W, int C, bf16_t* y
 
 hipError_t launch_head_finalize(const float* partial, int split, int B, int N, int Npad, const float* bias,
                                 int normalize, float* out, hipStream_t s) {
+    if (N % 4 || N > 1024 || Npad % 4) return hipErrorInvalidValue;
     hipLaunchKernelGGL(head_finalize_kernel, dim3(B), dim3(256), 0, s, partial, split, B, N, Npad, bias, normalize,
                        out);
     return hipGetLastError();
