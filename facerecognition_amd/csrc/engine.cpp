@@ -1643,7 +1643,7 @@ static int match_locked(fr_handle* h, const float* P, int B, int k, float* score
                                      h->cand_i, n_split, rps, scores, idx, h->match_fb, s));
         return FR_OK;
     }
-    match_split_plan(B, h->g_rows, &n_split, &rps);
+    match_split_plan(B, h->g_rows, h->g_dim, k, &n_split, &rps);
     int rc = ensure_cand(h, (size_t)B * n_split * k);
     if (rc) return rc;
     FR_HIP_CHECK(launch_match_topk(P, B, h->gallery, h->g_rows, h->g_dim, k, h->g_base, h->cand_s, h->cand_i,

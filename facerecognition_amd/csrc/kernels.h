@@ -167,6 +167,7 @@ hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* 
                            int64_t rows_per_split, float* out_s, int32_t* out_i, int* n_fallback, hipStream_t s);
 // Choose n_split / rows_per_split for a (B, N) match.
 void match_split_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split);
+void match_split_plan(int B, int64_t N, int D, int k, int* n_split, int64_t* rows_per_split);  // exact path
 hipError_t launch_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, int n_seg,
                                          float* out, hipStream_t s);
 // Gallery preparation: rows with |‖g‖-1| >= 1e-3 divided by ‖g‖ (cosine_similarity semantics).

@@ -17,6 +17,9 @@
 #include <float.h>
 #include <limits.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace fr {
 namespace {
 
@@ -158,6 +161,191 @@ __global__ __launch_bounds__(256) void match_partial_kernel(const float* __restr
     }
 }
 
+// D = 512 variant of match_partial_kernel with the same scores bit for bit (the same v_mfma_f32_16x16x4f32
+// sequence per output: k = 16 t16 + 4 (lane >> 4) + c) and the same candidate lists.  Each wave keeps its
+// 16 probes' A fragments in registers for the whole split (32 float4 per lane, loaded once), so only
+// gallery rows move through LDS: 64-row x 64-float chunks (256-B rows, 16-B slots XOR-swizzled with the
+// row: conflict-free fragment reads) LDS-DMA'd three chunks ahead into a 4-buffer ring, counted vmcnt
+// waits and one LDS-only barrier per chunk.  (The old kernel staged both operands per chunk through
+// registers behind full barriers; register prefetch one chunk ahead left each block one 16-KB load in
+// flight and ran 74 us at 256 x 10k, latency bound.)
+#ifndef FR_MATCH_EXP
+#define FR_MATCH_EXP 0  // timing-only experiments (WRONG results): 1 no MFMAs, 2 no top-k filter, 4 no chunk DMA
+#endif
+constexpr int D512 = 512;
+constexpr int NBUF = 4;                    // chunk ring depth (3 chunks in flight)
+constexpr int CHUNK_B = MG * KC * 4;       // 16384
+constexpr int P512_LDS = NBUF * CHUNK_B + MP * (MG + 1) * 4;
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// 16-B LDS-DMA from inline asm (lane l lands at lds_addr + 16 l): the compiler does not see the LDS write,
+// so it adds no vmcnt(0) before later LDS accesses; the kernel's own counted waits cover it
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16_asm(const v4i32& rsrc, uint32_t lds_addr, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                 :
+                 : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int KMAX>
+__global__ __launch_bounds__(256, 1) void match_p512_kernel(const float* __restrict__ P, int B,
+                                                            const float* __restrict__ G, int64_t N, int k,
+                                                            int64_t index_base, int64_t rows_per_split, int n_split,
+                                                            float* __restrict__ cs, int32_t* __restrict__ ci) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [NBUF chunks][sS]
+    float* sS = (float*)(smem + NBUF * CHUNK_B);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int p0 = blockIdx.x * MP;
+    const int split = blockIdx.y;
+    const int64_t g_begin = (int64_t)split * rows_per_split;
+    int64_t g_end = g_begin + rows_per_split;
+    if (g_end > N) g_end = N;
+    const int rows = (int)(g_end - g_begin);  // <= 64 tiles of 64 rows (the plan's bound)
+    const int ntiles = (rows + MG - 1) / MG;
+
+    // the wave's A fragments: pa[t] = P[p0 + 16 wave + (lane & 15)][16 t + 4 (lane >> 4) .. + 3]
+    float4 pa[D512 / 16];
+    {
+        const int p = p0 + 16 * wave + (lane & 15);
+        const float* src = P + (size_t)min(p, B - 1) * D512 + 4 * (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < D512 / 16; ++t) pa[t] = *(const float4*)(src + 16 * t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA wait counts below see only DMAs
+        const float z = p < B ? 1.f : 0.f;  // rows past the batch: zero probes (no branch around the loads)
+#pragma unroll
+        for (int t = 0; t < D512 / 16; ++t) pa[t] = make_float4(pa[t].x * z, pa[t].y * z, pa[t].z * z, pa[t].w * z);
+    }
+
+    // the split's rows as a buffer resource: rows past the split read 0 (out of range)
+    const uint64_t gp = (uint64_t)(G + (size_t)g_begin * D512);
+    const v4i32 gr = {(int)(uint32_t)gp, (int)((gp >> 32) & 0xffff), rows * D512 * 4, 0x00020000};
+    const uint32_t smem_base = (uint32_t)(uintptr_t)smem;
+    // chunk c = (tile c / 8, floats 64 (c % 8) ..) into ring buffer c % NBUF: wave w issues pieces w + 4u,
+    // piece q = rows 4q .. 4q + 3, lane -> row 4q + (lane >> 4), slot lane & 15 = column group
+    // (lane & 15) ^ (row & 15).  Chunks past the split are issued anyway (all out of range) so that every
+    // wait count is the same.
+    auto issue_chunk = [&](int c) {
+        const int t = c >> 3, d0 = (c & 7) * KC;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = wave + 4 * u, row = 4 * q + (lane >> 4), g = (lane & 15) ^ (row & 15);
+            const uint32_t off = (uint32_t)((t * MG + row) * (D512 * 4) + (d0 + 4 * g) * 4);
+            dma16_asm(gr, smem_base + (c % NBUF) * CHUNK_B + q * 1024, off);
+        }
+    };
+#pragma unroll
+    for (int c = 0; c < NBUF - 1; ++c) issue_chunk(c);
+
+    float ls[KMAX];
+    int li[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) { ls[q] = -INFINITY; li[q] = INT_MAX; }
+    const int my_p = tid >> 2, my_sub = tid & 3;
+
+    for (int tl = 0; tl < ntiles; ++tl) {
+        const int64_t t0 = g_begin + (int64_t)tl * MG;
+        f32x4_t acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ch = 0; ch < D512 / KC; ++ch) {
+            // chunk 8 tl + ch landed: only the two chunks issued after it (8 DMAs) may be in flight
+            __builtin_amdgcn_sched_barrier(0);
+            if (FR_MATCH_EXP & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            lds_barrier();
+            if (!(FR_MATCH_EXP & 4)) issue_chunk(8 * tl + ch + NBUF - 1);  // into the buffer read last chunk
+            else asm volatile("s_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0" ::: "memory");
+            const char* buf = smem + (ch % NBUF) * CHUNK_B;
+            // all 16 B fragments of the chunk first, one LDS wait (left alone the compiler waits before every
+            // 4 MFMAs, and one wave per SIMD cannot hide that), then the MFMAs with the 4 accumulators
+            // interleaved (a dependent f32 MFMA waits 40 cycles, the issue is 32): per accumulator the order
+            // is unchanged, x y z w per t16
+            float4 b4[KC / 16][4];
+#pragma unroll
+            for (int t16 = 0; t16 < KC / 16; ++t16) {
+                const int slot = (4 * t16 + (lane >> 4)) ^ (lane & 15);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) b4[t16][j] = *(const float4*)(buf + (16 * j + (lane & 15)) * 256 + slot * 16);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);  // nothing crosses the wait (MFMAs are not memory operations)
+#pragma unroll
+            for (int t16 = 0; t16 < KC / 16; ++t16) {
+                const float4 a4 = pa[(KC / 16) * ch + t16];
+                if (FR_MATCH_EXP & 1) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[j][0] += a4.x * b4[t16][j].x + b4[t16][j].w;
+                    continue;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4[t16][j].x, acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4[t16][j].y, acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4[t16][j].z, acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4[t16][j].w, acc[j], 0, 0, 0);
+            }
+        }
+        // scores -> LDS (its previous readers are 8 barriers back), then the filtered top-k insert
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                sS[(16 * wave + 4 * (lane >> 4) + r) * (MG + 1) + 16 * j + (lane & 15)] = acc[j][r];
+        lds_barrier();
+        if (!(FR_MATCH_EXP & 2)) {
+            const float thr = ls[KMAX - 1];
+            const int thri = li[KMAX - 1];
+            uint32_t mask = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int g = my_sub * 16 + i;
+                if (t0 + g < g_end && better(sS[my_p * (MG + 1) + g], (int)(t0 + g + index_base), thr, thri))
+                    mask |= 1u << i;
+            }
+            while (mask) {
+                const int i = __builtin_ctz(mask);
+                mask &= mask - 1;
+                const int g = my_sub * 16 + i;
+                topk_insert<KMAX>(ls, li, sS[my_p * (MG + 1) + g], (int)(t0 + g + index_base));
+            }
+        }
+    }
+
+    // merge the 4 sub-lists of each probe in the ring's LDS: the trailing (out-of-range) DMAs land first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* ms = (float*)smem;                 // [64][4][KMAX]
+    int* mi = (int*)(smem + MP * 4 * KMAX * 4);  // [64][4][KMAX]
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {
+        ms[(my_p * 4 + my_sub) * KMAX + q] = ls[q];
+        mi[(my_p * 4 + my_sub) * KMAX + q] = li[q];
+    }
+    __syncthreads();
+    if (my_sub == 0) {
+        for (int o = 1; o < 4; ++o)
+            for (int q = 0; q < KMAX; ++q)
+                topk_insert<KMAX>(ls, li, ms[(my_p * 4 + o) * KMAX + q], mi[(my_p * 4 + o) * KMAX + q]);
+        const int p = p0 + my_p;
+        if (p < B) {
+            for (int q = 0; q < k; ++q) {
+                const size_t o = ((size_t)p * n_split + split) * k + q;
+                const bool valid = li[q] != INT_MAX;
+                cs[o] = valid ? ls[q] : -INFINITY;
+                ci[o] = valid ? li[q] : -1;
+            }
+        }
+    }
+}
+
 // One wave per probe: lanes insert strided candidates into local lists, then k rounds of a
 // wave-wide (score desc, index asc) argmax pop.
 template <int KMAX>
@@ -201,6 +389,40 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
 
 }  // namespace
 
+static bool p512_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_MATCH_P512");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Split plan of the exact match.  match_p512_kernel (D = 512, k <= 8) keeps a wave's probes in registers,
+// so a split should span several 64-row tiles: choose the tiles per split r minimising (rounds of 256
+// resident blocks) x r, ties to the larger r (fewer candidate lists for the merge); e.g. 256 x 10k: 3
+// tiles per split, 212 blocks (one per CU) instead of 628 one-tile blocks.
+void match_split_plan(int B, int64_t N, int D, int k, int* n_split, int64_t* rows_per_split) {
+    if (D == D512 && k <= 8 && p512_enabled() && B > 0 && N > 0) {
+        const int64_t pb = (B + MP - 1) / MP, T = (N + MG - 1) / MG;
+        int64_t best_r = 1;
+        double best = 1e30;
+        static const int env_r = [] {
+            const char* e = getenv("FR_MATCH_TILES");  // experiments: tiles per split
+            return e ? atoi(e) : 0;
+        }();
+        for (int64_t r = 1; r <= T && r <= 64; ++r) {
+            if (env_r > 0 && r != std::min<int64_t>(env_r, std::min<int64_t>(T, 64))) continue;
+            const int64_t blocks = pb * ((T + r - 1) / r);
+            const double cost = (double)((blocks + 255) / 256) * r + 0.02 * (double)((T + r - 1) / r);
+            if (cost <= best) { best = cost; best_r = r; }
+        }
+        *rows_per_split = best_r * MG;
+        *n_split = (int)((T + best_r - 1) / best_r);
+        return;
+    }
+    match_split_plan(B, N, n_split, rows_per_split);
+}
+
 void match_split_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split) {
     const int pt = (B + MP - 1) / MP;
 #ifndef FR_MATCH_BLOCKS
@@ -220,6 +442,18 @@ void match_split_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split) {
 hipError_t launch_match_topk(const float* P, int B, const float* G, int64_t N, int D, int k, int64_t index_base,
                              float* cand_s, int32_t* cand_i, int n_split, int64_t rows_per_split, hipStream_t s) {
     dim3 grid((B + MP - 1) / MP, n_split);
+    if (D == D512 && p512_enabled() && B > 0 && k <= 8) {  // (16-deep lists would spill next to the register probes)
+        if (rows_per_split > 64 * MG) return hipErrorInvalidValue;  // the plan's bound (32-bit DMA offsets)
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)match_p512_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      P512_LDS);
+            attr = true;
+        }
+        hipLaunchKernelGGL(match_p512_kernel<8>, grid, dim3(256), P512_LDS, s, P, B, G, N, k, index_base,
+                           rows_per_split, n_split, cand_s, cand_i);
+        return hipGetLastError();
+    }
     if (k <= 8)
         hipLaunchKernelGGL(match_partial_kernel<8>, grid, dim3(256), 0, s, P, B, G, N, D, k, index_base,
                            rows_per_split, n_split, cand_s, cand_i);
