@@ -32,22 +32,23 @@ __device__ __forceinline__ bool better(float s1, int i1, float s2, int i2) {
     return s1 > s2 || (s1 == s2 && i1 < i2);
 }
 
+// Insert (s, idx) into a list sorted by better(): branch-free.  b[q] = the candidate beats entry q is
+// monotone in q, so entry q becomes entry q-1 (b[q-1]), the candidate (first b), or stays.  (A swap chain
+// compiled to a full list copy per step behind branches: the top-k filter then cost more than the MFMAs.)
 template <int KMAX>
 __device__ __forceinline__ void topk_insert(float (&ls)[KMAX], int (&li)[KMAX], float s, int idx) {
-    if (!better(s, idx, ls[KMAX - 1], li[KMAX - 1])) return;
-    float cs = s;
-    int ci = idx;
+    bool b[KMAX];
 #pragma unroll
-    for (int q = 0; q < KMAX; ++q) {
-        if (better(cs, ci, ls[q], li[q])) {
-            const float ts = ls[q];
-            const int ti = li[q];
-            ls[q] = cs;
-            li[q] = ci;
-            cs = ts;
-            ci = ti;
-        }
+    for (int q = 0; q < KMAX; ++q) b[q] = better(s, idx, ls[q], li[q]);
+#pragma unroll
+    for (int q = KMAX - 1; q > 0; --q) {
+        const float sh = b[q - 1] ? ls[q - 1] : s;
+        const int ih = b[q - 1] ? li[q - 1] : idx;
+        ls[q] = b[q] ? sh : ls[q];
+        li[q] = b[q] ? ih : li[q];
     }
+    ls[0] = b[0] ? s : ls[0];
+    li[0] = b[0] ? idx : li[0];
 }
 
 template <int KMAX>
@@ -301,20 +302,20 @@ __global__ __launch_bounds__(256, 1) void match_p512_kernel(const float* __restr
                 sS[(16 * wave + 4 * (lane >> 4) + r) * (MG + 1) + 16 * j + (lane & 15)] = acc[j][r];
         lds_barrier();
         if (!(FR_MATCH_EXP & 2)) {
+            // filter against the lane's current last entry (no branches: all 16 scores read, 32-bit
+            // indices), then the few inserts
             const float thr = ls[KMAX - 1];
             const int thri = li[KMAX - 1];
+            const int ibase = (int)(t0 + index_base) + my_sub * 16;
+            const int lim = (int)min((int64_t)MG, g_end - t0) - my_sub * 16;
+            const float* row = sS + my_p * (MG + 1) + my_sub * 16;
             uint32_t mask = 0;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int g = my_sub * 16 + i;
-                if (t0 + g < g_end && better(sS[my_p * (MG + 1) + g], (int)(t0 + g + index_base), thr, thri))
-                    mask |= 1u << i;
-            }
+            for (int i = 0; i < 16; ++i) mask |= (((i < lim) & better(row[i], ibase + i, thr, thri)) ? 1u : 0u) << i;
             while (mask) {
                 const int i = __builtin_ctz(mask);
                 mask &= mask - 1;
-                const int g = my_sub * 16 + i;
-                topk_insert<KMAX>(ls, li, sS[my_p * (MG + 1) + g], (int)(t0 + g + index_base));
+                topk_insert<KMAX>(ls, li, row[i], ibase + i);
             }
         }
     }
