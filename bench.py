@@ -35,9 +35,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "aligned faces/sec (embed+match) ArcFace@112 bs=256, 1/2/4/8 MI355X"
 GFLOP_PER_FACE = {"iresnet100": 24.179, "resnet50_arcface": 2.154, "irv1_facenet": 2.835}
-BF16_DENSE_PEAK_TFLOPS = 2500.0
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
 FP8_DENSE_PEAK_TFLOPS = 5000.0  # MI355X_MICROARCH.md: ~5 PF dense fp8 (block-scaled f8f6f4 MFMA)
-PROF_STRIDE = 8  # roofline: sample every 8th dominant-kernel launch (event overhead ~0.5 % instead of ~4 %)     # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec (about 6.3 TB/s achievable)
+PROF_STRIDE = 8  # roofline: sample every 8th dominant-kernel launch (event overhead ~0.5 % instead of ~4 %)
 
 
 def pmc_traffic(kernel, args):
@@ -315,7 +316,7 @@ def main():
         # launch (2*M*N*K of the conv it computes) / its mean launch duration (HIP events on the
         # stream it is launched on, over the timed steps)
         name = dominant
-        ms, launches, flops = kclasses[name]
+        ms, launches, flops, _ = kclasses[name]
         achieved = flops / (ms * 1e-3) / 1e12
         peak = FP8_DENSE_PEAK_TFLOPS if name.startswith("conv_fp8") else BF16_DENSE_PEAK_TFLOPS
         result["roofline"] = {
@@ -324,10 +325,21 @@ def main():
             "traffic": pmc_traffic(name, args), "sampled_launches": launches, "sample_stride": PROF_STRIDE,
             "us_per_launch": round(ms / launches * 1e3, 2), "gflop_per_launch": round(flops / launches / 1e9, 3),
             "share_of_forward": round(kclasses_all[name][0] / 2 / embed_ms, 4)}
-        # per-class breakdown from the untimed all-launch pass (2 steps)
-        result["kernels"] = {k: {"ms_per_step": round(v[0] / 2, 4), "launches": v[1] // 2,
-                                 "tflops": round(v[2] / (v[0] * 1e-3) / 1e12, 1) if v[2] else None}
-                             for k, v in sorted(kclasses_all.items(), key=lambda kv: -kv[1][0])}
+        # per-class breakdown from the untimed all-launch pass (2 steps), each class against both
+        # rooflines: MFMA (algorithmic FLOPs / time / dense peak) and HBM (algorithmic bytes -- every
+        # input, weight and output byte once -- / time / 8 TB/s); "bound" is the nearer one
+        def cls_entry(name, v):
+            ms, launches, fl, by = v
+            peak = FP8_DENSE_PEAK_TFLOPS if name.startswith("conv_fp8") else BF16_DENSE_PEAK_TFLOPS
+            tf = fl / (ms * 1e-3) / 1e12 if fl else None
+            gbs = by / (ms * 1e-3) / 1e9 if by else None
+            mf = tf / peak if tf else 0.0
+            hf = gbs / HBM_PEAK_GBPS if gbs else 0.0
+            return {"ms_per_step": round(ms / 2, 4), "launches": launches // 2,
+                    "tflops": round(tf, 1) if tf else None, "mfma_frac": round(mf, 3),
+                    "gbps": round(gbs, 1) if gbs else None, "hbm_frac": round(hf, 3),
+                    "bound": "mfma" if mf >= hf else "hbm"}
+        result["kernels"] = {k: cls_entry(k, v) for k, v in sorted(kclasses_all.items(), key=lambda kv: -kv[1][0])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.arch, args.cpu_seconds)
     if rank == 0:

@@ -86,6 +86,7 @@ _SIGS = {
     "fr_prof_only": (c_int, [c_void_p, ctypes.c_char_p]),
     "fr_prof_get": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t, ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
+    "fr_prof_get_bytes": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_double)]),
     "fr_debug_tensor_name": (ctypes.c_char_p, [c_void_p, c_int]),
     "fr_debug_tensor_shape": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                       ctypes.POINTER(c_int)]),
@@ -121,6 +122,8 @@ def lib() -> ctypes.CDLL:
                                    f"g.build()'` or `make -C facerecognition_amd/csrc`)")
             L = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in _SIGS.items():
+                if name in _OPTIONAL and not hasattr(L, name):
+                    continue  # an older experiment build (FR_LIBFRHIP) without this reporting entry point
                 f = getattr(L, name)
                 f.restype = res
                 f.argtypes = args
@@ -144,15 +147,20 @@ def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_OPTIONAL = {"fr_prof_get_bytes"}  # reporting only: may be absent from older variant builds
+
+
 def prof_read(handle):
-    """fr_prof_collect + fr_prof_get for every class → {name: (total_ms, launches, flops)}."""
+    """fr_prof_collect + fr_prof_get(_bytes) for every class → {name: (total_ms, launches, flops, bytes)}."""
     L = lib()
     n = L.fr_prof_collect(handle)
     check(n if n < 0 else 0, "fr_prof_collect")
     out = {}
     for i in range(n):
         name = ctypes.create_string_buffer(128)
-        ms, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        ms, cnt, fl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
         check(L.fr_prof_get(handle, i, name, 128, ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(fl)), "fr_prof_get")
-        out[name.value.decode()] = (ms.value, cnt.value, fl.value)
+        if hasattr(L, "fr_prof_get_bytes"):
+            check(L.fr_prof_get_bytes(handle, i, ctypes.byref(by)), "fr_prof_get_bytes")
+        out[name.value.decode()] = (ms.value, cnt.value, fl.value, by.value)
     return out

@@ -250,6 +250,11 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
 
     const bool has_up = part > 0, has_dn = part < PARTS - 1;
     int* const my_flag = p.flags + b * PARTS + part;
+    // Progress counters are never reset: each launch counts on from the value its own counter holds at
+    // the start (f0: only this workgroup writes it, and every part of an image has run the same convs in
+    // every launch of this stage), so no memset has to precede the launch.  A neighbour's counter
+    // reaching f0 + cv + 1 means its conv cv rows are published.
+    const int f0 = __hip_atomic_load(my_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const __amdgpu_buffer_rsrc_t xr_x = __builtin_amdgcn_make_buffer_rsrc(
         (void*)p.xchg, 0, (uint32_t)min((size_t)0x7fffffff, xchg_elems<G>(p.B) * 2), 0x00020000);
     // element offset of row `which` of part `pt`, parity `par`
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         if (wave == 0 && lane < 2 && !(FR_SPLIT_EXP & 1) && (lane == 0 ? has_up : has_dn)) {
             const int* nf = my_flag + (lane == 0 ? -1 : 1);
             int it = 0;
-            while (__hip_atomic_load(nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cv + 1) {
+            while ((int)((unsigned)__hip_atomic_load(nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (unsigned)f0) < cv + 1) {
                 if (++it == SPIN_LIMIT) {
                     __hip_atomic_fetch_add(p.spin_timeouts, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
@@ -431,7 +436,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (threadIdx.x == 0 && !(FR_SPLIT_EXP & 1))
-                __hip_atomic_store(my_flag, cv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(my_flag, (int)((unsigned)f0 + (unsigned)(cv + 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             pending = cv;
         }
     };
@@ -451,8 +456,7 @@ hipError_t launch_split_t(const StageArgs& a, hipStream_t s) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         attr[a.f16 ? 1 : 0] = true;
     }
-    hipError_t e = hipMemsetAsync(a.flags, 0, (size_t)G::PARTS * a.B * sizeof(int), s);
-    if (e != hipSuccess) return e;
+    // (no flag reset: the counters run on across launches, see f0 in the kernel)
     const dim3 grid((a.B + 7) / 8 * 8 * G::PARTS);
     if (a.ev0)
         hipExtLaunchKernelGGL(k, grid, dim3(64 * NW), G::LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);

@@ -95,6 +95,8 @@ struct StageRec {
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
+constexpr size_t FR_MAX_SPLIT_STAGES = 4;  // stage ops per plan (at most one per residual layer)
+
 }  // namespace
 
 struct fr_handle {
@@ -124,8 +126,8 @@ struct fr_handle {
     int32_t* cand_i = nullptr;
     size_t cand_cap = 0;
     // per-kernel-class event timing (fr_prof_*): events recorded on the launching stream
-    struct ProfRec { std::string cls; hipEvent_t a, b; double flops; };
-    struct ProfAcc { double ms = 0; int64_t launches = 0; double flops = 0; };
+    struct ProfRec { std::string cls; hipEvent_t a, b; double flops, bytes; };
+    struct ProfAcc { double ms = 0; int64_t launches = 0; double flops = 0, bytes = 0; };
     bool prof = false;
     int prof_stride = 1;        // time every n-th matching launch (sampling keeps the overhead small)
     uint64_t prof_seen = 0;
@@ -154,7 +156,7 @@ struct fr_handle {
     float* emb_pre = nullptr;  // [max_batch][512] IRV1 output before the projection
     float* amax = nullptr;     // FR_DTYPE_FP8: per-tensor max |x| of the current forward [ntensors]
     bf16_t* stage_xchg = nullptr;  // split-stage boundary rows (split_stage_xchg_elems(max_batch), reserve)
-    int* stage_flags = nullptr;    // split-stage per-part progress counters [max_batch][4]
+    int* stage_flags = nullptr;    // split-stage progress counters [stage][max_batch][4], never reset
     int* stage_spin = nullptr;     // split-stage bounded-wait overruns (fr_debug_stage_timeouts)
     int stage_mode = 1;       // FR_OPT_STAGE: 0 off, 1 auto (stage_runs), 2 always
     int stage_min_fill = 80;  // FR_OPT_STAGE_MIN_FILL (percent)
@@ -957,14 +959,18 @@ int reserve(fr_handle* h, int maxB) {
         h->emb_pre = (float*)q;
     }
     if (std::any_of(h->stages.begin(), h->stages.end(), [](const StageRec& r) { return r.parts > 1; })) {
+        if (h->stages.size() > FR_MAX_SPLIT_STAGES) { set_error("reserve: too many stage ops"); return FR_ERR_ARG; }
         void* q = nullptr;
         rc = dev_alloc(&q, split_stage_xchg_elems(maxB) * sizeof(bf16_t));
         if (rc) { free_acts(h); return rc; }
         h->act_allocs.push_back(q);
         h->stage_xchg = (bf16_t*)q;
-        rc = dev_alloc(&q, (size_t)maxB * 4 * sizeof(int));
+        // one counter region per split stage ([maxB][4] each: the counters run on across launches, so
+        // two stages with different part counts must not share slots); zeroed once here
+        rc = dev_alloc(&q, (size_t)maxB * 4 * FR_MAX_SPLIT_STAGES * sizeof(int));
         if (rc) { free_acts(h); return rc; }
         h->act_allocs.push_back(q);
+        FR_HIP_CHECK(hipMemset(q, 0, (size_t)maxB * 4 * FR_MAX_SPLIT_STAGES * sizeof(int)));
         h->stage_flags = (int*)q;
     }
     return fill_stage_dbg(h);
@@ -1039,7 +1045,7 @@ hipEvent_t prof_event(fr_handle* h) {
 // the totals line up with rocprofv3's per-kernel rows.
 struct ProfScope {
     fr_handle* h; hipStream_t s; hipEvent_t a = nullptr, b = nullptr; bool stamped = false;
-    std::string cls; double flops = 0;
+    std::string cls; double flops = 0, bytes = 0;  // algorithmic FLOPs and HBM bytes of the launch
     ProfScope(fr_handle* h_, hipStream_t s_) : h(h_), s(s_) {}
     // Call right before the launch once the class is known.  With `ka` the pair is handed to the
     // conv launcher, which stamps it from the dispatch packet (hipExtLaunchKernel: no extra stream
@@ -1057,11 +1063,24 @@ struct ProfScope {
     ~ProfScope() {
         if (!a) return;
         if (!stamped) (void)hipEventRecord(b, s);
-        h->prof_pending.push_back({cls, a, b, flops});
+        h->prof_pending.push_back({cls, a, b, flops, bytes});
     }
 };
 
 double conv_flops(const ConvArgs& a) { return 2.0 * (double)a.M * a.Cout * ((double)a.Cin * a.Kh * a.Kw + (a.x2 ? a.C2 : 0)); }
+
+// Algorithmic HBM bytes of a conv launch: its input channels once (all input pixels), the projection
+// input at the output's stride, the residual, the output and the weights once (activations 2 B; fp8
+// weights 1 B).  Re-reads through L2 / MALL are not counted: this is the roofline's traffic floor.
+double conv_bytes(const ConvArgs& a) {
+    const double act = 2.0;
+    double b = (double)a.B * a.H * a.W * a.Cin * act;
+    if (a.x2) b += (double)a.M * a.C2 * act;
+    if (a.res) b += (double)a.M * a.Cout * act;
+    b += (double)a.M * a.Cout * act * (a.y2 ? 2.0 : 1.0);
+    b += (double)a.Cout * ((double)a.Cin * a.Kh * a.Kw + (a.x2 ? a.C2 : 0)) * (a.w8 ? 1.0 : 2.0);
+    return b;
+}
 
 bool autotune_enabled() {
     static const bool on = [] {
@@ -1142,6 +1161,7 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     a.dbg = conv_dbg();
     ProfScope ps(h, s);
     ps.flops = conv_flops(a);
+    ps.bytes = conv_bytes(a);
     if (a.w8) {  // FR_DTYPE_FP8 conv (conv_fp8.hip)
         a.tile = conv_fp8_tile(a.M, a.Cout);
         a.split_k = 1;
@@ -1259,10 +1279,11 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.f16 = f16;
                 a.dbg = stage_dbg();
                 a.xchg = h->stage_xchg;
-                a.flags = h->stage_flags;
+                a.flags = h->stage_flags + (size_t)h->max_batch * 4 * op.stage;  // the stage's own counter region
                 a.spin_timeouts = h->stage_spin;
                 ProfScope ps(h, s);
                 ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
+                ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * 2.0;
                 ps.start(r.H == 14 ? "stage layer3" : (r.H == 28 ? "stage layer2" : "stage layer1"));
                 FR_HIP_CHECK(r.parts > 1 ? launch_split_stage(a, r.H, r.C, s) : launch_stage(a, s));
                 break;
@@ -1279,6 +1300,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                     if (stem_u8_supported(to.H, to.W, cv.cin, cw.K, cw.Kpad, cw.Cout, to.C, cv.out_off) && !cw.bias9 &&
                         cv.res < 0 && cv.out2 < 0 && cv.sh == 1 && cv.ph == 1 && cv.kh == 3 && cv.kw == 3) {
                         ps.flops = 2.0 * B * to.H * to.W * cw.Cout * 27.0;
+                        ps.bytes = (double)B * to.H * to.W * (3.0 + cw.Cout * 2.0);
                         ps.start("stem u8 fused");
                         FR_HIP_CHECK(launch_stem_u8((const uint8_t*)in, B, cw.w, cw.Kpad, cw.bias, cw.slope, cv.act,
                                                     to.dev, to.C, cv.out_off, f16, s));
@@ -1366,6 +1388,9 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.tile = tile;
                 a.split_k = split;
                 a.partial = h->partial;
+                // input, weights, the f32 split-K partials written and read back, the f32 embeddings
+                ps.bytes = (double)B * cw.K * 2.0 + (double)cw.K * cw.Cout * 2.0 + 2.0 * split * B * cw.Npad * 4.0 +
+                           (double)B * cw.Cout * 4.0;
                 FR_HIP_CHECK(launch_conv(a, s));
                 if (h->proj_d) {  // IRV1 L2 (always: InceptionResnetV1 classify=False) -> projection -> L2
                     FR_HIP_CHECK(launch_head_finalize(h->partial, split, B, cw.Cout, cw.Npad, cw.bias, 1, h->emb_pre, s));
@@ -1832,6 +1857,7 @@ int fr_prof_collect(fr_handle* h) {
         acc.ms += ms;
         acc.launches += 1;
         acc.flops += r.flops;
+        acc.bytes += r.bytes;
         h->ev_free.push_back(r.a);
         h->ev_free.push_back(r.b);
     }
@@ -1847,6 +1873,12 @@ int fr_prof_get(const fr_handle* h, int i, char* name, size_t n, double* total_m
     if (total_ms) *total_ms = e.second.ms;
     if (launches) *launches = e.second.launches;
     if (flops) *flops = e.second.flops;
+    return FR_OK;
+}
+
+int fr_prof_get_bytes(const fr_handle* h, int i, double* bytes) {
+    if (!h || i < 0 || i >= (int)h->prof_acc.size() || !bytes) { set_error("fr_prof_get_bytes: bad argument"); return FR_ERR_ARG; }
+    *bytes = h->prof_acc[i].second.bytes;
     return FR_OK;
 }
 

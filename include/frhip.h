@@ -263,6 +263,9 @@ int fr_prof_only(fr_handle* h, const char* kernel_class);
 int fr_prof_collect(fr_handle* h);
 int fr_prof_get(const fr_handle* h, int i, char* name, size_t n, double* total_ms, int64_t* launches,
                 double* flops);
+/* Algorithmic HBM bytes of class i over its timed launches (each input / weight / output byte once;
+ * re-reads through L2 and the Infinity Cache are not counted), for the class's HBM-roofline fraction. */
+int fr_prof_get_bytes(const fr_handle* h, int i, double* bytes);
 
 int fr_debug_tensor_count(const fr_handle* h);
 /* Text dump of the forward plan at batch B, one line per op:

@@ -348,6 +348,28 @@ def test_match_ties_lowest_index(gpu):
         assert s[r, 0] == s[r, 1] == s[r, 2]
 
 
+def test_match_ties_across_splits_multi_tile(gpu):
+    """The D = 512 register-probe kernel (several 64-row tiles per split, 4 sub-lists per probe) and the
+    merge keep the (score desc, index asc) order for exact ties spread over tiles and splits."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(21)
+    Ng = 20000
+    G = _norm(rng.standard_normal((Ng, 512)))
+    dup = [5, 4999, 10007, 15013, 19999]  # copies of row 5: other tiles, other splits, the last row
+    for r in dup[1:]:
+        G[r] = G[5]
+    P = _norm(rng.standard_normal((256, 512)))
+    P[:40] = _norm(G[5] + 0.02 * rng.standard_normal((40, 512)))
+    gal = DeviceGallery(G)
+    s, i = gal.search(P, 8)
+    rs, ri = _np_topk(P, G, 8)
+    for r in range(40):
+        assert list(i[r, :5]) == dup, i[r]
+        assert len(set(s[r, :5].tolist())) == 1
+    assert np.array_equal(i[:, 0], ri[:, 0])
+    assert np.allclose(s, rs, atol=1e-5)
+
+
 def test_match_unnormalized_rows_cosine(gpu):
     """cosine_similarity semantics: non-unit rows are divided by their norm, zero rows score 0."""
     from facerecognition_amd.gallery import DeviceGallery
