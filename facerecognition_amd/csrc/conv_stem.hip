@@ -40,7 +40,7 @@ constexpr int OFF_SWT = OFF_SY + SPIX * 8 * 16;               // 13312
 constexpr int OFF_SX = OFF_SWT + SCO * WROW * 2;              // 3648
 constexpr int OFF_SBS = OFF_SX + (SROWS + 2) * (SW + 2) * 8;  // 512
 constexpr int OFF_RAW = OFF_SBS + 2 * SCO * 4;                // 2048
-constexpr int STEM_LDS = OFF_RAW + 2 * 256 * 4;
+constexpr int STEM_LDS = OFF_RAW + 2 * 2 * 256 * 4;              // sraw: two tile buffers
 static_assert(OFF_SX % 16 == 0 && OFF_SBS % 16 == 0 && OFF_RAW % 16 == 0, "16-B aligned LDS arrays");
 
 // 4-byte LDS-DMA (buffer_load_dword ... lds; lane l lands at lds_addr + 4 l) issued from inline asm: the
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
     uint4* sy = (uint4*)(smem + OFF_SY);                                  // [SPIX * 8]
     uint16_t(*swt)[WROW] = (uint16_t(*)[WROW])(smem + OFF_SWT);          // [SCO][WROW] weight rows
     float(*sbs)[SCO] = (float(*)[SCO])(smem + OFF_SBS);                   // [2][SCO] bias, PReLU slope
-    uint32_t* sraw = (uint32_t*)(smem + OFF_RAW);                         // [2 * 256] u8 rows as dwords + pad
+    uint32_t* sraw = (uint32_t*)(smem + OFF_RAW);                         // [2][2 * 256] u8 rows as dwords + pad
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
     // the 64 x 96 weight rows, staged once per (persistent) block; the first tile's barrier after its
@@ -91,35 +91,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
         sbs[1][tid] = act == 2 ? slope[tid] : 0.f;
     }
 
-    // a tile's input rows r0-1 .. r0+2 (336 contiguous bytes each) as dwords, two per thread, loaded one
-    // tile ahead into registers so the HBM latency hides behind the previous tile's MFMA loop and stores
+    // a tile's input rows r0-1 .. r0+2 (336 contiguous bytes each) as dwords, two per thread
     constexpr int RAWD = (SROWS + 2) * (SW * 3 / 4);
     static_assert(RAWD <= 2 * 256, "two input dwords per thread");
-    // The rows go straight to LDS by LDS-DMA (4 B per lane, linear: dword e = tid + 256 j of sraw), branch
-    // free: rows outside the image and the pad dwords get an out-of-range offset, which reads 0.  The waits
-    // are explicit: at a tile's top the only VMEM operations issued after its DMA are the previous tile's
-    // 7 output stores, which stay in flight (vmcnt(7)).
+    // The rows go straight to LDS by LDS-DMA (4 B per lane, linear: dword e = tid + 256 j of the tile's
+    // sraw buffer), two tiles ahead (one DMA latency per tile, under write load, was most of a tile's
+    // time), branch free: rows outside the image, the pad dwords and tiles past the end get an
+    // out-of-range offset, which reads 0.  The waits are explicit (see the loop top).
     const uint64_t inp = (uint64_t)in;
     const v4i32 inr = {(int)(uint32_t)inp, (int)((inp >> 32) & 0xffff), (int)((ntiles / (SW / SROWS)) * (SW * SW * 3)),
                        0x00020000};
-    auto dma_raw = [&](int t) {
+    auto dma_raw = [&](int t, int buf) {
         const int b = t / (SW / SROWS), r0 = (t % (SW / SROWS)) * SROWS;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int e = tid + 256 * j, rr = e / (SW * 3 / 4), d = e % (SW * 3 / 4), ir = r0 - 1 + rr;
             const bool ok = e < RAWD && (unsigned)ir < (unsigned)SW;
             const uint32_t off = ok ? (uint32_t)(((b * SW + ir) * SW * 3) + 4 * d) : 0x80000000u;
-            dma_dword(inr, (uint32_t)(uintptr_t)&sraw[256 * j + 64 * wave], off);
+            dma_dword(inr, (uint32_t)(uintptr_t)&sraw[512 * buf + 256 * j + 64 * wave], off);
         }
     };
-    dma_raw(blockIdx.x);  // gridDim.x <= ntiles
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
+    dma_raw(blockIdx.x, 0);  // gridDim.x <= ntiles
+    dma_raw(blockIdx.x + gridDim.x, 1);
+    // the weight / table loads above went to registers first: done before the counted waits below
     // tiles t = blockIdx.x + j * gridDim.x; every wave runs the same trip count (block-uniform loop)
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    int j = 0;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x, ++j) {
         const int b = t / (SW / SROWS), r0 = (t % (SW / SROWS)) * SROWS;
+        const uint32_t* sr = sraw + 512 * (j & 1);
+        // this tile's DMA landed.  VMEM order: DMA 0, DMA 1, then per tile i: DMA i + 2 (2 ops), 7 stores;
+        // younger than DMA j: DMA 1 (j = 0); DMA 2 + stores 0 (j = 1); stores j-2, DMA j+1, stores j-1
+        if (j == 0) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if (j == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         // the previous tile's reads of sraw / sx / sy all precede a barrier every thread has passed
-        if (t != (int)blockIdx.x) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // this tile's DMA landed
         lds_barrier();
         // -> 2q - 255 in the activation dtype, zero halo columns (rows outside the image were zeroed above
         // but must also become 0, not -255)
@@ -127,7 +132,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
             const int rr = e / (SW + 2), cc = e % (SW + 2), ir = r0 - 1 + rr, ic = cc - 1;
             uint16_t v[3] = {0, 0, 0};
             if ((unsigned)ir < (unsigned)SW && (unsigned)ic < (unsigned)SW) {
-                const uint8_t* q = (const uint8_t*)&sraw[rr * (SW * 3 / 4)] + 3 * ic;
+                const uint8_t* q = (const uint8_t*)&sr[rr * (SW * 3 / 4)] + 3 * ic;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) v[c] = T::cvt(2.0f * (float)q[c] - 255.0f);
             }
@@ -168,7 +173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
                 for (int i = 0; i < 4; ++i) acc[u][i] = T::mfma(wa[i][ks], bq, acc[u][i]);
             }
         }
-        if (t + (int)gridDim.x < ntiles) dma_raw(t + gridDim.x);  // block-uniform; sraw's reads are behind barrier 2
+        dma_raw(t + 2 * gridDim.x, j & 1);  // unconditional (uniform wait counts); this buffer's reads are behind barrier 2
         // epilogue: lane holds channels 16i + 4(lane>>4) .. +3 of pixel 16f + (lane&15)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -206,6 +211,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
             *(uint4*)(y + (row0 + px) * Cy + y_off + 8 * ch) = sy[px * 8 + (ch ^ (px & 7))];
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (out-of-range) DMAs land before the LDS is released
 }
 
 }  // namespace
