@@ -22,6 +22,7 @@
 #include <hip/hip_ext.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace fr {
 namespace {
@@ -86,10 +87,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
     }
     // bias and slope in LDS too: global loads in the epilogue would make its vmcnt waits also wait for the
     // next tile's input prefetch (issued just before) and for nothing else
+    float sl_t = 1.f;
     if (tid < SCO) {
         sbs[0][tid] = bias[tid];
-        sbs[1][tid] = act == 2 ? slope[tid] : 0.f;
+        sbs[1][tid] = sl_t = act == 2 ? slope[tid] : 0.f;
     }
+    // PReLU as max(v, s v) when every slope is in (0, 1]: the same bits as v > 0 ? v : s v (for v > 0,
+    // s v <= v; for v <= 0, s v >= v; NaN stays NaN), one operation fewer per value
+    const bool slope01 = act == 2 && __syncthreads_and(tid >= SCO || (sl_t > 0.f && sl_t <= 1.f));
 
     // a tile's input rows r0-1 .. r0+2 (336 contiguous bytes each) as dwords, two per thread
     constexpr int RAWD = (SROWS + 2) * (SW * 3 / 4);
@@ -174,33 +179,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
             }
         }
         dma_raw(t + 2 * gridDim.x, j & 1);  // unconditional (uniform wait counts); this buffer's reads are behind barrier 2
-        // epilogue: lane holds channels 16i + 4(lane>>4) .. +3 of pixel 16f + (lane&15)
+        // epilogue: lane holds channels 16i + 4(lane>>4) .. +3 of pixel 16f + (lane&15).  One branch per
+        // tile picks the activation form (MODE 0: PReLU as max(v, s v); 1: PReLU by select; 2: ReLU;
+        // 3: none), so the unrolled (i, u) body is straight code
+        auto epilogue = [&](auto mode_tag) {
+            constexpr int MODE = decltype(mode_tag)::value;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int n = 16 * i + 4 * (lane >> 4);
-            const float4 bb = *(const float4*)&sbs[0][n];
-            const float4 sl = *(const float4*)&sbs[1][n];
+            for (int i = 0; i < 4; ++i) {
+                const int n = 16 * i + 4 * (lane >> 4);
+                const float4 bb = *(const float4*)&sbs[0][n];
+                const float4 sl = *(const float4*)&sbs[1][n];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int f = wave + 4 * u;
-                if (f >= SPIX / 16) break;
-                const int px = 16 * f + (lane & 15);
-                float v[8] = {acc[u][i][0] + bb.x, acc[u][i][1] + bb.y, acc[u][i][2] + bb.z, acc[u][i][3] + bb.w, 0, 0, 0, 0};
-                if (act == 2) {
-                    v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
-                    v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
-                    v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
-                    v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
-                } else if (act == 1) {
+                for (int u = 0; u < 4; ++u) {
+                    const int f = wave + 4 * u;
+                    if (f >= SPIX / 16) break;
+                    const int px = 16 * f + (lane & 15);
+                    // bias and slope products as packed pairs (v_pk_add_f32 / v_pk_mul_f32: the same IEEE
+                    // operations per element, half the instructions; the epilogue is most of the VALU)
+                    typedef float f2 __attribute__((ext_vector_type(2)));
+                    const f2 v01 = (f2){acc[u][i][0], acc[u][i][1]} + (f2){bb.x, bb.y};
+                    const f2 v23 = (f2){acc[u][i][2], acc[u][i][3]} + (f2){bb.z, bb.w};
+                    float v[8] = {v01.x, v01.y, v23.x, v23.y, 0, 0, 0, 0};
+                    if (MODE == 0) {
+                        const f2 p01 = v01 * (f2){sl.x, sl.y}, p23 = v23 * (f2){sl.z, sl.w};
+                        // v_max_f32 directly: fmaxf would first canonicalize both operands (two more
+                        // instructions each); these operands are arithmetic results, never signalling NaNs
+                        asm("v_max_f32 %0, %1, %2" : "=v"(v[0]) : "v"(v01.x), "v"(p01.x));
+                        asm("v_max_f32 %0, %1, %2" : "=v"(v[1]) : "v"(v01.y), "v"(p01.y));
+                        asm("v_max_f32 %0, %1, %2" : "=v"(v[2]) : "v"(v23.x), "v"(p23.x));
+                        asm("v_max_f32 %0, %1, %2" : "=v"(v[3]) : "v"(v23.y), "v"(p23.y));
+                    } else if (MODE == 1) {
+                        v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
+                        v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
+                        v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
+                        v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
+                    } else if (MODE == 2) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                    }
+                    const uint4 pk = T::pack8(v);
+                    // 16-B chunk n/8 of the pixel's 128-B row, XOR-swizzled by pixel; this lane owns half of it
+                    char* dst = (char*)&sy[px * 8 + ((n >> 3) ^ (px & 7))] + (n & 4) * 2;
+                    *(uint2*)dst = make_uint2(pk.x, pk.y);
                 }
-                const uint4 pk = T::pack8(v);
-                // 16-B chunk n/8 of the pixel's 128-B row, XOR-swizzled by pixel; this lane owns half of it
-                char* dst = (char*)&sy[px * 8 + ((n >> 3) ^ (px & 7))] + (n & 4) * 2;
-                *(uint2*)dst = make_uint2(pk.x, pk.y);
             }
-        }
+        };
+        if (slope01) epilogue(std::integral_constant<int, 0>{});
+        else if (act == 2) epilogue(std::integral_constant<int, 1>{});
+        else if (act == 1) epilogue(std::integral_constant<int, 2>{});
+        else epilogue(std::integral_constant<int, 3>{});
         lds_barrier();
         // coalesced stores: 224 pixels x 8 chunks of 16 B
         const size_t row0 = ((size_t)b * SW + r0) * SW;
