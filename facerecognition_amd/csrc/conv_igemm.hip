@@ -589,19 +589,17 @@ void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
 // at bs = 256, 43 us); splits that divide the K-steps evenly, >= 4 K-steps each.  FR_HEAD_PLAN=tile,split
 // overrides (experiments).
 void head_plan(int M, int Cout, int Kpad, int* tile, int* split) {
-    static const int env[2] = {-1, -1};
-    static const bool has_env = [] {
-        const char* e = getenv("FR_HEAD_PLAN");
-        if (!e) return false;
+    struct EnvPlan { int tile = -1, split = -1; };
+    static const EnvPlan env = [] {
+        EnvPlan e;
+        const char* v = getenv("FR_HEAD_PLAN");
         int t = -1, sp = -1;
-        if (sscanf(e, "%d,%d", &t, &sp) != 2 || t < 0 || sp < 1) return false;
-        const_cast<int*>(env)[0] = t;
-        const_cast<int*>(env)[1] = sp;
-        return true;
+        if (v && sscanf(v, "%d,%d", &t, &sp) == 2 && t >= 0 && sp >= 1) { e.tile = t; e.split = sp; }
+        return e;
     }();
-    if (has_env) {
-        *tile = env[0];
-        *split = env[1];
+    if (env.tile >= 0) {
+        *tile = env.tile;
+        *split = env.split;
         return;
     }
     const int nkt = Kpad / BK;
