@@ -302,10 +302,17 @@ __global__ __launch_bounds__(256, 1) void match_p512_kernel(const float* __restr
                 sS[(16 * wave + 4 * (lane >> 4) + r) * (MG + 1) + 16 * j + (lane & 15)] = acc[j][r];
         lds_barrier();
         if (!(FR_MATCH_EXP & 2)) {
-            // filter against the lane's current last entry (no branches: all 16 scores read, 32-bit
-            // indices), then the few inserts
-            const float thr = ls[KMAX - 1];
-            const int thri = li[KMAX - 1];
+            // filter (no branches: all 16 scores read, 32-bit indices), then the few inserts.  Threshold:
+            // the best of the probe's 4 sub-lists' last entries (lanes 4p .. 4p+3): that sub-list holds
+            // KMAX >= k entries at least that good, so nothing worse can reach the split's top k
+            float thr = ls[KMAX - 1];
+            int thri = li[KMAX - 1];
+#pragma unroll
+            for (int o = 1; o <= 2; o <<= 1) {
+                const float os = __shfl_xor(thr, o);
+                const int oi = __shfl_xor(thri, o);
+                if (better(os, oi, thr, thri)) { thr = os; thri = oi; }
+            }
             const int ibase = (int)(t0 + index_base) + my_sub * 16;
             const int lim = (int)min((int64_t)MG, g_end - t0) - my_sub * 16;
             const float* row = sS + my_p * (MG + 1) + my_sub * 16;
@@ -445,14 +452,15 @@ hipError_t launch_match_topk(const float* P, int B, const float* G, int64_t N, i
     dim3 grid((B + MP - 1) / MP, n_split);
     if (D == D512 && p512_enabled() && B > 0 && k <= 8) {  // (16-deep lists would spill next to the register probes)
         if (rows_per_split > 64 * MG) return hipErrorInvalidValue;  // the plan's bound (32-bit DMA offsets)
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)match_p512_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      P512_LDS);
-            attr = true;
+        // lists exactly as deep as needed for the usual k <= 5 (top-5 is the reference's default)
+        auto kern = k <= 5 ? match_p512_kernel<5> : match_p512_kernel<8>;
+        static bool attr[2] = {false, false};
+        if (!attr[k <= 5]) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, P512_LDS);
+            attr[k <= 5] = true;
         }
-        hipLaunchKernelGGL(match_p512_kernel<8>, grid, dim3(256), P512_LDS, s, P, B, G, N, k, index_base,
-                           rows_per_split, n_split, cand_s, cand_i);
+        hipLaunchKernelGGL(kern, grid, dim3(256), P512_LDS, s, P, B, G, N, k, index_base, rows_per_split, n_split,
+                           cand_s, cand_i);
         return hipGetLastError();
     }
     if (k <= 8)
