@@ -368,9 +368,23 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
 #pragma unroll
     for (int q = 0; q < KMAX; ++q) { ls[q] = -INFINITY; li[q] = INT_MAX; }
     const int n = n_lists * k;
-    for (int c = lane; c < n; c += 64) {
-        const int idx = ci[(size_t)p * n + c];
-        if (idx >= 0) topk_insert<KMAX>(ls, li, cs[(size_t)p * n + c], idx);
+    // 8 candidates per lane in flight per round (their loads issued together, then the inserts): one
+    // load at a time exposed the L2 latency per candidate
+    const float* ps = cs + (size_t)p * n;
+    const int32_t* pi = ci + (size_t)p * n;
+    for (int c0 = 0; c0 < n; c0 += 64 * 8) {
+        float sv[8];
+        int iv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int c = c0 + 64 * u + lane;
+            const bool ok = c < n;
+            sv[u] = ok ? ps[c] : -INFINITY;
+            iv[u] = ok ? pi[c] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (iv[u] >= 0) topk_insert<KMAX>(ls, li, sv[u], iv[u]);
     }
     int head = 0;
     for (int q = 0; q < k; ++q) {
