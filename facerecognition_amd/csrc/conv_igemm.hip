@@ -539,7 +539,8 @@ bool conv_tile_forced() { return env_tile_id() >= 0; }
 
 // Tiles worth timing for a conv with Cout output channels (the autotuner's candidate set).
 int conv_tile_candidates(int Cout, int* out) {
-    static const int tiles[] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128, TILE_256x128, TILE_128x256};
+    static const int tiles[] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128, TILE_256x128, TILE_128x256,
+                                TILE_128x64_S3, TILE_64x128_S3};  // 3-stage LDS rings of the small tiles too
     int n = 0;
     for (int t : tiles) {
         const int BN = conv_tile_bn(t);
@@ -556,7 +557,8 @@ void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
                                 TILE_128x256, TILE_128x64_S3, TILE_64x128_S3};
     // relative MFMA efficiency per tile, calibrated on the IResNet100 bs=256 per-layer sweep
     // (tools/tile_sweep.sh, profiles/r01_tile_sweep.txt); the 3-stage 128x128 ring is the slowest
-    // (0 = only when forced: not yet calibrated)
+    // (0 = not in the cost model; the autotuner, tune_conv, still times the 3-stage 128x64 / 64x128
+    // tiles: layer1.0's stride-2 transition runs 161 -> 152 us on the 3-stage 128x64)
     static const double eff[] = {1.0, 0.93, 0.92, 0.9, 0.7, 0.9, 0.92, 0.0, 0.0};
     constexpr int NV = sizeof(tiles) / sizeof(tiles[0]);
     const int nkt = Kpad / BK;
