@@ -587,8 +587,8 @@ void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
 }
 
 // The embedding head (M = batch, N = 512, K = 25,088 at 7x7x512): a few output tiles over a very long K, so
-// split-K wide enough to give every CU two blocks (conv_plan stops at 16 splits: 256 blocks of 24 K-steps
-// at bs = 256, 43 us); splits that divide the K-steps evenly, >= 4 K-steps each.  FR_HEAD_PLAN=tile,split
+// split-K wide enough to give every CU a block (conv_plan stopped at 16 splits of the 2-stage tile: 256 blocks
+// of 24 K-steps at bs = 256, 43 us); splits that divide the K-steps evenly, >= 4 K-steps each.  FR_HEAD_PLAN=tile,split
 // overrides (experiments).
 void head_plan(int M, int Cout, int Kpad, int* tile, int* split) {
     struct EnvPlan { int tile = -1, split = -1; };
@@ -604,19 +604,21 @@ void head_plan(int M, int Cout, int Kpad, int* tile, int* split) {
         *split = env.split;
         return;
     }
+    // 3-stage 128x64 tiles, at most one block per CU (tools/head_sweep.sh at bs = 256: 14 splits 28.8 us,
+    // the 2-stage tile with 28 splits 31.3 us, 56 splits 37 us)
     const int nkt = Kpad / BK;
     const long tiles = (long)((M + 127) / 128) * ((Cout + 63) / 64);
     int best = 1;
     for (int sp = 1; sp <= nkt / 4; ++sp) {
         if (nkt % sp) continue;
-        if (tiles * sp > 512) break;
+        if (tiles * sp > 256) break;
         best = sp;
     }
     if (best == 1) {  // no even split: fall back to the generic plan
         conv_plan(M, Cout, Kpad, tile, split);
         return;
     }
-    *tile = TILE_128x64;
+    *tile = TILE_128x64_S3;
     *split = best;
 }
 
