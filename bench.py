@@ -41,22 +41,55 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec (about 6.3 TB/s
 PROF_STRIDE = 8  # roofline: sample every 8th dominant-kernel launch (event overhead ~0.5 % instead of ~4 %)
 
 
-def pmc_traffic(kernel, args):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py:
-    FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE, separate --pmc passes of this same
-    command), or None when no summary for this workload exists."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
-        try:
-            with open(path) as f:
-                d = json.load(f)
-        except (OSError, ValueError):
-            continue
-        if d.get("arch") == args.arch and d.get("dtype") == args.dtype and d.get("batch") == args.batch:
-            k = d.get("kernels", {}).get(kernel)
-            if k:
-                return k["hbm_bytes_per_launch"]
-    return None
+# bench kernel class (fr_prof_get name prefix) -> rocprofv3 kernel-name fragment of its dispatches
+CLASS_KERNEL = [("stage layer3", "stage_kernel<"), ("stage layer2", "SplitGeo<28,"), ("stage layer1", "SplitGeo<56,"),
+                ("conv_wring", "conv_wring_kernel<"), ("stem u8 fused", "stem_u8_kernel<"),
+                ("conv3x3_rows", "conv_rows_kernel<"), ("conv_fp8", "conv_fp8_kernel<"),
+                ("stage8 layer3", "stage8_kernel<")]
+
+
+def pmc_passes(args):
+    """HBM traffic of THIS build, measured live: two separate rocprofv3 --pmc passes (FETCH_SIZE, then
+    WRITE_SIZE; never combined with a tracing domain) over a short child run of this same bench
+    configuration, started before this process touches the GPU.  Returns ({rocprof kernel name:
+    (fetch bytes, write bytes, dispatches)}, None) or (None, reason).  Corrections per
+    MI355X_MICROARCH.md's HBM section: both counters are in KiB and FETCH_SIZE counts half the bytes
+    of 16-B/lane streaming reads on gfx950 (doubled here)."""
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import per_kernel
+    if not shutil.which("rocprofv3"):
+        return None, "rocprofv3 not on PATH"
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+             "--no-prof", "--no-pmc", "--arch", args.arch, "--batch", str(args.batch), "--k", str(args.k)]
+    if args.dtype:
+        child += ["--dtype", args.dtype]
+    if args.gallery_rows:
+        child += ["--gallery-rows", str(args.gallery_rows)]
+    out = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            print(f"[bench] rocprofv3 --pmc {counter} pass", file=sys.stderr, flush=True)
+            cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", counter, "--output-format", "csv",
+                   "-d", os.path.join(d, counter), "-o", "run", "--"] + child
+            r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, text=True)
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {counter} pass failed (rc {r.returncode}): {r.stderr[-300:]}"
+            out[counter] = per_kernel(os.path.join(d, counter), counter)
+    f, w = out["FETCH_SIZE"], out["WRITE_SIZE"]
+    return {k: (2 * 1024 * f[k][0], 1024 * w[k][0], f[k][1]) for k in f if k in w and f[k][1] == w[k][1]}, None
+
+
+def class_traffic(cls, pmc):
+    """HBM bytes per launch of bench kernel class `cls` from pmc_passes' per-kernel totals."""
+    frag = next((k for c, k in CLASS_KERNEL if cls.startswith(c)), None)
+    if frag is None or not pmc:
+        return None
+    ks = [k for k in pmc if frag in k]
+    n = sum(pmc[k][2] for k in ks)
+    return round(sum(pmc[k][0] + pmc[k][1] for k in ks) / n) if n else None
 
 
 def parse():
@@ -74,6 +107,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip the per-kernel event timing (roofline)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live rocprofv3 --pmc traffic passes (roofline.traffic = null)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 and the collectives run on gloo "
                          "(staged through host memory); never a measurement")
@@ -199,6 +234,9 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.gallery_rows is None:
         args.gallery_rows = 10000 if world == 1 else 1000000
+    pmc, pmc_why = None, "not collected (--no-pmc / --no-prof / N > 1)"
+    if world == 1 and not args.no_pmc and not args.no_prof:  # before this process touches the GPU
+        pmc, pmc_why = pmc_passes(args)
     if args.share_device:
         local = 0
     torch.cuda.set_device(local)
@@ -239,7 +277,7 @@ def main():
             u8.copy_(u8_host, non_blocking=True)
         if i is not None:
             ev[i][0].record(stream)
-        model.embed(u8, out=emb)
+        model.embed(u8, out=emb, sync=False)  # FR_EMBED_ASYNC: checked once after the timed steps
         if i is not None:
             ev[i][1].record(stream)
         return matcher.search(emb)  # N > 1: RCCL all-gather + shard top-k + all-gather + merge
@@ -284,6 +322,11 @@ def main():
         N.check(N.lib().fr_prof_enable(model.handle, 0), "fr_prof_enable")
         N.check(N.lib().fr_prof_only(model.handle, None), "fr_prof_only")
     embed_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))  # forward duration on its stream
+    # a split-stage halo wait that ran out (FR_EMBED_ASYNC: NaN embeddings, latched) voids the run
+    model.sync_check()
+    timeouts = model.stage_timeouts()
+    if timeouts:
+        raise SystemExit(f"rank {rank}: {timeouts} split-stage halo waits ran out: embeddings invalid, no result")
     if dist:
         t = torch.tensor([elapsed, embed_ms], dtype=torch.float64, device="cpu" if args.share_device else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -318,11 +361,17 @@ def main():
         name = dominant
         ms, launches, flops, _ = kclasses[name]
         achieved = flops / (ms * 1e-3) / 1e12
+        traffic = class_traffic(name, pmc)
         peak = FP8_DENSE_PEAK_TFLOPS if name.startswith("conv_fp8") else BF16_DENSE_PEAK_TFLOPS
         result["roofline"] = {
             "bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-            "traffic": pmc_traffic(name, args), "sampled_launches": launches, "sample_stride": PROF_STRIDE,
+            "traffic": traffic,
+            "traffic_source": ("rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes (separate) of this build, run by "
+                               "this bench as a 2-step child of the same configuration; bytes per dispatch = "
+                               "2*FETCH_SIZE + WRITE_SIZE (KiB, gfx950 FETCH half-count correction)")
+                              if traffic is not None else (pmc_why if pmc is None else f"no rocprof kernel mapping for {name!r}"),
+            "sampled_launches": launches, "sample_stride": PROF_STRIDE,
             "us_per_launch": round(ms / launches * 1e3, 2), "gflop_per_launch": round(flops / launches / 1e9, 3),
             "share_of_forward": round(kclasses_all[name][0] / 2 / embed_ms, 4)}
         # per-class breakdown from the untimed all-launch pass (2 steps), each class against both
@@ -335,10 +384,15 @@ def main():
             gbs = by / (ms * 1e-3) / 1e9 if by else None
             mf = tf / peak if tf else 0.0
             hf = gbs / HBM_PEAK_GBPS if gbs else 0.0
-            return {"ms_per_step": round(ms / 2, 4), "launches": launches // 2,
-                    "tflops": round(tf, 1) if tf else None, "mfma_frac": round(mf, 3),
-                    "gbps": round(gbs, 1) if gbs else None, "hbm_frac": round(hf, 3),
-                    "bound": "mfma" if mf >= hf else "hbm"}
+            e = {"ms_per_step": round(ms / 2, 4), "launches": launches // 2,
+                 "tflops": round(tf, 1) if tf else None, "mfma_frac": round(mf, 3),
+                 "gbps": round(gbs, 1) if gbs else None, "hbm_frac": round(hf, 3),
+                 "bound": "mfma" if mf >= hf else "hbm"}
+            tb = class_traffic(name, pmc)
+            if tb is not None:  # PMC memory-side bytes per launch vs the algorithmic bytes per launch
+                e["pmc_bytes_per_launch"] = tb
+                e["pmc_over_algorithmic"] = round(tb / (by / launches), 2) if by else None
+            return e
         result["kernels"] = {k: cls_entry(k, v) for k, v in sorted(kclasses_all.items(), key=lambda kv: -kv[1][0])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.arch, args.cpu_seconds)

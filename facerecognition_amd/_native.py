@@ -24,6 +24,8 @@ FR_DTYPE = {"bf16": FR_DTYPE_BF16, "f16": FR_DTYPE_F16, "fp8": FR_DTYPE_FP8}
 FR_IN_U8_NHWC = 0
 FR_IN_F32_NCHW = 1
 FR_EMBED_RAW = 1
+FR_EMBED_ASYNC = 2
+FR_ERR_STAGE = -6
 FR_TILE_BAND = 7
 FR_TILE_IMG28 = 10
 FR_TILE_IMG56 = 11
@@ -34,6 +36,7 @@ FR_OPT_KEEP_INTERMEDIATES = 2
 FR_OPT_MATCH_EXACT = 3
 FR_OPT_X3_MIN_ROWS = 4
 FR_OPT_STAGE_MIN_FILL = 5
+FR_OPT_STAGE_SPIN_LIMIT = 6
 
 c_int, c_int64, c_size_t, c_void_p, c_float_p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p
 
@@ -78,6 +81,8 @@ _SIGS = {
     "fr_get_option": (c_int, [c_void_p, c_int]),
     "fr_debug_match_fallbacks": (c_int, [c_void_p]),
     "fr_debug_stage_timeouts": (c_int, [c_void_p]),
+    "fr_debug_stage_reruns": (c_int, [c_void_p]),
+    "fr_sync_check": (c_int, [c_void_p, c_void_p]),
     "fr_debug_tensor_count": (c_int, [c_void_p]),
     "fr_debug_tensor_dtype": (c_int, [c_void_p, c_int]),
     "fr_debug_plan": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t]),

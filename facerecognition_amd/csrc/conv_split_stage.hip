@@ -22,7 +22,10 @@
 //     conv2's bias into the accumulators; conv2: accumulator -> patch), plus the boundary-row exchange:
 //     after every conv but the last, each part writes its first row (for the part above) and its last
 //     row (for the part below) to xchg, publishes a per-part counter, waits for its neighbours'
-//     counters (bounded, overruns counted in spin_timeouts) and copies their rows into its halo rows.
+//     counters (bounded: spin_limit sleeps) and copies their rows into its halo rows.  A wait that runs
+//     out is counted (spin_timeouts), raises the host-mapped fail_host flag, and poisons the part's
+//     stage output with NaN, so the image's embedding is NaN rather than a plausible wrong vector
+//     (engine.cpp: fr_embed re-runs the forward without split stages, or latches FR_ERR_STAGE).
 //     Rows are double-buffered by conv parity: a part rewrites a parity only after its neighbours have
 //     consumed it (they have published the next conv, which needs it).  The hand-off uses no cache
 //     maintenance (MI355X_MICROARCH.md, "valid forms", first row of the sc1 hand-off table; one
@@ -58,7 +61,8 @@ struct SplitGeo {
     static constexpr int TAB_ROWS_B = 6 * C * 4;     // the 6 border classes a part can meet, [6][C] f32
     static constexpr int TS = TAB_ROWS_B + C * 4;      // + one row: the PReLU slope of the conv before
     static constexpr int TAB = PATCH_B + NSLOT * SLICE_B;
-    static constexpr int LDS = TAB + 2 * TS;
+    static constexpr int FAILED = TAB + 2 * TS;      // int: this part's bounded wait ran out
+    static constexpr int LDS = FAILED + 16;
     static constexpr int KSTEPS = (C / 32) * 9;
     static constexpr int NG = C / 64;                // channel groups of 64
     static constexpr int MG = 8 / NG;                // pixel groups
@@ -76,7 +80,7 @@ typedef SplitGeo<56, 64, 4, 64> Split56;   // layer1: 8 pixel groups x 1 channel
 constexpr int NW = 8;                     // waves
 constexpr int FN = 4;                     // channel fragments per wave
 constexpr uint32_t OOB = 0x80000000u;
-constexpr int SPIN_LIMIT = 1 << 21;       // x s_sleep 1 (64 cycles): ~0.1 s, then counted and abandoned
+constexpr int SPIN_LIMIT = 1 << 21;       // default: x s_sleep 1 (64 cycles): ~0.1 s, then the wait has run out
 constexpr int SC1 = 16;                   // buffer-load cache policy: sc1 (L1 bypass; gfx940+ cpol bit 4)
 
 #ifndef FR_SPLIT_EXP
@@ -245,8 +249,10 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     issue_w(1, 1);
     issue_w(2, 2);
     issue_tab(0, -1, 0);
+    if (threadIdx.x == 0) *(int*)(smem + G::FAILED) = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const int spin_limit = p.spin_limit > 0 ? p.spin_limit : (p.spin_limit == 0 ? SPIN_LIMIT : 0);
 
     const bool has_up = part > 0, has_dn = part < PARTS - 1;
     int* const my_flag = p.flags + b * PARTS + part;
@@ -270,9 +276,13 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         if (wave == 0 && lane < 2 && !(FR_SPLIT_EXP & 1) && (lane == 0 ? has_up : has_dn)) {
             const int* nf = my_flag + (lane == 0 ? -1 : 1);
             int it = 0;
-            while ((int)((unsigned)__hip_atomic_load(nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (unsigned)f0) < cv + 1) {
-                if (++it == SPIN_LIMIT) {
+            while (p.spin_limit < 0 ||
+                   (int)((unsigned)__hip_atomic_load(nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (unsigned)f0) < cv + 1) {
+                if (it++ >= spin_limit) {  // ran out: count it, flag the host, poison this part's output
                     __hip_atomic_fetch_add(p.spin_timeouts, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    *(volatile int*)p.fail_host = 1;
+                    *(volatile int*)(smem + G::FAILED) = 1;
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -417,9 +427,12 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
         bf16_t* const yo = second && cv == nconv - 1 ? p.y : dbg;
         if (yo) {  // the part's rows, NHWC (once per stage; every conv for intermediates)
+            // a part whose halo wait ran out writes NaN (16-bit quiet NaN in both dtypes' high half)
+            const uint32_t nan_or = *(const volatile int*)(smem + G::FAILED) ? 0x7FC07FC0u : 0u;
             for (int c = opaque_tid(); c < HR * IW * NPL; c += 64 * NW) {
                 const int pix = c / NPL, pl = c - pix * NPL, row = pix / IW, pos = pix - row * IW;
-                const uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((row + 1) * PC + pos + 1) * 16);
+                uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((row + 1) * PC + pos + 1) * 16);
+                v.x |= nan_or; v.y |= nan_or; v.z |= nan_or; v.w |= nan_or;
                 *(uint4*)(yo + ((size_t)(b * IW + r0 + row) * IW + pos) * C + pl * 8) = v;
             }
             if (dbg && yo != dbg) {
@@ -492,7 +505,7 @@ size_t split_stage_weight_bytes(int C, int nconv) { return (size_t)nconv * (C / 
 size_t split_stage_xchg_elems(int B) { return std::max(xchg_elems<Split28>(B), xchg_elems<Split56>(B)); }
 
 hipError_t launch_split_stage(const StageArgs& a, int H, int C, hipStream_t s) {
-    if (a.B <= 0 || !a.xchg || !a.flags || !a.spin_timeouts) return hipErrorInvalidValue;
+    if (a.B <= 0 || !a.xchg || !a.flags || !a.spin_timeouts || !a.fail_host) return hipErrorInvalidValue;
     if (H == Split28::IW && C == Split28::C) return launch_split_t<Split28>(a, s);
     if (H == Split56::IW && C == Split56::C) return launch_split_t<Split56>(a, s);
     return hipErrorInvalidValue;

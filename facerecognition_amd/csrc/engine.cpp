@@ -158,6 +158,15 @@ struct fr_handle {
     bf16_t* stage_xchg = nullptr;  // split-stage boundary rows (split_stage_xchg_elems(max_batch), reserve)
     int* stage_flags = nullptr;    // split-stage progress counters [stage][max_batch][4], never reset
     int* stage_spin = nullptr;     // split-stage bounded-wait overruns (fr_debug_stage_timeouts)
+    // split-stage failure reporting: a host-mapped flag the kernel sets when a halo wait runs out
+    // (fail_host: host view, fail_dev: the device alias the kernel stores to)
+    int* fail_host = nullptr;
+    int* fail_dev = nullptr;
+    int spin_limit = 0;            // FR_OPT_STAGE_SPIN_LIMIT (0: the kernel's default, < 0: every wait runs out)
+    bool no_split = false;         // re-run of a failed forward: split stages off
+    int64_t stage_reruns = 0;      // forwards re-run on the per-conv path after a run-out wait
+    hipEvent_t chk_ev = nullptr;   // completion of the last synchronous-checked forward
+    bool split_registered = false; // counted in the per-device split-stage handle registry (DevSerial)
     int stage_mode = 1;       // FR_OPT_STAGE: 0 off, 1 auto (stage_runs), 2 always
     int stage_min_fill = 80;  // FR_OPT_STAGE_MIN_FILL (percent)
     int n_cu = 256;
@@ -407,6 +416,12 @@ struct Builder {
         if ((rc = upload(h, &cw.bias, bias))) return -1;
         if (names.size() == 1) {
             const HostT* b9 = find(names[0] + ".b9");
+            if (b9 && !kcat.empty()) {  // bias9 replaces `bias`, which carries the folded downsample's bias
+                set_error("plan: conv " + names[0] + " has both a border-class bias (.b9) and a K-concatenated "
+                          "downsample; the downsample bias would be dropped");
+                rc = FR_ERR_WEIGHTS;
+                return -1;
+            }
             if (b9) {
                 if (b9->dims.size() != 2 || b9->dims[0] != 9 || b9->dims[1] != cout || kh != 3 || kw != 3) {
                     set_error("weights: mis-shaped " + names[0] + ".b9 (expects [9, Cout] on a 3x3 conv)");
@@ -1235,7 +1250,7 @@ static bool split_stage_enabled(int H) {
 
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r) {
     if (h->stage_mode == 0) return false;
-    if (r.parts > 1 && !split_stage_enabled(r.H)) return false;
+    if (r.parts > 1 && (h->no_split || !split_stage_enabled(r.H))) return false;
     const int cap = std::max(1, h->n_cu / r.parts);
     if (h->stage_mode == 2 || B <= cap) return true;
     const int64_t rounds = (B + cap - 1) / cap;
@@ -1253,6 +1268,49 @@ static bool op_skipped(const Op& op, const std::vector<char>& run) {
     if (op.kind == OP_STAGE) return !run[op.stage];
     return op.stage >= 0 && run[op.stage];
 }
+
+// Whether a forward at batch B runs a split stage (its parts wait for each other).
+static bool split_runs(const fr_handle* h, int B) {
+    for (const auto& r : h->stages)
+        if (r.parts > 1 && stage_runs(h, B, r)) return true;
+    return false;
+}
+
+// Co-residency of a split stage's parts holds while the stage kernel is the only long-running kernel
+// on the device.  Two split-stage forwards of different handles on one device could
+// each hold CUs the other's parts need, so the forwards of handles that share a device (in this
+// process) are chained on the GPU: each waits for the previous one's completion event and records its
+// own.  Handles alone on their device pay nothing.  (Other processes on the same device are not seen:
+// their kernels can only delay a wait, which the bounded wait and fr_embed's check then report.)
+struct DevSerial {
+    static std::mutex& mu() { static std::mutex m; return m; }
+    static std::unordered_map<int, int>& count() { static std::unordered_map<int, int> c; return c; }
+    static std::unordered_map<int, hipEvent_t>& last() { static std::unordered_map<int, hipEvent_t> e; return e; }
+    static void reg(fr_handle* h, bool on) {
+        std::lock_guard<std::mutex> lk(mu());
+        if (on == h->split_registered) return;
+        h->split_registered = on;
+        count()[h->device] += on ? 1 : -1;
+    }
+    std::unique_lock<std::mutex> lk;
+    hipEvent_t ev = nullptr;
+    hipStream_t s = nullptr;
+    DevSerial(fr_handle* h, bool split, hipStream_t s_) : lk(mu(), std::defer_lock), s(s_) {
+        if (!split) return;
+        lk.lock();
+        if (count()[h->device] <= 1) { lk.unlock(); return; }
+        hipEvent_t& e = last()[h->device];
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+        ev = e;
+        if (ev) (void)hipStreamWaitEvent(s, ev, 0);
+    }
+    void done() {
+        if (ev) (void)hipEventRecord(ev, s);
+        ev = nullptr;
+        if (lk.owns_lock()) lk.unlock();
+    }
+    ~DevSerial() { done(); }
+};
 
 int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
     const int f16 = h->dtype == FR_DTYPE_F16;
@@ -1281,6 +1339,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.xchg = h->stage_xchg;
                 a.flags = h->stage_flags + (size_t)h->max_batch * 4 * op.stage;  // the stage's own counter region
                 a.spin_timeouts = h->stage_spin;
+                a.fail_host = h->fail_dev;
+                a.spin_limit = h->spin_limit;
                 ProfScope ps(h, s);
                 ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
                 ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * 2.0;
@@ -1443,6 +1503,17 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         h->n_cu = prop.multiProcessorCount;
+    void* fh = nullptr;
+    if (hipHostMalloc(&fh, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&h->fail_dev, fh, 0) != hipSuccess ||
+        hipEventCreateWithFlags(&h->chk_ev, hipEventDisableTiming) != hipSuccess) {
+        if (fh) (void)hipHostFree(fh);
+        set_error("fr_create: host-mapped status word / event allocation failed");
+        delete h;
+        return FR_ERR_HIP;
+    }
+    h->fail_host = (int*)fh;
+    *(volatile int*)h->fail_host = 0;
     *out = h;
     return FR_OK;
 }
@@ -1463,6 +1534,9 @@ void fr_destroy(fr_handle* h) {
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     for (auto& r : h->prof_pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : h->ev_free) (void)hipEventDestroy(e);
+    DevSerial::reg(h, false);
+    if (h->chk_ev) (void)hipEventDestroy(h->chk_ev);
+    if (h->fail_host) (void)hipHostFree(h->fail_host);
     delete h;
 }
 
@@ -1488,9 +1562,11 @@ int fr_load_weights(fr_handle* h, const void* blob, size_t nbytes) {
         free_weights(h);
         h->tensors.clear();
         h->ops.clear();
+        DevSerial::reg(h, false);
         return b.rc;
     }
     h->loaded = true;
+    DevSerial::reg(h, std::any_of(h->stages.begin(), h->stages.end(), [](const StageRec& r) { return r.parts > 1; }));
     if (keep_batch > 0) return reserve(h, keep_batch);
     return FR_OK;
 }
@@ -1568,23 +1644,51 @@ static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, 
         return FR_ERR_ARG;
     }
     if (in_fmt != FR_IN_U8_NHWC && in_fmt != FR_IN_F32_NCHW) { set_error("fr_embed: bad in_fmt"); return FR_ERR_ARG; }
+    if (flags & ~(FR_EMBED_RAW | FR_EMBED_ASYNC)) { set_error("fr_embed: unknown flag bits"); return FR_ERR_ARG; }
     FR_HIP_CHECK(hipSetDevice(h->device));
+    if (*(volatile int*)h->fail_host) {  // an earlier FR_EMBED_ASYNC forward's split stage ran out (sticky)
+        *(volatile int*)h->fail_host = 0;
+        set_error("fr_embed: a split stage's halo wait ran out in an earlier FR_EMBED_ASYNC forward on this "
+                  "handle; the affected embeddings are NaN (reported once, see fr_sync_check)");
+        return FR_ERR_STAGE;
+    }
     if (B > h->max_batch) {
         int rc = reserve(h, B);
         if (rc) return rc;
     }
-    if (autotune_enabled() && !h->prof &&
-        std::find(h->tuned_batches.begin(), h->tuned_batches.end(), B) == h->tuned_batches.end()) {
-        // first call at this batch size: eager forward that times the tile candidates of every igemm
-        // shape on the way (results are exact: the last launch of each conv uses the chosen tile)
-        h->tuning = true;
-        const int rc = forward(h, in, in_fmt, B, out, flags, (hipStream_t)stream);
-        h->tuning = false;
-        if (rc) return rc;
-        h->tuned_batches.push_back(B);
-        return FR_OK;
+    const hipStream_t s = (hipStream_t)stream;
+    const int fflags = flags & FR_EMBED_RAW;  // what the forward (and its graph key) depends on
+    const bool split = split_runs(h, B);
+    int rc;
+    {
+        DevSerial ser(h, split, s);
+        if (autotune_enabled() && !h->prof &&
+            std::find(h->tuned_batches.begin(), h->tuned_batches.end(), B) == h->tuned_batches.end()) {
+            // first call at this batch size: eager forward that times the tile candidates of every igemm
+            // shape on the way (results are exact: the last launch of each conv uses the chosen tile)
+            h->tuning = true;
+            rc = forward(h, in, in_fmt, B, out, fflags, s);
+            h->tuning = false;
+            if (!rc) h->tuned_batches.push_back(B);
+        } else {
+            rc = forward_graph(h, in, in_fmt, B, out, fflags, s);
+        }
     }
-    return forward_graph(h, in, in_fmt, B, out, flags, (hipStream_t)stream);
+    if (rc || !split || (flags & FR_EMBED_ASYNC)) return rc;
+    // synchronous check: wait for this forward; if a split stage's halo wait ran out, its images are
+    // NaN-poisoned, so run the forward again on the per-conv path (no waits) and return that
+    FR_HIP_CHECK(hipEventRecord(h->chk_ev, s));
+    FR_HIP_CHECK(hipEventSynchronize(h->chk_ev));
+    if (!*(volatile int*)h->fail_host) return FR_OK;
+    *(volatile int*)h->fail_host = 0;
+    ++h->stage_reruns;
+    h->no_split = true;
+    rc = forward(h, in, in_fmt, B, out, fflags, s);
+    h->no_split = false;
+    if (rc) return rc;
+    FR_HIP_CHECK(hipEventRecord(h->chk_ev, s));
+    FR_HIP_CHECK(hipEventSynchronize(h->chk_ev));
+    return FR_OK;
 }
 
 int fr_embed(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, float* out, int flags, void* stream) {
@@ -1778,6 +1882,7 @@ int fr_set_option(fr_handle* h, int option, int value) {
             if (value < 1) { set_error("fr_set_option: FR_OPT_X3_MIN_ROWS must be >= 1"); return FR_ERR_ARG; }
             h->x3_min_rows = value;
             break;
+        case FR_OPT_STAGE_SPIN_LIMIT: h->spin_limit = value; break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;
     }
     drop_graphs(h);  // captured replays bake in the plan
@@ -1792,6 +1897,7 @@ int fr_get_option(const fr_handle* h, int option) {
         case FR_OPT_KEEP_INTERMEDIATES: return h->keep_inter ? 1 : 0;
         case FR_OPT_MATCH_EXACT: return h->match_exact ? 1 : 0;
         case FR_OPT_X3_MIN_ROWS: return (int)h->x3_min_rows;
+        case FR_OPT_STAGE_SPIN_LIMIT: return h->spin_limit;
         default: return FR_ERR_ARG;
     }
 }
@@ -1816,6 +1922,26 @@ int fr_debug_stage_timeouts(fr_handle* h) {
     FR_HIP_CHECK(hipDeviceSynchronize());
     FR_HIP_CHECK(hipMemcpy(&v, h->stage_spin, sizeof(int), hipMemcpyDeviceToHost));
     return v;
+}
+
+int fr_debug_stage_reruns(fr_handle* h) {
+    if (!h) return FR_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return (int)h->stage_reruns;
+}
+
+int fr_sync_check(fr_handle* h, void* stream) {
+    if (!h) { set_error("fr_sync_check: null handle"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    FR_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    if (*(volatile int*)h->fail_host) {
+        *(volatile int*)h->fail_host = 0;
+        set_error("fr_sync_check: a split stage's halo wait ran out in an FR_EMBED_ASYNC forward on this handle; "
+                  "the affected embeddings are NaN");
+        return FR_ERR_STAGE;
+    }
+    return FR_OK;
 }
 
 int fr_prof_enable(fr_handle* h, int on) {
@@ -1952,27 +2078,17 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         return FR_OK;
     }
     if (d->tile == FR_TILE_WRING + 1) {
-        // the substep images, packed on the stream into a scratch buffer kept for the next call with the
-        // same weight pointer and shape (repeated launches, tools/conv_bench.py, pay the packing once)
+        // the substep images, packed on the stream into stream-ordered scratch on every call (no cache
+        // keyed on the caller's weight pointer: new weights in the same buffer are always repacked)
         a.wimg = (const bf16_t*)1;
         if (!wring_supported(a)) { set_error("fr_op_conv2d: wring kernel not applicable"); return FR_ERR_ARG; }
-        static std::mutex mu;
-        static void* tw = nullptr;
-        static const void* tw_src = nullptr;
-        static int tw_kpad = 0, tw_npad = 0;
-        std::lock_guard<std::mutex> lk(mu);
         hipStream_t st = (hipStream_t)stream;
-        if (tw_src != d->w || tw_kpad != a.Kpad || tw_npad != a.Npad) {
-            FR_HIP_CHECK(hipStreamSynchronize(st));
-            if (tw) (void)hipFree(tw);
-            tw = nullptr;
-            tw_src = nullptr;
-            FR_HIP_CHECK(hipMalloc(&tw, wring_packed_elems(a.Kpad, a.Npad) * sizeof(bf16_t)));
-            FR_HIP_CHECK(wring_pack_weights(a.w, a.Kpad, a.Npad, (bf16_t*)tw, st));
-            tw_src = d->w; tw_kpad = a.Kpad; tw_npad = a.Npad;
-        }
+        void* tw = nullptr;
+        FR_HIP_CHECK(hipMallocAsync(&tw, wring_packed_elems(a.Kpad, a.Npad) * sizeof(bf16_t), st));
+        FR_HIP_CHECK(wring_pack_weights(a.w, a.Kpad, a.Npad, (bf16_t*)tw, st));
         a.wimg = (const bf16_t*)tw;
         FR_HIP_CHECK(launch_conv_wring(a, st));
+        FR_HIP_CHECK(hipFreeAsync(tw, st));
         return FR_OK;
     }
     if (d->tile == FR_TILE_ROWS + 1) {

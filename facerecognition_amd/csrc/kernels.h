@@ -110,6 +110,8 @@ struct StageArgs {
     bf16_t* xchg;              // [B][parts][2 rows][2 parities][W][C]
     int* flags;                // [B][parts] per-part progress (convs published), zeroed by the launcher
     int* spin_timeouts;        // bounded-wait overruns (fr_debug_stage_timeouts); 0 when healthy
+    int* fail_host;            // host-mapped flag: set to 1 (plain vector store) by any part whose wait ran out
+    int spin_limit;            // sleeps before a wait counts as run out; < 0: every wait runs out (debug)
     int B, nblk, f16, dbg;     // dbg: timing-only experiment switches (FR_STAGE_DBG), 0 in production
     void* ev0;
     void* ev1;

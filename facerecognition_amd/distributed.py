@@ -60,9 +60,10 @@ class ShardedMatcher:
     """
 
     def __init__(self, batch: int, dim: int, k: int, local_search: Callable, device: torch.device,
-                 merge: Optional[Callable] = None, group=None):
+                 merge: Optional[Callable] = None, group=None, always_exchange: bool = False):
         import torch.distributed as dist
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.always_exchange = always_exchange  # run steps 1-4 even at world 1 (tests of the collectives)
         self.group, self.k, self.B = group, k, batch
         self.local_search = local_search
         self.merge = merge or native_merge
@@ -74,7 +75,7 @@ class ShardedMatcher:
     def search(self, emb: torch.Tensor):
         """emb: this rank's normalized embeddings [B, D] → top-k of every rank's probes, identical on
         all ranks: (scores [world*B, k], idx [world*B, k]); row j*B + b is rank j's probe b."""
-        if self.world == 1:
+        if self.world == 1 and not self.always_exchange:
             return self.local_search(emb)
         _all_gather(self.all_emb, emb, self.group)
         s, i = self.local_search(self.all_emb)

@@ -29,6 +29,12 @@ import numpy as np
 
 from . import weights as Wt
 
+# Host/device memory bounds of the batched paths: decoded images stay at full resolution
+# until the device resize, so build_db flushes by decoded bytes as well as by image count, and one
+# _device_crops upload carries at most UPLOAD_BYTES of decoded pixels.
+FLUSH_IMAGES = 4096
+FLUSH_BYTES = 1 << 30
+UPLOAD_BYTES = 256 << 20
 ARCFACE_TEMPLATE = np.array([[38.2946, 51.6963], [73.5318, 51.5014], [56.0252, 71.7366],
                              [41.5493, 92.3655], [70.7299, 92.2041]], dtype=np.float32)
 IMG_EXTS = (".jpg", ".jpeg", ".png", ".webp")
@@ -114,10 +120,21 @@ def _load_u8(img_input, transform) -> np.ndarray:
     return np.asarray(img.convert("RGB"), dtype=np.uint8)
 
 
+def _check_transform(model, transform) -> None:
+    """The transform's Resize target must be the model's input side (the reference resizes to the
+    transform's image_size: get_transform / get_facenet_transform, extract_embeddings.py:170-185)."""
+    if not isinstance(transform, _Transform):
+        raise TypeError("transform must come from get_transform()/get_facenet_transform()")
+    if transform.size != model.input_size:
+        raise ValueError(f"transform resizes to {transform.size}x{transform.size} but the {model.arch} model "
+                         f"takes {model.input_size}x{model.input_size} crops")
+
+
 def _device_crops(arrays: List[np.ndarray], size: int, device):
     """Decoded RGB u8 images of any sizes -> device u8 [n, size, size, 3]: images already size x size are
-    copied, the others go through fr_resize_u8 (Pillow's BILINEAR resize, bit-exact) one launch per
-    distinct input size."""
+    copied, the others go through fr_resize_u8 (Pillow's BILINEAR resize, bit-exact), one launch per
+    distinct input size and upload of at most UPLOAD_BYTES decoded bytes (large photos are not staged
+    256 at a time)."""
     import torch
     from .align import resize_u8
     out = torch.empty((len(arrays), size, size, 3), dtype=torch.uint8, device=device)
@@ -125,10 +142,13 @@ def _device_crops(arrays: List[np.ndarray], size: int, device):
     for i, a in enumerate(arrays):
         by_shape.setdefault(a.shape, []).append(i)
     for shape, idx in by_shape.items():
-        x = torch.from_numpy(np.ascontiguousarray(np.stack([arrays[i] for i in idx]))).to(device, non_blocking=True)
-        if shape[:2] != (size, size):
-            x = resize_u8(x, size, size)
-        out[torch.as_tensor(idx, device=device)] = x
+        per = max(1, UPLOAD_BYTES // max(1, int(np.prod(shape))))
+        for c in range(0, len(idx), per):
+            part = idx[c:c + per]
+            x = torch.from_numpy(np.ascontiguousarray(np.stack([arrays[i] for i in part]))).to(device, non_blocking=True)
+            if shape[:2] != (size, size):
+                x = resize_u8(x, size, size)
+            out[torch.as_tensor(part, device=device)] = x
     return out
 
 
@@ -149,6 +169,7 @@ def _embed_u8(model, arrays) -> np.ndarray:
 def extract_embedding_single(img_input, model, transform, device: str = "cuda",
                              model_type: str = "arcface") -> Optional[np.ndarray]:
     try:
+        _check_transform(model, transform)
         u8 = _load_u8(img_input, transform)
         return _embed_u8(model, [u8])[0].astype(np.float32).flatten()
     except Exception as e:  # reference: any failure → None (extract_embeddings.py:386-389)
@@ -170,6 +191,7 @@ def extract_embeddings_batch(image_paths: List[str], model, transform, device: s
                 print(f"Skip {path}: {e}")
         if not imgs:
             continue
+        _check_transform(model, transform)
         embeddings.append(_embed_u8(model, imgs))
         valid_paths.extend(paths)
     if not embeddings:
@@ -223,6 +245,7 @@ def extract_embedding_for_folder(folder: str, model, transform, device: str = "c
                                  model_type: str = "arcface") -> Optional[np.ndarray]:
     if not os.path.exists(folder):
         return None
+    _check_transform(model, transform)
     if preprocessor is not None:
         print("[WARN] face detection/alignment is out of scope for facerecognition_amd; using raw images")
     return segment_means(model, [_folder_crops(folder, transform)])[0]
@@ -301,9 +324,8 @@ def build_db(model_path: str, root_folder: str = "data/celeb", save_path: str = 
     persons = [p for p in os.listdir(root_folder) if os.path.isdir(os.path.join(root_folder, p))]
     print(f"\nTim thay {len(persons)} celebrities")
     # identities are embedded together: crops of consecutive persons are collected
-    # until about FLUSH images, then embedded in 256-image fr_embed batches and reduced per person by one
-    # segmented-mean launch; host memory stays bounded by one flush
-    FLUSH = 4096
+    # until FLUSH_IMAGES images or FLUSH_BYTES decoded bytes, then embedded in 256-image fr_embed batches
+    # and reduced per person by one segmented-mean launch; host memory stays bounded by one flush
     pending: List[str] = []
     groups: List[List[np.ndarray]] = []
 
@@ -317,7 +339,7 @@ def build_db(model_path: str, root_folder: str = "data/celeb", save_path: str = 
     for person in persons:
         pending.append(person)
         groups.append(_folder_crops(os.path.join(root_folder, person), transform))
-        if sum(len(g) for g in groups) >= FLUSH:
+        if sum(len(g) for g in groups) >= FLUSH_IMAGES or sum(a.nbytes for g in groups for a in g) >= FLUSH_BYTES:
             flush()
     flush()
     if not db:

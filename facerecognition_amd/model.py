@@ -98,18 +98,35 @@ class FRModel:
         x = x.to(self.device, non_blocking=True).contiguous()
         return x, fmt, int(H), int(W)
 
-    def embed(self, x, normalize: bool = True, out=None):
-        """Device f32 [B, 512] embeddings (L2-normalized unless normalize=False)."""
+    def embed(self, x, normalize: bool = True, out=None, sync: bool = True):
+        """Device f32 [B, 512] embeddings (L2-normalized unless normalize=False).
+
+        sync=True (default): a forward that ran an IResNet100 split stage is waited for and re-run on
+        the per-conv path if a split-stage wait ran out, so the result is always valid.  sync=False
+        (FR_EMBED_ASYNC, pipelined callers such as bench.py): returns once enqueued; a run-out wait
+        leaves that image's embedding NaN and is reported by sync_check() / the next embed()."""
         import torch
 
         x, fmt, H, W = self._prep(x)
         B = int(x.shape[0])
         if out is None:
             out = torch.empty((B, self.embedding_size), dtype=torch.float32, device=self.device)
-        flags = 0 if normalize else N.FR_EMBED_RAW
+        flags = (0 if normalize else N.FR_EMBED_RAW) | (0 if sync else N.FR_EMBED_ASYNC)
         N.check(N.lib().fr_embed(self._h, N.ptr(x), fmt, B, H, W, N.ptr(out), flags, N.stream_ptr(self.device)),
                 "fr_embed")
         return out
+
+    def sync_check(self) -> None:
+        """Synchronize the current stream; raise if an async forward's split-stage wait ran out."""
+        N.check(N.lib().fr_sync_check(self._h, N.stream_ptr(self.device)), "fr_sync_check")
+
+    def stage_timeouts(self) -> int:
+        """Split-stage waits that ran out on this handle (fr_debug_stage_timeouts; 0 when healthy)."""
+        return int(N.lib().fr_debug_stage_timeouts(self._h))
+
+    def stage_reruns(self) -> int:
+        """Forwards re-run on the per-conv path after a run-out wait (fr_debug_stage_reruns)."""
+        return int(N.lib().fr_debug_stage_reruns(self._h))
 
     def __call__(self, x, labels=None):
         """Reference semantics: ArcFaceModel(x, labels=None) returns the un-normalized embedding;

@@ -30,6 +30,8 @@ extern "C" {
 #define FR_ERR_WEIGHTS (-3) /* weight blob malformed or tensor missing        */
 #define FR_ERR_STATE (-4)   /* call order violated (no weights, no gallery)   */
 #define FR_ERR_OOM (-5)     /* device allocation failed                       */
+#define FR_ERR_STAGE (-6)   /* a split stage's bounded halo wait ran out in an FR_EMBED_ASYNC forward:
+                             * that forward's affected embeddings are NaN (see fr_sync_check)   */
 
 /* ---- backbone architectures ---- */
 #define FR_ARCH_RESNET50_ARCFACE 0 /* models/arcface/arcface_model.py:65-202 (ArcFaceModel, ResNet-50 trunk) */
@@ -52,6 +54,14 @@ extern "C" {
 
 /* ---- fr_embed flags ---- */
 #define FR_EMBED_RAW 1 /* return the un-normalized head output (= model(x, labels=None)); default is F.normalize'd */
+/* Return as soon as the forward is enqueued.  Without this flag, a forward that runs an IResNet100 split
+ * stage (layer1 / layer2: several workgroups per image waiting for each other's boundary rows, bounded)
+ * is waited for before fr_embed returns, and if any of those waits ran out the forward is run again on
+ * the per-conv path (no waits), so the returned embeddings are always valid (fr_debug_stage_reruns counts
+ * the re-runs).  With it, a part whose wait ran out writes NaN into its image's activations (the
+ * embedding is NaN, never a plausible wrong vector) and the handle latches FR_ERR_STAGE, returned once by
+ * fr_sync_check or by the next fr_embed / fr_embed_match on the handle. */
+#define FR_EMBED_ASYNC 2
 
 typedef struct fr_handle fr_handle;
 
@@ -85,6 +95,10 @@ int fr_input_size(const fr_handle* h);
  * extract_embeddings_batch (:430-435); FaceNetModel.forward (facenet_model.py:28-36). */
 int fr_embed(fr_handle* h, const void* in, int in_fmt, int B, int H, int W,
              float* out, int flags, void* stream);
+
+/* Synchronize `stream`, then report (once) a split-stage wait that ran out in an FR_EMBED_ASYNC forward
+ * of this handle since the last report: FR_ERR_STAGE, else FR_OK. */
+int fr_sync_check(fr_handle* h, void* stream);
 
 /* ---- gallery + match (replaces RecognitionEngine.recognize_with_db's loop,
  *      recognition_engine.py:267-289, the notebook np.dot+argmax/argsort,
@@ -235,15 +249,22 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * the next fr_gallery_set); below it the f32 kernel is as fast. */
 #define FR_OPT_X3_MIN_ROWS 4
 #define FR_OPT_STAGE_MIN_FILL 5
+/* FR_OPT_STAGE_SPIN_LIMIT (default 0 = the kernel's bound, ~0.1 s): sleeps (64 cycles each) a split-stage
+ * part waits for a neighbour's boundary rows before the wait counts as run out.  < 0 makes every wait
+ * run out at once (debug: exercises the NaN poisoning, the re-run and FR_ERR_STAGE deterministically). */
+#define FR_OPT_STAGE_SPIN_LIMIT 6
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);
 /* Number of probes (since the gallery was first split) whose bf16x3 candidate proof failed and were
  * rescanned exactly (synchronizes the device). */
 int fr_debug_match_fallbacks(fr_handle* h);
-/* Number of bounded waits of the layer2 split stage kernel (two workgroups per image exchanging a
- * boundary row per conv) that ran out before the partner published; 0 on a healthy device.  Each one
- * means that image's embedding is wrong (synchronizes the device). */
+/* Number of bounded waits of the split stage kernels (layer2: two workgroups per image, layer1: four,
+ * exchanging boundary rows per conv) that ran out before the partner published; 0 on a healthy device
+ * (synchronizes the device).  Each one was either re-run (fr_embed's default) or reported as
+ * FR_ERR_STAGE with NaN embeddings (FR_EMBED_ASYNC): never returned as a valid embedding. */
 int fr_debug_stage_timeouts(fr_handle* h);
+/* Number of forwards fr_embed ran again on the per-conv path because a split-stage wait ran out. */
+int fr_debug_stage_reruns(fr_handle* h);
 
 /* ---- debug: named intermediate tensors of the forward plan (per-layer drift tests) ----
  * Tensor names are the reference/oracle module whose output the tensor equals

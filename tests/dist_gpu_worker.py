@@ -34,8 +34,29 @@ def data(dev):
     return G, P
 
 
+C4_ROWS, C4_B = 1_000_000, 256  # BASELINE config 4 per-rank probe count against its 1M-row gallery
+
+
+def data_config4(dev, lo, hi):
+    """Config-4 shape: rows [lo, hi) of the 1M-row synthetic gallery (generated per shard, identical
+    whatever the sharding) and 2 x 256 probes, the first 64 of each rank planted near gallery rows spread
+    over both shards."""
+    from facerecognition_amd.synthetic import synthetic_gallery_rows
+    G = synthetic_gallery_rows(lo, hi, dev, seed=11)
+    g = torch.Generator(device=dev)
+    g.manual_seed(123)
+    P = torch.randn((2 * C4_B, D), generator=g, device=dev)
+    planted = torch.arange(128, device=dev) * 7_777 + 3
+    rows = synthetic_gallery_rows(0, C4_ROWS, dev, seed=11)[planted] if hi - lo < C4_ROWS else G[planted]
+    for r in range(2):
+        P[r * C4_B:r * C4_B + 64] = rows[r * 64:(r + 1) * 64] + 0.05 * P[r * C4_B:r * C4_B + 64] / D ** 0.5
+    P /= P.norm(dim=1, keepdim=True)
+    return G, P
+
+
 def main():
     rank, world, out_dir = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    mode = sys.argv[4] if len(sys.argv) > 4 else "ties"
     import torch.distributed as dist
     from facerecognition_amd.distributed import ShardedMatcher, shard_range
     from facerecognition_amd.gallery import DeviceGallery
@@ -44,12 +65,17 @@ def main():
     dev = torch.device("cuda", 0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        G, P = data(dev)
-        lo, hi = shard_range(ROWS, rank, world)
+        rows, b = (C4_ROWS, C4_B) if mode == "config4" else (ROWS, B)
+        lo, hi = shard_range(rows, rank, world)
+        if mode == "config4":
+            Gs, P = data_config4(dev, lo, hi)
+        else:
+            G, P = data(dev)
+            Gs = G[lo:hi].contiguous()
         gal = DeviceGallery(device=0, index_base=lo)
-        gal.set_device_rows(G[lo:hi].contiguous())
-        m = ShardedMatcher(B, D, K, lambda p: gal.search_device(p, K), dev)  # merge = native_merge
-        s, i = m.search(P[rank * B:(rank + 1) * B].contiguous())
+        gal.set_device_rows(Gs)
+        m = ShardedMatcher(b, D, K, lambda p: gal.search_device(p, K), dev)  # merge = native_merge
+        s, i = m.search(P[rank * b:(rank + 1) * b].contiguous())
         torch.cuda.synchronize(dev)
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), s=s.cpu().numpy(), i=i.cpu().numpy(),
                  fallbacks=gal.fallbacks())

@@ -124,12 +124,51 @@ def test_irv1_bf16_parity(gpu):
     assert np.all(1 - cos <= COS_TOL), f"irv1 bf16: 1-cos = {1 - cos}"
 
 
+def _full_batch_parity(arch, m, a, u8, seed):
+    """All B faces of a full batch against the fp32 oracle: every 1-cos at the bar (max and p99 printed),
+    identical top-1 on a 10k gallery planted from the ORACLE's embeddings (device top-1 == the planted
+    rows == the oracle's own top-1), and the non-planted top-1 agreement rate on a random 10k gallery
+    (SURVEY.md §8d), each flip inside the bound the embedding error allows."""
+    from facerecognition_amd.gallery import DeviceGallery
+    from oracle.match import topk_dot
+    ref = _oracle_embed(arch, u8.numpy())
+    ref = ref / np.linalg.norm(ref, axis=1, keepdims=True)
+    got = a.numpy()
+    d = 1 - (got * ref).sum(1)
+    B = len(got)
+    print(f"{arch} {m.dtype} bs={B}: 1-cos vs oracle max {d.max():.2e} p99 {np.quantile(d, 0.99):.2e} "
+          f"median {np.median(d):.2e}")
+    assert float(d.max()) <= COS_TOL, f"{arch}: {int((d > COS_TOL).sum())} faces above the bar, max {d.max():.2e}"
+    rng = np.random.default_rng(seed)
+    G = rng.standard_normal((10000, 512)).astype(np.float32)
+    perm = rng.permutation(10000)[:B]
+    G[perm] = ref + 0.03 * rng.standard_normal((B, 512)).astype(np.float32)
+    G /= np.linalg.norm(G, axis=1, keepdims=True)
+    gal = DeviceGallery(G)
+    _, idx = gal.search(got, 5)
+    _, ri = topk_dot(ref, G, 5)
+    assert np.array_equal(ri[:, 0], perm) and np.array_equal(idx[:, 0], ri[:, 0])
+    gal.close()
+    R = rng.standard_normal((10000, 512)).astype(np.float32)
+    R /= np.linalg.norm(R, axis=1, keepdims=True)
+    gal = DeviceGallery(R)
+    _, gi = gal.search(got, 2)
+    gal.close()
+    rs, ri = topk_dot(ref, R, 2)
+    agree = gi[:, 0] == ri[:, 0]
+    gap = rs[:, 0] - rs[:, 1]
+    err = np.linalg.norm(got - ref, axis=1)
+    print(f"{arch} {m.dtype} bs={B}: non-planted top-1 agreement {agree.mean():.4f} ({int(agree.sum())}/{B}) on a "
+          f"random 10k gallery; oracle top-1/top-2 gap min {gap.min():.2e} median {np.median(gap):.2e}; "
+          f"flips at gaps {np.sort(gap[~agree])[:8]}")
+    assert np.all(agree | (gap <= 2 * err)), "a top-1 flip where the oracle's gap exceeds the error bound"
+    return agree.mean()
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_irv1_full_batch_bs256(gpu, dtype):
     """BASELINE config-3 size (InceptionResnetV1 @160, bs = 256): deterministic replay, finite unit-norm
-    rows, batch independence against a 5-face call, an oracle sample at the 1e-3 bar, and identical top-1
-    against the oracle's ranking on a planted 10k gallery."""
-    from facerecognition_amd.gallery import DeviceGallery
+    rows, batch independence against a 5-face call, and _full_batch_parity: all 256 faces vs the oracle."""
     from facerecognition_amd.model import FRModel
     m = FRModel.synthetic("irv1_facenet", dtype=dtype)
     u8 = torch.from_numpy(_probes("irv1_facenet", 256, seed=31))
@@ -139,18 +178,7 @@ def test_irv1_full_batch_bs256(gpu, dtype):
     assert torch.isfinite(a).all() and torch.allclose(a.norm(dim=1), torch.ones(256), atol=1e-5)
     small = m.embed(u8[60:65]).cpu()
     assert float((1 - (a[60:65] * small).sum(1)).max()) <= COS_TOL
-    ref = _oracle_embed("irv1_facenet", u8[:4].numpy())
-    cos_o = (a[:4].numpy() * ref).sum(1) / np.linalg.norm(ref, axis=1)
-    assert float((1 - cos_o).max()) <= COS_TOL, 1 - cos_o
-    rng = np.random.default_rng(32)
-    G = rng.standard_normal((10000, 512)).astype(np.float32)
-    perm = rng.permutation(10000)[:256]
-    G[perm] = a.numpy() + 0.03 * rng.standard_normal((256, 512)).astype(np.float32)
-    G /= np.linalg.norm(G, axis=1, keepdims=True)
-    gal = DeviceGallery(G)
-    _, idx = gal.search(a.numpy(), 5)
-    assert np.array_equal(idx[:, 0], perm)
-    gal.close()
+    assert _full_batch_parity("irv1_facenet", m, a, u8, 32) >= 0.9
     m.close()
 
 
@@ -208,11 +236,8 @@ def test_facenet_projection_head(gpu):
 
 def test_full_batch_properties_bs256(gpu):
     """BASELINE config-2 size (IResNet100 bf16, bs = 256: every production kernel at its real grid --
-    fused stem, layer2 band kernel, layer3 stage, 10k-row match).  Size-independent properties:
-    deterministic replay, finite unit-norm rows, batch independence against a 5-face call, a
-    bs=256 sample against the fp32 oracle at the 1e-3 bar, and identical top-1 on a planted gallery
-    built from the embeddings themselves."""
-    from facerecognition_amd.gallery import DeviceGallery
+    fused stem, split stages, layer3 stage, 10k-row match): deterministic replay, finite unit-norm rows,
+    batch independence against a 5-face call, and _full_batch_parity: all 256 faces vs the oracle."""
     from facerecognition_amd.model import FRModel
     m = FRModel.synthetic("iresnet100", dtype="bf16")
     u8 = torch.from_numpy(_probes("iresnet100", 256, seed=21))
@@ -224,18 +249,7 @@ def test_full_batch_properties_bs256(gpu):
     small = m.embed(u8[100:105]).cpu()
     cos_b = (a[100:105] * small).sum(1)
     assert float((1 - cos_b).max()) <= COS_TOL
-    ref = _oracle_embed("iresnet100", u8[:4].numpy())
-    cos_o = (a[:4].numpy() * ref).sum(1) / np.linalg.norm(ref, axis=1)
-    assert float((1 - cos_o).max()) <= COS_TOL, 1 - cos_o
-    rng = np.random.default_rng(22)
-    G = rng.standard_normal((10000, 512)).astype(np.float32)
-    perm = rng.permutation(10000)[:256]
-    G[perm] = a.numpy() + 0.03 * rng.standard_normal((256, 512)).astype(np.float32)
-    G /= np.linalg.norm(G, axis=1, keepdims=True)
-    gal = DeviceGallery(G)
-    _, idx = gal.search(a.numpy(), 5)
-    assert np.array_equal(idx[:, 0], perm)
-    gal.close()
+    assert _full_batch_parity("iresnet100", m, a, u8, 22) >= 0.9
     m.close()
 
 

@@ -535,3 +535,92 @@ def test_match_large_k_takes_exact_path(gpu):
     rs, ri = _np_topk(P, G, 16)
     assert np.array_equal(i[:, 0], ri[:, 0]) and np.allclose(s, rs, atol=1e-5)
     gal.close()
+
+
+def _host_top1_f64(P, G, chunk=131_072):
+    """Chunked float64 argmax (lowest index on ties) + the gap to the runner-up, per probe."""
+    P = P.astype(np.float64)
+    best = np.full(len(P), -np.inf)
+    second = np.full(len(P), -np.inf)
+    arg = np.zeros(len(P), np.int64)
+    for c in range(0, len(G), chunk):
+        S = P @ G[c:c + chunk].astype(np.float64).T
+        a = np.argmax(S, axis=1)
+        m = S[np.arange(len(S)), a]
+        S[np.arange(len(S)), a] = -np.inf
+        m2 = S.max(axis=1) if S.shape[1] > 1 else np.full(len(S), -np.inf)
+        upd = m > best
+        second = np.where(upd, np.maximum(best, m2), np.maximum(second, m))
+        arg, best = np.where(upd, a + c, arg), np.where(upd, m, best)
+    return arg, best - second
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("B,Ng", [(2048, 125_000), (256, 1_000_000)])
+def test_match_config4_per_rank_shapes(gpu, B, Ng):
+    """BASELINE config 4's per-rank match shapes (2048 gathered probes x a 125k-row shard, and one rank's
+    256 probes x the whole 1M rows) through fr_match_topk's bf16x3 path: equal to the exact f32 kernel
+    (FR_OPT_MATCH_EXACT) bit for bit, and top-1 equal to a float64 host argmax wherever the runner-up
+    gap exceeds the f32 scoring noise (the near-tie count and the proof fallbacks are reported)."""
+    from facerecognition_amd.gallery import DeviceGallery
+    from facerecognition_amd.synthetic import synthetic_gallery_rows
+    G = synthetic_gallery_rows(0, Ng, gpu, seed=5)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(B)
+    P = torch.randn((B, 512), generator=g, device=gpu)
+    plant = torch.arange(B // 4, device=gpu) * (Ng // (B // 4)) + 1
+    P[: B // 4] = G[plant] + 0.05 / np.sqrt(512) * P[: B // 4]
+    P /= P.norm(dim=1, keepdim=True)
+    gal = DeviceGallery(device=0)
+    gal.set_device_rows(G)
+    fb0 = gal.fallbacks()
+    s3, i3 = (t.cpu().numpy() for t in gal.search_device(P, 5))
+    fb = gal.fallbacks() - fb0
+    gal.set_exact(True)
+    se, ie = (t.cpu().numpy() for t in gal.search_device(P, 5))
+    assert np.array_equal(i3, ie)
+    assert np.array_equal(s3.view(np.uint32), se.view(np.uint32))
+    assert np.array_equal(i3[: B // 4, 0], plant.cpu().numpy())
+    arg, gap = _host_top1_f64(P.cpu().numpy(), G.cpu().numpy())
+    clear = gap > 1e-5
+    assert clear.mean() > 0.9
+    assert np.array_equal(i3[clear, 0], arg[clear])
+    print(f"{B}x{Ng}: bf16x3 == exact f32 bit for bit; {fb} proof fallbacks; "
+          f"{int((~clear).sum())} near-tie probes (gap <= 1e-5) of {B}")
+    gal.close()
+
+
+def test_nccl_world1_all_gather(gpu):
+    """The RCCL ("nccl") branch of distributed._all_gather (config 4's collective) on a world-1 group on
+    the device (RCCL refuses two ranks on one GPU, and the test box has one): all_gather_into_tensor of
+    embeddings, then ShardedMatcher's four exchange steps (all-gather, shard top-k, candidate all-gather,
+    fr_topk_merge) through RCCL, equal to the plain search bit for bit."""
+    import socket
+    import torch.distributed as dist
+    from facerecognition_amd.distributed import ShardedMatcher, _all_gather
+    from facerecognition_amd.gallery import DeviceGallery
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=gpu)
+    try:
+        assert dist.get_backend() == "nccl"
+        x = torch.randn(256, 512, device=gpu)
+        out = torch.empty(256, 512, device=gpu)
+        _all_gather(out, x)
+        torch.cuda.synchronize()
+        assert torch.equal(out, x)
+        rng = np.random.default_rng(3)
+        G = _norm(rng.standard_normal((40_000, 512)))
+        gal = DeviceGallery(G)
+        P = torch.from_numpy(_norm(rng.standard_normal((64, 512)))).to(gpu)
+        m = ShardedMatcher(64, 512, 5, lambda p: gal.search_device(p, 5), gpu, always_exchange=True)
+        s, i = m.search(P)
+        s0, i0 = gal.search_device(P, 5)
+        torch.cuda.synchronize()
+        assert torch.equal(i, i0) and torch.equal(s, s0)
+        rs, ri = _np_topk(P.cpu().numpy(), G, 5)
+        assert np.array_equal(i.cpu().numpy()[:, 0], ri[:, 0])
+        gal.close()
+    finally:
+        dist.destroy_process_group()

@@ -75,3 +75,18 @@ def test_align_then_embed_matches_host_path(gpu):
     e_host = m.embed(torch.from_numpy(host)).cpu().numpy()
     m.close()
     assert np.array_equal(e_dev, e_host)
+
+
+def test_device_crops_upload_chunks_by_bytes(gpu, monkeypatch):
+    """Large decoded photos are uploaded in pieces of at most UPLOAD_BYTES (a 256-image batch
+    of multi-megapixel photos is not staged at once); the crops equal PIL's resize either way."""
+    from PIL import Image
+    import facerecognition_amd.extract_embeddings as EE
+    rng = np.random.default_rng(4)
+    imgs = [rng.integers(0, 256, (1200, 900, 3), dtype=np.uint8) for _ in range(5)] + \
+           [rng.integers(0, 256, (112, 112, 3), dtype=np.uint8), rng.integers(0, 256, (300, 200, 3), dtype=np.uint8)]
+    monkeypatch.setattr(EE, "UPLOAD_BYTES", 2 * 1200 * 900 * 3)  # two big photos per upload
+    got = EE._device_crops(imgs, 112, gpu).cpu().numpy()
+    for a, g in zip(imgs, got):
+        ref = np.asarray(Image.fromarray(a).resize((112, 112), Image.BILINEAR)) if a.shape[:2] != (112, 112) else a
+        assert np.array_equal(g, ref)

@@ -159,3 +159,63 @@ def test_split_stage_batches_and_exchange(gpu, last, first_t, parts, B):
                 d = (a[i, r] - b[i, r]).norm() / (b[i, r].norm() + 1e-12)
                 assert d < 2e-2, f"{n} image {i} rows {r}: rel err {d:.3e}"
     assert np.all(1 - np.sum(e_stage * e_conv, axis=1) <= 3e-4)
+
+
+def test_split_stage_wait_runout_never_returns_valid_looking_embeddings(gpu):
+    """A split-stage halo wait that runs out (FR_OPT_STAGE_SPIN_LIMIT < 0 forces every wait to) is never
+    returned as a valid embedding: fr_embed's default waits for the forward and re-runs it on the
+    per-conv path (correct results, fr_debug_stage_reruns), and FR_EMBED_ASYNC leaves the affected
+    embeddings NaN and latches FR_ERR_STAGE, reported once by fr_sync_check or the next fr_embed."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("iresnet100")
+    x = torch.from_numpy(synthetic_crops(6, 112, seed=77)).cuda()
+    m.set_option(N.FR_OPT_STAGE, 2)
+    good = m.embed(x).cpu().numpy()
+    assert m.stage_timeouts() == 0 and m.stage_reruns() == 0
+    m.set_option(N.FR_OPT_STAGE_SPIN_LIMIT, -1)
+    e = m.embed(x).cpu().numpy()  # synchronous: detected and re-run without split stages
+    assert m.stage_timeouts() > 0 and m.stage_reruns() == 1
+    assert np.all(np.isfinite(e)) and np.all(1 - np.sum(e * good, axis=1) <= 3e-4)
+    e2 = m.embed(x, sync=False)  # asynchronous: NaN embeddings + a latched error
+    with pytest.raises(RuntimeError, match=r"rc=-6"):
+        m.sync_check()
+    assert bool(torch.isnan(e2).any(dim=1).all())
+    m.sync_check()  # reported once
+    m.embed(x, sync=False)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match=r"rc=-6"):
+        m.embed(x)  # the next call reports the earlier async failure
+    m.set_option(N.FR_OPT_STAGE_SPIN_LIMIT, 0)
+    e3 = m.embed(x).cpu().numpy()
+    assert np.array_equal(e3, good) and m.stage_reruns() == 1
+    m.close()
+
+
+def test_two_handles_share_a_device(gpu):
+    """Two handles on one device, forwards on two streams: their split-stage forwards are chained on
+    the GPU (DevSerial), no wait runs out, and each result equals its single-handle result."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    a, b = FRModel.synthetic("iresnet100"), FRModel.synthetic("iresnet100")
+    xa = torch.from_numpy(synthetic_crops(128, 112, seed=1)).cuda()
+    xb = torch.from_numpy(synthetic_crops(128, 112, seed=2)).cuda()
+    ra, rb = a.embed(xa).cpu().numpy(), b.embed(xb).cpu().numpy()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(3):
+        with torch.cuda.stream(sa):
+            oa = a.embed(xa, sync=False)
+        with torch.cuda.stream(sb):
+            ob = b.embed(xb, sync=False)
+        outs.append((oa, ob))
+    torch.cuda.synchronize()
+    for oa, ob in outs:
+        assert np.array_equal(oa.cpu().numpy(), ra) and np.array_equal(ob.cpu().numpy(), rb)
+    with torch.cuda.stream(sa):
+        a.sync_check()
+    with torch.cuda.stream(sb):
+        b.sync_check()
+    assert a.stage_timeouts() == 0 and b.stage_timeouts() == 0
+    a.close()
+    b.close()

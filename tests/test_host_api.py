@@ -234,3 +234,18 @@ def test_build_job_logs_capped():
     assert len(j.to_dict()["logs"]) == 50 and j.to_dict()["elapsed_time"] is None
     j.update_progress(150)
     assert j.progress == 100.0
+
+
+def test_transform_size_must_match_model():
+    """the device resize targets the transform's image_size, and a transform whose size is not
+    the model's input side is an error (the reference would feed the model a wrong-size crop)."""
+    import facerecognition_amd.extract_embeddings as EE
+
+    class _M:
+        arch, input_size = "iresnet100", 112
+    EE._check_transform(_M(), EE.get_transform(112))
+    with pytest.raises(ValueError):
+        EE._check_transform(_M(), EE.get_transform(160))
+    with pytest.raises(TypeError):
+        EE._check_transform(_M(), object())
+    assert EE.extract_embedding_single(np.zeros((112, 112, 3), np.uint8), _M(), EE.get_transform(160)) is None
