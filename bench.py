@@ -41,10 +41,11 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec (about 6.3 TB/s
 PROF_STRIDE = 8  # roofline: sample every 8th dominant-kernel launch (event overhead ~0.5 % instead of ~4 %)
 
 
-# bench kernel class (fr_prof_get name prefix) -> rocprofv3 kernel-name fragment of its dispatches
+# bench kernel class (fr_prof_get name prefix) -> rocprofv3 kernel-name fragment of its dispatches (only
+# classes whose kernel instantiation serves no other class: the two conv_rows classes share one)
 CLASS_KERNEL = [("stage layer3", "stage_kernel<"), ("stage layer2", "SplitGeo<28,"), ("stage layer1", "SplitGeo<56,"),
                 ("conv_wring", "conv_wring_kernel<"), ("stem u8 fused", "stem_u8_kernel<"),
-                ("conv3x3_rows", "conv_rows_kernel<"), ("conv_fp8", "conv_fp8_kernel<"),
+                ("conv_fp8", "conv_fp8_kernel<"),
                 ("stage8 layer3", "stage8_kernel<")]
 
 

@@ -37,6 +37,7 @@ FR_OPT_MATCH_EXACT = 3
 FR_OPT_X3_MIN_ROWS = 4
 FR_OPT_STAGE_MIN_FILL = 5
 FR_OPT_STAGE_SPIN_LIMIT = 6
+FR_OPT_STAGE_VARIANT = 7
 
 c_int, c_int64, c_size_t, c_void_p, c_float_p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p
 
@@ -97,6 +98,12 @@ _SIGS = {
                                       ctypes.POINTER(c_int)]),
     "fr_debug_copy_tensor": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "fr_op_conv2d": (c_int, [ctypes.POINTER(FrConvDesc), c_void_p]),
+    "fr_area_resample_u8": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "fr_mtcnn_conv": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                              c_void_p, c_void_p]),
+    "fr_mtcnn_maxpool": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "fr_mtcnn_dense": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "fr_mtcnn_head": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "fr_op_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "fr_op_maxpool": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                               c_int, c_int, c_int, c_int, c_int, c_void_p]),

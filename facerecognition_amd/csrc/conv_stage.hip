@@ -53,9 +53,13 @@ constexpr int SNW = 8;                       // waves per workgroup: 2 pixel hal
 constexpr int FN = 4;                        // 16-channel fragments per wave
 constexpr int NPW = 16 * FN;                 // output channels per wave
 
+#ifndef FR_STAGE_SINGLE
+#define FR_STAGE_SINGLE 1  // 13-fragment kernel: one in-place refilled fragment set (0: two sets, A/B)
+#endif
 #ifndef FR_STAGE_EXP
 #define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 8 trivial epilogue (MFMAs kept), 16 no
-                        // patch reads in the loop, 128 epilogue tables replaced by constants (no loads)
+                        // patch reads in the loop, 32 every weight load reads K-step 0 (stage13), 128
+                        // epilogue tables replaced by constants (no loads)
 #endif
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -322,6 +326,255 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's weight loads retire before the wave ends
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// 13-fragment stage kernel (default).  The 196 pixels of an image are packed row-major into 13 fragments
+// of 16 (208 slots, 12 spare) instead of one fragment per 16-position row (14 fragments, 2 halo columns
+// each computed and discarded): 7 % fewer MFMAs.  The patch stores the halo ROWS too (16 rows x 16
+// positions per plane: row -1 and row 14 zero, columns -1 and 14 zero), so every tap of every lane is
+// base(pixel) + a compile-time shift: no per-lane border selects in the K loop.  Waves 0-3 take
+// fragments 0-6, waves 4-7 fragments 7-12 (one body per count): waves w and w + 4 share a SIMD (the
+// dispatcher places a workgroup's waves 0->2->1->3 cyclically), so every SIMD runs one 7- and one
+// 6-fragment wave, 13 fragments per SIMD (was 14).  Same K-steps, MFMA sequence per output and epilogue
+// arithmetic as stage_kernel: bit-identical results (tests/test_gpu_stage.py).
+constexpr int PROWS13 = 16;                     // stored rows: -1 .. 14
+constexpr int PLANE13_B = PROWS13 * SWP * 16;   // 4096
+constexpr int PATCH13_B = (SC / 8) * PLANE13_B; // 131072
+constexpr int TAB13 = PATCH13_B;
+constexpr int STAGE13_LDS = TAB13 + 2 * TS;     // 151552
+
+__device__ __forceinline__ int pix_pos13(int P) {  // patch position of pixel P (spare slots -> pixel 195)
+    P = P < SPIX ? P : SPIX - 1;
+    const int r = P / SW;
+    return (r + 1) * SWP + (P - r * SW) + 1;
+}
+
+template <bool F16, int FM, int NWV, bool SINGLE>
+__device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, const int wave, const int lane,
+                                             const int wn, const int f0) {
+    typedef Num<F16> T;
+    typedef typename T::frag frag;
+    const int b = blockIdx.x;
+    const int nconv = 2 * p.nblk;
+    const int total = nconv * KSTEPS;
+    const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)total * SLICE_B);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
+
+    // ---- initial patch (halo rows and columns read as zeros): 128 pieces of 1 KiB
+    {
+        const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * SPIX * SC * 2);
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
+        for (int u = 0; u < PATCH13_B / 1024 / NWV; ++u) {
+            const int piece = wave + NWV * u, q = piece * 64 + lane;
+            const int plane = q >> 8, pos = q & 255, r = (pos >> 4) - 1, c = (pos & 15) - 1;
+            const uint32_t src = (unsigned)r < (unsigned)SW && (unsigned)c < (unsigned)SW
+                                     ? (uint32_t)((((b * SPIX + r * SW + c) * SC) + plane * 8) * 2)
+                                     : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(smem + piece * 1024), 16, src, 0, 0, 0);
+        }
+    }
+    // B (patch) fragment j: pixel 16 (f0 + j) + (lane & 15) at plane (lane >> 4) of the K-step's group
+    int aoff[FM];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) aoff[j] = (lane >> 4) * PLANE13_B + pix_pos13(16 * (f0 + j) + (lane & 15)) * 16;
+    const uint32_t wvo = (uint32_t)((lane >> 4) * 4096 + (wn * NPW + (lane & 15)) * 16);
+
+    f32x4_t acc[FN][FM];
+    frag pA[FM], pB[FM];
+    auto pread = [&](frag (&pf)[FM], int cg, int tap) {
+        const char* pa = smem + cg * 4 * PLANE13_B + ((tap / 3 - 1) * SWP + tap % 3 - 1) * 16;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) pf[j] = *(const frag*)(pa + aoff[j]);
+    };
+    frag wq[3][FN];
+    auto wload = [&](frag (&w)[FN], int g) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+            w[i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wvo + i * 256,
+                                                                                  (FR_STAGE_EXP & 32) ? 0u : (uint32_t)g * SLICE_B, 0));
+    };
+    auto kstep = [&](int g, int r, frag (&cur)[FM], frag (&nxt)[FM], int cg_n, int tap_n) {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#if !(FR_STAGE_EXP & 16)
+        pread(nxt, cg_n, tap_n);
+#endif
+        wload(wq[(r + 2) % 3], g + 2 < total ? g + 2 : total - 1);
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wq[r][i], cur[j], acc[i][j]);
+    };
+    // SINGLE: ONE fragment set, refilled in place -- the 4 MFMAs of fragment j (one per weight fragment),
+    // then fragment j of the next step is read into the same registers, 4 (FM - 1) MFMAs of this wave
+    // before the next step uses it (the order is pinned: left alone, the scheduler sinks every read to
+    // the end of the step and the next step waits for them)
+    auto kstep1 = [&](int g, int r, frag (&pf)[FM], int cg_n, int tap_n) {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        wload(wq[(r + 2) % 3], g + 2 < total ? g + 2 : total - 1);
+        const char* pa = smem + cg_n * 4 * PLANE13_B + ((tap_n / 3 - 1) * SWP + tap_n % 3 - 1) * 16;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+#pragma unroll
+            for (int i = 0; i < FN; ++i) acc[i][j] = T::mfma(wq[r][i], pf[j], acc[i][j]);
+#if !(FR_STAGE_EXP & 16)
+            pf[j] = *(const frag*)(pa + aoff[j]);
+#endif
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, FN, 0);
+#pragma unroll
+        for (int q = 0; q < FM; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+    };
+
+    const size_t img = (size_t)b * SPIX * SC;
+    const __amdgpu_buffer_rsrc_t epr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.ep, 0, (uint32_t)((size_t)nconv * TAB_ROWS_B), 0x00020000);
+    const __amdgpu_buffer_rsrc_t slr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv * SC * 4), 0x00020000);
+    auto issue_tab = [&](int cv, int cv_slope, int slot) {
+        char* dst = smem + TAB13 + slot * TS;
+        int ln = opaque_tid() & 63;
+#pragma unroll
+        for (int u = 0; u < (TAB_ROWS_B / 1024 + NWV - 1) / NWV; ++u) {
+            const int piece = wave + NWV * u;
+            if (piece < TAB_ROWS_B / 1024)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(epr, (lds_void*)(dst + piece * 1024), 16,
+                                                         (uint32_t)(piece * 1024 + ln * 16), (uint32_t)(cv * TAB_ROWS_B), 0, 0);
+        }
+        if (cv_slope >= 0 && wave == NWV - 1)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(slr, (lds_void*)(dst + TAB_ROWS_B), 16, (uint32_t)(ln * 16),
+                                                     (uint32_t)(cv_slope * SC * 4), 0, 0);
+    };
+    // table-row byte offset of the border class of the lane's pixel in fragment j (ln: an opaque lane copy)
+    auto tab_row = [&](int j, int ln) {
+        int P = 16 * (f0 + j) + (ln & 15);
+        P = P < SPIX ? P : SPIX - 1;
+        const int r = P / SW, c = P - r * SW;
+        const int rc = r == 0 ? 0 : (r == SW - 1 ? 2 : 1), cc = c == 0 ? 0 : (c == SW - 1 ? 2 : 1);
+        return (3 * rc + cc) * SC * 4;
+    };
+    auto seed_bias = [&]() {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const char* t = smem + TAB13 + (wn * NPW + 4 * (ln >> 4)) * 4;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            const int tr = tab_row(j, ln);
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const float4 bb = *(const float4*)(t + tr + 64 * i);
+                acc[i][j] = (f32x4_t){bb.x, bb.y, bb.z, bb.w};
+            }
+        }
+    };
+    issue_tab(0, -1, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    wload(wq[0], 0);
+    wload(wq[1], 1);
+
+    auto run_conv = [&](int cv, auto second_tag) {
+        constexpr bool second = decltype(second_tag)::value;
+        if (!second) {
+            seed_bias();
+            if (cv + 1 < nconv) issue_tab(cv + 1, cv, 1);
+        } else if (cv + 1 < nconv) {
+            issue_tab(cv + 1, -1, 0);
+        }
+        pread(pA, 0, 0);
+        const int g0 = cv * KSTEPS;
+#pragma unroll 1
+        for (int cg = 0; cg < SC / 32; cg += 2) {
+#pragma unroll
+            for (int t = 0; t < 18; ++t) {
+                const int cgl = cg + t / 9, tap = t % 9;
+                const int cgn = t == 8 ? cg + 1 : (t == 17 ? cg + 2 : cgl);
+                const int tapn = t == 8 || t == 17 ? 0 : tap + 1;
+                if (SINGLE) kstep1(g0 + cgl * 9 + tap, tap % 3, pA, cgn, tapn);
+                else if (t & 1) kstep(g0 + cgl * 9 + tap, tap % 3, pB, pA, cgn, tapn);
+                else kstep(g0 + cgl * 9 + tap, tap % 3, pA, pB, cgn, tapn);
+            }
+        }
+        // ---- epilogue (as stage_kernel's): accumulators -> patch; spare-slot lanes write nothing
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int cl = ln & 15;
+        const char* t2 = smem + TAB13 + TS;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+            const int n = wn * NPW + 16 * i + 4 * (ln >> 4);
+            char* const pl = smem + (n >> 3) * PLANE13_B + (n & 7) * 2;
+            uint2 xin[FM];
+            float4 s1;
+            if (!second) {
+                const float4 sl = *(const float4*)(t2 + TAB_ROWS_B + n * 4);
+                s1 = make_float4(sl.x - 1.f, sl.y - 1.f, sl.z - 1.f, sl.w - 1.f);
+#pragma unroll
+                for (int j = 0; j < FM; ++j) xin[j] = *(const uint2*)(pl + pix_pos13(16 * (f0 + j) + cl) * 16);
+            }
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                const int P = 16 * (f0 + j) + cl;
+                char* slot = pl + pix_pos13(P) * 16;
+                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                if (!second) {
+                    v[0] = fmaf(s1.x, fminf(v[0], 0.f), v[0]);
+                    v[1] = fmaf(s1.y, fminf(v[1], 0.f), v[1]);
+                    v[2] = fmaf(s1.z, fminf(v[2], 0.f), v[2]);
+                    v[3] = fmaf(s1.w, fminf(v[3], 0.f), v[3]);
+                }
+                float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+                const uint4 pk = T::pack8(o8);
+                if (!second) {
+                    float f[8];
+                    T::unpack8(make_uint4(xin[j].x, xin[j].y, 0, 0), f);
+                    const float4 bb = *(const float4*)(t2 + tab_row(j, ln) + n * 4);
+                    acc[i][j] = (f32x4_t){f[0] + bb.x, f[1] + bb.y, f[2] + bb.z, f[3] + bb.w};
+                }
+                if (FM == 7 || (f0 + j) * 16 + 15 < SPIX || P < SPIX) *(uint2*)slot = make_uint2(pk.x, pk.y);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        bf16_t* dbg = nullptr;
+        if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
+        bf16_t* const yo = second && cv == nconv - 1 ? p.y : dbg;
+        if (yo) {
+            for (int c = opaque_tid(); c < SPIX * (SC / 8); c += 64 * NWV) {
+                const int pix = c / (SC / 8), pl = c - pix * (SC / 8);
+                const uint4 v = *(const uint4*)(smem + pl * PLANE13_B + pix_pos13(pix) * 16);
+                *(uint4*)(yo + img + (size_t)pix * SC + pl * 8) = v;
+            }
+            if (dbg && yo != dbg) {
+                for (int c = opaque_tid(); c < SPIX * (SC / 8); c += 64 * NWV) {
+                    const int pix = c / (SC / 8), pl = c - pix * (SC / 8);
+                    const uint4 v = *(const uint4*)(smem + pl * PLANE13_B + pix_pos13(pix) * 16);
+                    *(uint4*)(dbg + img + (size_t)pix * SC + pl * 8) = v;
+                }
+            }
+        }
+    };
+#pragma unroll 1
+    for (int blk = 0; blk < p.nblk; ++blk) {
+        run_conv(2 * blk, std::false_type{});
+        run_conv(2 * blk + 1, std::true_type{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool F16>
+__global__ __launch_bounds__(64 * SNW, 1) void stage13_kernel(StageArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave < 4) stage13_body<F16, 7, SNW, FR_STAGE_SINGLE>(p, smem, wave, lane, wave, 0);  // fragments 0..6
+    else stage13_body<F16, 6, SNW, FR_STAGE_SINGLE>(p, smem, wave, lane, wave - 4, 7);       // fragments 7..12
+}
+
 }  // namespace
 
 bool stage_supported(int B, int H, int W, int C) { return B > 0 && H == SW && W == SW && C == SC; }
@@ -343,16 +596,21 @@ void stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out) {
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t s) {
-    auto k = a.f16 ? stage_kernel<true> : stage_kernel<false>;
-    static bool attr[2] = {false, false};
-    if (!attr[a.f16 ? 1 : 0]) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, STAGE_LDS);
-        attr[a.f16 ? 1 : 0] = true;
+    // variant 1: the legacy 14-fragment kernel (bit-identical; FR_OPT_STAGE_VARIANT)
+    const int v = a.variant == 1 ? 1 : 0;
+    auto k = v == 1 ? (a.f16 ? stage_kernel<true> : stage_kernel<false>) : (a.f16 ? stage13_kernel<true> : stage13_kernel<false>);
+    const int lds = v == 1 ? STAGE_LDS : STAGE13_LDS;
+    const int threads = 64 * SNW;
+    static bool attr[4] = {false, false, false, false};
+    const int ai = 2 * v + (a.f16 ? 1 : 0);
+    if (!attr[ai]) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr[ai] = true;
     }
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, dim3(a.B), dim3(64 * SNW), STAGE_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
+        hipExtLaunchKernelGGL(k, dim3(a.B), dim3(threads), lds, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
     else
-        hipLaunchKernelGGL(k, dim3(a.B), dim3(64 * SNW), STAGE_LDS, s, a);
+        hipLaunchKernelGGL(k, dim3(a.B), dim3(threads), lds, s, a);
     return hipGetLastError();
 }
 

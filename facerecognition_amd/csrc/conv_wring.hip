@@ -44,9 +44,11 @@ struct WGeo {
     static constexpr int PPW = SROWS * ROWB / 1024 / NW;  // DMA pieces per wave per stage
     static constexpr int P = PPW + 2 * KSS;               // VMEM ops per stage (DMA + weight loads)
     static constexpr int LDS = EPI_B > NST * STAGE_B ? EPI_B : NST * STAGE_B;
-    // vmcnt when stage t waits for its DMA: ops younger than it (prologue DMA0..2, W0..2, then P a stage)
-    static constexpr int Y3 = 2 * KSS + 2 * P, Y0 = 2 * PPW + 6, Y1 = PPW + 6 + P;
-    static constexpr int Y2 = 6 + 2 * P < Y3 ? 6 + 2 * P : Y3;
+    // vmcnt when stage t's last substep waits for DMA(t + 1): VMEM ops younger than it (the prologue
+    // issues DMA0..3 then W0..2; stage t issues its KSS weight loads (2 ops each) and, after the
+    // boundary, DMA(t + 4)): t = 0 / 1 / >= 2
+    static constexpr int Yb0 = 2 * PPW + 2 * KSS + 6, Yb1 = 2 * PPW + 4 * KSS + 6, Yb = 2 * PPW + 6 * KSS;
+    static_assert(Yb0 <= 63 && Yb1 <= 63 && Yb <= 63, "vmcnt field");
     __device__ static int swz(int row) { return KSS == 2 ? (row >> 1) & 7 : row & 15; }
 };
 
@@ -117,12 +119,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
     }
     const int K1 = p.x2 ? p.K1 : p.Kpad;
     int r_cur = 0, s_cur = 0, c_cur = 0, k_cur = 0;  // the next stage to issue: tap (r, s), channel base
-    auto issue = [&](int slot) {
-        const char* dst = smem + slot * STAGE_B;
+    // a stage's DMA in two halves: prep (offsets of the next stage, VALU; may run before a barrier) and
+    // fire (the LDS-DMA issue into `slot`)
+    uint32_t d_off[PPW];
+    bool d_x2 = false;
+    auto prep = [&]() {
         // branch-free (x or the projection input x2 by selects): a branch around the DMAs made the
         // compiler's counted waits for the weight registers conservative
-        const bool kx2 = k_cur >= K1;  // projection K-steps: x2 at the output's stride-st2 position
-        const __amdgpu_buffer_rsrc_t rs = kx2 ? x2r : xr;
+        d_x2 = k_cur >= K1;  // projection K-steps: x2 at the output's stride-st2 position
         const uint32_t c2 = (uint32_t)((k_cur - K1) * 2);
         const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
 #pragma unroll
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
             const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
             const uint32_t o1 = ok ? a_base[i] + (uint32_t)soff : OOB;
             const uint32_t o2 = a_base2[i] == OOB ? OOB : a_base2[i] + c2;
-            dma16(rs, dst + (wave + NW * i) * 1024, kx2 ? o2 : o1);
+            d_off[i] = d_x2 ? o2 : o1;
         }
         if (FR_WRING_EXP & 2) return;
         k_cur += CH;
@@ -140,6 +144,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
             c_cur = 0;
             if (++s_cur == p.Kw) { s_cur = 0; ++r_cur; }
         }
+    };
+    auto fire = [&](int slot) {
+        const char* dst = smem + slot * STAGE_B;
+        const __amdgpu_buffer_rsrc_t rs = d_x2 ? x2r : xr;
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) dma16(rs, dst + (wave + NW * i) * 1024, d_off[i]);
+    };
+    auto issue = [&](int slot) {
+        prep();
+        fire(slot);
     };
 
     // ---- operand A: packed weights, lane (n = 16 i + (lane & 15) of the wave's 32, group lane >> 4)
@@ -173,62 +187,76 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-    // ---- prologue: stages 0..2, weight substeps 0..2 (vmcnt order: DMA0 DMA1 DMA2 (KSS ops each),
-    // W0 W1 W2 (2 each))
+    // ---- prologue: stages 0..3 into the four slots, weight substeps 0..2 (vmcnt order: DMA0 .. DMA3
+    // (PPW ops each), W0 W1 W2 (2 each)); stage 0 landed, its first B fragments read
     issue(0);
     issue(1);
     issue(2);
+    issue(3);
     wload(wq[0], 0);
     wload(wq[1], 1);
     wload(wq[2], 2);
+    wait_vm<3 * PPW + 6>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    bread(bq[0], 0, 0);
 
-    // Stage t issues (after its barrier) DMA(t + 3), then the weight loads of the substeps 3 ahead of its
-    // own: P = PPW + 2 KSS VMEM ops per stage, so WGeo::Y3 ops are younger than DMA(t) when stage t waits
-    // for it (t >= 3; Y0..Y2 before the ring is full).  Every stage issues all of them,
-    // unconditionally (a branch around them makes the compiler's own waits for the weight registers drain
-    // everything): past the end the DMAs re-fill slots nobody reads again (zeros, or in-bounds bytes of
-    // x2) and the weight loads repeat the last substep.
     auto mfmas = [&](int slot_w, frag (&b)[FM]) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wq[slot_w][i], b[j], acc[i][j]);
     };
+    // Stage t's LAST substep opens with the stage boundary: every wave's DMA of stage t + 1 landed (counted
+    // vmcnt + barrier), every wave is past its reads of stage t (all issued one substep earlier and drained
+    // by the lgkmcnt(0) before the barrier), so stage t's slot is refilled with stage t + 4 and stage
+    // t + 1's first B fragments are read while the last substep's MFMAs run: the barrier and the cold
+    // fragment read of a stage overlap MFMAs instead of preceding them.  Every stage issues all of its
+    // VMEM ops unconditionally (past the end the DMAs re-fill slots nobody reads again: zeros, or in-bounds
+    // bytes of x2, and the weight loads repeat the last substep); a branch around them made the compiler's
+    // own waits for the weight registers drain everything.  VMEM ops younger than DMA(t + 1) at that wait:
+    // WGeo::Yb(t) (the prologue's order makes t = 0, 1 differ).
     // 16 substeps per loop iteration: at the loop head the compiler cannot track the register ring
-    // carried around the back edge and waits for every outstanding load (the stage DMAs issued just
-    // before included), so the head should come rarely; a partial last iteration breaks out
+    // carried around the back edge, so the head should come rarely; a partial last iteration breaks out.
 #pragma unroll 1
     for (int s4 = 0; s4 < nks; s4 += 16) {
 #pragma unroll
         for (int u = 0; u < 16 / KSS; ++u) {
-            const int t = s4 / KSS + u, slot = t & (NST - 1);
+            const int t = s4 / KSS + u;
             if (u > 0 && KSS * t >= nks) break;
-            if (t >= 3) wait_vm<Gm::Y3>();
-            else if (t == 2) wait_vm<Gm::Y2>();
-            else if (t == 1) wait_vm<Gm::Y1>();
-            else wait_vm<Gm::Y0>();
-            // every wave's DMA of stage t landed; every wave is past its reads of stage t - 1, whose slot
-            // stage t + 3 refills
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            issue((t + 3) & (NST - 1));
-            bread(bq[0], slot, 0);
+            const int slot = t & (NST - 1), nslot = (t + 1) & (NST - 1);
 #pragma unroll
             for (int kk = 0; kk < KSS; ++kk) {
                 const int s = t * KSS + kk, w = (u * KSS + kk) & 3;  // s4 % 4 == 0: compile-time ring slots
                 __builtin_amdgcn_sched_barrier(0);
                 wload(wq[(w + 3) & 3], s + 3 < nks ? s + 3 : nks - 1);
-                if (kk + 1 < KSS) bread(bq[(kk + 1) & 1], slot, kk + 1);
-                mfmas(w, bq[kk & 1]);
-#if FR_WRING_SCHED
                 if (kk + 1 < KSS) {
+                    bread(bq[(kk + 1) & 1], slot, kk + 1);
+                    mfmas(w, bq[kk & 1]);
+#if FR_WRING_SCHED
 #pragma unroll
                     for (int q = 0; q < FM; ++q) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     }
-                }
 #endif
+                } else {
+                    prep();  // stage t + 4's offsets while the previous substep's MFMAs run
+                    if (t >= 2) wait_vm<Gm::Yb>();
+                    else if (t == 1) wait_vm<Gm::Yb1>();
+                    else wait_vm<Gm::Yb0>();
+                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                    fire(slot);  // stage t + 4 into stage t's slot
+                    bread(bq[(kk + 1) & 1], nslot, 0);
+                    mfmas(w, bq[kk & 1]);
+#if FR_WRING_SCHED
+#pragma unroll
+                    for (int q = 0; q < FM; ++q) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+#endif
+                }
             }
         }
     }

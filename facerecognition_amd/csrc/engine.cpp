@@ -163,6 +163,7 @@ struct fr_handle {
     int* fail_host = nullptr;
     int* fail_dev = nullptr;
     int spin_limit = 0;            // FR_OPT_STAGE_SPIN_LIMIT (0: the kernel's default, < 0: every wait runs out)
+    int stage_variant = 0;         // FR_OPT_STAGE_VARIANT (1: the legacy 14-fragment layer3 stage kernel)
     bool no_split = false;         // re-run of a failed forward: split stages off
     int64_t stage_reruns = 0;      // forwards re-run on the per-conv path after a run-out wait
     hipEvent_t chk_ev = nullptr;   // completion of the last synchronous-checked forward
@@ -1341,6 +1342,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.spin_timeouts = h->stage_spin;
                 a.fail_host = h->fail_dev;
                 a.spin_limit = h->spin_limit;
+                a.variant = h->stage_variant;
                 ProfScope ps(h, s);
                 ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
                 ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * 2.0;
@@ -1500,6 +1502,7 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->dtype = dtype;
     h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
     h->stage_mode = stage_default();
+    if (const char* e = getenv("FR_STAGE_VARIANT")) h->stage_variant = atoi(e) == 1 ? 1 : 0;  // A/B timing
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         h->n_cu = prop.multiProcessorCount;
@@ -1883,6 +1886,10 @@ int fr_set_option(fr_handle* h, int option, int value) {
             h->x3_min_rows = value;
             break;
         case FR_OPT_STAGE_SPIN_LIMIT: h->spin_limit = value; break;
+        case FR_OPT_STAGE_VARIANT:
+            if (value < 0 || value > 1) { set_error("fr_set_option: FR_OPT_STAGE_VARIANT is 0 or 1"); return FR_ERR_ARG; }
+            h->stage_variant = value;
+            break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;
     }
     drop_graphs(h);  // captured replays bake in the plan
@@ -1898,6 +1905,7 @@ int fr_get_option(const fr_handle* h, int option) {
         case FR_OPT_MATCH_EXACT: return h->match_exact ? 1 : 0;
         case FR_OPT_X3_MIN_ROWS: return (int)h->x3_min_rows;
         case FR_OPT_STAGE_SPIN_LIMIT: return h->spin_limit;
+        case FR_OPT_STAGE_VARIANT: return h->stage_variant;
         default: return FR_ERR_ARG;
     }
 }
@@ -2255,6 +2263,51 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
     }
     FR_HIP_CHECK(launch_conv(a, (hipStream_t)stream));
     FR_HIP_CHECK(launch_head_finalize(partial, split_k, B, N, Npad, bias, normalize, out, (hipStream_t)stream));
+    return FR_OK;
+}
+
+/* ---- MTCNN face detector building blocks (mtcnn.hip) ---- */
+int fr_area_resample_u8(const uint8_t* img, int H, int W, const int32_t* regions, int n, int oh, int ow, float* out,
+                        void* stream) {
+    if (!img || !regions || !out || H <= 0 || W <= 0 || n <= 0 || oh <= 0 || ow <= 0) {
+        set_error("fr_area_resample_u8: bad argument");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_area_resample(img, H, W, regions, n, oh, ow, out, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_mtcnn_conv(const float* x, int B, int H, int W, int Cin, const float* w, const float* bias, const float* slope,
+                  int Cout, int kh, int kw, float* y, void* stream) {
+    if (!x || !w || !y || B <= 0 || Cin <= 0 || Cout <= 0 || kh <= 0 || kw <= 0 || H < kh || W < kw) {
+        set_error("fr_mtcnn_conv: bad argument");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_mtcnn_conv(x, B, H, W, Cin, w, bias, slope, Cout, kh, kw, y, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_mtcnn_maxpool(const float* x, int B, int H, int W, int C, int k, int stride, float* y, void* stream) {
+    if (!x || !y || B <= 0 || C <= 0 || k <= 0 || stride <= 0 || H < 1 || W < 1) {
+        set_error("fr_mtcnn_maxpool: bad argument");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_mtcnn_maxpool(x, B, H, W, C, k, stride, pool_ceil_out(H, k, stride), pool_ceil_out(W, k, stride),
+                                      y, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_mtcnn_dense(const float* x, int B, int K, const float* w, const float* bias, const float* slope, int N, float* y,
+                   void* stream) {
+    if (!x || !w || !y || B <= 0 || K <= 0 || N <= 0) { set_error("fr_mtcnn_dense: bad argument"); return FR_ERR_ARG; }
+    FR_HIP_CHECK(launch_mtcnn_dense(x, B, K, w, bias, slope, N, y, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_mtcnn_head(const float* x, int64_t M, int C, const float* w, const float* bias, int n_out, float* out,
+                  void* stream) {
+    if (!x || !w || !bias || !out || M <= 0 || C <= 0 || n_out < 2) { set_error("fr_mtcnn_head: bad argument"); return FR_ERR_ARG; }
+    FR_HIP_CHECK(launch_mtcnn_head(x, M, C, w, bias, n_out, out, (hipStream_t)stream));
     return FR_OK;
 }
 

@@ -112,6 +112,7 @@ struct StageArgs {
     int* spin_timeouts;        // bounded-wait overruns (fr_debug_stage_timeouts); 0 when healthy
     int* fail_host;            // host-mapped flag: set to 1 (plain vector store) by any part whose wait ran out
     int spin_limit;            // sleeps before a wait counts as run out; < 0: every wait runs out (debug)
+    int variant;               // kernel variant (FR_OPT_STAGE_VARIANT): 0 default, 1 the legacy layout
     int B, nblk, f16, dbg;     // dbg: timing-only experiment switches (FR_STAGE_DBG), 0 in production
     void* ev0;
     void* ev1;
@@ -180,5 +181,18 @@ hipError_t launch_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out
                             hipStream_t s);
 hipError_t launch_warp_affine_u8(const uint8_t* in, int B, int H, int W, const double* M, uint8_t* out, int OH, int OW,
                                  hipStream_t s);
+
+// MTCNN face-detector building blocks (mtcnn.hip): f32 NHWC.
+hipError_t launch_area_resample(const uint8_t* img, int H, int W, const int32_t* regions, int n, int oh, int ow,
+                                float* out, hipStream_t s);
+hipError_t launch_mtcnn_conv(const float* x, int B, int H, int W, int Cin, const float* w, const float* bias,
+                             const float* slope, int Cout, int kh, int kw, float* y, hipStream_t s);
+hipError_t launch_mtcnn_maxpool(const float* x, int B, int H, int W, int C, int k, int st, int Ho, int Wo, float* y,
+                                hipStream_t s);
+hipError_t launch_mtcnn_dense(const float* x, int B, int K, const float* w, const float* bias, const float* slope,
+                              int N, float* y, hipStream_t s);
+hipError_t launch_mtcnn_head(const float* x, int64_t M, int C, const float* w, const float* bias, int NO, float* out,
+                             hipStream_t s);
+int pool_ceil_out(int H, int k, int s);
 
 }  // namespace fr

@@ -16,9 +16,10 @@ Reference → here:
   compute_prototypes :555-592 / build_faiss_index :595-645 (→ DeviceGallery, IndexFlatIP surface; the
                                  .faiss flat-index file format without faiss: faiss_io.py)
   build_db :765-835, extract_embeddings_from_csv :446-552, full_pipeline :838-888
-Face detection/alignment (FacePreprocessor, MTCNN) and t-SNE plotting are out of scope (SURVEY.md
-§2.1 rows 1/11): requesting them prints a warning and the raw image is used, exactly as the reference
-does when its detector is unavailable.
+  FacePreprocessor / FaceNetPreprocessor :188-345   device MTCNN + device alignment warp (face_detector.py,
+                                 SURVEY.md §8f row 4); without MTCNN weights the raw image is used, as the
+                                 reference does when its detector is unavailable.  t-SNE plotting is out of
+                                 scope.
 """
 from __future__ import annotations
 
@@ -230,12 +231,83 @@ def segment_means(model, groups: List[List[np.ndarray]]) -> List[Optional[np.nda
     return out
 
 
-def _folder_crops(folder: str, transform) -> List[np.ndarray]:
+class FacePreprocessor:
+    """Detect + align before embedding (reference :188-280): the device MTCNN (face_detector.FaceDetector,
+    confidence 0.9, largest face) and the device 5-point warp to ARCFACE_TEMPLATE; the margin crop when a
+    face has no landmarks.  Without MTCNN weights the detector is None and ``process`` returns the raw
+    image, as the reference does without facenet-pytorch."""
+
+    out_size = 112
+
+    def __init__(self, device: str = "cuda", weights_dir: str = None, detector=None):
+        self.device = device
+        self.detector = detector
+        if self.detector is None:
+            try:
+                from .face_detector import FaceDetector
+                self.detector = FaceDetector(backend="mtcnn", device=device, confidence_threshold=0.9,
+                                             select_largest=True, weights_dir=weights_dir)
+                print(f"[OK] {type(self).__name__} initialized (MTCNN)")
+            except Exception as e:
+                print(f"[WARN] Khong the khoi tao Face Detector: {e}")
+                self.detector = None
+
+    def _raw(self, rgb):
+        from PIL import Image
+        return Image.fromarray(rgb)
+
+    def _face(self, rgb, det):
+        from PIL import Image
+        from .align import align_faces
+        import torch
+        lm = det.get("landmarks")
+        if lm:
+            x = torch.as_tensor(np.ascontiguousarray(rgb))[None].to(self.detector.detector.device)
+            crops, ok = align_faces(x, [lm])
+            if ok[0]:
+                return Image.fromarray(crops[0].cpu().numpy())
+        return self._crop(rgb)
+
+    def _crop(self, rgb):
+        from PIL import Image
+        c = self.detector.crop_face(np.ascontiguousarray(rgb[..., ::-1]), margin=0.2,
+                                    target_size=(self.out_size, self.out_size))
+        return Image.fromarray(np.ascontiguousarray(c[..., ::-1])) if c is not None else None
+
+    def process(self, img_input):
+        """Path or BGR u8 array -> PIL RGB face (or the raw image without a detector), None if no face."""
+        from PIL import Image
+        if isinstance(img_input, str):
+            rgb = np.asarray(Image.open(img_input).convert("RGB"), dtype=np.uint8)
+        else:
+            rgb = np.ascontiguousarray(np.asarray(img_input, dtype=np.uint8)[..., ::-1])
+        if self.detector is None:
+            return self._raw(rgb)
+        det = self.detector.detect_rgb(rgb)
+        return None if det is None else self._face(rgb, det)
+
+
+class FaceNetPreprocessor(FacePreprocessor):
+    """FaceNet's detect + crop (reference :283-345): the margin-0.2 crop resized to 160 x 160 (no alignment);
+    without a detector the raw image resized to 160 x 160."""
+
+    out_size = 160
+
+    def _raw(self, rgb):
+        from PIL import Image
+        return Image.fromarray(rgb).resize((160, 160))
+
+    def _face(self, rgb, det):
+        return self._crop(rgb)
+
+
+def _folder_crops(folder: str, transform, preprocessor=None) -> List[np.ndarray]:
     paths = [os.path.join(folder, f) for f in os.listdir(folder) if f.lower().endswith(IMG_EXTS)]
     imgs = []
     for p in paths:  # os.listdir order, as the reference
         try:
-            imgs.append(_load_u8(p, transform))
+            face = preprocessor.process(p) if preprocessor is not None else None  # reference :744-749
+            imgs.append(_load_u8(face if face is not None else p, transform))
         except Exception as e:
             print(f"Loi xu ly {p}: {e}")
     return imgs
@@ -246,9 +318,7 @@ def extract_embedding_for_folder(folder: str, model, transform, device: str = "c
     if not os.path.exists(folder):
         return None
     _check_transform(model, transform)
-    if preprocessor is not None:
-        print("[WARN] face detection/alignment is out of scope for facerecognition_amd; using raw images")
-    return segment_means(model, [_folder_crops(folder, transform)])[0]
+    return segment_means(model, [_folder_crops(folder, transform, preprocessor)])[0]
 
 
 def compute_prototypes(embeddings: np.ndarray, labels: np.ndarray, output_path: str = None) -> np.ndarray:
@@ -318,8 +388,9 @@ def build_db(model_path: str, root_folder: str = "data/celeb", save_path: str = 
     else:
         model, _ = load_arcface_model(model_path, device)
         transform = get_transform(Wt.INPUT_SIZE[model.arch])
-    if use_face_detection:
-        print("[WARN] face detection/alignment is out of scope for facerecognition_amd; using raw images")
+    preprocessor = None
+    if use_face_detection:  # reference :800-805
+        preprocessor = (FaceNetPreprocessor if model_type == "facenet" else FacePreprocessor)(device=device)
     db: Dict[str, np.ndarray] = {}
     persons = [p for p in os.listdir(root_folder) if os.path.isdir(os.path.join(root_folder, p))]
     print(f"\nTim thay {len(persons)} celebrities")
@@ -338,7 +409,7 @@ def build_db(model_path: str, root_folder: str = "data/celeb", save_path: str = 
 
     for person in persons:
         pending.append(person)
-        groups.append(_folder_crops(os.path.join(root_folder, person), transform))
+        groups.append(_folder_crops(os.path.join(root_folder, person), transform, preprocessor))
         if sum(len(g) for g in groups) >= FLUSH_IMAGES or sum(a.nbytes for g in groups for a in g) >= FLUSH_BYTES:
             flush()
     flush()

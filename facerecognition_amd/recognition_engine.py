@@ -16,8 +16,11 @@ Reference → here:
   add_to_db / save_db / get_db_identities / set_threshold :391-435, :165-167
   FaceNetMatcher                      the FaceNet web route's matcher (web_app.py:537-559): renormalized
                                        rows, score + L2 distance, threshold
-Face detection/alignment (MTCNN) is out of scope: with ``use_face_detection=True`` the engine reports the
-detector as unavailable and continues without it — the reference's own fallback (:122-124).
+  detect_and_align / align_face :169-242  device MTCNN (face_detector.FaceDetector) +
+                                       the device 5-point warp to ARCFACE_TEMPLATE (align.align_faces); the
+                                       crop fallback when a face has no landmarks.  Without MTCNN weights
+                                       the detector is unavailable and the engine runs on the raw image:
+                                       the reference's own fallback without facenet-pytorch (:122-124).
 
 The device gallery is rebuilt lazily whenever the db changes (``engine.db = {...}``, ``add_to_db``, or
 item assignment on ``engine.db``).  Scores are f32 inner products computed on the GPU; they agree with
@@ -123,7 +126,8 @@ class _TrackedDB(dict):
 class RecognitionEngine:
     def __init__(self, model_path: str = "models/checkpoints/arcface/arcface_best.pth", db_path: str = None,
                  faiss_index_path: str = None, prototypes_path: str = None, label_mapping_path: str = None,
-                 device: str = None, threshold: float = 0.5, use_face_detection: bool = True, model=None):
+                 device: str = None, threshold: float = 0.5, use_face_detection: bool = True, model=None,
+                 face_detector=None, mtcnn_weights: str = None):
         self.device = device or "cuda"
         self.threshold = threshold
         self.use_face_detection = use_face_detection
@@ -133,10 +137,16 @@ class RecognitionEngine:
         elif model_path and os.path.exists(model_path):
             self.model, self.model_info = load_arcface_model(model_path, self.device)
         self.transform = get_transform(Wt.INPUT_SIZE[self.model.arch] if self.model is not None else 112)
-        self.face_detector = None
-        if self.use_face_detection:
-            print("Khong the khoi tao Face Detector: face detection is out of scope for facerecognition_amd")
-            self.use_face_detection = False
+        self.face_detector = face_detector
+        if self.use_face_detection and self.face_detector is None:
+            try:
+                from .face_detector import FaceDetector
+                self.face_detector = FaceDetector(backend="mtcnn", device=self.device, confidence_threshold=0.9,
+                                                  select_largest=True, weights_dir=mtcnn_weights)
+                print("Face detector initialized (MTCNN)")
+            except Exception as e:  # reference :122-124
+                print(f"Khong the khoi tao Face Detector: {e}")
+                self.use_face_detection = False
         self._db = None
         self._g = None          # (key, DeviceGallery, names)
         self.faiss_index = None
@@ -179,11 +189,55 @@ class RecognitionEngine:
         self.threshold = threshold
         print(f"Threshold set to: {threshold}")
 
-    def align_face(self, image, landmarks):  # detector-based alignment: out of scope
-        return None
+    def align_face(self, image: np.ndarray, landmarks: Dict) -> Optional[np.ndarray]:
+        """5-point similarity warp of a u8 [H, W, 3] image to ARCFACE_TEMPLATE (112 x 112, border 0) on the
+        device (reference :169-204: skimage SimilarityTransform + cv2.warpAffine); None when every
+        landmark is zero.  Channel order is kept (the reference passes BGR, the warp is per channel)."""
+        import torch
+        from .align import align_faces
+        try:
+            dev = self.model.device if self.model is not None else torch.device("cuda", _device_index(self.device))
+            x = torch.as_tensor(np.ascontiguousarray(image, dtype=np.uint8))[None].to(dev)
+            crops, ok = align_faces(x, [landmarks])
+            return crops[0].cpu().numpy() if ok[0] else None
+        except Exception as e:
+            print(f"Loi align face: {e}")
+            return None
 
-    def detect_and_align(self, img_input):  # MTCNN: out of scope
-        return None
+    def detect_and_align(self, img_input):
+        """Detect (device MTCNN) and align the largest confident face: PIL RGB 112 x 112, the margin crop
+        when the face has no landmarks, or None (reference :206-242)."""
+        from PIL import Image
+        if self.face_detector is None:
+            return None
+        try:
+            if isinstance(img_input, str):
+                rgb = np.asarray(Image.open(img_input).convert("RGB"), dtype=np.uint8)
+            elif isinstance(img_input, Image.Image):
+                rgb = np.asarray(img_input.convert("RGB"), dtype=np.uint8)
+            else:  # numpy BGR, as the reference's cv2 images
+                rgb = np.ascontiguousarray(np.asarray(img_input, dtype=np.uint8)[..., ::-1])
+        except Exception:
+            return None
+        det = self.face_detector.detect_rgb(rgb)
+        if det is None:
+            return None
+        lm = det.get("landmarks")
+        if lm:
+            aligned = self.align_face(rgb, lm)
+            if aligned is not None:
+                return Image.fromarray(aligned)
+        cropped = self.face_detector.crop_face(np.ascontiguousarray(rgb[..., ::-1]), margin=0.2, target_size=(112, 112))
+        return Image.fromarray(np.ascontiguousarray(cropped[..., ::-1])) if cropped is not None else None
+
+    def _detected(self, img_input):
+        """The image the embedding is taken from: the aligned face when detection is on and finds one
+        (reference extract_embedding :256-263), else the input."""
+        if self.use_face_detection and self.face_detector is not None:
+            aligned = self.detect_and_align(img_input)
+            if aligned is not None:
+                return aligned
+        return img_input
 
     def _db_gallery(self):
         """Device copies of the dict db for cosine_similarity semantics (recognition_engine.py:41-63):
@@ -216,7 +270,7 @@ class RecognitionEngine:
         if self.model is None:
             print("Model chua duoc load")
             return None
-        return extract_embedding_single(img_input, self.model, self.transform, self.device)
+        return extract_embedding_single(self._detected(img_input), self.model, self.transform, self.device)
 
     # ------------------------------------------------------------------ matching
     @staticmethod
@@ -316,7 +370,7 @@ class RecognitionEngine:
         if self.model is not None:
             for n, img in enumerate(img_inputs):
                 try:
-                    crops.append(_load_u8(img, self.transform))
+                    crops.append(_load_u8(self._detected(img), self.transform))
                     ok.append(n)
                 except Exception as e:
                     if isinstance(img, str):
@@ -354,7 +408,7 @@ class RecognitionEngine:
         if self.model is not None:
             for img in img_inputs:
                 try:
-                    crops.append(_load_u8(img, self.transform))
+                    crops.append(_load_u8(self._detected(img), self.transform))
                 except Exception as e:
                     if isinstance(img, str):
                         print(f"Loi xu ly {img}: {e}")

@@ -153,6 +153,28 @@ int fr_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, i
 int fr_warp_affine_u8(const uint8_t* in, int B, int H, int W, const double* M, uint8_t* out, int OH, int OW,
                       void* stream);
 
+/* ---- face detection before the path: the building blocks of the device MTCNN
+ *      (facerecognition_amd/face_detector.py), replacing facenet-pytorch's MTCNN behind
+ *      FaceDetector._detect_mtcnn (preprocessing/face_detector.py:78-97, 144-210).  f32 NHWC tensors. ---- */
+
+/* F.interpolate(mode='area') of u8 RGB regions + (x - 127.5) * 0.0078125 (detect_face's imresample and
+ * normalisation): regions (device int32 [n][5]) = image index, y0, x0, h, w inside img [*, H, W, 3];
+ * out (device f32) [n, oh, ow, 3].  Bit-identical to torch's CPU adaptive average pooling. */
+int fr_area_resample_u8(const uint8_t* img, int H, int W, const int32_t* regions, int n, int oh, int ow, float* out,
+                        void* stream);
+/* Valid (unpadded) stride-1 conv, weights [Cout][kh][kw][Cin], + bias, then PReLU when slope != NULL. */
+int fr_mtcnn_conv(const float* x, int B, int H, int W, int Cin, const float* w, const float* bias, const float* slope,
+                  int Cout, int kh, int kw, float* y, void* stream);
+/* MaxPool2d(k, stride, ceil_mode=True): y [B, Ho, Wo, C] with Ho = ceil((H - k) / stride) + 1 (torch's rule). */
+int fr_mtcnn_maxpool(const float* x, int B, int H, int W, int C, int k, int stride, float* y, void* stream);
+/* Linear: y [B, N] = x [B, K] . w [N, K]^T + bias, then PReLU when slope != NULL. */
+int fr_mtcnn_dense(const float* x, int B, int K, const float* w, const float* bias, const float* slope, int N, float* y,
+                   void* stream);
+/* Net heads: out [M, n_out] = x [M, C] . w [n_out, C]^T + bias, columns 0-1 replaced by their softmax
+ * (face probability in column 1), the rest raw (box regression, landmarks). */
+int fr_mtcnn_head(const float* x, int64_t M, int C, const float* w, const float* bias, int n_out, float* out,
+                  void* stream);
+
 /* ---- op-level entry points (kernel parity tests and custom graphs) ---- */
 
 /* Implicit-GEMM convolution on NHWC bf16 with fused epilogue:
@@ -253,6 +275,10 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * part waits for a neighbour's boundary rows before the wait counts as run out.  < 0 makes every wait
  * run out at once (debug: exercises the NaN poisoning, the re-run and FR_ERR_STAGE deterministically). */
 #define FR_OPT_STAGE_SPIN_LIMIT 6
+/* FR_OPT_STAGE_VARIANT (default 0): the layer3 stage kernel's pixel layout -- 0: 13 fragments of 16 pixels
+ * per image (196 of 208 slots used), 1: the legacy 14 rows of 16 positions (2 halo columns computed and
+ * discarded per row).  Both give the same bits (A/B and regression tests). */
+#define FR_OPT_STAGE_VARIANT 7
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);
 /* Number of probes (since the gallery was first split) whose bf16x3 candidate proof failed and were

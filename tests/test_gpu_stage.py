@@ -219,3 +219,27 @@ def test_two_handles_share_a_device(gpu):
     assert a.stage_timeouts() == 0 and b.stage_timeouts() == 0
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("dtype,B", [("bf16", 5), ("f16", 3), ("bf16", 256)])
+def test_stage_variants_bit_identical(gpu, dtype, B):
+    """The 13-fragment layer3 stage kernel (default) and the legacy 14-row layout (FR_OPT_STAGE_VARIANT 1)
+    run the same K-steps and epilogue arithmetic: every layer3 intermediate and every embedding is
+    bit-identical, at padded fragment counts and at the full bs = 256 grid."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("iresnet100", dtype=dtype)
+    x = torch.from_numpy(synthetic_crops(B, 112, seed=60 + B))
+    names = {"layer3.1.prelu", "layer3.1", "layer3.2.prelu", "layer3.15", "layer3.29"}
+    m.set_option(N.FR_OPT_STAGE, 2)
+    m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)
+    out = {}
+    for v in (0, 1):
+        m.set_option(N.FR_OPT_STAGE_VARIANT, v)
+        e = m.embed(x).cpu().numpy()
+        out[v] = (e, _named(m, B, names))
+    m.close()
+    for v in (1,):
+        assert np.array_equal(out[0][0], out[v][0]), v
+        for n in names:
+            assert torch.equal(out[0][1][n], out[v][1][n]), (v, n)
