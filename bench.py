@@ -43,10 +43,10 @@ PROF_STRIDE = 8  # roofline: sample every 8th dominant-kernel launch (event over
 
 # bench kernel class (fr_prof_get name prefix) -> rocprofv3 kernel-name fragment of its dispatches (only
 # classes whose kernel instantiation serves no other class: the two conv_rows classes share one)
-CLASS_KERNEL = [("stage layer3", "stage_kernel<"), ("stage layer2", "SplitGeo<28,"), ("stage layer1", "SplitGeo<56,"),
-                ("conv_wring", "conv_wring_kernel<"), ("stem u8 fused", "stem_u8_kernel<"),
-                ("conv_fp8", "conv_fp8_kernel<"),
-                ("stage8 layer3", "stage8_kernel<")]
+CLASS_KERNEL = [("stage layer3", ("::stage13_kernel", "::stage_kernel<")), ("stage layer2", ("SplitGeo<28,",)),
+                ("stage layer1", ("SplitGeo<56,",)), ("conv_wring", ("conv_wring_kernel<",)),
+                ("stem u8 fused", ("stem_u8_kernel<",)), ("conv_fp8", ("conv_fp8_kernel<",)),
+                ("stage8 layer3", ("::stage8_kernel",))]
 
 
 def pmc_passes(args):
@@ -88,7 +88,7 @@ def class_traffic(cls, pmc):
     frag = next((k for c, k in CLASS_KERNEL if cls.startswith(c)), None)
     if frag is None or not pmc:
         return None
-    ks = [k for k in pmc if frag in k]
+    ks = [k for k in pmc if any(f in k for f in frag)]
     n = sum(pmc[k][2] for k in ks)
     return round(sum(pmc[k][0] + pmc[k][1] for k in ks) / n) if n else None
 

@@ -91,6 +91,9 @@ struct StageRec {
     float* ep = nullptr;                  // [2*nblk][9][256] epilogue bias per border class
     float* slope = nullptr;               // [2*nblk][256] negative-side factor (slope / 0 / 1)
     bf16_t** dbg = nullptr;               // [2*nblk] device pointer table: x outputs then t outputs
+    bool fp8 = false;                     // e4m3 stage (conv_stage8.hip): the members carry .wscale
+    uint8_t* w8 = nullptr;                // fp8: stage8_pack_weights images of all convs
+    float* wscale = nullptr;              // fp8: [2*nblk][256] per-channel weight scales
 };
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -155,6 +158,7 @@ struct fr_handle {
     int proj_d = 0;
     float* emb_pre = nullptr;  // [max_batch][512] IRV1 output before the projection
     float* amax = nullptr;     // FR_DTYPE_FP8: per-tensor max |x| of the current forward [ntensors]
+    std::vector<char> need_amax;  // per tensor: the input of a per-conv e4m3 conv (its producer writes amax)
     bf16_t* stage_xchg = nullptr;  // split-stage boundary rows (split_stage_xchg_elems(max_batch), reserve)
     int* stage_flags = nullptr;    // split-stage progress counters [stage][max_batch][4], never reset
     int* stage_spin = nullptr;     // split-stage bounded-wait overruns (fr_debug_stage_timeouts)
@@ -502,14 +506,16 @@ struct Builder {
     }
 
     // whether a residual block's downsample folds into its last conv (igemm K-concatenation): not for
-    // fp8 (its conv kernel has no projection source) and only on the 64-channel fast-K path;
+    // e4m3 convs (the fp8 kernel has no projection source) and only on the 64-channel fast-K path;
     // FR_NO_DS_FUSE=1 keeps the separate downsample conv (A/B)
-    bool fuse_ds(int cin, int c2) const {
+    // whether conv `name` runs in e4m3 (FR_DTYPE_FP8 and the blob's plan gave it a .wscale)
+    bool is_fp8(const std::string& name) { return h->dtype == FR_DTYPE_FP8 && find(name + ".wscale"); }
+    bool fuse_ds(int cin, int c2, const std::string& pre) {
         static const bool off = [] {
             const char* e = getenv("FR_NO_DS_FUSE");
             return e && e[0] == '1';
         }();
-        return !off && h->dtype != FR_DTYPE_FP8 && cin % 64 == 0 && c2 % 64 == 0;
+        return !off && !is_fp8(pre + ".conv2") && !is_fp8(pre + ".downsample") && cin % 64 == 0 && c2 % 64 == 0;
     }
     void maxpool(int in, int out, int out_off, int k, int s, int p) {
         Op op;
@@ -565,8 +571,10 @@ struct Builder {
 // Packs a stage's weights (from the member convs' [Npad][Kpad] device images) and its epilogue table.
 int build_stage(fr_handle* h, StageRec& r) {
     const int nconv = 2 * r.nblk, C = r.C;
-    const size_t wbytes = r.parts > 1 ? split_stage_weight_bytes(C, nconv) : stage_weight_bytes(nconv);
+    const size_t wbytes = r.fp8 ? 0 : (r.parts > 1 ? split_stage_weight_bytes(C, nconv) : stage_weight_bytes(nconv));
     std::vector<bf16_t> packed(wbytes / sizeof(bf16_t));
+    std::vector<uint8_t> packed8(r.fp8 ? stage8_weight_bytes(nconv) : 0);
+    std::vector<float> wsc(r.fp8 ? (size_t)nconv * C : 0);
     std::vector<StageConv> tab(nconv);
     std::vector<float> ep((size_t)nconv * 9 * C, 0.f), sl((size_t)nconv * C, 0.f);
     const size_t per = packed.size() / nconv;
@@ -582,10 +590,21 @@ int build_stage(fr_handle* h, StageRec& r) {
             set_error("plan: stage member conv has an unexpected activation / residual");
             return FR_ERR_ARG;
         }
-        std::vector<bf16_t> rows((size_t)cw.Npad * cw.Kpad);
-        FR_HIP_CHECK(hipMemcpy(rows.data(), cw.w, rows.size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
-        if (r.parts > 1) split_stage_pack_weights(rows.data(), cw.Kpad, C, packed.data() + c * per);
-        else stage_pack_weights(rows.data(), cw.Kpad, C, packed.data() + c * per);
+        if (r.fp8) {
+            if (!cw.w8 || !cw.wscale || cw.Kpad8 != 9 * C || C != 256) {
+                set_error("plan: fp8 stage member conv without e4m3 weights");
+                return FR_ERR_ARG;
+            }
+            std::vector<uint8_t> rows8((size_t)cw.Npad * cw.Kpad8);
+            FR_HIP_CHECK(hipMemcpy(rows8.data(), cw.w8, rows8.size(), hipMemcpyDeviceToHost));
+            stage8_pack_weights(rows8.data(), cw.Kpad8, packed8.data() + (size_t)c * (packed8.size() / nconv));
+            FR_HIP_CHECK(hipMemcpy(wsc.data() + (size_t)c * C, cw.wscale, C * sizeof(float), hipMemcpyDeviceToHost));
+        } else {
+            std::vector<bf16_t> rows((size_t)cw.Npad * cw.Kpad);
+            FR_HIP_CHECK(hipMemcpy(rows.data(), cw.w, rows.size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
+            if (r.parts > 1) split_stage_pack_weights(rows.data(), cw.Kpad, C, packed.data() + c * per);
+            else stage_pack_weights(rows.data(), cw.Kpad, C, packed.data() + c * per);
+        }
         tab[c].bias = cw.bias9 ? nullptr : cw.bias;
         tab[c].bias9 = cw.bias9;
         tab[c].slope = cw.slope;
@@ -607,8 +626,9 @@ int build_stage(fr_handle* h, StageRec& r) {
         else
             std::fill(f, f + C, op.act == 1 ? 0.f : 1.f);
     }
-    int rc = upload(h, &r.w, packed);
+    int rc = r.fp8 ? upload(h, &r.w8, packed8) : upload(h, &r.w, packed);
     if (rc) return rc;
+    if (r.fp8 && (rc = upload(h, &r.wscale, wsc))) return rc;
     rc = upload(h, &r.table, tab);
     if (rc) return rc;
     if ((rc = upload(h, &r.ep, ep))) return rc;
@@ -657,30 +677,47 @@ void build_iresnet100(Builder& b) {
     int H = 112, C = 64;
     for (int l = 0; l < 4; ++l) {
         const int P = planes[l], Ho = H / 2;
-        // layer3 blocks 1.. (stride 1, 14x14x256) and layer2 blocks 1.. (28x28x128): also emitted as one
-        // LDS-resident stage op each
+        // layer3 blocks 1.. (stride 1, 14x14x256) and layer2 / layer1 blocks 1..: also emitted as
+        // LDS-resident stage ops.  Under FR_DTYPE_FP8 the blocks whose convs carry .wscale (the mixed
+        // plan, weights.FP8_PLAN) form an e4m3 stage of their own (14x14x256 only), the rest bf16 stages.
         int st_op = -1;
         StageRec rec;
+        auto close_stage = [&]() {
+            if (st_op >= 0 && !b.rc) {
+                rec.out = x;
+                rec.nblk = (int)rec.t_tensors.size();
+                for (int oi : rec.conv_ops) h->ops[oi].stage = h->ops[st_op].stage;
+                b.rc = build_stage(h, rec);
+                h->stages.push_back(rec);
+            }
+            st_op = -1;
+        };
         for (int i = 0; i < nblk[l]; ++i) {
             const bool s14 = stage_supported(1, Ho, Ho, P);
             const int parts = split_stage_parts(Ho, Ho, P);
-            if (i == 1 && h->dtype != FR_DTYPE_FP8 && (s14 || parts) && P == C) {
+            const std::string pre = L(l + 1, i);
+            const bool f8 = b.is_fp8(pre + ".conv1") && b.is_fp8(pre + ".conv2");
+            const bool mixed = b.is_fp8(pre + ".conv1") != b.is_fp8(pre + ".conv2");
+            const bool can = i >= 1 && P == C && !mixed && (f8 ? s14 : (s14 || parts > 0));
+            if (st_op >= 0 && (!can || f8 != rec.fp8)) close_stage();
+            if (can && st_op < 0) {
                 st_op = (int)h->ops.size();
+                rec = StageRec{};
                 rec.in = x;
                 rec.parts = s14 ? 1 : parts;
                 rec.H = Ho;
                 rec.C = P;
+                rec.fp8 = f8;
                 Op op;
                 op.kind = OP_STAGE;
                 op.stage = (int)h->stages.size();
                 h->ops.push_back(op);
             }
-            const std::string pre = L(l + 1, i);
             const int Hin = i == 0 ? H : Ho, st = i == 0 ? 2 : 1;
             const int hmid = b.tensor(Hin, Hin, P, pre + ".prelu");
             b.conv({pre + ".conv1"}, x, 0, C, hmid, 0, 3, 3, 1, 1, 1, 1, 2);
             int res = x;
-            const bool fuse = i == 0 && b.fuse_ds(P, C);
+            const bool fuse = i == 0 && b.fuse_ds(P, C, pre);
             if (i == 0 && !fuse) {
                 res = b.tensor(Ho, Ho, P, pre + ".downsample");
                 b.conv({pre + ".downsample"}, x, 0, C, res, 0, 1, 1, 2, 2, 0, 0, 0);
@@ -700,13 +737,7 @@ void build_iresnet100(Builder& b) {
             x = y;
             C = P;
         }
-        if (st_op >= 0 && !b.rc) {
-            rec.out = x;
-            rec.nblk = (int)rec.t_tensors.size();
-            for (int oi : rec.conv_ops) h->ops[oi].stage = h->ops[st_op].stage;
-            b.rc = build_stage(h, rec);
-            h->stages.push_back(rec);
-        }
+        close_stage();
         H = Ho;
     }
     b.head(x);
@@ -728,7 +759,7 @@ int build_img_weights(fr_handle* h) {
         if (op.res >= 0) { a.res = (const bf16_t*)1; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
         a.f16 = h->dtype == FR_DTYPE_F16;
         int ic = 0;
-        if (h->dtype == FR_DTYPE_FP8) continue;
+        if (cw.w8) continue;  // e4m3 convs: conv_fp8.hip or the fp8 stage only
         if (!cw.wring) {  // conv_wring.hip substep images (the autotuner decides per shape whether they run)
             ConvArgs w = a;
             w.K = cw.K;
@@ -808,7 +839,7 @@ void build_resnet50(Builder& b) {
             const int h2 = b.tensor(Ho, Ho, P);
             b.conv({pre + ".conv2"}, h1, 0, P, h2, 0, 3, 3, s, s, 1, 1, 1);
             int id = x;
-            const bool fuse = i == 0 && b.fuse_ds(P, C);
+            const bool fuse = i == 0 && b.fuse_ds(P, C, pre);
             if (i == 0 && !fuse) {
                 id = b.tensor(Ho, Ho, 4 * P, pre + ".downsample");
                 b.conv({pre + ".downsample"}, x, 0, C, id, 0, 1, 1, s, s, 0, 0, 0);
@@ -960,7 +991,7 @@ int reserve(fr_handle* h, int maxB) {
     h->partial = (float*)p;
     h->partial_floats = need;
     h->max_batch = maxB;
-    if (h->dtype == FR_DTYPE_FP8) {
+    if (std::any_of(h->need_amax.begin(), h->need_amax.end(), [](char c) { return c != 0; })) {
         void* q = nullptr;
         rc = dev_alloc(&q, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float));
         if (rc) { free_acts(h); return rc; }
@@ -1345,17 +1376,24 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.variant = h->stage_variant;
                 ProfScope ps(h, s);
                 ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
-                ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * 2.0;
+                ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * (r.fp8 ? 1.0 : 2.0);
+                if (r.fp8) {
+                    a.w = (const bf16_t*)r.w8;
+                    a.wscale = r.wscale;
+                    ps.start("stage8 layer3");
+                    FR_HIP_CHECK(launch_stage8(a, s));
+                    break;
+                }
                 ps.start(r.H == 14 ? "stage layer3" : (r.H == 28 ? "stage layer2" : "stage layer1"));
                 FR_HIP_CHECK(r.parts > 1 ? launch_split_stage(a, r.H, r.C, s) : launch_stage(a, s));
                 break;
             }
             case OP_PRE: {
                 ProfScope ps(h, s);
-                // u8 crops: preprocess + stem conv in one launch (conv_stem.hip).  Not under fp8, whose
-                // next conv needs the stem output's amax from the conv epilogue.
-                if (op.fuse_stem && in_fmt == FR_IN_U8_NHWC && !h->amax && stem_fuse_enabled() && oi + 1 < h->ops.size() &&
-                    h->ops[oi + 1].kind == OP_CONV) {
+                // u8 crops: preprocess + stem conv in one launch (conv_stem.hip).  Not when an e4m3 conv
+                // reads the stem output (it needs the amax from the conv epilogue).
+                if (op.fuse_stem && in_fmt == FR_IN_U8_NHWC && stem_fuse_enabled() && oi + 1 < h->ops.size() &&
+                    h->ops[oi + 1].kind == OP_CONV && !(h->amax && h->need_amax[h->ops[oi + 1].out])) {
                     const Op& cv = h->ops[oi + 1];
                     const auto& cw = h->convw[cv.wi];
                     const auto& to = h->tensors[cv.out];
@@ -1401,13 +1439,13 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                     a.y2 = h->tensors[op.out2].dev; a.Cy2 = h->tensors[op.out2].C; a.y2_off = 0;
                     a.aff_s = cw.aff_s; a.aff_b = cw.aff_b;
                 }
-                if (h->amax) {
+                if (h->amax && h->need_amax[op.out]) {
                     a.y_amax = h->amax + (size_t)op.out * FR_AMAX_SLOTS;
                     a.amax_slots = FR_AMAX_SLOTS;
-                    if (cw.w8 && op.in_off == 0) {
-                        a.w8 = cw.w8; a.wscale = cw.wscale; a.Kpad = cw.Kpad8;
-                        a.x_amax = h->amax + (size_t)op.in * FR_AMAX_SLOTS;
-                    }
+                }
+                if (h->amax && cw.w8 && op.in_off == 0) {
+                    a.w8 = cw.w8; a.wscale = cw.wscale; a.Kpad = cw.Kpad8;
+                    a.x_amax = h->amax + (size_t)op.in * FR_AMAX_SLOTS;
                 }
                 int rc = run_conv_args(h, a, s);
                 if (rc) return rc;
@@ -1561,6 +1599,11 @@ int fr_load_weights(fr_handle* h, const void* blob, size_t nbytes) {
     else if (h->arch == FR_ARCH_RESNET50_ARCFACE) build_resnet50(b);
     else build_irv1(b);
     if (!b.rc) b.rc = build_img_weights(h);
+    // the tensors whose producers record amax: inputs of e4m3 convs that run per-conv (an fp8 stage
+    // scales its own input; its member convs are its fallback when the stage does not run)
+    h->need_amax.assign(h->tensors.size(), 0);
+    for (const auto& op : h->ops)
+        if (op.kind == OP_CONV && op.wi >= 0 && h->convw[op.wi].w8 && op.in_off == 0) h->need_amax[op.in] = 1;
     if (b.rc) {
         free_weights(h);
         h->tensors.clear();
@@ -1824,7 +1867,7 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
         if (op.kind == OP_STAGE) {
             const StageRec& r = h->stages[op.stage];
             const std::string K = std::to_string(9 * r.C);
-            out += "stage " + std::to_string(B * r.H * r.H) + " " + std::to_string(r.C) + " " + K + " " + K + " " +
+            out += std::string(r.fp8 ? "stage8 " : "stage ") + std::to_string(B * r.H * r.H) + " " + std::to_string(r.C) + " " + K + " " + K + " " +
                    std::to_string(2 * r.nblk) + " 1 3x3 " + h->tensors[r.out].name + "\n";
             continue;
         }

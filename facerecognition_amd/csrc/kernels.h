@@ -104,6 +104,7 @@ struct StageArgs {
     const StageConv* conv;     // [2*nblk] device table
     const float* ep;           // [2*nblk][9][256] epilogue bias per border class (bias9, or bias broadcast)
     const float* slope;        // [2*nblk][256] negative-side factor: PReLU slope, 0 (ReLU) or 1 (none)
+    const float* wscale;       // fp8 stage (conv_stage8.hip) only: [2*nblk][256] per-channel e4m3 weight scales
     bf16_t* const* dbg_x;      // optional [nblk] per-block outputs / [nblk] conv1 outputs (device
     bf16_t* const* dbg_t;      //   pointer tables; null = do not materialise intermediates)
     // split stages (conv_split_stage.hip) only: boundary-row exchange between an image's workgroups
@@ -121,6 +122,11 @@ bool stage_supported(int B, int H, int W, int C);
 size_t stage_weight_bytes(int nconv);
 void stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out);
 hipError_t launch_stage(const StageArgs& a, hipStream_t s);
+// The same stage with e4m3 weights and activations (conv_stage8.hip, BASELINE config 5): a.w = the
+// stage8_pack_weights images of all convs, a.wscale their per-channel scales; the residual stays bf16.
+size_t stage8_weight_bytes(int nconv);
+void stage8_pack_weights(const uint8_t* rows, int Kpad8, uint8_t* out);
+hipError_t launch_stage8(const StageArgs& a, hipStream_t s);
 // Split LDS-resident stages (conv_split_stage.hip): 28x28x128 (IResNet100 layer2.1 .. layer2.12) in two
 // workgroups per image, 56x56x64 (layer1.1 .. layer1.2) in four, 14 output rows each, exchanging their
 // boundary rows per conv through xchg / flags.  split_stage_parts: workgroups per image, 0 = unsupported.

@@ -57,7 +57,7 @@ class FRModel:
     def load_state_dict(self, state_dict, strict: bool = True) -> None:
         folded = Wt.fold_state_dict(self.arch, state_dict)
         if self.dtype == "fp8":
-            folded = Wt.quantize_fp8(folded)
+            folded = Wt.quantize_fp8(folded, convs=Wt.fp8_plan(self.arch))
         blob = Wt.pack_blob(folded)
         buf = ctypes.create_string_buffer(blob, len(blob))
         N.check(N.lib().fr_load_weights(self._h, buf, len(blob)), "fr_load_weights")

@@ -356,16 +356,38 @@ def fold_state_dict(arch: str, sd) -> Dict[str, np.ndarray]:
     return out
 
 
-def quantize_fp8(folded: Dict[str, np.ndarray], min_cin: int = 64) -> Dict[str, np.ndarray]:
-    """FR_DTYPE_FP8 weights (BASELINE config 5): every folded conv weight "<name>.w" [Cout, kh, kw, Cin]
-    with Cin % 64 == 0 becomes per-output-channel scaled OCP e4m3: s[o] = max|w[o]| / 448 (f32),
-    "<name>.w" = e4m3(w / s) as exactly representable f32 values (torch.float8_e4m3fn cast, RNE,
-    saturating), "<name>.wscale" = s.  The stem (Cin 3) and the 2-D head stay bf16.  Dequantized
-    weight = w * s.  Biases, border-class tables and PReLU slopes are unchanged."""
+# Mixed fp8 / bf16 plans (BASELINE config 5): the convs that run in e4m3.  IResNet100: the tail of layer3
+# (blocks 16..29, conv1 + conv2: 28 convs, 28 % of the FLOPs), the least sensitive convs of the per-conv
+# sweep in profiles/r03_fp8_plan.json (tools/fp8_plan.py: together 1 - cos ~6e-4 against fp32, under
+# the 1e-3 bar; all of layer3 measures 1.6e-3, every conv 8.6e-3).  They run as one e4m3 LDS-resident
+# stage (conv_stage8.hip).  Other archs: no plan measured, every eligible conv.
+FP8_PLAN = {
+    "iresnet100": tuple(f"layer3.{i}.conv{j}" for i in range(16, 30) for j in (1, 2)),
+}
+
+
+def fp8_plan(arch: str):
+    """The conv names FR_DTYPE_FP8 quantizes for `arch` (None = every eligible conv).  FR_FP8_PLAN=all
+    overrides the plan (every eligible conv; A/B only)."""
+    if os.environ.get("FR_FP8_PLAN") == "all":
+        return None
+    return FP8_PLAN.get(arch)
+
+
+def quantize_fp8(folded: Dict[str, np.ndarray], min_cin: int = 64, convs=None) -> Dict[str, np.ndarray]:
+    """FR_DTYPE_FP8 weights (BASELINE config 5): the folded conv weights "<name>.w" [Cout, kh, kw, Cin]
+    with Cin % 64 == 0 -- those named in `convs`, or every one when None -- become per-output-channel
+    scaled OCP e4m3: s[o] = max|w[o]| / 448 (f32), "<name>.w" = e4m3(w / s) as exactly representable f32
+    values (torch.float8_e4m3fn cast, RNE, saturating), "<name>.wscale" = s.  The stem (Cin 3) and the
+    2-D head stay bf16.  Dequantized weight = w * s.  Biases, border-class tables and PReLU slopes are
+    unchanged; convs without a .wscale run in bf16."""
     import torch
     out = dict(folded)
+    want = None if convs is None else set(convs)
     for k, w in folded.items():
         if not k.endswith(".w") or w.ndim != 4 or w.shape[3] % min_cin != 0:
+            continue
+        if want is not None and k[:-2] not in want:
             continue
         w64 = np.asarray(w, dtype=np.float32)
         amax = np.abs(w64).reshape(w64.shape[0], -1).max(axis=1)
