@@ -56,6 +56,27 @@ constexpr int NPW = 16 * FN;                 // output channels per wave
 #ifndef FR_STAGE_SINGLE
 #define FR_STAGE_SINGLE 1  // 13-fragment kernel: one in-place refilled fragment set (0: two sets, A/B)
 #endif
+// FR_STAGE_TRACE (timing experiments only, tools/stage_trace.py): workgroups 0 and TRACE_WG2 of the
+// 13-fragment kernel record the low 32 bits of the shader clock at four points of each of their first
+// TRACE_CONVS convs per wave (K loop start / end, after the epilogue's entry barrier, after its exit
+// barrier) into 2 KiB of LDS past the kernel's own (uniform ds_write: no registers held, no spills),
+// copied to g_stage_trace at the end and read back by fr_stage_trace_read.
+#ifdef FR_STAGE_TRACE
+constexpr int TRACE_CONVS = 16, TRACE_WG2 = 200, TRACE_LDS = 151552, TRACE_B = 8 * TRACE_CONVS * 4 * 4;
+__device__ unsigned int g_stage_trace[2][8][TRACE_CONVS][4];
+#define STAGE_TRACE(cv, k)                                                                              \
+    do {                                                                                                \
+        if ((blockIdx.x == 0 || blockIdx.x == TRACE_WG2) && (cv) < TRACE_CONVS) {                       \
+            const unsigned t_ = (unsigned)__builtin_readcyclecounter();                                  \
+            *(volatile __attribute__((address_space(3))) unsigned*)(uintptr_t)(                        \
+                TRACE_LDS + ((wave * TRACE_CONVS + (cv)) * 4 + (k)) * 4) = t_;                           \
+        }                                                                                               \
+    } while (0)
+#else
+#define STAGE_TRACE(cv, k) \
+    do {                   \
+    } while (0)
+#endif
 #ifndef FR_STAGE_EXP
 #define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 8 trivial epilogue (MFMAs kept), 16 no
                         // patch reads in the loop, 32 every weight load reads K-step 0 (stage13), 128
@@ -64,12 +85,16 @@ constexpr int NPW = 16 * FN;                 // output channels per wave
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-// threadIdx.x through an empty asm: loop-invariant copy-out addresses are recomputed where they are used
-// instead of being hoisted to the kernel's start and spilled across the K loops
+// The lane id / thread id recomputed where used (v_mbcnt; volatile, so never hoisted, CSE'd or kept
+// live across the conv loop): a long-lived copy of threadIdx.x gets spilled, and each scratch reload
+// waits for every outstanding VMEM load (vmcnt(0)), i.e. drains the weight prefetch ring.
+__device__ __forceinline__ int fresh_lane() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 __device__ __forceinline__ int opaque_tid() {
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return t;
+    return (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63) + fresh_lane();
 }
 
 template <bool F16>
@@ -437,7 +462,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv * SC * 4), 0x00020000);
     auto issue_tab = [&](int cv, int cv_slope, int slot) {
         char* dst = smem + TAB13 + slot * TS;
-        int ln = opaque_tid() & 63;
+        int ln = fresh_lane();
 #pragma unroll
         for (int u = 0; u < (TAB_ROWS_B / 1024 + NWV - 1) / NWV; ++u) {
             const int piece = wave + NWV * u;
@@ -458,8 +483,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         return (3 * rc + cc) * SC * 4;
     };
     auto seed_bias = [&]() {
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
+        int ln = fresh_lane();
         const char* t = smem + TAB13 + (wn * NPW + 4 * (ln >> 4)) * 4;
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
@@ -487,6 +511,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         }
         pread(pA, 0, 0);
         const int g0 = cv * KSTEPS;
+        STAGE_TRACE(cv, 0);
 #pragma unroll 1
         for (int cg = 0; cg < SC / 32; cg += 2) {
 #pragma unroll
@@ -500,9 +525,10 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             }
         }
         // ---- epilogue (as stage_kernel's): accumulators -> patch; spare-slot lanes write nothing
+        STAGE_TRACE(cv, 1);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
+        STAGE_TRACE(cv, 2);
+        int ln = fresh_lane();
         const int cl = ln & 15;
         const char* t2 = smem + TAB13 + TS;
 #pragma unroll
@@ -540,6 +566,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        STAGE_TRACE(cv, 3);
         bf16_t* dbg = nullptr;
         if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
         bf16_t* const yo = second && cv == nconv - 1 ? p.y : dbg;
@@ -563,6 +590,13 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         run_conv(2 * blk, std::false_type{});
         run_conv(2 * blk + 1, std::true_type{});
     }
+#ifdef FR_STAGE_TRACE
+    __syncthreads();
+    if (blockIdx.x == 0 || blockIdx.x == TRACE_WG2) {
+        const int c = opaque_tid();
+        if (c < 512) ((unsigned*)g_stage_trace)[(blockIdx.x == 0 ? 0 : 512) + c] = ((const unsigned*)(smem + TRACE_LDS))[c];
+    }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -576,6 +610,14 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage13_kernel(StageArgs p) {
 }
 
 }  // namespace
+
+#ifdef FR_STAGE_TRACE
+extern "C" int fr_stage_trace_read(unsigned int* out, int n) {
+    const int all = (int)(sizeof(g_stage_trace) / sizeof(unsigned int));
+    if (n < all) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_trace), sizeof(g_stage_trace)) == hipSuccess ? all : -2;
+}
+#endif
 
 bool stage_supported(int B, int H, int W, int C) { return B > 0 && H == SW && W == SW && C == SC; }
 
@@ -599,7 +641,12 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t s) {
     // variant 1: the legacy 14-fragment kernel (bit-identical; FR_OPT_STAGE_VARIANT)
     const int v = a.variant == 1 ? 1 : 0;
     auto k = v == 1 ? (a.f16 ? stage_kernel<true> : stage_kernel<false>) : (a.f16 ? stage13_kernel<true> : stage13_kernel<false>);
+#ifdef FR_STAGE_TRACE
+    static_assert(TRACE_LDS == STAGE13_LDS, "trace area");
+    const int lds = v == 1 ? STAGE_LDS : STAGE13_LDS + TRACE_B;
+#else
     const int lds = v == 1 ? STAGE_LDS : STAGE13_LDS;
+#endif
     const int threads = 64 * SNW;
     static bool attr[4] = {false, false, false, false};
     const int ai = 2 * v + (a.f16 ? 1 : 0);

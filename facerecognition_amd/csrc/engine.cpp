@@ -1798,13 +1798,30 @@ static int ensure_cand(fr_handle* h, size_t need) {
 }
 
 static int match_locked(fr_handle* h, const float* P, int B, int k, float* scores, int32_t* idx, void* stream) {
-    if (!P || !scores || !idx || B <= 0 || k <= 0 || k > 16) {
-        set_error("fr_match_topk: bad argument (1 <= k <= 16)");
+    if (!P || !scores || !idx || B <= 0 || k <= 0 || k > FR_TOPK_LARGE_MAX) {
+        set_error("fr_match_topk: bad argument (1 <= k <= " + std::to_string(FR_TOPK_LARGE_MAX) + ")");
         return FR_ERR_ARG;
     }
     if (!h->gallery || h->g_rows <= 0) { set_error("fr_match_topk: no gallery"); return FR_ERR_STATE; }
     FR_HIP_CHECK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
+    if (k > 16) {  // exact score rows in stream-ordered scratch, <= 256 MiB per probe chunk, + radix select
+        if (h->g_rows > 0x7fffffff) { set_error("fr_match_topk: k > 16 needs a gallery below 2^31 rows"); return FR_ERR_ARG; }
+        const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(B, ((int64_t)1 << 26) / h->g_rows));
+        float* S = nullptr;
+        FR_HIP_CHECK(hipMallocAsync((void**)&S, (size_t)chunk * h->g_rows * sizeof(float), s));
+        for (int b0 = 0; b0 < B; b0 += chunk) {
+            const int nb = std::min(chunk, B - b0);
+            const hipError_t e = launch_match_topk_large(P + (size_t)b0 * h->g_dim, nb, h->gallery, h->g_rows, h->g_dim, k,
+                                                         h->g_base, S, scores + (size_t)b0 * k, idx + (size_t)b0 * k, s);
+            if (e != hipSuccess) {
+                (void)hipFreeAsync(S, s);
+                FR_HIP_CHECK(e);
+            }
+        }
+        FR_HIP_CHECK(hipFreeAsync(S, s));
+        return FR_OK;
+    }
     int n_split;
     int64_t rps;
     // bf16x3 candidates + exact f32 rescoring (match_x3.hip).  Its proof needs the k-th exact score to

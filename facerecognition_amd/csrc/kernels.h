@@ -166,6 +166,10 @@ hipError_t launch_match_topk(const float* P, int B, const float* G, int64_t N, i
                              int64_t rows_per_split, hipStream_t s);
 hipError_t launch_topk_merge(const float* cs, const int32_t* ci, int B, int n_lists, int k, float* out_s,
                              int32_t* out_i, hipStream_t s);
+// k > 16 (match.hip): exact score rows S [B][N] (the caller's scratch) + a per-probe radix select.
+constexpr int FR_TOPK_LARGE_MAX = 4096;
+hipError_t launch_match_topk_large(const float* P, int B, const float* G, int64_t N, int D, int k, int64_t index_base,
+                                   float* S, float* out_s, int32_t* out_i, hipStream_t s);
 // Large-gallery match (match_x3.hip): bf16x3 candidates, exact f32 rescoring with a proof / fallback.
 constexpr int64_t X3_MIN_ROWS = 32768;  // below: the exact f32 kernel is as fast (10k x 256: 0.105 vs 0.16 ms)
 hipError_t launch_split_bf16(const float* G, size_t n, bf16_t* hi, bf16_t* lo, hipStream_t s);

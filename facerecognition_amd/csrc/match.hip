@@ -496,4 +496,217 @@ hipError_t launch_topk_merge(const float* cs, const int32_t* ci, int B, int n_li
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Large k (17 .. FR_TOPK_LARGE_MAX): IndexFlatIP.search with any k (recognition_engine.py:291-326 passes
+// the caller's k straight to faiss).  Register top-k lists do not scale past 16, so the large path
+// materialises the exact score rows -- the SAME v_mfma_f32_16x16x4f32 sequence per output as
+// match_partial_kernel, so a large-k list starts with exactly the small-k list -- and selects per probe
+// with a radix select on the order-preserving u32 image of the score (3 digit passes of 11/11/10 bits
+// over the row, histograms in LDS), takes every score above the k-th and the lowest-index ties at it,
+// and bitonic-sorts the k survivors (score desc, index asc) in LDS.
+namespace {
+
+__global__ __launch_bounds__(256) void match_scores_kernel(const float* __restrict__ P, int B, const float* __restrict__ G,
+                                                           int64_t N, int D, float* __restrict__ S) {
+    __shared__ __attribute__((aligned(16))) float sPG[2 * MP * LD];
+    float* sP = sPG;
+    float* sG = sPG + MP * LD;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int p0 = blockIdx.x * MP;
+    const int64_t t0 = (int64_t)blockIdx.y * MG;
+    const int64_t g_end = N;
+    f32x4_t acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int d0 = 0; d0 < D; d0 += KC) {  // match_partial_kernel's tile, operation for operation
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q >> 4, c4 = (q & 15) * 4;
+            float4 pv = make_float4(0.f, 0.f, 0.f, 0.f), gv = pv;
+            if (p0 + row < B && d0 + c4 < D) pv = *(const float4*)(P + (size_t)(p0 + row) * D + d0 + c4);
+            if (t0 + row < g_end && d0 + c4 < D) gv = *(const float4*)(G + (size_t)(t0 + row) * D + d0 + c4);
+            *(float4*)(sP + row * LD + c4) = pv;
+            *(float4*)(sG + row * LD + c4) = gv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t16 = 0; t16 < KC / 16; ++t16) {
+            const int kof = 16 * t16 + 4 * (lane >> 4);
+            const float4 a4 = *(const float4*)(sP + (16 * wave + (lane & 15)) * LD + kof);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 b4 = *(const float4*)(sG + (16 * j + (lane & 15)) * LD + kof);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4.w, acc[j], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // acc[j][r] = score(probe 16 wave + 4 (lane >> 4) + r, row t0 + 16 j + (lane & 15))
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int p = p0 + 16 * wave + 4 * (lane >> 4) + r;
+            const int64_t g = t0 + 16 * j + (lane & 15);
+            if (p < B && g < N) S[(size_t)p * N + g] = acc[j][r];
+        }
+}
+
+// order-preserving u32 image of a score (-0 folds onto +0: the small-k comparator ties them)
+__device__ __forceinline__ uint32_t skey(float v) {
+    const uint32_t b = __float_as_uint(v == 0.f ? 0.f : v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+constexpr int TK_THREADS = 1024;
+
+// Block-wide exclusive prefix sum of one int per thread (+ the total).
+__device__ __forceinline__ int block_excl_scan(int v, int* red, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) red[wave] = x;
+    __syncthreads();
+    int before = 0, all = 0;
+    for (int w = 0; w < TK_THREADS / 64; ++w) {
+        const int c = red[w];
+        before += w < wave ? c : 0;
+        all += c;
+    }
+    __syncthreads();
+    *total = all;
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(TK_THREADS) void topk_large_kernel(const float* __restrict__ S, int64_t N, int k,
+                                                                int64_t index_base, float* __restrict__ out_s,
+                                                                int32_t* __restrict__ out_i) {
+    __shared__ uint32_t hist[2048];
+    __shared__ unsigned long long keys[FR_TOPK_LARGE_MAX];
+    __shared__ int red[TK_THREADS / 64];
+    __shared__ int sel[3];
+    const int tid = threadIdx.x;
+    const float* row = S + (size_t)blockIdx.x * N;
+    const int kk = (int)(N < (int64_t)k ? N : (int64_t)k);
+    uint32_t prefix = 0, pmask = 0;
+    int kr = kk;
+    // ---- radix select: the exact u32 key T of the kk-th largest score, and how many ties at T to take
+    for (int pass = 0; pass < 3; ++pass) {
+        const int shift = pass == 0 ? 21 : (pass == 1 ? 10 : 0);
+        const int nb = pass < 2 ? 2048 : 1024;
+        for (int i = tid; i < 2048; i += TK_THREADS) hist[i] = 0;
+        __syncthreads();
+        for (int64_t i = tid; i < N; i += TK_THREADS) {
+            const uint32_t u = skey(row[i]);
+            if ((u & pmask) == prefix) atomicAdd(&hist[(u >> shift) & (nb - 1)], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {  // wave 0: lane l owns bins nb-1-l*per .. (descending), find where the count reaches kr
+            const int per = nb / 64;
+            int c = 0;
+            for (int q = 0; q < per; ++q) c += (int)hist[nb - 1 - tid * per - q];
+            int x = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (tid >= o) x += y;
+            }
+            const int before = x - c;
+            if (before < kr && x >= kr) {
+                int acc = before;
+                for (int q = 0; q < per; ++q) {
+                    const int d = nb - 1 - tid * per - q;
+                    const int h = (int)hist[d];
+                    if (acc + h >= kr) {
+                        sel[0] = d;
+                        sel[1] = acc;
+                        break;
+                    }
+                    acc += h;
+                }
+            }
+        }
+        __syncthreads();
+        prefix |= (uint32_t)sel[0] << shift;
+        pmask |= (uint32_t)(nb - 1) << shift;
+        kr -= sel[1];
+        __syncthreads();
+    }
+    const uint32_t T = prefix;
+    // ---- gather: every key above T (unordered), then the kr lowest-index rows equal to T (ordered scan)
+    if (tid == 0) sel[2] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < N; i += TK_THREADS) {
+        const uint32_t u = skey(row[i]);
+        if (u > T) {
+            const int slot = atomicAdd(&sel[2], 1);
+            keys[slot] = ((unsigned long long)u << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)i);
+        }
+    }
+    __syncthreads();
+    const int above = sel[2];
+    int taken = 0;
+    for (int64_t c0 = 0; c0 < N && taken < kr; c0 += TK_THREADS) {
+        const int64_t i = c0 + tid;
+        const int eq = i < N && skey(row[i]) == T;
+        int total;
+        const int pos = block_excl_scan(eq, red, &total);
+        if (eq && taken + pos < kr)
+            keys[above + taken + pos] = ((unsigned long long)T << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)i);
+        taken += total;
+    }
+    __syncthreads();
+    // ---- bitonic sort of the kk keys, descending (pad with 0: below every real key)
+    int P2 = 1;
+    while (P2 < kk) P2 <<= 1;
+    for (int i = kk + tid; i < P2; i += TK_THREADS) keys[i] = 0ull;
+    __syncthreads();
+    for (int size = 2; size <= P2; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < P2; i += TK_THREADS) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool desc = (i & size) == 0;
+                    const unsigned long long a = keys[i], b = keys[j];
+                    if (desc ? a < b : a > b) {
+                        keys[i] = b;
+                        keys[j] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int q = tid; q < k; q += TK_THREADS) {
+        float sc = -INFINITY;
+        int32_t ix = -1;
+        if (q < kk) {
+            const unsigned long long kv = keys[q];
+            const uint32_t u = (uint32_t)(kv >> 32);
+            const uint32_t b = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+            sc = __uint_as_float(b);
+            ix = (int32_t)((int64_t)(0xFFFFFFFFu - (uint32_t)kv) + index_base);
+        }
+        out_s[(size_t)blockIdx.x * k + q] = sc;
+        out_i[(size_t)blockIdx.x * k + q] = ix;
+    }
+}
+
+}  // namespace
+
+// S: B x N f32 scratch (the caller's, stream-ordered).  out: [B][k].
+hipError_t launch_match_topk_large(const float* P, int B, const float* G, int64_t N, int D, int k, int64_t index_base,
+                                   float* S, float* out_s, int32_t* out_i, hipStream_t s) {
+    if (B <= 0 || N <= 0 || k <= 0 || k > FR_TOPK_LARGE_MAX || N > 0x7fffffff) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(match_scores_kernel, dim3((B + MP - 1) / MP, (unsigned)((N + MG - 1) / MG)), dim3(256), 0, s, P,
+                       B, G, N, D, S);
+    hipLaunchKernelGGL(topk_large_kernel, dim3(B), dim3(TK_THREADS), 0, s, S, N, k, index_base, out_s, out_i);
+    return hipGetLastError();
+}
+
 }  // namespace fr

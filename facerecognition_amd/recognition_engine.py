@@ -40,7 +40,7 @@ from . import weights as Wt
 from .extract_embeddings import (_device_index, _embed_u8, _load_u8, extract_embedding_single,
                                  get_transform, load_arcface_model, read_index, segment_means)
 
-MAX_K = 16  # fr_match_topk limit
+MAX_K = 4096  # fr_match_topk limit (k > 16: exact score rows + a device radix select)
 
 
 def cosine_similarity(a: np.ndarray, b: np.ndarray) -> float:

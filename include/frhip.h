@@ -116,7 +116,11 @@ int64_t fr_gallery_rows(const fr_handle* h);
 /* Top-k of P [B, D] (device f32, L2-normalized probes) against the gallery.
  * Results (device): scores [B, k] f32 descending, idx [B, k] int32; ties are
  * broken by lower index (stable sort(reverse=True) / np.argmax semantics).
- * Rows past the gallery end come back as score -inf, idx -1.  k <= 16. */
+ * Rows past the gallery end come back as score -inf, idx -1.  1 <= k <= 4096 (faiss
+ * IndexFlatIP.search takes any k, recognition_engine.py:291,304): k <= 16 keeps register
+ * top-k lists; larger k materialises the exact score rows in stream-ordered scratch
+ * (<= 256 MiB per probe chunk) and radix-selects per probe -- the same scores bit for bit,
+ * so a large-k list starts with the small-k list.  k > 16 needs N < 2^31. */
 int fr_match_topk(fr_handle* h, const float* P, int B, int k, float* scores, int32_t* idx, void* stream);
 
 /* Merge n_lists candidate lists per probe: cand_s/cand_i [B, n_lists, k] → [B, k]

@@ -624,3 +624,69 @@ def test_nccl_world1_all_gather(gpu):
         gal.close()
     finally:
         dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------ match, k > 16
+@pytest.mark.parametrize("B,Ng,k", [(5, 20000, 17), (3, 20000, 100), (2, 5000, 1000), (1, 9000, 4096), (4, 300, 700)])
+def test_match_large_k(gpu, B, Ng, k):
+    """k > 16 (IndexFlatIP.search with any k): exact score rows + device radix select, against the
+    oracle's (score desc, index asc) order; rows past the gallery end are (-inf, -1)."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(B * 7 + Ng + k)
+    G = _norm(rng.standard_normal((Ng, 512)))
+    G[Ng // 2] = G[1]  # an exact tie
+    P = _norm(rng.standard_normal((B, 512)))
+    P[0] = _norm((G[1] + 0.01 * rng.standard_normal(512))[None])[0]
+    gal = DeviceGallery(G)
+    s, i = gal.search(P, k)
+    rs, ri = _np_topk(P, G, k)
+    kk = min(k, Ng)
+    assert np.all(np.diff(s[:, :kk], axis=1) <= 0)
+    assert np.allclose(s[:, :kk], rs[:, :kk], atol=1e-5)
+    gap_ok = np.ones((B, kk), dtype=bool)
+    gap_ok[:, :-1] = (rs[:, :kk - 1] - rs[:, 1:kk]) > 1e-5
+    gap_ok[:, 1:] &= gap_ok[:, :-1].copy() | ((rs[:, :kk - 1] - rs[:, 1:kk]) > 1e-5)
+    assert np.array_equal(i[:, :kk][gap_ok], ri[:, :kk][gap_ok])
+    assert list(i[0, :2]) == [1, Ng // 2] and s[0, 0] == s[0, 1]  # the tie: lower index first
+    if k > Ng:
+        assert np.all(s[:, Ng:] == -np.inf) and np.all(i[:, Ng:] == -1)
+    # the small-k list is a prefix of the large-k list, bit for bit (the same MFMA score sequence)
+    s16, i16 = gal.search(P, 16)
+    m = min(16, kk)
+    assert np.array_equal(s[:, :m], s16[:, :m]) and np.array_equal(i[:, :m], i16[:, :m])
+    gal.close()
+
+
+def test_match_large_k_x3_gallery_prefix(gpu):
+    """On a gallery that takes the bf16x3 path for small k (>= X3_MIN_ROWS rows), the large-k list still
+    starts with the small-k list (the x3 path rescores exactly)."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(5)
+    G = _norm(rng.standard_normal((40000, 512)))
+    P = _norm(rng.standard_normal((8, 512)))
+    P[:4] = _norm(G[:4] + 0.05 * rng.standard_normal((4, 512)))
+    gal = DeviceGallery(G)
+    s5, i5 = gal.search(P, 5)
+    s, i = gal.search(P, 64)
+    gal.close()
+    assert np.array_equal(i[:, :5], i5) and np.array_equal(s[:, :5], s5)
+
+
+def test_recognize_with_faiss_large_k(gpu, tmp_path):
+    """recognize_with_faiss with k = 40 > 16 against oracle.match.faiss_flat_ip_search."""
+    from facerecognition_amd import extract_embeddings as EE
+    from facerecognition_amd.recognition_engine import RecognitionEngine
+    from oracle.match import faiss_flat_ip_search
+    rng = np.random.default_rng(8)
+    protos = _norm(rng.standard_normal((300, 512)))
+    EE.build_faiss_index(protos, str(tmp_path / "idx.faiss"))
+    eng = RecognitionEngine.__new__(RecognitionEngine)  # only the FAISS state: no model, no db
+    eng.threshold, eng.id_to_label, eng.faiss_index, eng.prototypes = 0.5, None, None, None
+    eng._load_faiss(str(tmp_path / "idx.faiss"))
+    assert eng.faiss_index is not None
+    probe = protos[17] + 0.02 * rng.standard_normal(512).astype(np.float32)
+    name, score, res = eng.recognize_with_faiss(probe, k=40)
+    s_ref, i_ref = faiss_flat_ip_search(protos, probe, 40)
+    assert [r[0] for r in res] == [f"ID_{j}" for j in i_ref[0]]
+    assert np.allclose([r[1] for r in res], s_ref[0], atol=1e-5)
+    assert name == "ID_17"
