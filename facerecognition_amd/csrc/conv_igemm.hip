@@ -319,7 +319,7 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
             rr[it] = *(const uint4*)(p.res + (size_t)(m < p.M ? m : 0) * p.Cres + p.res_off + nn);
         }
     };
-    if (STAGES == 2) {
+    if constexpr (STAGES == 2) {
         // DMA for step t+1 overlaps the MFMAs of step t; one vmcnt(0) + barrier per step.
         if (kt0 < kt1) {
             issue(kt0, 0);
@@ -349,11 +349,14 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
         int buf = 0;
         for (int kt = kt0; kt < kt1; ++kt) {
             if (kt + 1 < kt1) {
+                static_assert(GROUP >= 2 && GROUP <= 9 && GROUP != 7, "counted wait for this DMA group size");
                 if constexpr (GROUP == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
                 else if constexpr (GROUP == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
                 else if constexpr (GROUP == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else if constexpr (GROUP == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
                 else if constexpr (GROUP == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else if constexpr (GROUP == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
