@@ -9,5 +9,7 @@ for b in bench bench_noprof bench_host bench_irv1 bench_irv1_f16 bench_r50 bench
 cp "$(find $O/prof -name '*kernel_stats.csv' | head -1)" profiles/${R}_bench_kernel_stats.csv
 grep '^{' $O/match_bench.log > profiles/${R}_match_bench.jsonl
 cp $O/pmc_traffic.json profiles/${R}_pmc_traffic.json
-grep -v "^\s*$" $O/tests.log | tail -40 > profiles/${R}_gpu_tests.log
+grep -v "^\s*$" $O/tests.log | tail -40 > profiles/${R}_gpu_tests.txt
+grep -E "1-cos|agreement|rel err|bs=256" $O/tests.log > profiles/${R}_parity_stats.txt || true
+[ -f $O/layer_profile.txt ] && cp $O/layer_profile.txt profiles/${R}_layer_profile.txt
 echo "collected $T -> profiles/${R}_*"

@@ -12,7 +12,7 @@ R=$(pwd); O=$R/gpurun_out/$T
 mkdir -p $O
 step() { local name=$1 lim=$2; shift 2; echo "[$(date +%T)] $name"; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; if [ $rc -ne 0 ]; then echo "$name failed rc=$rc"; tail -20 $O/$name.log; exit $rc; fi; }
 if [ -z "$SKIP_TESTS" ]; then
-  step tests 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread
+  step tests 900 python -u -m pytest tests -m gpu -q -s -p no:cacheprovider -x --timeout 120 --timeout-method thread
   tail -3 $O/tests.log
 fi
 step bench 400 python bench.py
@@ -38,4 +38,5 @@ step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pw -o ru
 cd $R
 python tools/pmc_traffic.py --fetch $O/pf --write $O/pw --out $O/pmc_traffic.json
 find $O/prof -name "*kernel_stats.csv" | head -1 | xargs -r head -12
+cd $R && bash tools/gpu_layer_profile.sh ${T}_iresnet100 > $O/layer_profile.log 2>&1 && cp gpurun_out/lp_${T}_iresnet100/summary.txt $O/layer_profile.txt
 echo "[$(date +%T)] done"
