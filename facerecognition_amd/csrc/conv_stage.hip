@@ -77,6 +77,9 @@ __device__ unsigned int g_stage_trace[2][8][TRACE_CONVS][4];
     do {                   \
     } while (0)
 #endif
+#ifndef FR_STAGE13_RING7
+#define FR_STAGE13_RING7 2  // weight-ring depth of the 13-fragment kernel's 7-fragment waves (3: as the others)
+#endif
 #ifndef FR_STAGE_EXP
 #define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 8 trivial epilogue (MFMAs kept), 16 no
                         // patch reads in the loop, 32 every weight load reads K-step 0 (stage13), 128
@@ -411,7 +414,11 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 #pragma unroll
         for (int j = 0; j < FM; ++j) pf[j] = *(const frag*)(pa + aoff[j]);
     };
-    frag wq[3][FN];
+    // weight ring depth: 3 K-steps (loads 2 ahead); the 7-fragment waves (which wait ~30 % of each conv at
+    // the epilogue barrier for the 6-fragment ones) take 2 (1 ahead) and 16 VGPRs fewer: their body then
+    // fits 256 VGPRs without the epilogue spills (FR_STAGE13_RING7, A/B)
+    constexpr int RING = FM == 7 ? FR_STAGE13_RING7 : 3;
+    frag wq[RING][FN];
     auto wload = [&](frag (&w)[FN], int g) {
 #pragma unroll
         for (int i = 0; i < FN; ++i)
@@ -424,7 +431,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 #if !(FR_STAGE_EXP & 16)
         pread(nxt, cg_n, tap_n);
 #endif
-        wload(wq[(r + 2) % 3], g + 2 < total ? g + 2 : total - 1);
+        wload(wq[(r + RING - 1) % RING], g + RING - 1 < total ? g + RING - 1 : total - 1);
 #pragma unroll
         for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -437,7 +444,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     auto kstep1 = [&](int g, int r, frag (&pf)[FM], int cg_n, int tap_n) {
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        wload(wq[(r + 2) % 3], g + 2 < total ? g + 2 : total - 1);
+        wload(wq[(r + RING - 1) % RING], g + RING - 1 < total ? g + RING - 1 : total - 1);
         const char* pa = smem + cg_n * 4 * PLANE13_B + ((tap_n / 3 - 1) * SWP + tap_n % 3 - 1) * 16;
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
@@ -499,7 +506,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     wload(wq[0], 0);
-    wload(wq[1], 1);
+    if (RING == 3) wload(wq[1 % RING], 1);
 
     auto run_conv = [&](int cv, auto second_tag) {
         constexpr bool second = decltype(second_tag)::value;
@@ -519,9 +526,10 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
                 const int cgl = cg + t / 9, tap = t % 9;
                 const int cgn = t == 8 ? cg + 1 : (t == 17 ? cg + 2 : cgl);
                 const int tapn = t == 8 || t == 17 ? 0 : tap + 1;
-                if (SINGLE) kstep1(g0 + cgl * 9 + tap, tap % 3, pA, cgn, tapn);
-                else if (t & 1) kstep(g0 + cgl * 9 + tap, tap % 3, pB, pA, cgn, tapn);
-                else kstep(g0 + cgl * 9 + tap, tap % 3, pA, pB, cgn, tapn);
+                const int rs = RING == 3 ? tap % 3 : t % RING;  // = global K-step % RING (72, 9 and 18 are multiples)
+                if (SINGLE) kstep1(g0 + cgl * 9 + tap, rs, pA, cgn, tapn);
+                else if (t & 1) kstep(g0 + cgl * 9 + tap, rs, pB, pA, cgn, tapn);
+                else kstep(g0 + cgl * 9 + tap, rs, pA, pB, cgn, tapn);
             }
         }
         // ---- epilogue (as stage_kernel's): accumulators -> patch; spare-slot lanes write nothing

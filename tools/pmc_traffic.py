@@ -25,8 +25,10 @@ BAND_TH = {14: 14, 28: 7, 56: 4, 112: 2}
 
 
 def class_pattern(cls: str, f16: bool) -> str:
-    if cls == "stage layer3":
-        return f"stage_kernel<{str(f16).lower()}>"
+    if cls == "stage layer3":  # the 13-fragment default (FR_OPT_STAGE_VARIANT 1: "::stage_kernel<")
+        return f"stage13_kernel<{str(f16).lower()}>"
+    if cls == "stage8 layer3":
+        return "stage8_kernel("
     m = re.match(r"conv3x3_band W(\d+) v(\d+)", cls)
     if m:
         W, v = int(m.group(1)), int(m.group(2))
