@@ -536,38 +536,37 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         STAGE_TRACE(cv, 1);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         STAGE_TRACE(cv, 2);
+        // Fragment-major: the lane's slot for (j, i) is its B-fragment base aoff[j] moved to the output
+        // channel plane (n >> 3 = 8 wn + 2 i + (g >> 1), byte (n & 7) * 2 = (g & 1) * 8), and x (conv1) is
+        // read right where it is consumed (preloaded per n-fragment, the 7 x were spilled to scratch)
         int ln = fresh_lane();
-        const int cl = ln & 15;
+        const int cl = ln & 15, g = ln >> 4;
         const char* t2 = smem + TAB13 + TS;
+        const int cb = (8 * wn + (g >> 1) - g) * PLANE13_B + (g & 1) * 8;
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-            const int n = wn * NPW + 16 * i + 4 * (ln >> 4);
-            char* const pl = smem + (n >> 3) * PLANE13_B + (n & 7) * 2;
-            uint2 xin[FM];
-            float4 s1;
-            if (!second) {
-                const float4 sl = *(const float4*)(t2 + TAB_ROWS_B + n * 4);
-                s1 = make_float4(sl.x - 1.f, sl.y - 1.f, sl.z - 1.f, sl.w - 1.f);
+        for (int j = 0; j < FM; ++j) {
+            const int P = 16 * (f0 + j) + cl;
+            char* const sj = smem + aoff[j] + cb;
+            const int tr = second ? 0 : tab_row(j, ln);
 #pragma unroll
-                for (int j = 0; j < FM; ++j) xin[j] = *(const uint2*)(pl + pix_pos13(16 * (f0 + j) + cl) * 16);
-            }
-#pragma unroll
-            for (int j = 0; j < FM; ++j) {
-                const int P = 16 * (f0 + j) + cl;
-                char* slot = pl + pix_pos13(P) * 16;
+            for (int i = 0; i < FN; ++i) {
+                const int n = wn * NPW + 16 * i + 4 * g;
+                char* const slot = sj + 2 * i * PLANE13_B;
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
                 if (!second) {
-                    v[0] = fmaf(s1.x, fminf(v[0], 0.f), v[0]);
-                    v[1] = fmaf(s1.y, fminf(v[1], 0.f), v[1]);
-                    v[2] = fmaf(s1.z, fminf(v[2], 0.f), v[2]);
-                    v[3] = fmaf(s1.w, fminf(v[3], 0.f), v[3]);
+                    const float4 sl = *(const float4*)(t2 + TAB_ROWS_B + n * 4);
+                    v[0] = fmaf(sl.x - 1.f, fminf(v[0], 0.f), v[0]);
+                    v[1] = fmaf(sl.y - 1.f, fminf(v[1], 0.f), v[1]);
+                    v[2] = fmaf(sl.z - 1.f, fminf(v[2], 0.f), v[2]);
+                    v[3] = fmaf(sl.w - 1.f, fminf(v[3], 0.f), v[3]);
                 }
                 float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
                 const uint4 pk = T::pack8(o8);
                 if (!second) {
+                    const uint2 xin = *(const uint2*)slot;
                     float f[8];
-                    T::unpack8(make_uint4(xin[j].x, xin[j].y, 0, 0), f);
-                    const float4 bb = *(const float4*)(t2 + tab_row(j, ln) + n * 4);
+                    T::unpack8(make_uint4(xin.x, xin.y, 0, 0), f);
+                    const float4 bb = *(const float4*)(t2 + tr + n * 4);
                     acc[i][j] = (f32x4_t){f[0] + bb.x, f[1] + bb.y, f[2] + bb.z, f[3] + bb.w};
                 }
                 if (FM == 7 || (f0 + j) * 16 + 15 < SPIX || P < SPIX) *(uint2*)slot = make_uint2(pk.x, pk.y);
