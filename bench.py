@@ -93,6 +93,16 @@ def class_traffic(cls, pmc):
     return round(sum(pmc[k][0] + pmc[k][1] for k in ks) / n) if n else None
 
 
+def dtype_label(args) -> str:
+    """The arithmetic the path computes in: IRV1's bf16 plan keeps its high-resolution stem in f16
+    (DESIGN.md §5), IResNet100's fp8 plan is e4m3 for the layer3 tail only (weights.FP8_PLAN)."""
+    if args.arch == "irv1_facenet" and args.dtype == "bf16" and os.environ.get("FR_IRV1_BF16_STEM") != "1":
+        return "bf16 (f16 stem)"
+    if args.dtype == "fp8" and os.environ.get("FR_FP8_PLAN") != "all":
+        return "fp8 e4m3 (layer3.16-29) + bf16" if args.arch == "iresnet100" else "fp8 e4m3 + bf16"
+    return args.dtype
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -343,7 +353,7 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "faces/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "scaling": "weak", "vs_baseline": None, "dtype": dtype_label(args),
         "data": f"synthetic u8 {size}x{size}x3 aligned crops ({'pinned host, H2D per step' if args.host_input else 'HBM-resident'}), "
                 "random-init BN-calibrated weights, random unit-norm gallery",
         "config": {"workload": f"{args.arch} {args.dtype} embed bs={B}/GPU + top-{K} match vs "

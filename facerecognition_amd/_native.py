@@ -70,6 +70,7 @@ _SIGS = {
     "fr_embed": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "fr_gallery_set": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int64, c_int]),
     "fr_gallery_rows": (c_int64, [c_void_p]),
+    "fr_gallery_write": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_int]),
     "fr_match_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "fr_topk_merge": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "fr_embed_match": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,

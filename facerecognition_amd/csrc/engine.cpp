@@ -118,6 +118,7 @@ struct fr_handle {
     // gallery
     float* gallery = nullptr;
     int64_t g_rows = 0;
+    int64_t g_cap = 0;       // rows allocated (fr_gallery_write grows it geometrically)
     int g_dim = 0;
     int64_t g_base = 0;
     bf16_t* g_hi = nullptr;  // bf16 hi/lo split of the prepared gallery (match_x3.hip), N >= X3_MIN_ROWS
@@ -1754,6 +1755,7 @@ int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index
     if (h->g_hi) { (void)hipFree(h->g_hi); h->g_hi = nullptr; }
     if (h->g_lo) { (void)hipFree(h->g_lo); h->g_lo = nullptr; }
     h->g_rows = 0;
+    h->g_cap = N;
     if (N > 0) {
         void* p = nullptr;
         int rc = dev_alloc(&p, (size_t)N * D * sizeof(float));
@@ -1777,6 +1779,60 @@ int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index
     h->g_rows = N;
     h->g_dim = D;
     h->g_base = index_base;
+    return FR_OK;
+}
+
+// Rows [row0, row0 + n) of the gallery from G (host or device): an in-place update of existing rows and/or an
+// append (row0 <= rows).  Only the written rows are prepared (norm rule) and, on the bf16x3 path, split;
+// appends grow the allocation geometrically, so n single-row appends cost O(n) row copies amortised
+// instead of a full re-upload each (a served gallery under add_to_db traffic).
+int fr_gallery_write(fr_handle* h, const float* G, int64_t row0, int64_t n, int D, int g_on_device) {
+    if (!h || !G || n <= 0 || row0 < 0 || D <= 0 || D % 4 != 0) {
+        set_error("fr_gallery_write: bad argument");
+        return FR_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->g_rows > 0 && D != h->g_dim) { set_error("fr_gallery_write: D differs from the gallery's"); return FR_ERR_ARG; }
+    if (row0 > h->g_rows) { set_error("fr_gallery_write: row0 past the end (appends must be contiguous)"); return FR_ERR_ARG; }
+    const int64_t rows = std::max(h->g_rows, row0 + n);
+    if (rows + h->g_base > INT32_MAX) { set_error("fr_gallery_write: indices must fit int32"); return FR_ERR_ARG; }
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    const bool x3 = rows >= h->x3_min_rows && D == 512;
+    if (rows > h->g_cap || !h->gallery) {  // grow: 2x, copy the old rows on the device
+        const int64_t cap = std::max<int64_t>(rows, std::max<int64_t>(2 * h->g_cap, 1024));
+        float* g = nullptr;
+        int rc = dev_alloc((void**)&g, (size_t)cap * D * sizeof(float));
+        if (rc) return rc;
+        if (h->g_rows > 0)
+            FR_HIP_CHECK(hipMemcpy(g, h->gallery, (size_t)h->g_rows * D * sizeof(float), hipMemcpyDeviceToDevice));
+        if (h->gallery) (void)hipFree(h->gallery);
+        h->gallery = g;
+        if (h->g_hi) { (void)hipFree(h->g_hi); h->g_hi = nullptr; }  // re-split below at the new capacity
+        if (h->g_lo) { (void)hipFree(h->g_lo); h->g_lo = nullptr; }
+        h->g_cap = cap;
+    }
+    FR_HIP_CHECK(hipMemcpy(h->gallery + (size_t)row0 * D, G, (size_t)n * D * sizeof(float),
+                           g_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+    FR_HIP_CHECK(launch_gallery_prepare(h->gallery + (size_t)row0 * D, n, D, nullptr));
+    if (x3) {
+        int64_t s0 = row0, sn = n;
+        if (!h->g_hi) {  // first time on the bf16x3 path (or re-grown): split every row
+            int rc = dev_alloc((void**)&h->g_hi, (size_t)h->g_cap * D * sizeof(bf16_t));
+            if (!rc) rc = dev_alloc((void**)&h->g_lo, (size_t)h->g_cap * D * sizeof(bf16_t));
+            if (!rc && !h->match_fb) {
+                rc = dev_alloc((void**)&h->match_fb, sizeof(int));
+                if (!rc) FR_HIP_CHECK(hipMemset(h->match_fb, 0, sizeof(int)));
+            }
+            if (rc) return rc;
+            s0 = 0;
+            sn = rows;
+        }
+        FR_HIP_CHECK(launch_split_bf16(h->gallery + (size_t)s0 * D, (size_t)sn * D, h->g_hi + (size_t)s0 * D,
+                                       h->g_lo + (size_t)s0 * D, nullptr));
+    }
+    FR_HIP_CHECK(hipDeviceSynchronize());
+    h->g_rows = rows;
+    h->g_dim = D;
     return FR_OK;
 }
 

@@ -38,9 +38,8 @@ class DeviceGallery:
         self._h = handle
         if x3_min_rows is not None:  # FR_OPT_X3_MIN_ROWS: smallest gallery given the bf16x3 path
             N.check(N.lib().fr_set_option(self._h, N.FR_OPT_X3_MIN_ROWS, int(x3_min_rows)), "fr_set_option")
-        self._rows = torch.empty((0, dim), dtype=torch.float32)  # host copy (rows added from the host)
-        self._rows_dev = None  # device rows installed by set_device_rows (no host copy is made)
-        self._n = 0
+        self._n = 0  # rows live on the device only (fr_gallery_write appends in place)
+        N.check(N.lib().fr_gallery_set(self._h, None, 0, dim, self.index_base, 0), "fr_gallery_set")  # base, dim
         if rows is not None:
             self.add(rows)
 
@@ -49,33 +48,37 @@ class DeviceGallery:
         return self._n
 
     def reset(self) -> None:
-        import torch
-        self._rows = torch.empty((0, self.d), dtype=torch.float32)
-        self._rows_dev, self._n = None, 0
+        self._n = 0
         N.check(N.lib().fr_gallery_set(self._h, None, 0, self.d, self.index_base, 0), "fr_gallery_set")
 
-    def add(self, rows) -> None:
-        """Append rows (IndexFlatIP.add); re-uploads the whole matrix (gallery builds are rare)."""
+    def _write(self, row0: int, rows) -> int:
+        """fr_gallery_write of rows [row0, row0 + n) from host or device memory; returns n."""
         import torch
 
-        r = torch.as_tensor(np.asarray(rows, dtype=np.float32) if not torch.is_tensor(rows) else rows)
-        r = r.detach().float().cpu().reshape(-1, self.d)
-        if self._rows_dev is not None:  # rows installed from the device: bring them over once
-            self._rows, self._rows_dev = self._rows_dev.cpu(), None
-        self._rows = torch.cat([self._rows, r], 0).contiguous()
-        self._n = int(self._rows.shape[0])
-        self._upload()
+        r = rows if torch.is_tensor(rows) else torch.from_numpy(np.ascontiguousarray(np.asarray(rows, np.float32)))
+        r = r.detach().float().reshape(-1, self.d).contiguous()
+        n = int(r.shape[0])
+        if n:
+            N.check(N.lib().fr_gallery_write(self._h, N.ptr(r), int(row0), n, self.d, int(r.is_cuda)),
+                    "fr_gallery_write")
+        return n
+
+    def add(self, rows) -> None:
+        """Append rows (IndexFlatIP.add): written in place on the device, amortised O(new rows)."""
+        self._n += self._write(self._n, rows)
+
+    def update(self, row0: int, rows) -> None:
+        """Overwrite rows [row0, row0 + n) (a dict-db entry re-embedded); row0 + n may run past the end."""
+        if not 0 <= row0 <= self._n:
+            raise IndexError(f"row {row0} outside a {self._n}-row gallery")
+        self._n = max(self._n, row0 + self._write(row0, rows))
 
     def set_device_rows(self, rows_dev) -> None:
         """Install rows already resident on the GPU (no host round trip; the library copies them)."""
         rows_dev = rows_dev.float().contiguous()
         N.check(N.lib().fr_gallery_set(self._h, N.ptr(rows_dev), int(rows_dev.shape[0]), self.d, self.index_base, 1),
                 "fr_gallery_set")
-        self._rows_dev, self._n = rows_dev.detach(), int(rows_dev.shape[0])
-
-    def _upload(self) -> None:
-        N.check(N.lib().fr_gallery_set(self._h, N.ptr(self._rows), self._n, self.d, self.index_base, 0),
-                "fr_gallery_set")
+        self._n = int(rows_dev.shape[0])
 
     def set_exact(self, exact: bool) -> None:
         """FR_OPT_MATCH_EXACT: force the f32-MFMA kernel (default: bf16x3 candidates + exact rescoring

@@ -84,24 +84,51 @@ def load_npy_object(path: str):
     return arr.item() if isinstance(arr, np.ndarray) and arr.shape == () else arr
 
 
-class _TrackedDB(dict):
-    """dict that counts mutations so the device copy knows when to refresh."""
-    version = 0
+class _Grow:
+    """A numpy vector with amortised O(1) append (capacity doubling); `view` is the live prefix."""
 
-    def _bump(self):
+    def __init__(self, a):
+        a = np.asarray(a)
+        self._buf = np.empty(max(16, 2 * len(a)), dtype=a.dtype)
+        self._buf[:len(a)] = a
+        self._n = len(a)
+
+    def append(self, x):
+        if self._n == len(self._buf):
+            self._buf = np.concatenate([self._buf, np.empty_like(self._buf)])
+        self._buf[self._n] = x
+        self._n += 1
+
+    @property
+    def view(self):
+        return self._buf[:self._n]
+
+
+class _TrackedDB(dict):
+    """dict that counts mutations so the device copy knows when to refresh, and journals plain item
+    assignments (the add_to_db / db[name] = emb pattern) so the device copy can apply them in place
+    instead of rebuilding; any other mutation (del, pop, clear, ...) marks the journal unusable."""
+    version = 0
+    journal = None  # [keys assigned since the device copy synced] or None: rebuild
+
+    def _bump(self, key=None):
         self.version += 1
+        if key is None:
+            self.journal = None
+        elif self.journal is not None:
+            self.journal.append(key)
 
     def __setitem__(self, k, v):
         super().__setitem__(k, v)
-        self._bump()
+        self._bump(k)
 
     def __delitem__(self, k):
         super().__delitem__(k)
         self._bump()
 
     def update(self, *a, **k):
-        super().update(*a, **k)
-        self._bump()
+        for key, v in dict(*a, **k).items():
+            self[key] = v
 
     def pop(self, *a):
         r = super().pop(*a)
@@ -118,9 +145,9 @@ class _TrackedDB(dict):
         self._bump()
 
     def setdefault(self, k, v=None):
-        r = super().setdefault(k, v)
-        self._bump()
-        return r
+        if k not in self:
+            self[k] = v
+        return self[k]
 
 
 class RecognitionEngine:
@@ -250,6 +277,9 @@ class RecognitionEngine:
         (every fr_embed output) then take one search."""
         from .gallery import DeviceGallery
         key = (id(self._db), self._db.version)
+        if self._g is not None and self._g[0] != key and self._g[0][0] == id(self._db) and self._db.journal is not None:
+            if self._db_apply_journal():
+                self._g = (key, self._g[1], self._g[2])
         if self._g is None or self._g[0] != key:
             names = list(self._db.keys())
             rows = np.stack([np.asarray(v, dtype=np.float32).reshape(-1) for v in self._db.values()])
@@ -257,12 +287,54 @@ class RecognitionEngine:
             on = np.abs(n - 1.0) < 1e-3
             dev = self.model.device.index if self.model is not None else _device_index(self.device)
             unit = rows / np.where(n > 0, n, 1.0)[:, None]
-            parts = {"dev": dev, "unit": unit, "dim": rows.shape[1]}
+            parts = {"dev": dev, "dim": rows.shape[1], "pos": {k: i for i, k in enumerate(names)},
+                     "on_mask": _Grow(on)}
             for tag, mask, src in (("on", on, rows), ("off", ~on, unit)):
                 idx = np.nonzero(mask)[0]
-                parts[tag] = (DeviceGallery(src[idx], dim=rows.shape[1], device=dev), idx) if len(idx) else None
+                parts[tag] = (DeviceGallery(src[idx], dim=rows.shape[1], device=dev), _Grow(idx)) if len(idx) else None
             self._g = (key, parts, names)
+        self._db.journal = []
         return self._g[1], self._g[2]
+
+    def _db_apply_journal(self) -> bool:
+        """Apply the db's journaled assignments to the device copy in place: a new name appends one row
+        to its part (and to the 'all' copy), a re-assigned name overwrites its row when its norm class
+        ('on' / 'off') is unchanged.  False (-> rebuild) for anything else."""
+        from .gallery import DeviceGallery
+        parts, names = self._g[1], self._g[2]
+        for k in self._db.journal:
+            v = np.asarray(self._db[k], dtype=np.float32).reshape(1, -1)
+            if v.shape[1] != parts["dim"]:
+                return False
+            nv = float(np.linalg.norm(v))
+            on = abs(nv - 1.0) < 1e-3
+            u = v / (nv if nv > 0 else 1.0)
+            tag = "on" if on else "off"
+            src = v if on else u
+            if k in parts["pos"]:
+                i = parts["pos"][k]
+                if bool(parts["on_mask"].view[i]) != on:
+                    return False
+                g, idx = parts[tag]
+                g.update(int(np.searchsorted(idx.view, i)), src)
+                if "all" in parts:
+                    parts["all"][0].update(i, u)
+            else:
+                i = len(names)
+                names.append(k)
+                parts["pos"][k] = i
+                parts["on_mask"].append(on)
+                if parts[tag] is None:
+                    parts[tag] = (DeviceGallery(src, dim=parts["dim"], device=parts["dev"]), _Grow(np.array([i])))
+                else:
+                    g, idx = parts[tag]
+                    g.add(src)
+                    idx.append(i)
+                if "all" in parts:
+                    g, idx = parts["all"]
+                    g.add(u)
+                    idx.append(i)
+        return True
 
     # ------------------------------------------------------------------ embedding
     # ------------------------------------------------------------------ embedding
@@ -279,7 +351,7 @@ class RecognitionEngine:
         import torch
         g, idx = part
         s, i = g.search_device(torch.from_numpy(np.ascontiguousarray(P)).to(g.device), min(k, g.ntotal))
-        return s.cpu().numpy(), idx[i.cpu().numpy()]
+        return s.cpu().numpy(), idx.view[i.cpu().numpy()]
 
     @staticmethod
     def _merge(lists, k):
@@ -311,8 +383,10 @@ class RecognitionEngine:
         if len(sel):  # other probes (zero probes stay zero: every score 0.0): dot / (|p| |g|) everywhere
             if "all" not in parts:
                 from .gallery import DeviceGallery
-                parts["all"] = (DeviceGallery(parts["unit"], dim=parts["dim"], device=parts["dev"]),
-                                np.arange(len(names)))
+                rows = np.stack([np.asarray(self._db[nm], dtype=np.float32).reshape(-1) for nm in names])
+                nr = np.linalg.norm(rows, axis=1)
+                parts["all"] = (DeviceGallery(rows / np.where(nr > 0, nr, 1.0)[:, None], dim=parts["dim"],
+                                              device=parts["dev"]), _Grow(np.arange(len(names))))
             S[sel], I[sel] = self._search_mapped(parts["all"], E_unit[sel], k)
         return S, I, names
 

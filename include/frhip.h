@@ -113,6 +113,13 @@ int fr_sync_check(fr_handle* h, void* stream);
 int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index_base, int g_on_device);
 int64_t fr_gallery_rows(const fr_handle* h);
 
+/* Write rows [row0, row0 + n) of the gallery from G [n, D] (host or device): an in-place update of
+ * existing rows and/or a contiguous append (row0 <= fr_gallery_rows).  Only the written rows are
+ * prepared as in fr_gallery_set (and split for the bf16x3 path); appends grow the allocation
+ * geometrically.  Replaces the rebuild-per-edit of the reference's dict db / IndexFlatIP.add
+ * (recognition_engine.py:406-418 add_to_db; extract_embeddings.py:625-632). */
+int fr_gallery_write(fr_handle* h, const float* G, int64_t row0, int64_t n, int D, int g_on_device);
+
 /* Top-k of P [B, D] (device f32, L2-normalized probes) against the gallery.
  * Results (device): scores [B, k] f32 descending, idx [B, k] int32; ties are
  * broken by lower index (stable sort(reverse=True) / np.argmax semantics).

@@ -258,3 +258,32 @@ def test_facenet_matcher_vs_web_route():
         assert got["identity"] == name and [t[0] for t in got["top_k"]] == [t[0] for t in top]
         assert abs(got["confidence"] - score) < 1e-5 and abs(got["distance"] - dist) < 1e-5
         assert np.allclose([t[2] for t in got["top_k"]], [t[2] for t in top], atol=1e-5)
+
+
+def test_db_edits_in_place_on_device():
+    """The journaled add_to_db edits through the real device galleries (fr_gallery_write) answer like the
+    reference's recognize_with_db over the same dict, before and after a rebuild."""
+    from facerecognition_amd.recognition_engine import RecognitionEngine
+    from oracle.match import recognize_with_db
+    from test_host_api import mixed_norm_case
+    db, probes = mixed_norm_case()
+    eng = RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.0)
+    eng.db = dict(db)
+    rng = np.random.default_rng(10)
+
+    def check():
+        for p in probes:
+            name, _, top = eng.recognize_with_db(p)
+            rname, _, rtop = recognize_with_db(p, dict(eng.db), 0.0)
+            assert name == rname and [t[0] for t in top] == [t[0] for t in rtop]
+            assert np.allclose([t[1] for t in top], [t[1] for t in rtop], atol=1e-6)
+
+    check()
+    parts0 = eng._g[1]
+    for j in range(40):  # many single-row appends (capacity growth) + in-place updates
+        v = rng.standard_normal(8).astype(np.float32)
+        eng.db[f"n{j}"] = v / np.linalg.norm(v) if j % 2 else 3.0 * v
+        if j % 7 == 0:
+            eng.db["A"] = np.roll(db["A"], j % 3)
+        check()
+    assert eng._g[1] is parts0

@@ -690,3 +690,33 @@ def test_recognize_with_faiss_large_k(gpu, tmp_path):
     assert [r[0] for r in res] == [f"ID_{j}" for j in i_ref[0]]
     assert np.allclose([r[1] for r in res], s_ref[0], atol=1e-5)
     assert name == "ID_17"
+
+
+def test_gallery_write_appends_and_updates_equal_rebuild(gpu):
+    """fr_gallery_write: single-row appends (crossing the bf16x3 threshold and several capacity
+    doublings), batch appends and in-place row updates give the same top-k, bit for bit, as one
+    fr_gallery_set of the final matrix."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(17)
+    G = _norm(rng.standard_normal((3000, 512)))
+    G[100] *= 3.0  # a non-unit row: the norm rule must apply to written rows too
+    gal = DeviceGallery(dim=512, x3_min_rows=2048)
+    for r in range(1500):
+        gal.add(G[r:r + 1])
+    gal.add(torch.from_numpy(G[1500:2600]).cuda())  # device rows: crosses x3_min_rows
+    gal.add(G[2600:])
+    upd = _norm(rng.standard_normal((3, 512)))
+    for j, r in enumerate((7, 2047, 2999)):
+        G[r] = upd[j]
+        gal.update(r, upd[j:j + 1])
+    assert gal.ntotal == 3000
+    ref = DeviceGallery(G, x3_min_rows=2048)
+    P = _norm(rng.standard_normal((64, 512)))
+    P[:3] = upd
+    for k in (1, 5, 16, 40):
+        s, i = gal.search(P, k)
+        rs, ri = ref.search(P, k)
+        assert np.array_equal(s, rs) and np.array_equal(i, ri), k
+    assert list(gal.search(P[:3], 1)[1][:, 0]) == [7, 2047, 2999]
+    gal.close()
+    ref.close()

@@ -137,6 +137,20 @@ class _NumpyGallery:
     def ntotal(self):
         return len(self.rows)
 
+    def _prep(self, rows):
+        r = np.asarray(rows, np.float32).reshape(-1, self.rows.shape[1]).copy()
+        n = np.linalg.norm(r, axis=1)
+        fix = (np.abs(n - 1) >= 1e-3) & (n > 0)
+        r[fix] /= n[fix, None]
+        return r
+
+    def add(self, rows):  # fr_gallery_write append
+        self.rows = np.concatenate([self.rows, self._prep(rows)], 0)
+
+    def update(self, row0, rows):  # fr_gallery_write in place
+        r = self._prep(rows)
+        self.rows[row0:row0 + len(r)] = r
+
     def search_device(self, P, k):
         import torch
         s, i = OMT.topk_dot(P.numpy(), self.rows, k)
@@ -155,6 +169,41 @@ def test_recognize_with_db_mixed_norm_semantics(monkeypatch):
         assert name == rname and [t[0] for t in top] == [t[0] for t in rtop]
         assert np.allclose([t[1] for t in top], [t[1] for t in rtop], atol=1e-6)
     assert eng.recognize_with_db(probes[0])[0] == "A"  # the near-tie resolves as the reference does
+
+
+def test_db_edits_apply_in_place_and_match_a_rebuild(monkeypatch):
+    """add_to_db-style edits (new names, re-assigned names in the same norm class) are applied to the
+    device copy in place (no rebuild); a class change or a deletion rebuilds; every state answers like
+    the reference's recognize_with_db over the same dict."""
+    from facerecognition_amd import gallery
+    monkeypatch.setattr(gallery, "DeviceGallery", _NumpyGallery)
+    db, probes = mixed_norm_case()
+    eng = RE.RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.0)
+    eng.db = dict(db)
+    rng = np.random.default_rng(9)
+
+    def check():
+        for p in probes + [rng.standard_normal(8).astype(np.float32)]:
+            name, _, top = eng.recognize_with_db(p)
+            rname, _, rtop = OMT.recognize_with_db(p, dict(eng.db), 0.0)
+            assert name == rname and [t[0] for t in top] == [t[0] for t in rtop]
+            assert np.allclose([t[1] for t in top], [t[1] for t in rtop], atol=1e-6)
+
+    check()
+    parts0 = eng._g[1]
+    v = rng.standard_normal(8).astype(np.float32)
+    eng.db["new_unit"] = v / np.linalg.norm(v)      # append to 'on'
+    eng.db["new_off"] = 2.0 * v                     # append to 'off'
+    eng.db["A"] = np.roll(db["A"], 1)               # same class, in place
+    check()
+    assert eng._g[1] is parts0, "journaled edits must not rebuild the device copy"
+    eng.db["big"] = db["big"] / 3.0                 # 'off' -> 'on': rebuild
+    check()
+    assert eng._g[1] is not parts0
+    parts1 = eng._g[1]
+    del eng.db["B"]                                 # deletion: rebuild
+    check()
+    assert eng._g[1] is not parts1
 
 
 def test_extract_batch_empty_and_bad_paths():
