@@ -36,6 +36,11 @@ constexpr int NST = 4;                      // LDS stages
 // KSS = 32-deep substeps per LDS stage (2: 128-B rows, 16 KiB stages; 4: 256-B rows, 32 KiB stages, half
 // the barriers, needs Cin % 128 == 0); NW = waves = output channels / 32 (8: 256 channels, one block per
 // CU; 4: 128 channels, two blocks per CU)
+#ifndef FR_WRING_DEPTH
+#define FR_WRING_DEPTH 4  // weight register ring: substeps in flight + 1 (4: 3 ahead; 8: 7 ahead), divides 16
+#endif
+static_assert(16 % FR_WRING_DEPTH == 0, "ring slots must be compile-time within a 16-substep iteration");
+
 template <int KSS, int NW>
 struct WGeo {
     static constexpr int BN = 32 * NW, EPI_LD = BN + 4, EPI_B = BM * EPI_LD * 4;
@@ -47,7 +52,8 @@ struct WGeo {
     // vmcnt when stage t's last substep waits for DMA(t + 1): VMEM ops younger than it (the prologue
     // issues DMA0..3 then W0..2; stage t issues its KSS weight loads (2 ops each) and, after the
     // boundary, DMA(t + 4)): t = 0 / 1 / >= 2
-    static constexpr int Yb0 = 2 * PPW + 2 * KSS + 6, Yb1 = 2 * PPW + 4 * KSS + 6, Yb = 2 * PPW + 6 * KSS;
+    static constexpr int WP = 2 * (FR_WRING_DEPTH - 1);  // VMEM ops of the prologue's weight loads
+    static constexpr int Yb0 = 2 * PPW + 2 * KSS + WP, Yb1 = 2 * PPW + 4 * KSS + WP, Yb = 2 * PPW + 6 * KSS;
     static_assert(Yb0 <= 63 && Yb1 <= 63 && Yb <= 63, "vmcnt field");
     __device__ static int swz(int row) { return KSS == 2 ? (row >> 1) & 7 : row & 15; }
 };
@@ -68,6 +74,26 @@ constexpr uint32_t OOB = 0x80000000u;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// FR_WRING_TRACE (timing experiments only, tools/wring_trace.py): blocks 0 and WTRACE_B2 stamp the low 32
+// bits of the shader clock per wave at kernel start (0), after the prologue (1), before each of the first
+// WTRACE_ST stage-boundary waits (2 + 2t) and after its barrier (3 + 2t), at the main loop's end and at the
+// kernel's end, into LDS past the kernel's own; copied to g_wring_trace at the end (the last launch wins).
+#ifdef FR_WRING_TRACE
+constexpr int WTRACE_ST = 40, WTRACE_N = 4 + 2 * WTRACE_ST, WTRACE_B2 = 100;
+__device__ unsigned int g_wring_trace[2][8][WTRACE_N];
+#define WTRACE(ldsb, k)                                                                                     \
+    do {                                                                                                    \
+        if ((blockIdx.x == 0 || blockIdx.x == WTRACE_B2) && (k) < WTRACE_N) {                               \
+            const unsigned t_ = (unsigned)__builtin_readcyclecounter();                                      \
+            *(volatile __attribute__((address_space(3))) unsigned*)(uintptr_t)((ldsb) + (wave * WTRACE_N + (k)) * 4) = t_; \
+        }                                                                                                   \
+    } while (0)
+#else
+#define WTRACE(ldsb, k) \
+    do {                \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
 }
@@ -83,6 +109,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    WTRACE(Gm::LDS, 0);
     const int lid = xcd_remap(blockIdx.x, gridDim.x);
     const int tn = lid / tiles_m, tm = lid - tn * tiles_m;  // pixels fastest: an XCD keeps one weight half
     const int m0 = tm * BM, n0 = tn * BN;
@@ -161,7 +188,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
         (void*)p.wimg, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)p.Kpad * p.Npad * 2), 0x00020000);
     const uint32_t wvo = (uint32_t)(((lane >> 4) * p.Npad + n0 + 32 * wave + (lane & 15)) * 16);
     const uint32_t wstep = (uint32_t)(64 * p.Npad);  // bytes per substep image
-    frag wq[4][2];
+    constexpr int WD = FR_WRING_DEPTH;
+    frag wq[WD][2];
     auto wload = [&](frag (&w)[2], int s) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -193,11 +221,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
     issue(1);
     issue(2);
     issue(3);
-    wload(wq[0], 0);
-    wload(wq[1], 1);
-    wload(wq[2], 2);
-    wait_vm<3 * PPW + 6>();
+#pragma unroll
+    for (int q = 0; q < WD - 1; ++q) wload(wq[q], q);
+    wait_vm<3 * PPW + Gm::WP>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    WTRACE(Gm::LDS, 1);
     bread(bq[0], 0, 0);
 
     auto mfmas = [&](int slot_w, frag (&b)[FM]) {
@@ -226,9 +254,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
             const int slot = t & (NST - 1), nslot = (t + 1) & (NST - 1);
 #pragma unroll
             for (int kk = 0; kk < KSS; ++kk) {
-                const int s = t * KSS + kk, w = (u * KSS + kk) & 3;  // s4 % 4 == 0: compile-time ring slots
+                const int s = t * KSS + kk, w = (u * KSS + kk) % WD;  // s4 % 16 == 0: compile-time ring slots
                 __builtin_amdgcn_sched_barrier(0);
-                wload(wq[(w + 3) & 3], s + 3 < nks ? s + 3 : nks - 1);
+                wload(wq[(w + WD - 1) % WD], s + WD - 1 < nks ? s + WD - 1 : nks - 1);
                 if (kk + 1 < KSS) {
                     bread(bq[(kk + 1) & 1], slot, kk + 1);
                     mfmas(w, bq[kk & 1]);
@@ -241,10 +269,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
 #endif
                 } else {
                     prep();  // stage t + 4's offsets while the previous substep's MFMAs run
+                    WTRACE(Gm::LDS, 2 + 2 * t);
                     if (t >= 2) wait_vm<Gm::Yb>();
                     else if (t == 1) wait_vm<Gm::Yb1>();
                     else wait_vm<Gm::Yb0>();
                     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                    WTRACE(Gm::LDS, 3 + 2 * t);
                     __builtin_amdgcn_sched_barrier(0);
                     fire(slot);  // stage t + 4 into stage t's slot
                     bread(bq[(kk + 1) & 1], nslot, 0);
@@ -262,6 +292,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
     }
 
     // ---- epilogue: accumulators -> f32 LDS tile [BM][EPI_LD] -> coalesced 8-channel groups
+    WTRACE(Gm::LDS, WTRACE_N - 2);
     constexpr int G = BN / 8, RS = 64 * NW / G, ITER = BM / RS;  // 32 groups, 16 rows per pass, 7 passes
     static_assert(RS * G == 64 * NW && ITER * RS == BM, "epilogue mapping");
     const int g = tid % G, ml0 = tid / G, n = n0 + g * 8;
@@ -324,6 +355,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
         }
         *(uint4*)(p.y + (size_t)m * p.Cy + p.y_off + n) = F16 && p.y_bf16 ? Num<false>::pack8(v) : T::pack8(v);
     }
+#ifdef FR_WRING_TRACE
+    WTRACE(Gm::LDS, WTRACE_N - 1);
+    __syncthreads();
+    if (blockIdx.x == 0 || blockIdx.x == WTRACE_B2)
+        for (int c = tid; c < NW * WTRACE_N; c += 64 * NW)
+            ((unsigned*)g_wring_trace)[(blockIdx.x == 0 ? 0 : 8 * WTRACE_N) + c] =
+                *(volatile __attribute__((address_space(3))) unsigned*)(uintptr_t)(Gm::LDS + c * 4);
+#endif
 }
 
 // out[s][g][n][e] = w[n][32 s + 8 g + e]: one 32-deep substep image per s
@@ -364,16 +403,21 @@ hipError_t launch_kss(const ConvArgs& a, hipStream_t s) {
     typedef WGeo<KSS, NW> Gm;
     const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.Cout / Gm::BN;
     auto k = a.f16 ? conv_wring_kernel<true, KSS, NW> : conv_wring_kernel<false, KSS, NW>;
+#ifdef FR_WRING_TRACE
+    const int lds = Gm::LDS + 8 * WTRACE_N * 4;
+#else
+    const int lds = Gm::LDS;
+#endif
     static bool attr[2] = {false, false};
     if (!attr[a.f16 ? 1 : 0]) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, Gm::LDS);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr[a.f16 ? 1 : 0] = true;
     }
     const dim3 grid((unsigned)(tiles_m * tiles_n));
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, grid, dim3(64 * NW), Gm::LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, tiles_m);
+        hipExtLaunchKernelGGL(k, grid, dim3(64 * NW), lds, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, tiles_m);
     else
-        hipLaunchKernelGGL(k, grid, dim3(64 * NW), Gm::LDS, s, a, tiles_m);
+        hipLaunchKernelGGL(k, grid, dim3(64 * NW), lds, s, a, tiles_m);
     return hipGetLastError();
 }
 
@@ -386,6 +430,14 @@ static bool use_kss4(const ConvArgs& a) {
     const bool ok = a.Cin % 128 == 0 && (!a.x2 || a.C2 % 128 == 0) && a.Kpad % 128 == 0 && a.Kpad / 128 >= 3;
     return ok && force != 2;
 }
+
+#ifdef FR_WRING_TRACE
+extern "C" int fr_wring_trace_read(unsigned int* out, int n) {
+    const int all = (int)(sizeof(g_wring_trace) / sizeof(unsigned int));
+    if (n < all) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wring_trace), sizeof(g_wring_trace)) == hipSuccess ? all : -2;
+}
+#endif
 
 hipError_t launch_conv_wring(const ConvArgs& a, hipStream_t s) {
     if (!wring_supported(a) || !a.wimg) return hipErrorInvalidValue;
