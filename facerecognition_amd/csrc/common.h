@@ -74,6 +74,13 @@ static inline float host_bf2f(bf16_t v) {
     return f;
 }
 
+// min(v, 0) as a raw v_min_f32: fminf first canonicalizes its operand (one more VALU op per value); the
+// epilogues apply it to MFMA accumulators, which are never signalling NaNs, so the result bits are the same
+__device__ __forceinline__ float min0_raw(float v) {
+    float r;
+    asm("v_min_f32 %0, 0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
 // Pack two floats into two bf16 (RNE): one v_cvt_pk_bf16_f32 on gfx950 (two scalar casts can come out

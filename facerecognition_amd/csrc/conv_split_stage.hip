@@ -387,10 +387,10 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
                     char* slot = slot0 + ((f / QPR) * PC + 16 * q) * 16;
                     float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
                     if (!second) {
-                        v[0] = fmaf(s1.x, fminf(v[0], 0.f), v[0]);
-                        v[1] = fmaf(s1.y, fminf(v[1], 0.f), v[1]);
-                        v[2] = fmaf(s1.z, fminf(v[2], 0.f), v[2]);
-                        v[3] = fmaf(s1.w, fminf(v[3], 0.f), v[3]);
+                        v[0] = fmaf(s1.x, min0_raw(v[0]), v[0]);
+                        v[1] = fmaf(s1.y, min0_raw(v[1]), v[1]);
+                        v[2] = fmaf(s1.z, min0_raw(v[2]), v[2]);
+                        v[3] = fmaf(s1.w, min0_raw(v[3]), v[3]);
                     }
                     float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
                     const uint4 pk = T::pack8(o8);

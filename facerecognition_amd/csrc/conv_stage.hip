@@ -77,6 +77,13 @@ __device__ unsigned int g_stage_trace[2][8][TRACE_CONVS][4];
     do {                   \
     } while (0)
 #endif
+#ifndef FR_STAGE_PRIO
+#define FR_STAGE_PRIO 0  // A/B: 1 = the 6-fragment waves at s_setprio 1; 2 = priority alternating between the two
+                         // waves of a SIMD every 18 K-steps
+#endif
+#ifndef FR_STAGE13_RING6
+#define FR_STAGE13_RING6 3  // weight-ring depth of the 6-fragment waves (18 % RING == 0)
+#endif
 #ifndef FR_STAGE13_RING7
 #define FR_STAGE13_RING7 2  // weight-ring depth of the 13-fragment kernel's 7-fragment waves (3: as the others)
 #endif
@@ -306,10 +313,10 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
                 char* slot = slot0 + j * 256;  // position m + 1 = wm*112 + 16j + cc + 1
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
                 if (!second) {
-                    v[0] = fmaf(s1.x, fminf(v[0], 0.f), v[0]);
-                    v[1] = fmaf(s1.y, fminf(v[1], 0.f), v[1]);
-                    v[2] = fmaf(s1.z, fminf(v[2], 0.f), v[2]);
-                    v[3] = fmaf(s1.w, fminf(v[3], 0.f), v[3]);
+                    v[0] = fmaf(s1.x, min0_raw(v[0]), v[0]);
+                    v[1] = fmaf(s1.y, min0_raw(v[1]), v[1]);
+                    v[2] = fmaf(s1.z, min0_raw(v[2]), v[2]);
+                    v[3] = fmaf(s1.w, min0_raw(v[3]), v[3]);
                 }
                 float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
                 const uint4 pk = T::pack8(o8);
@@ -344,6 +351,10 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
                     *(uint4*)(dbg + img + (size_t)pix * SC + pl * 8) = v;
                 }
             }
+            // drained here, in this rarely taken branch: with global stores possibly pending at the K loop's
+            // head, the compiler's waitcnt pass treats vmcnt as out of order there and emits vmcnt(0) (the whole
+            // weight prefetch ring) at every cg-loop head
+            __builtin_amdgcn_s_waitcnt(0);
         }
     };
 #pragma unroll 1
@@ -417,7 +428,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     // weight ring depth: 3 K-steps (loads 2 ahead); the 7-fragment waves (which wait ~30 % of each conv at
     // the epilogue barrier for the 6-fragment ones) take 2 (1 ahead) and 16 VGPRs fewer: their body then
     // fits 256 VGPRs without the epilogue spills (FR_STAGE13_RING7, A/B)
-    constexpr int RING = FM == 7 ? FR_STAGE13_RING7 : 3;
+    constexpr int RING = FM == 7 ? FR_STAGE13_RING7 : FR_STAGE13_RING6;
     frag wq[RING][FN];
     auto wload = [&](frag (&w)[FN], int g) {
 #pragma unroll
@@ -506,7 +517,10 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     wload(wq[0], 0);
-    if (RING == 3) wload(wq[1 % RING], 1);
+    static_assert(18 % RING == 0, "ring slot = K-step % RING must be compile-time in the 18-step body");
+    if (FR_STAGE_PRIO == 1 && FM == 6) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 1; q < RING - 1; ++q) wload(wq[q], q);
 
     auto run_conv = [&](int cv, auto second_tag) {
         constexpr bool second = decltype(second_tag)::value;
@@ -521,6 +535,10 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         STAGE_TRACE(cv, 0);
 #pragma unroll 1
         for (int cg = 0; cg < SC / 32; cg += 2) {
+            if (FR_STAGE_PRIO == 2) {
+                if (((cg >> 1) & 1) == (FM == 7 ? 1 : 0)) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
 #pragma unroll
             for (int t = 0; t < 18; ++t) {
                 const int cgl = cg + t / 9, tap = t % 9;
@@ -555,10 +573,10 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
                 if (!second) {
                     const float4 sl = *(const float4*)(t2 + TAB_ROWS_B + n * 4);
-                    v[0] = fmaf(sl.x - 1.f, fminf(v[0], 0.f), v[0]);
-                    v[1] = fmaf(sl.y - 1.f, fminf(v[1], 0.f), v[1]);
-                    v[2] = fmaf(sl.z - 1.f, fminf(v[2], 0.f), v[2]);
-                    v[3] = fmaf(sl.w - 1.f, fminf(v[3], 0.f), v[3]);
+                    v[0] = fmaf(sl.x - 1.f, min0_raw(v[0]), v[0]);
+                    v[1] = fmaf(sl.y - 1.f, min0_raw(v[1]), v[1]);
+                    v[2] = fmaf(sl.z - 1.f, min0_raw(v[2]), v[2]);
+                    v[3] = fmaf(sl.w - 1.f, min0_raw(v[3]), v[3]);
                 }
                 float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
                 const uint4 pk = T::pack8(o8);
@@ -590,6 +608,10 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
                     *(uint4*)(dbg + img + (size_t)pix * SC + pl * 8) = v;
                 }
             }
+            // drained here, in this rarely taken branch: with global stores possibly pending at the K loop's
+            // head, the compiler's waitcnt pass treats vmcnt as out of order there and emits vmcnt(0) (the whole
+            // weight prefetch ring) at every cg-loop head
+            __builtin_amdgcn_s_waitcnt(0);
         }
     };
 #pragma unroll 1

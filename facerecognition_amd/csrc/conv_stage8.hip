@@ -241,10 +241,10 @@ __global__ __launch_bounds__(64 * NW, 1) void stage8_kernel(StageArgs p) {
             for (int j = 0; j < FM; ++j) {
                 float v0 = acc[i][j][0] * sc.x, v1 = acc[i][j][1] * sc.y, v2 = acc[i][j][2] * sc.z, v3 = acc[i][j][3] * sc.w;
                 if (!second) {
-                    v0 = fmaf(s1.x, fminf(v0, 0.f), v0);
-                    v1 = fmaf(s1.y, fminf(v1, 0.f), v1);
-                    v2 = fmaf(s1.z, fminf(v2, 0.f), v2);
-                    v3 = fmaf(s1.w, fminf(v3, 0.f), v3);
+                    v0 = fmaf(s1.x, min0_raw(v0), v0);
+                    v1 = fmaf(s1.y, min0_raw(v1), v1);
+                    v2 = fmaf(s1.z, min0_raw(v2), v2);
+                    v3 = fmaf(s1.w, min0_raw(v3), v3);
                 } else {  // the block output is the bf16 residual; the next conv quantizes that same value
                     const uint32_t a01 = pack2_bf16(v0, v1), a23 = pack2_bf16(v2, v3);
                     v0 = __uint_as_float(a01 << 16);
@@ -298,6 +298,7 @@ __global__ __launch_bounds__(64 * NW, 1) void stage8_kernel(StageArgs p) {
                 const int plane = c / SPIX, pix = c - plane * SPIX;
                 *(uint4*)(yo + img + (size_t)pix * SC + plane * 8) = *(const uint4*)(X + c * 16);
             }
+            __builtin_amdgcn_s_waitcnt(0);  // drained here, not by a compiler vmcnt(0) at every K-loop head
         }
     };
 #pragma unroll 1
