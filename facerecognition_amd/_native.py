@@ -31,6 +31,7 @@ FR_TILE_IMG28 = 10
 FR_TILE_IMG56 = 11
 FR_TILE_ROWS = 12
 FR_TILE_WRING = 13
+FR_TILE_DIRECT = 14
 FR_OPT_STAGE = 1
 FR_OPT_KEEP_INTERMEDIATES = 2
 FR_OPT_MATCH_EXACT = 3

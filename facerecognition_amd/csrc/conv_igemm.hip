@@ -631,6 +631,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
         w.wimg = a.wring_;
         return launch_conv_wring(w, s);
     }
+    if (a.tile == TILE_DIRECT) return launch_conv_direct(a, 0, s);  // conv_direct.hip (an autotuner pick)
     return a.f16 ? launch_dtype<true>(a, s) : launch_dtype<false>(a, s);
 }
 

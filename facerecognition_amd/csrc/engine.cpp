@@ -1161,6 +1161,14 @@ static bool wring_enabled() {
     return on;
 }
 
+static bool direct_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_DIRECT");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     int cand[16];
     int nc = conv_tile_candidates(a.Cout, cand);
@@ -1170,6 +1178,7 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
         w.partial = nullptr;
         if (wring_supported(w)) cand[nc++] = TILE_WRING;
     }
+    if (direct_enabled() && direct_supported(a)) cand[nc++] = TILE_DIRECT;  // small-K direct conv
     hipEvent_t e0, e1;
     FR_HIP_CHECK(hipEventCreate(&e0));
     FR_HIP_CHECK(hipEventCreate(&e1));
@@ -1259,7 +1268,10 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
     while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) split /= 2;
     if (split > 1) a.partial = h->partial;
     a.split_k = split;
-    ps.start(tile == TILE_WRING ? std::string("conv_wring") : "conv_igemm tile" + std::to_string(tile) + (split > 1 ? " splitk" : ""), &a);
+    ps.start(tile == TILE_WRING ? std::string("conv_wring")
+             : tile == TILE_DIRECT ? std::string("conv_direct")
+                                   : "conv_igemm tile" + std::to_string(tile) + (split > 1 ? " splitk" : ""),
+             &a);
     FR_HIP_CHECK(launch_conv(a, s));
     if (split > 1 && a.y) FR_HIP_CHECK(launch_splitk_epilogue(a, s));
     return FR_OK;
@@ -2213,6 +2225,11 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         a.wimg = (const bf16_t*)tw;
         FR_HIP_CHECK(launch_conv_wring(a, st));
         FR_HIP_CHECK(hipFreeAsync(tw, st));
+        return FR_OK;
+    }
+    if (d->tile == FR_TILE_DIRECT + 1) {
+        if (!direct_supported(a)) { set_error("fr_op_conv2d: direct kernel not applicable"); return FR_ERR_ARG; }
+        FR_HIP_CHECK(launch_conv_direct(a, 0, (hipStream_t)stream));
         return FR_OK;
     }
     if (d->tile == FR_TILE_ROWS + 1) {

@@ -9,7 +9,8 @@ namespace fr {
 enum { TILE_128x128 = 0, TILE_256x64 = 1, TILE_128x64 = 2, TILE_64x128 = 3,
        TILE_128x128_S3 = 4, TILE_256x128 = 5, TILE_128x256 = 6,  // *_S3 / 8-wave tiles: 3-stage DMA ring
        TILE_128x64_S3 = 8, TILE_64x128_S3 = 9, NUM_TILE_IDS = 10,     // (7 = the band kernel's id in the ABI)
-       TILE_WRING = 13 };  // conv_wring.hip (= FR_TILE_WRING), an autotuner candidate beside the igemm tiles
+       TILE_WRING = 13,    // conv_wring.hip (= FR_TILE_WRING), an autotuner candidate beside the igemm tiles
+       TILE_DIRECT = 14 }; // conv_direct.hip (= FR_TILE_DIRECT), the same
 
 // Implicit-GEMM convolution, NHWC bf16 in/out, f32 accumulate, fused epilogue.
 // GEMM view: M = B*Ho*Wo output pixels, N = Cout, K = Kh*Kw*Cin (c fastest).
@@ -53,6 +54,10 @@ bool wring_supported(const ConvArgs& a);
 size_t wring_packed_elems(int Kpad, int Npad);
 hipError_t wring_pack_weights(const bf16_t* w, int Kpad, int Npad, bf16_t* out, hipStream_t s);
 hipError_t launch_conv_wring(const ConvArgs& a, hipStream_t s);
+// Persistent small-K direct conv (conv_direct.hip): any Kh x Kw / stride / padding, Cin % 8 == 0, Kpad <= 384,
+// Cout % 32 == 0, bias + activation epilogue only; equal to conv_igemm tile 0 bit for bit.  n_cu <= 0: queried.
+bool direct_supported(const ConvArgs& a);
+hipError_t launch_conv_direct(const ConvArgs& a, int n_cu, hipStream_t s);
 // Persistent weight-resident 3x3/s1/p1 conv with 64 input channels (conv_rows.hip); a.wimg = the
 // rows_pack_weights image, a.ep / a.negf set.
 bool rows_supported(const ConvArgs& a);

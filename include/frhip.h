@@ -239,6 +239,8 @@ typedef struct fr_conv_desc {
                               * H % 4 == 0, bf16 (conv_rows.hip); auto-selected (env FR_NO_ROWS=1: off) */
 #define FR_TILE_WRING 13     /* implicit GEMM with a register weight ring (conv_wring.hip): Cin % 64 == 0, Cout % 256 == 0;
                                 autotuned per shape against the igemm tiles (env FR_NO_WRING=1: off) */
+#define FR_TILE_DIRECT 14    /* persistent small-K direct conv (conv_direct.hip): Cin % 8 == 0, Kpad <= 384, Cout % 32 == 0,
+                                bias + activation epilogue; autotuned per shape (env FR_NO_DIRECT=1: off) */
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 

@@ -189,6 +189,56 @@ def test_conv_wring(gpu, case):
         conv_op(x, torch.randn(64, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_WRING)
 
 
+DIRECT_CASES = [
+    # B, H, W, Cin, Cout, kh, kw, stride, pad, act   (FaceNet IRV1 shapes, smaller images)
+    (2, 41, 41, 8, 32, 3, 3, (2, 2), (0, 0), 1),      # conv2d_1a (Cin padded to 8, K = 72)
+    (2, 23, 23, 32, 32, 3, 3, (1, 1), (0, 0), 1),     # conv2d_2a (valid)
+    (3, 40, 40, 32, 64, 3, 3, (1, 1), (1, 1), 1),     # conv2d_2b (several units per image)
+    (2, 17, 17, 32, 32, 3, 3, (1, 1), (1, 1), 0),     # Block35 3x3
+    (2, 17, 17, 256, 96, 1, 1, (1, 1), (0, 0), 2),    # Block35 fused 1x1 256 -> 3 x 32 (PReLU path)
+    (2, 17, 17, 96, 256, 1, 1, (1, 1), (0, 0), 0),    # Block35 up 1x1 (K = 96)
+    (2, 8, 8, 256, 896, 1, 1, (1, 1), (0, 0), 1),     # Block17 up 1x1 (14 channel groups)
+    (1, 3, 3, 384, 1792, 1, 1, (1, 1), (0, 0), 0),    # Block8 up 1x1 (K = 384, the register limit)
+]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("case", DIRECT_CASES)
+def test_conv_direct(gpu, case, dtype):
+    """Persistent small-K direct conv (conv_direct.hip, forced): bias + ReLU / PReLU / none; it sums K in
+    the igemm's 32-deep MFMA chunks and applies the igemm's epilogue arithmetic, so it must equal tile 0
+    bit for bit (the autotuner times it beside the igemm tiles)."""
+    B, H, W, Cin, Cout, kh, kw, st, pd, act = case
+    g = torch.Generator().manual_seed(B + H + Cin + Cout + kh)
+    x = torch.randn(B, H, W, Cin, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    w = torch.randn(Cout, Cin, kh, kw, generator=g) / np.sqrt(Cin * kh * kw)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    slope = torch.rand(Cout, generator=g) * 0.5 if act == 2 else None
+    kw_ = dict(stride=st, pad=pd, bias=bias, act=act, slope=slope, dtype=dtype)
+    y = conv_op(x, w, tile=N.FR_TILE_DIRECT, **kw_)
+    _close(y, conv_ref(x, w, stride=st, pad=pd, bias=bias, act=act, slope=slope, dtype=dtype))
+    assert torch.equal(y, conv_op(x, w, tile=0, **kw_))
+
+
+def test_conv_direct_channel_slices_and_applicability(gpu):
+    """Input / output channel slices (IRV1 concatenations: x_off / Cx, y_off / Cy); shapes past the register
+    limit are refused (fail loudly, no silent fallback)."""
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(2, 17, 17, 320, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(32, 32, 3, 3, generator=g) / 17
+    out = torch.randn(2, 17, 17, 128, generator=g).to(torch.bfloat16).to(gpu)
+    before = out.clone()
+    conv_op(x, w, pad=(1, 1), x_off=96, cin=32, act=1, y=out, y_off=64, tile=N.FR_TILE_DIRECT)
+    _close(out[..., 64:96], conv_ref(x, w, pad=(1, 1), x_off=96, cin=32, act=1))
+    ref = out.clone()
+    out.copy_(before)
+    conv_op(x, w, pad=(1, 1), x_off=96, cin=32, act=1, y=out, y_off=64, tile=0)
+    assert torch.equal(out, ref)
+    assert torch.equal(ref[..., :64], before[..., :64]) and torch.equal(ref[..., 96:], before[..., 96:])
+    with pytest.raises(RuntimeError, match="direct"):  # K = 3 * 3 * 64 = 576 > 384
+        conv_op(x[..., :64].contiguous(), torch.randn(64, 64, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_DIRECT)
+
+
 def test_conv_img28_channel_slices_and_applicability(gpu):
     """img28 reads channels [128:256) of a 256-ch buffer and writes [64:192) of another; other shapes
     are refused (fail loudly, no silent fallback)."""
