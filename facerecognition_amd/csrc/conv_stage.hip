@@ -84,6 +84,9 @@ __device__ unsigned int g_stage_trace[2][8][TRACE_CONVS][4];
 #ifndef FR_STAGE13_RING6
 #define FR_STAGE13_RING6 3  // weight-ring depth of the 6-fragment waves (18 % RING == 0)
 #endif
+#ifndef FR_STAGE13_RING13
+#define FR_STAGE13_RING13 6  // weight-ring depth of the one-wave-per-SIMD 13-fragment variant (stage13w)
+#endif
 #ifndef FR_STAGE13_RING7
 #define FR_STAGE13_RING7 2  // weight-ring depth of the 13-fragment kernel's 7-fragment waves (3: as the others)
 #endif
@@ -428,7 +431,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     // weight ring depth: 3 K-steps (loads 2 ahead); the 7-fragment waves (which wait ~30 % of each conv at
     // the epilogue barrier for the 6-fragment ones) take 2 (1 ahead) and 16 VGPRs fewer: their body then
     // fits 256 VGPRs without the epilogue spills (FR_STAGE13_RING7, A/B)
-    constexpr int RING = FM == 7 ? FR_STAGE13_RING7 : FR_STAGE13_RING6;
+    constexpr int RING = FM == 13 ? FR_STAGE13_RING13 : (FM == 7 ? FR_STAGE13_RING7 : FR_STAGE13_RING6);
     frag wq[RING][FN];
     auto wload = [&](frag (&w)[FN], int g) {
 #pragma unroll
@@ -638,6 +641,19 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage13_kernel(StageArgs p) {
     else stage13_body<F16, 6, SNW, FR_STAGE_SINGLE>(p, smem, wave, lane, wave - 4, 7);       // fragments 7..12
 }
 
+// One wave per SIMD (variant 2): 4 waves, each all 13 pixel fragments x its 64 output channels (52 MFMAs per
+// K-step, accumulators in AGPRs, up to 512 registers per wave).  Every weight fragment is loaded by ONE wave
+// per CU (the 8-wave kernel loads each twice, once per pixel half, ~1/3 of a conv apart: two L2 reads) and
+// the ring runs 5 K-steps ahead; no second wave shares the SIMD, so none waits at the epilogue barrier
+// for its partner's K loop either.
+template <bool F16>
+__global__ __launch_bounds__(256, 1) void stage13w_kernel(StageArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    stage13_body<F16, 13, 4, FR_STAGE_SINGLE>(p, smem, wave, lane, wave, 0);
+}
+
 }  // namespace
 
 #ifdef FR_STAGE_TRACE
@@ -667,17 +683,20 @@ void stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out) {
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t s) {
-    // variant 1: the legacy 14-fragment kernel (bit-identical; FR_OPT_STAGE_VARIANT)
-    const int v = a.variant == 1 ? 1 : 0;
-    auto k = v == 1 ? (a.f16 ? stage_kernel<true> : stage_kernel<false>) : (a.f16 ? stage13_kernel<true> : stage13_kernel<false>);
+    // variant 1: the legacy 14-fragment kernel; 2: the one-wave-per-SIMD 13-fragment kernel (both
+    // bit-identical; FR_OPT_STAGE_VARIANT)
+    const int v = a.variant == 1 || a.variant == 2 ? a.variant : 0;
+    auto k = v == 1   ? (a.f16 ? stage_kernel<true> : stage_kernel<false>)
+             : v == 2 ? (a.f16 ? stage13w_kernel<true> : stage13w_kernel<false>)
+                      : (a.f16 ? stage13_kernel<true> : stage13_kernel<false>);
 #ifdef FR_STAGE_TRACE
     static_assert(TRACE_LDS == STAGE13_LDS, "trace area");
     const int lds = v == 1 ? STAGE_LDS : STAGE13_LDS + TRACE_B;
 #else
     const int lds = v == 1 ? STAGE_LDS : STAGE13_LDS;
 #endif
-    const int threads = 64 * SNW;
-    static bool attr[4] = {false, false, false, false};
+    const int threads = v == 2 ? 256 : 64 * SNW;
+    static bool attr[6] = {false, false, false, false, false, false};
     const int ai = 2 * v + (a.f16 ? 1 : 0);
     if (!attr[ai]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

@@ -168,7 +168,7 @@ struct fr_handle {
     int* fail_host = nullptr;
     int* fail_dev = nullptr;
     int spin_limit = 0;            // FR_OPT_STAGE_SPIN_LIMIT (0: the kernel's default, < 0: every wait runs out)
-    int stage_variant = 0;         // FR_OPT_STAGE_VARIANT (1: the legacy 14-fragment layer3 stage kernel)
+    int stage_variant = 0;         // FR_OPT_STAGE_VARIANT (1: the legacy 14-fragment layer3 stage kernel, 2: one wave per SIMD)
     bool no_split = false;         // re-run of a failed forward: split stages off
     int64_t stage_reruns = 0;      // forwards re-run on the per-conv path after a run-out wait
     hipEvent_t chk_ev = nullptr;   // completion of the last synchronous-checked forward
@@ -1553,7 +1553,10 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->dtype = dtype;
     h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
     h->stage_mode = stage_default();
-    if (const char* e = getenv("FR_STAGE_VARIANT")) h->stage_variant = atoi(e) == 1 ? 1 : 0;  // A/B timing
+    if (const char* e = getenv("FR_STAGE_VARIANT")) {  // A/B timing
+        const int v = atoi(e);
+        h->stage_variant = v == 1 || v == 2 ? v : 0;
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         h->n_cu = prop.multiProcessorCount;
@@ -2015,7 +2018,7 @@ int fr_set_option(fr_handle* h, int option, int value) {
             break;
         case FR_OPT_STAGE_SPIN_LIMIT: h->spin_limit = value; break;
         case FR_OPT_STAGE_VARIANT:
-            if (value < 0 || value > 1) { set_error("fr_set_option: FR_OPT_STAGE_VARIANT is 0 or 1"); return FR_ERR_ARG; }
+            if (value < 0 || value > 2) { set_error("fr_set_option: FR_OPT_STAGE_VARIANT is 0, 1 or 2"); return FR_ERR_ARG; }
             h->stage_variant = value;
             break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;

@@ -290,7 +290,8 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
 #define FR_OPT_STAGE_SPIN_LIMIT 6
 /* FR_OPT_STAGE_VARIANT (default 0): the layer3 stage kernel's pixel layout -- 0: 13 fragments of 16 pixels
  * per image (196 of 208 slots used), 1: the legacy 14 rows of 16 positions (2 halo columns computed and
- * discarded per row).  Both give the same bits (A/B and regression tests). */
+ * discarded per row), 2: the 13-fragment layout at one wave per SIMD (each weight fragment loaded once per
+ * CU).  All give the same bits (A/B and regression tests). */
 #define FR_OPT_STAGE_VARIANT 7
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);
