@@ -339,6 +339,13 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
                 const int hs = t == HALO_POS || t == HALO_POS + 1 ? halo : 0;
                 if (t & 1) kstep(g0 + cg * 9 + t, t % 3, pB, pA, cgn, tapn, hs);
                 else kstep(g0 + cg * 9 + t, t % 3, pA, pB, cgn, tapn, hs);
+                // publish the previous conv's boundary rows: step 1's wait (vmcnt(1): everything but the
+                // step-0 weight DMA) and barrier have completed every wave's row stores, so the counter can
+                // go out without a drain of its own (a vmcnt(0) + barrier after the epilogue also drained
+                // the weight ring and cost ~6 % of the stage, FR_SPLIT_EXP 2 timing)
+                if (t == 1 && cg == 0 && pending >= 0 && !(FR_SPLIT_EXP & 2) && threadIdx.x == 0 && !(FR_SPLIT_EXP & 1))
+                    __hip_atomic_store(my_flag, (int)((unsigned)f0 + (unsigned)(pending + 1)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             }
             halo = 0;
         }
@@ -444,12 +451,8 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
             }
         }
         if (exch && !(FR_SPLIT_EXP & 2)) {
-            // publish: every storing wave's rows are complete, a barrier, one sc1 counter store; the
-            // neighbours' rows are imported during the next conv (import_halo)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0 && !(FR_SPLIT_EXP & 1))
-                __hip_atomic_store(my_flag, (int)((unsigned)f0 + (unsigned)(cv + 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the rows are published at the next conv's K-step 1 (above), once every wave's stores are
+            // complete; the neighbours' rows are imported at its K-step 2 (import_halo)
             pending = cv;
         }
     };
