@@ -28,6 +28,8 @@
 
 #include <hip/hip_ext.h>
 
+#include <cstdlib>
+
 namespace fr {
 namespace {
 
@@ -304,6 +306,189 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
     }
 }
 
+// Ping-pong variant (FR_ROWS_PP, default): 8 waves = two groups of 4, each with its own patch buffer,
+// processing alternate units of the workgroup's list, synchronised by LDS-counter group barriers instead of
+// s_barrier.  A SIMD then holds one wave of each group: while one group waits for its patch DMA or runs
+// its epilogue and copy-out, the other group's K loop keeps the MFMA pipe busy (the single-group kernel
+// above issues all of them from one wave per SIMD, so they add up: FR_ROWS_EXP timings).  No patch
+// prefetch within a group (the other group covers the DMA); the group counters live in the unused tail
+// of each patch buffer (its DMA lanes past PSLOTS are masked off).
+constexpr int PP_SPIN_LIMIT = 1 << 22;  // group-barrier spins (x s_sleep 1) before giving up (a bug, not a wait)
+
+template <bool RES, int ACT>
+__global__ __launch_bounds__(512, 1) void conv_rows_pp_kernel(ConvArgs p, int NG, int units) {
+    typedef Num<false> T;
+    typedef T::frag frag;
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [weights 72 KiB][patch 0][patch 1]
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = wave >> 2, gw = wave & 3;
+    const int wm = gw & 1, wn = gw >> 1;
+    const int H = p.H, W = p.W;
+    const int ng = blockIdx.x % NG, k0 = blockIdx.x / NG, kstride = gridDim.x / NG;
+    if (k0 >= units) return;
+
+    const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * H * W * p.Cx * 2);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.wimg + (size_t)ng * (W_B / 2)), 0, (uint32_t)W_B, 0x00020000);
+    const int pbase = W_B + grp * PATCH_B;  // this group's patch buffer (LDS byte offset)
+    typedef __attribute__((address_space(3))) int lds_int;
+    lds_int* const gctr = (lds_int*)(uintptr_t)(pbase + PSLOTS * 16);
+
+    // the n-group's weights: 72 pieces over the 8 waves; the group counters start at 0
+#pragma unroll
+    for (int t = 0; t < W_B / 1024 / 8; ++t) {
+        const int piece = 8 * t + wave;
+        dma16(wr, smem + piece * 1024, (uint32_t)(piece * 1024 + lane * 16));
+    }
+    if (lane == 0 && gw == 0) *gctr = 0;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    int gphase = 0;
+    // group barrier: every wave's LDS work (and, with vm, its vector-memory ops) done, then the 4 waves meet
+    auto gbar = [&](bool vm) {
+        if (vm) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __atomic_fetch_add(gctr, 1, __ATOMIC_RELAXED);
+        gphase += 4;
+        for (int it = 0; it < PP_SPIN_LIMIT; ++it) {
+            if (__atomic_load_n(gctr, __ATOMIC_RELAXED) >= gphase) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("" ::: "memory");
+    };
+    // DMA of a unit's patch into the group's buffer (slots past PSLOTS masked: the counters live there)
+    auto issue_patch = [&](const Unit& u) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int t = 0; t < PPIECES / 4; ++t) {
+            const int piece = 4 * t + gw, q = piece * 64 + ln;
+            const int row = q / (PPOS * 8), rem = q - row * (PPOS * 8), pos = rem >> 3, ch = rem & 7;
+            const int g = ch ^ (pos & 7);
+            const int ir = u.r0 - 1 + row, ic = u.c0 - 1 + pos;
+            const bool in = (unsigned)ir < (unsigned)H && (unsigned)ic < (unsigned)W;
+            const uint32_t off =
+                in ? (uint32_t)(((((size_t)u.b * H + ir) * W + ic) * p.Cx + p.x_off + g * 8) * 2) : OOB;
+            if (q < PSLOTS) dma16(xr, smem + pbase + piece * 1024, off);
+        }
+    };
+
+    int prr[7], pcc[7], poff[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+        const int m = 112 * wm + 16 * j + (lane & 15);
+        prr[j] = m / RCOLS;
+        pcc[j] = m - prr[j] * RCOLS;
+        poff[j] = prr[j] * W + pcc[j];
+    }
+    const int nl = 64 * ng + 32 * wn + 4 * (lane >> 4);
+    int pa[7][3];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+        const int m = 112 * wm + 16 * j + (lane & 15), rr = m / RCOLS, c = m - rr * RCOLS;
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw) {
+            const int pos = c + dw;
+            pa[j][dw] = pbase + (rr * PPOS + pos) * 128 + (((lane >> 4) ^ (pos & 7)) * 16);
+        }
+    }
+    const int wa = (lane >> 4) * 1024 + (32 * wn + (lane & 15)) * 16;
+    f32x4_t acc[2][7];
+    frag fa[2][2], fb[2][7];
+    auto read_step = [&](int s, int sl) {
+        const int cg = s / 9, tap = s % 9, dh = tap / 3, dw = tap % 3;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[sl][i] = *(const frag*)(smem + wa + s * WSLICE_B + i * 256);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) fb[sl][j] = *(const frag*)(smem + ((pa[j][dw] + dh * (PPOS * 128)) ^ (cg << 6)));
+    };
+
+#pragma unroll 1
+    for (int k = k0 + grp * kstride; k < units; k += 2 * kstride) {
+        const Unit cur = unit_of(k, H, W);
+        issue_patch(cur);
+        // accumulator seeds: bias of the pixel's border class (+ the residual), loaded while the DMA flies
+        {
+            const size_t base = ((size_t)cur.b * H + cur.r0) * W + cur.c0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const int cls = border_class(cur.r0 + prr[j], cur.c0 + pcc[j], H, W);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int n = nl + 16 * i;
+                    float4 sb = *(const float4*)(p.ep + cls * p.Npad + n);
+                    if (RES) {
+                        const uint2 r = *(const uint2*)(p.res + (base + poff[j]) * p.Cres + p.res_off + n);
+                        float f[8];
+                        T::unpack8(make_uint4(r.x, r.y, 0, 0), f);
+                        sb.x += f[0]; sb.y += f[1]; sb.z += f[2]; sb.w += f[3];
+                    }
+                    acc[i][j] = (f32x4_t){sb.x, sb.y, sb.z, sb.w};
+                }
+            }
+        }
+        gbar(true);  // every wave's patch pieces landed
+        read_step(0, 0);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+#if FR_ROWS_SCHED
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            if (s + 1 < NKS) read_step(s + 1, (s + 1) & 1);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(fa[s & 1][i], fb[s & 1][j], acc[i][j]);
+#if FR_ROWS_SCHED
+            if (s + 1 < NKS) {
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
+            }
+#endif
+        }
+        gbar(false);  // every wave of the group is past its patch reads: the buffer becomes the output tile
+        const size_t base = ((size_t)cur.b * H + cur.r0) * W + cur.c0;
+        char* stg = smem + pbase;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int nloc = 32 * wn + 16 * i + 4 * (lane >> 4), cl = nloc >> 3, half = (nloc >> 2) & 1;
+            float4 nf = make_float4(1.f, 1.f, 1.f, 1.f);
+            if (ACT) nf = *(const float4*)(p.negf + 64 * ng + nloc);
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const int m = 112 * wm + 16 * j + (lane & 15);
+                float o[8] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3], 0, 0, 0, 0};
+                if (ACT) {
+                    o[0] = o[0] > 0.f ? o[0] : o[0] * nf.x;
+                    o[1] = o[1] > 0.f ? o[1] : o[1] * nf.y;
+                    o[2] = o[2] > 0.f ? o[2] : o[2] * nf.z;
+                    o[3] = o[3] > 0.f ? o[3] : o[3] * nf.w;
+                }
+                const uint4 pk = T::pack8(o);
+                *(uint2*)(stg + m * 128 + ((cl ^ (m & 7)) * 16) + half * 8) = make_uint2(pk.x, pk.y);
+            }
+        }
+        gbar(false);  // the output tile is complete
+        const int gt = gw * 64 + lane;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            const int idx = gt + 256 * q, m = idx >> 3, cl = idx & 7;
+            const int rr = m / RCOLS, c = m - rr * RCOLS;
+            const uint4 v = *(const uint4*)(stg + m * 128 + ((cl ^ (m & 7)) * 16));
+            *(uint4*)(p.y + (base + rr * W + c) * p.Cy + p.y_off + 64 * ng + cl * 8) = v;
+        }
+        gbar(false);  // the copy-out reads are done before the next unit's DMA overwrites the buffer
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // out[ng][s = cg*9 + tap][g][n][e] = w[64 ng + n][tap*64 + 32 cg + 8 g + e]
 __global__ __launch_bounds__(256) void rows_pack_kernel(const bf16_t* __restrict__ w, int Kpad, int NG,
                                                         bf16_t* __restrict__ out) {
@@ -340,8 +525,15 @@ hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s) {
     int grid = (n_cu / NG) * NG;                       // every workgroup owns one n-group
     if (grid > units * NG) grid = units * NG;
     const bool act = a.act != 0;
-    auto k = a.res ? (act ? conv_rows_kernel<true, 2> : conv_rows_kernel<true, 0>)
-                   : (act ? conv_rows_kernel<false, 2> : conv_rows_kernel<false, 0>);
+    static const bool pp = [] {
+        const char* e = getenv("FR_ROWS_PP");
+        return !(e && e[0] == '0');
+    }();
+    auto k = pp ? (a.res ? (act ? conv_rows_pp_kernel<true, 2> : conv_rows_pp_kernel<true, 0>)
+                         : (act ? conv_rows_pp_kernel<false, 2> : conv_rows_pp_kernel<false, 0>))
+                : (a.res ? (act ? conv_rows_kernel<true, 2> : conv_rows_kernel<true, 0>)
+                         : (act ? conv_rows_kernel<false, 2> : conv_rows_kernel<false, 0>));
+    const int threads = pp ? 512 : 256;
     const int v = (a.res ? 2 : 0) + (act ? 1 : 0);
     static bool attr[4] = {false, false, false, false};
     if (!attr[v]) {
@@ -349,10 +541,10 @@ hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s) {
         attr[v] = true;
     }
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, dim3(grid), dim3(256), ROWS_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, NG,
+        hipExtLaunchKernelGGL(k, dim3(grid), dim3(threads), ROWS_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, NG,
                               units);
     else
-        hipLaunchKernelGGL(k, dim3(grid), dim3(256), ROWS_LDS, s, a, NG, units);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(threads), ROWS_LDS, s, a, NG, units);
     return hipGetLastError();
 }
 
