@@ -28,7 +28,8 @@ namespace fr {
 namespace {
 
 constexpr int DNW = 4;    // waves, one per SIMD
-constexpr int KSR = 12;   // register-resident K-steps: Kpad <= 384
+constexpr int KSR1 = 12;  // register-resident K-steps at one workgroup per CU: Kpad <= 384
+constexpr int KSR2 = 10;  // ... at two (NF = 2 only): Kpad <= 320
 constexpr uint32_t OOB = 0x80000000u;
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -48,8 +49,11 @@ struct DGeo {
 template <int NF, int FW>
 __host__ __device__ constexpr int direct_upx() { return 16 * FW * DNW; }
 
-template <bool F16, int NF, int FW>
-__global__ __launch_bounds__(64 * DNW, 1) void conv_direct_kernel(ConvArgs p, DGeo g) {
+// OCC: workgroups per CU (2: up to 256 registers per wave, 10 register K-steps; for the small convs whose
+// per-unit DMA latency one workgroup cannot hide)
+template <bool F16, int NF, int FW, int OCC>
+__global__ __launch_bounds__(64 * DNW, OCC) void conv_direct_kernel(ConvArgs p, DGeo g) {
+    constexpr int KSR = OCC == 2 ? KSR2 : KSR1;
     typedef Num<F16> T;
     typedef typename T::frag frag;
     constexpr int UPX = direct_upx<NF, FW>();
@@ -222,12 +226,12 @@ DGeo direct_geo(const ConvArgs& a, const DCfg& c, int* lds);
 // configuration of a shape: NF (16-channel fragments per wave = channels per workgroup / 16) and FW
 // (pixel fragments per wave); 0 = unsupported
 struct DCfg {
-    int nf, fw;
+    int nf, fw, occ;
 };
 DCfg direct_cfg(const ConvArgs& a) {
-    DCfg c{0, 0};
+    DCfg c{0, 0, 1};
     if (a.Kh <= 0 || a.Kw <= 0 || a.x2 || a.y2 || a.res || a.partial || a.w8 || a.y_amax || a.bias9 || a.Cin % 8 || a.Cx % 8 || a.x_off % 8 ||
-        a.Cy % 4 || a.y_off % 4 || a.Kpad % 32 || a.Kpad / 32 > KSR || a.K > a.Kpad || a.sh < 1 || a.sw < 1 ||
+        a.Cy % 4 || a.y_off % 4 || a.Kpad % 32 || a.Kpad / 32 > KSR1 || a.K > a.Kpad || a.sh < 1 || a.sw < 1 ||
         a.B <= 0 || a.Ho <= 0 || a.Wo <= 0)
         return c;
     c.nf = a.Cout % 64 == 0 ? 4 : (a.Cout % 32 == 0 ? 2 : 0);
@@ -242,7 +246,7 @@ DCfg direct_cfg(const ConvArgs& a) {
     for (int fw = fw_max; fw >= 1; fw /= 2) {
         const int u = (hw + 64 * fw - 1) / (64 * fw) * 64 * fw;
         if (u * 100 > best_u * 105) continue;
-        DCfg t{c.nf, fw};
+        DCfg t{c.nf, fw, 1};
         int lds = 0;
         (void)direct_geo(a, t, &lds);
         if (lds <= 160 * 1024) {
@@ -251,6 +255,12 @@ DCfg direct_cfg(const ConvArgs& a) {
         }
     }
     if (!c.fw) c.nf = 0;
+    // two workgroups per CU when their registers (NF = 2, <= 10 K-steps) and LDS allow
+    if (c.nf == 2 && c.fw <= 4 && a.Kpad / 32 <= KSR2) {
+        int lds = 0;
+        (void)direct_geo(a, c, &lds);
+        if (2 * lds <= 160 * 1024) c.occ = 2;
+    }
     return c;
 }
 
@@ -307,23 +317,26 @@ hipError_t launch_conv_direct(const ConvArgs& a, int n_cu, hipStream_t s) {
         }
         n_cu = cus[dev];
     }
-    int grid = (n_cu / g.ngroups) * g.ngroups;
+    int grid = (c.occ * n_cu / g.ngroups) * g.ngroups;
     if (grid < g.ngroups) grid = g.ngroups;
     if (grid > g.units * g.ngroups) grid = g.units * g.ngroups;
     typedef void (*KFn)(ConvArgs, DGeo);
     static const KFn kt[2][4][2] = {
-        {{conv_direct_kernel<false, 2, 1>, conv_direct_kernel<true, 2, 1>},
-         {conv_direct_kernel<false, 2, 2>, conv_direct_kernel<true, 2, 2>},
-         {conv_direct_kernel<false, 2, 4>, conv_direct_kernel<true, 2, 4>},
-         {conv_direct_kernel<false, 2, 8>, conv_direct_kernel<true, 2, 8>}},
-        {{conv_direct_kernel<false, 4, 1>, conv_direct_kernel<true, 4, 1>},
-         {conv_direct_kernel<false, 4, 2>, conv_direct_kernel<true, 4, 2>},
-         {conv_direct_kernel<false, 4, 4>, conv_direct_kernel<true, 4, 4>},
-         {conv_direct_kernel<false, 4, 4>, conv_direct_kernel<true, 4, 4>}}};  // (FW = 8: not used with NF = 4)
+        {{conv_direct_kernel<false, 2, 1, 1>, conv_direct_kernel<true, 2, 1, 1>},
+         {conv_direct_kernel<false, 2, 2, 1>, conv_direct_kernel<true, 2, 2, 1>},
+         {conv_direct_kernel<false, 2, 4, 1>, conv_direct_kernel<true, 2, 4, 1>},
+         {conv_direct_kernel<false, 2, 8, 1>, conv_direct_kernel<true, 2, 8, 1>}},
+        {{conv_direct_kernel<false, 4, 1, 1>, conv_direct_kernel<true, 4, 1, 1>},
+         {conv_direct_kernel<false, 4, 2, 1>, conv_direct_kernel<true, 4, 2, 1>},
+         {conv_direct_kernel<false, 4, 4, 1>, conv_direct_kernel<true, 4, 4, 1>},
+         {conv_direct_kernel<false, 4, 4, 1>, conv_direct_kernel<true, 4, 4, 1>}}};  // (FW = 8: not used with NF = 4)
+    static const KFn kt2[3][2] = {{conv_direct_kernel<false, 2, 1, 2>, conv_direct_kernel<true, 2, 1, 2>},
+                                  {conv_direct_kernel<false, 2, 2, 2>, conv_direct_kernel<true, 2, 2, 2>},
+                                  {conv_direct_kernel<false, 2, 4, 2>, conv_direct_kernel<true, 2, 4, 2>}};
     const int ni = c.nf == 4 ? 1 : 0, fi = c.fw == 8 ? 3 : (c.fw == 4 ? 2 : (c.fw == 2 ? 1 : 0)), di = a.f16 ? 1 : 0;
-    const KFn k = kt[ni][fi][di];
-    static int attr_lds[16] = {0};  // the largest size set per instantiation
-    const int ai = (ni * 4 + fi) * 2 + di;
+    const KFn k = c.occ == 2 ? kt2[fi][di] : kt[ni][fi][di];
+    static int attr_lds[32] = {0};  // the largest size set per instantiation
+    const int ai = ((c.occ == 2 ? 2 : 0) + ni) * 8 + fi * 2 + di;
     if (lds > attr_lds[ai]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr_lds[ai] = lds;
