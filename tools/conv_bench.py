@@ -22,21 +22,32 @@ def main():
     ap.add_argument("--tile", type=int, default=-1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--res", action="store_true", help="residual input (the conv2 epilogue)")
+    ap.add_argument("--kh", type=int, default=3)
+    ap.add_argument("--kw", type=int, default=3)
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--pad", type=int, default=-1, help="default: kernel // 2")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--act", type=int, default=0)
     a = ap.parse_args()
-    from tests.helpers import conv_op
+    from tests.helpers import TORCH_DT, conv_op
     g = torch.Generator().manual_seed(0)
-    x = torch.randn(a.batch, a.hw, a.hw, a.cin, generator=g).to(torch.bfloat16).cuda()
-    w = torch.randn(a.cout, a.cin, 3, 3, generator=g) / np.sqrt(9 * a.cin)
+    dt = TORCH_DT[a.dtype]
+    ph, pw = (a.kh // 2, a.kw // 2) if a.pad < 0 else (a.pad, a.pad)
+    Ho = (a.hw + 2 * ph - a.kh) // a.stride + 1
+    Wo = (a.hw + 2 * pw - a.kw) // a.stride + 1
+    x = torch.randn(a.batch, a.hw, a.hw, a.cin, generator=g).to(dt).cuda()
+    w = torch.randn(a.cout, a.cin, a.kh, a.kw, generator=g) / np.sqrt(a.kh * a.kw * a.cin)
     bias = torch.randn(a.cout, generator=g) * 0.1
-    res = torch.randn(a.batch, a.hw, a.hw, a.cout, generator=g).to(torch.bfloat16).cuda() if a.res else None
-    y = torch.empty(a.batch, a.hw, a.hw, a.cout, dtype=torch.bfloat16, device="cuda")
+    res = torch.randn(a.batch, Ho, Wo, a.cout, generator=g).to(dt).cuda() if a.res else None
+    y = torch.empty(a.batch, Ho, Wo, a.cout, dtype=dt, device="cuda")
     tile = None if a.tile < 0 else a.tile
-    conv_op(x, w, pad=(1, 1), bias=bias, res=res, y=y, tile=tile, timed_iters=3)
-    _, ms = conv_op(x, w, pad=(1, 1), bias=bias, res=res, y=y, tile=tile, timed_iters=a.iters)
+    kw = dict(stride=(a.stride, a.stride), pad=(ph, pw), bias=bias, res=res, y=y, tile=tile, dtype=a.dtype, act=a.act)
+    conv_op(x, w, timed_iters=3, **kw)
+    _, ms = conv_op(x, w, timed_iters=a.iters, **kw)
     us = float(np.median(ms)) * 1e3
-    flop = 2.0 * a.batch * a.hw * a.hw * a.cout * 9 * a.cin
-    print(json.dumps({"hw": a.hw, "cin": a.cin, "cout": a.cout, "tile": a.tile, "us": round(us, 1),
-                      "tflops": round(flop / us / 1e6, 1)}))
+    flop = 2.0 * a.batch * Ho * Wo * a.cout * a.kh * a.kw * a.cin
+    print(json.dumps({"hw": a.hw, "cin": a.cin, "cout": a.cout, "k": [a.kh, a.kw], "stride": a.stride, "tile": a.tile,
+                      "us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}))
 
 
 if __name__ == "__main__":
