@@ -220,22 +220,153 @@ __global__ __launch_bounds__(64 * DNW, OCC) void conv_direct_kernel(ConvArgs p, 
     }
 }
 
+// 1x1 / stride-1 / unpadded convs: a unit's pixels are contiguous NHWC rows, so operand B goes straight
+// from global memory into registers (no patch, no LDS): every K-step's fragment of the unit at once,
+// the next unit's during this unit's MFMAs (two register sets).  Units run over all B * H * W pixels.
+// Epilogue as conv_igemm's epilogue8: bias, residual, activation.
+template <bool F16, int NF, int FW, int KSR>  // KSR: K-steps compiled (>= Kpad / 32; the rest read zeros)
+__global__ __launch_bounds__(64 * DNW, 1) void conv_direct1_kernel(ConvArgs p, DGeo g) {
+    typedef Num<F16> T;
+    typedef typename T::frag frag;
+    constexpr int UPX = 16 * FW * DNW;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lg = lane >> 4, lr = lane & 15;
+    const int ng = blockIdx.x % g.ngroups, k0 = blockIdx.x / g.ngroups, kstride = gridDim.x / g.ngroups;
+    if (k0 >= g.units) return;
+    const int n0 = ng * 16 * NF, M = p.M;
+
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.w, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2), 0x00020000);
+    frag wa[KSR][NF];
+#pragma unroll
+    for (int ks = 0; ks < KSR; ++ks)
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const uint32_t off = ks < g.KS ? (uint32_t)(((n0 + 16 * i + lr) * p.Kpad + 32 * ks + 8 * lg) * 2) : OOB;
+            wa[ks][i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+        }
+    float4 bias4[NF], slope4[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int n = n0 + 16 * i + 4 * lg;
+        bias4[i] = p.bias ? *(const float4*)(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        slope4[i] = p.act == 2 ? *(const float4*)(p.slope + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)M * p.Cx * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.y, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)M * p.Cy * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.res ? p.res : p.y), 0, (uint32_t)(p.res ? min((size_t)0x7fffffff, (size_t)M * p.Cres * 2) : 0), 0x00020000);
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+    auto load_unit = [&](int k, frag (&fb)[KSR][FW], u32x2 (&rs)[NF][FW]) {
+#pragma unroll
+        for (int j = 0; j < FW; ++j) {
+            const int px = k * UPX + 16 * (FW * wave + j) + lr;
+            const bool ok = px < M;
+#pragma unroll
+            for (int ks = 0; ks < KSR; ++ks) {  // branch free: steps past Kpad / 32 read zeros
+                const uint32_t off =
+                    ok && ks < g.KS ? (uint32_t)(((size_t)px * p.Cx + p.x_off + 32 * ks + 8 * lg) * 2) : OOB;
+                fb[ks][j] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+            }
+            if (p.res) {
+#pragma unroll
+                for (int i = 0; i < NF; ++i) {
+                    const uint32_t off =
+                        ok ? (uint32_t)(((size_t)px * p.Cres + p.res_off + n0 + 16 * i + 4 * lg) * 2) : OOB;
+                    rs[i][j] = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
+                }
+            }
+        }
+    };
+    auto run_unit = [&](int k, const frag (&fb)[KSR][FW], const u32x2 (&rs)[NF][FW]) {
+        f32x4_t acc[NF][FW];
+#pragma unroll
+        for (int i = 0; i < NF; ++i)
+#pragma unroll
+            for (int j = 0; j < FW; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KSR; ++ks)
+#pragma unroll
+            for (int i = 0; i < NF; ++i)
+#pragma unroll
+                for (int j = 0; j < FW; ++j) acc[i][j] = T::mfma(wa[ks][i], fb[ks][j], acc[i][j]);
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int n = n0 + 16 * i + 4 * lg;
+            const float4 bb = bias4[i], sl = slope4[i];
+#pragma unroll
+            for (int j = 0; j < FW; ++j) {
+                float v[8] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3], 0.f, 0.f, 0.f, 0.f};
+                if (p.bias) {
+                    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+                }
+                if (p.res) {
+                    float f[8];
+                    T::unpack8(make_uint4(rs[i][j].x, rs[i][j].y, 0u, 0u), f);
+                    v[0] += f[0]; v[1] += f[1]; v[2] += f[2]; v[3] += f[3];
+                }
+                if (p.act == 1) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                } else if (p.act == 2) {
+                    v[0] = v[0] > 0.f ? v[0] : v[0] * sl.x;
+                    v[1] = v[1] > 0.f ? v[1] : v[1] * sl.y;
+                    v[2] = v[2] > 0.f ? v[2] : v[2] * sl.z;
+                    v[3] = v[3] > 0.f ? v[3] : v[3] * sl.w;
+                }
+                const uint4 pk = F16 && p.y_bf16 ? Num<false>::pack8(v) : T::pack8(v);
+                const int px = k * UPX + 16 * (FW * wave + j) + lr;
+                const uint32_t off = px < M ? (uint32_t)(((size_t)px * p.Cy + p.y_off + n) * 2) : OOB;
+                __builtin_amdgcn_raw_buffer_store_b64((u32x2){pk.x, pk.y}, yr, off, 0, 0);
+            }
+        }
+    };
+    frag fA[KSR][FW], fB[KSR][FW];
+    u32x2 rA[NF][FW], rB[NF][FW];
+    int k = k0;
+    load_unit(k, fA, rA);
+#pragma unroll 1
+    while (true) {
+        if (k + kstride < g.units) load_unit(k + kstride, fB, rB);
+        run_unit(k, fA, rA);
+        k += kstride;
+        if (k >= g.units) break;
+        if (k + kstride < g.units) load_unit(k + kstride, fA, rA);
+        run_unit(k, fB, rB);
+        k += kstride;
+        if (k >= g.units) break;
+    }
+}
+
 struct DCfg;
 DGeo direct_geo(const ConvArgs& a, const DCfg& c, int* lds);
 
 // configuration of a shape: NF (16-channel fragments per wave = channels per workgroup / 16) and FW
 // (pixel fragments per wave); 0 = unsupported
 struct DCfg {
-    int nf, fw, occ;
+    int nf, fw, occ, mode;  // mode 1: 1x1 / stride 1 / unpadded, operand B from global (conv_direct1_kernel)
 };
+static bool direct1_shape(const ConvArgs& a) {
+    return a.Kh == 1 && a.Kw == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.Ho == a.H && a.Wo == a.W;
+}
 DCfg direct_cfg(const ConvArgs& a) {
-    DCfg c{0, 0, 1};
-    if (a.Kh <= 0 || a.Kw <= 0 || a.x2 || a.y2 || a.res || a.partial || a.w8 || a.y_amax || a.bias9 || a.Cin % 8 || a.Cx % 8 || a.x_off % 8 ||
+    DCfg c{0, 0, 1, 0};
+    if (a.res && (!direct1_shape(a) || a.Cres % 4 || a.res_off % 4)) return c;  // residual: the 1x1 kernel only
+    if (a.Kh <= 0 || a.Kw <= 0 || a.x2 || a.y2 || a.partial || a.w8 || a.y_amax || a.bias9 || a.Cin % 8 || a.Cx % 8 || a.x_off % 8 ||
         a.Cy % 4 || a.y_off % 4 || a.Kpad % 32 || a.Kpad / 32 > KSR1 || a.K > a.Kpad || a.sh < 1 || a.sw < 1 ||
         a.B <= 0 || a.Ho <= 0 || a.Wo <= 0)
         return c;
     c.nf = a.Cout % 64 == 0 ? 4 : (a.Cout % 32 == 0 ? 2 : 0);
     if (!c.nf) return c;
+    if (direct1_shape(a)) {  // no patch: one or two fragments per wave (the registers hold two units' operands)
+        c.mode = 1;
+        c.fw = c.nf == 4 ? 1 : 2;
+        return c;
+    }
     // pixel fragments per wave: the largest unit (8, 4, 2 or 1 fragments per wave; larger units re-read
     // fewer halo rows) whose padded pixel count is
     // within 5 % of the least padded one and whose two patch buffers fit the LDS
@@ -266,6 +397,14 @@ DCfg direct_cfg(const ConvArgs& a) {
 
 DGeo direct_geo(const ConvArgs& a, const DCfg& c, int* lds) {
     DGeo g{};
+    if (c.mode == 1) {
+        g.KS = a.Kpad / 32;
+        g.units = (a.M + 16 * c.fw * DNW - 1) / (16 * c.fw * DNW);
+        g.upi = g.units;
+        g.ngroups = a.Cout / (16 * c.nf);
+        *lds = 0;
+        return g;
+    }
     const int cinb = a.Cin * 2;
     g.CH16 = a.Cin / 8;
     // 16-B slots per position: for >= 4 data chunks the next count = 2 (mod 4), so that 16 consecutive
@@ -298,7 +437,7 @@ bool direct_supported(const ConvArgs& a) {
     const DGeo g = direct_geo(a, c, &lds);
     (void)g;
     return lds <= 160 * 1024 && (size_t)a.B * a.H * a.W * a.Cx * 2 < 0x7fffffffull &&
-           (size_t)a.M * a.Cy * 2 < 0x7fffffffull;
+           (size_t)a.M * a.Cy * 2 < 0x7fffffffull && (!a.res || (size_t)a.M * a.Cres * 2 < 0x7fffffffull);
 }
 
 hipError_t launch_conv_direct(const ConvArgs& a, int n_cu, hipStream_t s) {
@@ -334,10 +473,16 @@ hipError_t launch_conv_direct(const ConvArgs& a, int n_cu, hipStream_t s) {
                                   {conv_direct_kernel<false, 2, 2, 2>, conv_direct_kernel<true, 2, 2, 2>},
                                   {conv_direct_kernel<false, 2, 4, 2>, conv_direct_kernel<true, 2, 4, 2>}};
     const int ni = c.nf == 4 ? 1 : 0, fi = c.fw == 8 ? 3 : (c.fw == 4 ? 2 : (c.fw == 2 ? 1 : 0)), di = a.f16 ? 1 : 0;
-    const KFn k = c.occ == 2 ? kt2[fi][di] : kt[ni][fi][di];
+#define D1(F16, NF, FW) \
+    { conv_direct1_kernel<F16, NF, FW, 2>, conv_direct1_kernel<F16, NF, FW, 4>, conv_direct1_kernel<F16, NF, FW, 8>, \
+      conv_direct1_kernel<F16, NF, FW, 12> }
+    static const KFn kt1[2][2][4] = {{D1(false, 2, 2), D1(true, 2, 2)}, {D1(false, 4, 1), D1(true, 4, 1)}};
+#undef D1
+    const int ks = a.Kpad / 32, ki = ks <= 2 ? 0 : (ks <= 4 ? 1 : (ks <= 8 ? 2 : 3));
+    const KFn k = c.mode == 1 ? kt1[ni][di][ki] : (c.occ == 2 ? kt2[fi][di] : kt[ni][fi][di]);
     static int attr_lds[32] = {0};  // the largest size set per instantiation
     const int ai = ((c.occ == 2 ? 2 : 0) + ni) * 8 + fi * 2 + di;
-    if (lds > attr_lds[ai]) {
+    if (c.mode == 0 && lds > attr_lds[ai]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr_lds[ai] = lds;
     }

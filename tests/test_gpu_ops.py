@@ -220,6 +220,30 @@ def test_conv_direct(gpu, case, dtype):
     assert torch.equal(y, conv_op(x, w, tile=0, **kw_))
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("case", [
+    # B, H, W, Cin, Cout, act   (1x1 / stride 1: operand B straight from global memory; + residual)
+    (2, 17, 17, 96, 256, 1),    # Block35 up: x + conv(cat), ReLU (the 0.17 scale folded into the weights)
+    (2, 8, 8, 256, 896, 1),     # Block17 up
+    (3, 3, 3, 384, 1792, 0),    # Block8 up (K = 384, no activation on the last block)
+    (2, 38, 38, 64, 96, 2),     # conv2d_3b-like (K = 64, Cout % 64 != 0)
+])
+def test_conv_direct_1x1_residual(gpu, case, dtype):
+    """conv_direct's 1x1 kernel (operand B from global memory, two units in registers): bias + residual +
+    activation; equal to igemm tile 0 bit for bit."""
+    B, H, W, Cin, Cout, act = case
+    g = torch.Generator().manual_seed(H + Cin + Cout)
+    x = torch.randn(B, H, W, Cin, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    w = torch.randn(Cout, Cin, 1, 1, generator=g) / np.sqrt(Cin)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    res = torch.randn(B, H, W, Cout, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    slope = torch.rand(Cout, generator=g) * 0.5 if act == 2 else None
+    kw_ = dict(bias=bias, res=res, act=act, slope=slope, dtype=dtype)
+    y = conv_op(x, w, tile=N.FR_TILE_DIRECT, **kw_)
+    _close(y, conv_ref(x, w, bias=bias, res=res, act=act, slope=slope, dtype=dtype))
+    assert torch.equal(y, conv_op(x, w, tile=0, **kw_))
+
+
 def test_conv_direct_channel_slices_and_applicability(gpu):
     """Input / output channel slices (IRV1 concatenations: x_off / Cx, y_off / Cy); shapes past the register
     limit are refused (fail loudly, no silent fallback)."""
