@@ -84,6 +84,13 @@ __device__ unsigned int g_stage_trace[2][8][TRACE_CONVS][4];
 #ifndef FR_STAGE13_RING6
 #define FR_STAGE13_RING6 3  // weight-ring depth of the 6-fragment waves (18 % RING == 0)
 #endif
+#ifndef FR_STAGE13_SPLIT
+#define FR_STAGE13_SPLIT 0  // 1: fragment 6 split between the two waves of a SIMD (26 + 26 MFMAs per K-step instead of
+                            // 28 + 24; A/B: bit-identical, 1 % slower: 5.35-5.39 vs 5.35-5.36 ms)
+#endif
+#ifndef FR_STAGE13_RINGS
+#define FR_STAGE13_RINGS 2  // weight-ring depth of the split variant's waves 4-7 (3 spills 15 VGPRs)
+#endif
 #ifndef FR_STAGE13_RING13
 #define FR_STAGE13_RING13 6  // weight-ring depth of the one-wave-per-SIMD 13-fragment variant (stage13w)
 #endif
@@ -391,9 +398,14 @@ __device__ __forceinline__ int pix_pos13(int P) {  // patch position of pixel P 
     return (r + 1) * SWP + (P - r * SW) + 1;
 }
 
-template <bool F16, int FM, int NWV, bool SINGLE>
+// F0 >= 0: the first fragment as a compile-time constant (else the f0 argument); HJ >= 0: fragment HJ of the
+// wave is HALF a fragment -- only n-fragments HI0, HI0 + 1 (the split variant shares one fragment between
+// the two waves of a SIMD); RINGT > 0: the weight-ring depth
+template <bool F16, int FM, int NWV, bool SINGLE, int F0 = -1, int HJ = -1, int HI0 = 0, int RINGT = 0>
 __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, const int wave, const int lane,
-                                             const int wn, const int f0) {
+                                             const int wn, const int f0_arg) {
+    const int f0 = F0 >= 0 ? F0 : f0_arg;
+    auto active = [](int i, int j) { return !(j == HJ && (i < HI0 || i >= HI0 + 2)); };
     typedef Num<F16> T;
     typedef typename T::frag frag;
     const int b = blockIdx.x;
@@ -431,7 +443,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     // weight ring depth: 3 K-steps (loads 2 ahead); the 7-fragment waves (which wait ~30 % of each conv at
     // the epilogue barrier for the 6-fragment ones) take 2 (1 ahead) and 16 VGPRs fewer: their body then
     // fits 256 VGPRs without the epilogue spills (FR_STAGE13_RING7, A/B)
-    constexpr int RING = FM == 13 ? FR_STAGE13_RING13 : (FM == 7 ? FR_STAGE13_RING7 : FR_STAGE13_RING6);
+    constexpr int RING = RINGT > 0 ? RINGT : (FM == 13 ? FR_STAGE13_RING13 : (FM == 7 ? FR_STAGE13_RING7 : FR_STAGE13_RING6));
     frag wq[RING][FN];
     auto wload = [&](frag (&w)[FN], int g) {
 #pragma unroll
@@ -449,7 +461,8 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 #pragma unroll
         for (int i = 0; i < FN; ++i)
 #pragma unroll
-            for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(wq[r][i], cur[j], acc[i][j]);
+            for (int j = 0; j < FM; ++j)
+                if (active(i, j)) acc[i][j] = T::mfma(wq[r][i], cur[j], acc[i][j]);
     };
     // SINGLE: ONE fragment set, refilled in place -- the 4 MFMAs of fragment j (one per weight fragment),
     // then fragment j of the next step is read into the same registers, 4 (FM - 1) MFMAs of this wave
@@ -463,7 +476,8 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
 #pragma unroll
-            for (int i = 0; i < FN; ++i) acc[i][j] = T::mfma(wq[r][i], pf[j], acc[i][j]);
+            for (int i = 0; i < FN; ++i)
+                if (active(i, j)) acc[i][j] = T::mfma(wq[r][i], pf[j], acc[i][j]);
 #if !(FR_STAGE_EXP & 16)
             pf[j] = *(const frag*)(pa + aoff[j]);
 #endif
@@ -471,7 +485,8 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         __builtin_amdgcn_sched_group_barrier(0x020, FN, 0);
 #pragma unroll
         for (int q = 0; q < FM; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+            if (q == HJ) __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            else __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
     };
@@ -511,6 +526,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             const int tr = tab_row(j, ln);
 #pragma unroll
             for (int i = 0; i < FN; ++i) {
+                if (!active(i, j)) continue;
                 const float4 bb = *(const float4*)(t + tr + 64 * i);
                 acc[i][j] = (f32x4_t){bb.x, bb.y, bb.z, bb.w};
             }
@@ -571,6 +587,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             const int tr = second ? 0 : tab_row(j, ln);
 #pragma unroll
             for (int i = 0; i < FN; ++i) {
+                if (!active(i, j)) continue;
                 const int n = wn * NPW + 16 * i + 4 * g;
                 char* const slot = sj + 2 * i * PLANE13_B;
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
@@ -590,7 +607,8 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
                     const float4 bb = *(const float4*)(t2 + tr + n * 4);
                     acc[i][j] = (f32x4_t){f[0] + bb.x, f[1] + bb.y, f[2] + bb.z, f[3] + bb.w};
                 }
-                if (FM == 7 || (f0 + j) * 16 + 15 < SPIX || P < SPIX) *(uint2*)slot = make_uint2(pk.x, pk.y);
+                if ((F0 >= 0 ? (F0 + j) * 16 + 15 < SPIX : FM == 7) || (f0 + j) * 16 + 15 < SPIX || P < SPIX)
+                    *(uint2*)slot = make_uint2(pk.x, pk.y);
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -637,8 +655,15 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage13_kernel(StageArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if FR_STAGE13_SPLIT
+    // fragment 6 shared: waves 0-3 take fragments 0..5 and n-fragments 0-1 of fragment 6, waves 4-7 n-fragments
+    // 2-3 of fragment 6 and fragments 7..12: 26 MFMAs per K-step for both waves of a SIMD
+    if (wave < 4) stage13_body<F16, 7, SNW, FR_STAGE_SINGLE, 0, 6, 0, FR_STAGE13_RING7>(p, smem, wave, lane, wave, 0);
+    else stage13_body<F16, 7, SNW, FR_STAGE_SINGLE, 6, 0, 2, FR_STAGE13_RINGS>(p, smem, wave, lane, wave - 4, 6);
+#else
     if (wave < 4) stage13_body<F16, 7, SNW, FR_STAGE_SINGLE>(p, smem, wave, lane, wave, 0);  // fragments 0..6
     else stage13_body<F16, 6, SNW, FR_STAGE_SINGLE>(p, smem, wave, lane, wave - 4, 7);       // fragments 7..12
+#endif
 }
 
 // One wave per SIMD (variant 2): 4 waves, each all 13 pixel fragments x its 64 output channels (52 MFMAs per
