@@ -144,6 +144,10 @@ struct fr_handle {
     struct GraphEnt { const void* in; float* out; int fmt, B, flags; hipGraphExec_t exec; bool no_graph; uint64_t used; };
     std::vector<GraphEnt> graphs;
     hipStream_t cap_stream = nullptr;
+    // branch-parallel capture (forward_graph): a second capturing stream and one event per op
+    hipStream_t aux_stream = nullptr;
+    std::vector<hipEvent_t> op_events;
+    bool ms_on = false;
     uint64_t tick = 0;
     // per-shape igemm tile autotuning (numerically invisible: every tile accumulates K in the same
     // order; split-K choices stay with the cost model)
@@ -1357,15 +1361,100 @@ struct DevSerial {
     ~DevSerial() { done(); }
 };
 
-int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s) {
+// Branch-parallel scheduling of a captured forward (h->ms_on, set by forward_graph; opt-in, see ms_enabled): a conv or max-pool
+// that does not depend on the last op of the main stream goes to a second stream, with an event wait for
+// each dependency on the other stream; every other op kind joins both streams.  Dependencies come from
+// the channel ranges each op reads and writes (RAW / WAR / WAW), the split-K partials counting as one
+// shared range.  In the captured graph these become edges: IRV1's Inception branches (Block35's 3x3 paths,
+// mixed_6a / mixed_7a) and ResNet-50's downsample projections run concurrently.
+namespace {
+struct Rgn {
+    int t, lo, hi;
+};
+constexpr int RGN_ALL = -3;  // the range of a joining op: overlaps everything
+bool rgn_hit(const std::vector<Rgn>& a, const std::vector<Rgn>& b) {
+    for (const auto& x : a)
+        for (const auto& y : b)
+            if (x.t == RGN_ALL || y.t == RGN_ALL || (x.t == y.t && x.lo < y.hi && y.lo < x.hi)) return true;
+    return false;
+}
+}  // namespace
+
+// Opt-in (FR_BRANCH_STREAMS=1, read at each capture): measured slower on IRV1 (104.2k vs 107.0k faces/s,
+// 3 same-box pairs) and ResNet-50 (157.0-157.9k vs 157.8-158.5k): the branches' kernels size their grids
+// for the whole GPU (persistent conv_direct / conv_rows, full igemm tile grids), so two of them at once
+// share the CUs instead of filling idle ones.
+static bool ms_enabled() {
+    const char* e = getenv("FR_BRANCH_STREAMS");
+    return e && e[0] == '1';
+}
+
+int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s_main) {
     const int f16 = h->dtype == FR_DTYPE_F16;
     const std::vector<char> stage_run = stage_plan(h, B);
-    if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s));
+    if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s_main));
+    const bool ms = h->ms_on;
+    const size_t nops = h->ops.size();
+    std::vector<std::vector<Rgn>> rd, wr;
+    std::vector<int> on_stream;
+    int tail[2] = {-1, -1};      // last op launched on each stream
+    int joined_aux = -1;         // last aux op the main stream has waited for
+    hipStream_t strm[2] = {s_main, h->aux_stream};
+    if (ms) {
+        rd.resize(nops);
+        wr.resize(nops);
+        on_stream.assign(nops, -1);
+        while (h->op_events.size() < nops + 1) {
+            hipEvent_t e;
+            FR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            h->op_events.push_back(e);
+        }
+        // fork: the aux stream joins the capture behind everything issued so far
+        FR_HIP_CHECK(hipEventRecord(h->op_events[nops], s_main));
+        FR_HIP_CHECK(hipStreamWaitEvent(strm[1], h->op_events[nops], 0));
+    }
     bool skip_next = false;
     for (size_t oi = 0; oi < h->ops.size(); ++oi) {
         const Op& op = h->ops[oi];
         if (skip_next) { skip_next = false; continue; }
         if (op_skipped(op, stage_run)) continue;
+        int target = 0;
+        if (ms) {
+            // the op's ranges
+            bool branchable = false;
+            if (op.kind == OP_CONV && op.wi >= 0) {
+                const auto& cw = h->convw[op.wi];
+                rd[oi].push_back({op.in, op.in_off, op.in_off + op.cin});
+                if (op.res >= 0) rd[oi].push_back({op.res, op.res_off, op.res_off + cw.Cout});
+                if (op.x2 >= 0) rd[oi].push_back({op.x2, op.x2_off, op.x2_off + cw.C2});
+                wr[oi].push_back({op.out, op.out_off, op.out_off + cw.Cout});
+                if (op.out2 >= 0) wr[oi].push_back({op.out2, 0, cw.Cout});
+                int tile, split;
+                const auto& to = h->tensors[op.out];
+                conv_plan(B * to.H * to.W, cw.Cout, cw.Kpad, &tile, &split);
+                if (split > 1) wr[oi].push_back({-2, 0, 1});  // the shared split-K partials
+                branchable = true;
+            } else if (op.kind == OP_MAXPOOL) {
+                rd[oi].push_back({op.in, 0, h->tensors[op.in].C});
+                wr[oi].push_back({op.out, op.out_off, op.out_off + h->tensors[op.in].C});
+                branchable = true;
+            }
+            if (!branchable) wr[oi].push_back({RGN_ALL, 0, 1});  // joins both streams, runs on main
+            auto dep = [&](int j) {
+                return j >= 0 && (rgn_hit(rd[oi], wr[j]) || rgn_hit(wr[oi], rd[j]) || rgn_hit(wr[oi], wr[j]));
+            };
+            // main if it depends on main's last op (or is a joining op), else the second stream
+            target = !branchable || tail[0] < 0 || dep(tail[0]) ? 0 : 1;
+            // wait for the latest dependency on the other stream (stream order covers the earlier ones)
+            const int other = 1 - target;
+            for (int j = (int)oi - 1; j >= 0; --j)
+                if (on_stream[j] == other && dep(j)) {
+                    if (!(target == 0 && j <= joined_aux)) FR_HIP_CHECK(hipStreamWaitEvent(strm[target], h->op_events[j], 0));
+                    if (target == 0 && j > joined_aux) joined_aux = j;
+                    break;
+                }
+        }
+        const hipStream_t s = strm[target];
         switch (op.kind) {
             case OP_STAGE: {
                 const StageRec& r = h->stages[op.stage];
@@ -1516,7 +1605,14 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 break;
             }
         }
+        if (ms) {
+            FR_HIP_CHECK(hipEventRecord(h->op_events[oi], s));
+            on_stream[oi] = target;
+            tail[target] = (int)oi;
+            if (skip_next) on_stream[oi + 1] = -1;  // the fused stem ran the next op (a joining op: covers it)
+        }
     }
+    if (ms && tail[1] > joined_aux) FR_HIP_CHECK(hipStreamWaitEvent(strm[0], h->op_events[tail[1]], 0));  // join
     return FR_OK;
 }
 
@@ -1589,6 +1685,8 @@ void fr_destroy(fr_handle* h) {
     if (h->cand_i) (void)hipFree(h->cand_i);
     drop_graphs(h);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
+    if (h->aux_stream) (void)hipStreamDestroy(h->aux_stream);
+    for (auto e : h->op_events) (void)hipEventDestroy(e);
     for (auto& r : h->prof_pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : h->ev_free) (void)hipEventDestroy(e);
     DevSerial::reg(h, false);
@@ -1678,8 +1776,13 @@ static int forward_graph(fr_handle* h, const void* in, int in_fmt, int B, float*
     if (e->no_graph) return forward(h, in, in_fmt, B, out, flags, s);
     if (!e->exec) {
         if (!h->cap_stream) FR_HIP_CHECK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+        // branch-parallel capture only without split stages (their parts must own the device, DevSerial)
+        // and without the fp8 amax buffers
+        h->ms_on = ms_enabled() && !split_runs(h, B) && !h->amax;
+        if (h->ms_on && !h->aux_stream) FR_HIP_CHECK(hipStreamCreateWithFlags(&h->aux_stream, hipStreamNonBlocking));
         FR_HIP_CHECK(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
         const int rc = forward(h, in, in_fmt, B, out, flags, h->cap_stream);
+        h->ms_on = false;
         hipGraph_t g = nullptr;
         const hipError_t ec = hipStreamEndCapture(h->cap_stream, &g);
         hipGraphExec_t x = nullptr;

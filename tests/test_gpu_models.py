@@ -282,3 +282,26 @@ def test_top1_agreement_random_gallery(gpu):
     # to ~3e-4, below what bf16 storage through 100 layers (|e - e_ref| ~ 1e-2) can resolve
     assert agree.mean() >= 0.85
     assert np.all(agree | (gap <= 2 * err)), "a top-1 flip where the oracle's gap exceeds the error bound"
+
+
+@pytest.mark.parametrize("arch", ["irv1_facenet", "resnet50_arcface"])
+def test_branch_parallel_graph_replay(gpu, arch):
+    """Captured forwards of the plans without split stages put independent branches (IRV1's Inception
+    branches, ResNet-50's downsample projections) on a second stream (engine.cpp forward, h->ms_on); the
+    replays must equal the eager (single-stream) forward bit for bit.  Opt-in (FR_BRANCH_STREAMS=1, read at
+    each capture), measured slower than the single-stream graph."""
+    import os
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    os.environ["FR_BRANCH_STREAMS"] = "1"
+    m = FRModel.synthetic(arch)
+    x = torch.from_numpy(synthetic_crops(64, m.input_size, seed=9)).cuda()
+    out = torch.empty((64, m.embedding_size), dtype=torch.float32, device="cuda")
+    runs = []
+    for _ in range(5):  # tuning pass, first sighting (eager), capture + replay, replays
+        m.embed(x, out=out)
+        runs.append(out.cpu().numpy().copy())
+    m.close()
+    del os.environ["FR_BRANCH_STREAMS"]
+    for r in runs[1:]:
+        assert np.array_equal(r, runs[0])
