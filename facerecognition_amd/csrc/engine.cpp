@@ -141,7 +141,13 @@ struct fr_handle {
     std::vector<std::pair<std::string, ProfAcc>> prof_acc;
     // forward replays as hipGraphs, keyed by the call's pointers / shape (captured on the second call
     // with a key; the first call runs eagerly and warms per-kernel attributes)
-    struct GraphEnt { const void* in; float* out; int fmt, B, flags; hipGraphExec_t exec; bool no_graph; uint64_t used; };
+    struct GraphEnt { const void* in; float* out; int fmt, B, flags, slot; hipGraphExec_t exec; bool no_graph; uint64_t used; };
+    // graph-slot timing (fr_prof_slots): an event pair per slot around the first launch of one kernel
+    // class, captured into the graph of that slot, so timed steps replay graphs and still time the class
+    std::string slot_class;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> slot_events;
+    int slot = -1;         // the slot the next forward captures / replays (-1: none)
+    bool slot_done = false;  // the slot's pair is placed in the current forward
     std::vector<GraphEnt> graphs;
     hipStream_t cap_stream = nullptr;
     // branch-parallel capture (forward_graph): a second capturing stream and one event per op
@@ -1102,8 +1108,15 @@ struct ProfScope {
     // Call right before the launch once the class is known.  With `ka` the pair is handed to the
     // conv launcher, which stamps it from the dispatch packet (hipExtLaunchKernel: no extra stream
     // commands); otherwise the pair is recorded around the launch(es) with hipEventRecord.
+    bool slot_pair = false;
     void start(const std::string& c, ConvArgs* ka = nullptr) {
         cls = c;
+        if (!h->prof && h->slot >= 0 && !h->slot_done && cls == h->slot_class) {  // graph-slot timing
+            (void)hipEventRecord(h->slot_events[h->slot].first, s);
+            h->slot_done = true;
+            slot_pair = true;
+            return;
+        }
         if (!h->prof || (!h->prof_only.empty() && h->prof_only != cls)) return;
         if (h->prof_seen++ % h->prof_stride != 0) return;
         a = prof_event(h);
@@ -1113,6 +1126,7 @@ struct ProfScope {
         else (void)hipEventRecord(a, s);
     }
     ~ProfScope() {
+        if (slot_pair) (void)hipEventRecord(h->slot_events[h->slot].second, s);
         if (!a) return;
         if (!stamped) (void)hipEventRecord(b, s);
         h->prof_pending.push_back({cls, a, b, flops, bytes});
@@ -1393,6 +1407,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
     const int f16 = h->dtype == FR_DTYPE_F16;
     const std::vector<char> stage_run = stage_plan(h, B);
     if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s_main));
+    h->slot_done = false;
     const bool ms = h->ms_on;
     const size_t nops = h->ops.size();
     std::vector<std::vector<Rgn>> rd, wr;
@@ -1685,6 +1700,10 @@ void fr_destroy(fr_handle* h) {
     if (h->cand_i) (void)hipFree(h->cand_i);
     drop_graphs(h);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
+    for (auto& pr : h->slot_events) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
     if (h->aux_stream) (void)hipStreamDestroy(h->aux_stream);
     for (auto e : h->op_events) (void)hipEventDestroy(e);
     for (auto& r : h->prof_pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
@@ -1757,9 +1776,9 @@ static int forward_graph(fr_handle* h, const void* in, int in_fmt, int B, float*
     if (!graphs_enabled() || h->prof) return forward(h, in, in_fmt, B, out, flags, s);
     fr_handle::GraphEnt* e = nullptr;
     for (auto& g : h->graphs)
-        if (g.in == in && g.out == out && g.fmt == in_fmt && g.B == B && g.flags == flags) e = &g;
+        if (g.in == in && g.out == out && g.fmt == in_fmt && g.B == B && g.flags == flags && g.slot == h->slot) e = &g;
     if (!e) {
-        if (h->graphs.size() >= 8) {  // evict the least recently used
+        if (h->graphs.size() >= 8 + h->slot_events.size()) {  // evict the least recently used
             auto lru = h->graphs.begin();
             for (auto it = h->graphs.begin(); it != h->graphs.end(); ++it)
                 if (it->used < lru->used) lru = it;
@@ -1769,7 +1788,7 @@ static int forward_graph(fr_handle* h, const void* in, int in_fmt, int B, float*
             }
             h->graphs.erase(lru);
         }
-        h->graphs.push_back({in, out, in_fmt, B, flags, nullptr, false, ++h->tick});
+        h->graphs.push_back({in, out, in_fmt, B, flags, h->slot, nullptr, false, ++h->tick});
         return forward(h, in, in_fmt, B, out, flags, s);  // first sighting: eager
     }
     e->used = ++h->tick;
@@ -2207,6 +2226,50 @@ int fr_prof_only(fr_handle* h, const char* kernel_class) {
     if (!h) { set_error("fr_prof_only: null handle"); return FR_ERR_ARG; }
     std::lock_guard<std::mutex> lk(h->mu);
     h->prof_only = kernel_class ? kernel_class : "";
+    return FR_OK;
+}
+
+int fr_prof_slots(fr_handle* h, const char* kernel_class, int n) {
+    if (!h || n < 0 || n > 4096 || (n > 0 && (!kernel_class || !*kernel_class))) {
+        set_error("fr_prof_slots: bad argument");
+        return FR_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    FR_HIP_CHECK(hipDeviceSynchronize());
+    for (auto& g : h->graphs)  // graphs of the old slots hold the old events
+        if (g.slot >= 0 && g.exec) (void)hipGraphExecDestroy(g.exec);
+    h->graphs.erase(std::remove_if(h->graphs.begin(), h->graphs.end(), [](const fr_handle::GraphEnt& g) { return g.slot >= 0; }),
+                    h->graphs.end());
+    for (auto& pr : h->slot_events) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    h->slot_events.clear();
+    h->slot = -1;
+    h->slot_class = n > 0 ? kernel_class : "";
+    for (int i = 0; i < n; ++i) {
+        hipEvent_t a, b;
+        FR_HIP_CHECK(hipEventCreate(&a));
+        FR_HIP_CHECK(hipEventCreate(&b));
+        h->slot_events.push_back({a, b});
+    }
+    return FR_OK;
+}
+
+int fr_prof_slot_select(fr_handle* h, int slot) {
+    if (!h || slot < -1 || slot >= (int)h->slot_events.size()) { set_error("fr_prof_slot_select: bad slot"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->slot = slot;
+    return FR_OK;
+}
+
+int fr_prof_slot_ms(fr_handle* h, int slot, float* ms) {
+    if (!h || !ms || slot < 0 || slot >= (int)h->slot_events.size()) { set_error("fr_prof_slot_ms: bad argument"); return FR_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(h->mu);
+    FR_HIP_CHECK(hipSetDevice(h->device));
+    FR_HIP_CHECK(hipEventSynchronize(h->slot_events[slot].second));
+    FR_HIP_CHECK(hipEventElapsedTime(ms, h->slot_events[slot].first, h->slot_events[slot].second));
     return FR_OK;
 }
 

@@ -207,6 +207,54 @@ def test_repeated_calls_replay_identically(gpu):
     assert torch.equal(out, e2) and not torch.equal(out, ref)
 
 
+def test_prof_slot_graph_timing(gpu):
+    """bench.py's timing of the dominant kernel class during graph replay (fr_prof_slots): each slot
+    captures its own graph with an event pair around the class's first launch; replays stay bit-identical
+    to eager and every pair reads a positive duration no longer than the whole forward."""
+    import ctypes
+    import math
+    import torch
+    from facerecognition_amd import _native as N
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    L = N.lib()
+    m = FRModel.synthetic("iresnet100", max_batch=8)
+    x = torch.from_numpy(synthetic_crops(8, 112, seed=7)).cuda()
+    out = torch.empty((8, 512), device="cuda")
+    m.embed(x, out=out)
+    torch.cuda.synchronize()
+    ref = out.clone()
+    N.check(L.fr_prof_enable(m.handle, 1), "fr_prof_enable")
+    m.embed(x, out=out)
+    torch.cuda.synchronize()
+    classes = N.prof_read(m.handle)
+    N.check(L.fr_prof_enable(m.handle, 0), "fr_prof_enable")
+    once = [c for c, v in classes.items() if v[1] == 1]
+    assert once, classes
+    cls = max(once, key=lambda c: classes[c][0])
+    n = 3
+    N.check(L.fr_prof_slots(m.handle, cls.encode(), n), "fr_prof_slots")
+    try:
+        for i in range(n):
+            N.check(L.fr_prof_slot_select(m.handle, i), "fr_prof_slot_select")
+            for _ in range(3):  # first sighting (eager), capture, replay
+                out.zero_()
+                m.embed(x, out=out)
+                torch.cuda.synchronize()
+                assert torch.equal(out, ref)
+        for i in range(n):
+            v = ctypes.c_float(0.0)
+            N.check(L.fr_prof_slot_ms(m.handle, i, ctypes.byref(v)), "fr_prof_slot_ms")
+            assert math.isfinite(v.value) and 0.0 < v.value < 1000.0
+        assert L.fr_prof_slot_select(m.handle, n) != 0  # out of range
+    finally:
+        N.check(L.fr_prof_slot_select(m.handle, -1), "fr_prof_slot_select")
+        N.check(L.fr_prof_slots(m.handle, None, 0), "fr_prof_slots")
+    m.embed(x, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
 def test_facenet_projection_head(gpu):
     """FaceNetModel with embedding_size=128 (projection Linear(512,128) + F.normalize after IRV1's own
     L2, facenet_model.py:20-23,32-35) vs the oracle, and the raw (pre-normalize) projection output."""
