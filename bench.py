@@ -107,8 +107,8 @@ def dtype_label(args) -> str:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)  # >= 50 iterations after 10 warm-up
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--gallery-rows", type=int, default=None,
                     help="default 10000 at --gpus 1 (config 2), 1000000 at --gpus > 1 (config 4)")

@@ -249,7 +249,7 @@ def test_iresnet100_fp8_guard_and_top1(gpu):
 def test_iresnet100_fp8_bs256(gpu):
     """BASELINE config-5 size (IResNet100 fp8, bs = 256, the autotuner's bs=256 tiles): deterministic replay,
     finite unit-norm rows, the distribution of 1-cos against bf16 at the same batch (guard bar; the spec
-    bar is the xfail above), an oracle sample, and identical top-1 on a planted 10k gallery."""
+    bar is test_iresnet100_fp8_meets_config5_bar), an oracle sample, and identical top-1 on a planted 10k gallery."""
     from facerecognition_amd.gallery import DeviceGallery
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
