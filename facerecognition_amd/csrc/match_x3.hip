@@ -35,7 +35,13 @@ namespace {
 constexpr int XW = 8;         // waves per block
 constexpr int XP = 16 * XW;   // probes per block
 constexpr int XG = 64;        // gallery rows per tile
-constexpr int XC = 64;        // dims per LDS chunk
+#ifndef FR_X3_ORDER
+#define FR_X3_ORDER 0  // A/B: 1 = a k-step's fragments loaded together, MFMAs product-major
+#endif
+#ifndef FR_X3_XC
+#define FR_X3_XC 64  // dims per LDS chunk (A/B: 128 = 32-KiB chunks, 4-slot ring, half the barriers)
+#endif
+constexpr int XC = FR_X3_XC;  // dims per LDS chunk
 constexpr int XD = 512;       // embedding dim (the kernel is specialised)
 constexpr int KP = 8;         // candidates per (probe, split, sub-lane): 4 sub-lanes per probe
 constexpr int KO = 16;        // candidates written per (probe, split) ...
@@ -98,12 +104,21 @@ __global__ __launch_bounds__(256) void split_bf16_kernel(const float* __restrict
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
 
-constexpr int XSLOT = 7;                       // LDS ring depth (chunks): XSLOT - 1 in flight
+#ifndef FR_X3_SLOTS
+#define FR_X3_SLOTS 0  // A/B: LDS ring depth override (0: 7 chunks of 16 KiB / 4 of 32 KiB)
+#endif
+constexpr int XSLOT = FR_X3_SLOTS ? FR_X3_SLOTS : (XC == 64 ? 7 : 4);  // LDS ring depth (chunks): XSLOT - 1 in flight
 constexpr int XCHUNK_B = 2 * XG * XC * 2;      // 16 KiB: [hi 64 rows x 128 B][lo 64 rows x 128 B]
+constexpr int XRB = XC * 2;                    // LDS row bytes
+constexpr int XPIECES = XCHUNK_B / 1024;       // 1-KiB DMA pieces per chunk
+constexpr int XPPW = XPIECES / 8;              // pieces per wave per chunk
+constexpr int XRPP = 1024 / XRB;               // rows per piece
+constexpr int XLPR = XRB / 16;                 // lanes (16-B slots) per row
+static_assert(XC == 64 || XC == 128, "chunk width");
 typedef __attribute__((address_space(3))) void lds_void;
 constexpr uint32_t XOOB = 0x80000000u;
 
-__device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+__device__ __forceinline__ int xswz(int row, int chunk) { return XC == 64 ? chunk ^ ((row >> 1) & 7) : chunk ^ (row & 15); }
 
 __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__ P, int B, const bf16_t* __restrict__ Gh,
                                                        const bf16_t* __restrict__ Gl, int64_t N, int64_t index_base,
@@ -159,10 +174,10 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
         return;
 #endif
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int piece = 2 * wave + u, half = piece >> 3;
-            const int row = 8 * (piece & 7) + (lane >> 3);
-            const int cl = (lane & 7) ^ ((row >> 1) & 7);
+        for (int u = 0; u < XPPW; ++u) {
+            const int piece = XPPW * wave + u, half = piece / (XPIECES / 2);
+            const int row = XRPP * (piece % (XPIECES / 2)) + lane / XLPR;
+            const int cl = xswz(row, lane % XLPR);
             const int64_t gr = t0 + row;
             const uint32_t off = gr < g_end ? (uint32_t)((gr * XD + XC * c + 8 * cl) * 2) : XOOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(half ? rl : rh, (lds_void*)(smem + slot * XCHUNK_B + piece * 1024),
@@ -188,8 +203,9 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
         for (int c = 0; c < XD / XC; ++c) {
             // chunk c landed (the XSLOT - 2 younger chunks' pieces may stay in flight); every wave is
             // past chunk c-1, so its slot takes chunk c + XSLOT - 1
-            static_assert(XSLOT == 7, "vmcnt below counts 2 pieces x (XSLOT - 2) younger chunks");
-            asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+            // (the XPPW x (XSLOT - 2) younger chunks' DMAs may stay in flight)
+            static_assert(XPPW * (XSLOT - 2) < 64, "vmcnt range");
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(XPPW * (XSLOT - 2)) : "memory");
             issue_next();
             const char* ch = smem + s_read * XCHUNK_B;
             if (++s_read == XSLOT) s_read = 0;
@@ -197,10 +213,27 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
             for (int tt = 0; tt < XC / 32; ++tt) {
                 const int t = c * (XC / 32) + tt;
                 const int kch = 4 * tt + (lane >> 4);
+#if FR_X3_ORDER == 1  // A/B: the k-step's 8 fragments first, then the MFMAs product-major (same order per accumulator)
+                bf8v gh4[4], gl4[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int row = 16 * j + (lane & 15);
-                    const int o = row * 128 + xswz(row, kch) * 16;
+                    const int o = row * XRB + xswz(row, kch) * 16;
+                    gh4[j] = *(const bf8v*)(ch + o);
+                    gl4[j] = *(const bf8v*)(ch + XCHUNK_B / 2 + o);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh4[j], ph[t], acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl4[j], ph[t], acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh4[j], pl[t], acc[j], 0, 0, 0);
+                continue;
+#endif
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int row = 16 * j + (lane & 15);
+                    const int o = row * XRB + xswz(row, kch) * 16;
                     const bf8v gh = *(const bf8v*)(ch + o);
                     const bf8v gl = *(const bf8v*)(ch + XCHUNK_B / 2 + o);
                     // gallery rows as the A operand: D[row][probe], so each lane's accumulators belong to
