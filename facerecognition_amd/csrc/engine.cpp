@@ -121,8 +121,7 @@ struct fr_handle {
     int64_t g_cap = 0;       // rows allocated (fr_gallery_write grows it geometrically)
     int g_dim = 0;
     int64_t g_base = 0;
-    bf16_t* g_hi = nullptr;  // bf16 hi/lo split of the prepared gallery (match_x3.hip), N >= X3_MIN_ROWS
-    bf16_t* g_lo = nullptr;
+    bf16_t* g_hi = nullptr;  // bf16 hi/lo split of the prepared gallery in chunk order (match_x3.hip), N >= X3_MIN_ROWS
     int* match_fb = nullptr;  // device counter of exact-rescan fallbacks (fr_debug_match_fallbacks)
     bool match_exact = false; // FR_OPT_MATCH_EXACT: always the f32-MFMA kernel
     int64_t x3_min_rows = X3_MIN_ROWS;  // FR_OPT_X3_MIN_ROWS
@@ -1694,7 +1693,6 @@ void fr_destroy(fr_handle* h) {
     free_weights(h);
     if (h->gallery) (void)hipFree(h->gallery);
     if (h->g_hi) (void)hipFree(h->g_hi);
-    if (h->g_lo) (void)hipFree(h->g_lo);
     if (h->match_fb) (void)hipFree(h->match_fb);
     if (h->cand_s) (void)hipFree(h->cand_s);
     if (h->cand_i) (void)hipFree(h->cand_i);
@@ -1890,7 +1888,6 @@ int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index
     FR_HIP_CHECK(hipSetDevice(h->device));
     if (h->gallery) { (void)hipFree(h->gallery); h->gallery = nullptr; }
     if (h->g_hi) { (void)hipFree(h->g_hi); h->g_hi = nullptr; }
-    if (h->g_lo) { (void)hipFree(h->g_lo); h->g_lo = nullptr; }
     h->g_rows = 0;
     h->g_cap = N;
     if (N > 0) {
@@ -1902,14 +1899,14 @@ int fr_gallery_set(fr_handle* h, const float* G, int64_t N, int D, int64_t index
                                g_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
         FR_HIP_CHECK(launch_gallery_prepare(h->gallery, N, D, nullptr));
         if (N >= h->x3_min_rows && D == 512) {  // bf16 hi/lo copy for the candidate pass (match_x3.hip)
-            int rc2 = dev_alloc((void**)&h->g_hi, (size_t)N * D * sizeof(bf16_t));
-            if (!rc2) rc2 = dev_alloc((void**)&h->g_lo, (size_t)N * D * sizeof(bf16_t));
+            int rc2 = dev_alloc((void**)&h->g_hi, x3_gallery_elems(N) * sizeof(bf16_t));
+            if (!rc2) FR_HIP_CHECK(hipMemset(h->g_hi, 0, x3_gallery_elems(N) * sizeof(bf16_t)));
             if (!rc2 && !h->match_fb) {
                 rc2 = dev_alloc((void**)&h->match_fb, sizeof(int));
                 if (!rc2) FR_HIP_CHECK(hipMemset(h->match_fb, 0, sizeof(int)));
             }
             if (rc2) return rc2;
-            FR_HIP_CHECK(launch_split_bf16(h->gallery, (size_t)N * D, h->g_hi, h->g_lo, nullptr));
+            FR_HIP_CHECK(launch_split_x3(h->gallery, 0, N, h->g_hi, nullptr));
         }
         FR_HIP_CHECK(hipDeviceSynchronize());
     }
@@ -1945,7 +1942,6 @@ int fr_gallery_write(fr_handle* h, const float* G, int64_t row0, int64_t n, int 
         if (h->gallery) (void)hipFree(h->gallery);
         h->gallery = g;
         if (h->g_hi) { (void)hipFree(h->g_hi); h->g_hi = nullptr; }  // re-split below at the new capacity
-        if (h->g_lo) { (void)hipFree(h->g_lo); h->g_lo = nullptr; }
         h->g_cap = cap;
     }
     FR_HIP_CHECK(hipMemcpy(h->gallery + (size_t)row0 * D, G, (size_t)n * D * sizeof(float),
@@ -1954,8 +1950,8 @@ int fr_gallery_write(fr_handle* h, const float* G, int64_t row0, int64_t n, int 
     if (x3) {
         int64_t s0 = row0, sn = n;
         if (!h->g_hi) {  // first time on the bf16x3 path (or re-grown): split every row
-            int rc = dev_alloc((void**)&h->g_hi, (size_t)h->g_cap * D * sizeof(bf16_t));
-            if (!rc) rc = dev_alloc((void**)&h->g_lo, (size_t)h->g_cap * D * sizeof(bf16_t));
+            int rc = dev_alloc((void**)&h->g_hi, x3_gallery_elems(h->g_cap) * sizeof(bf16_t));
+            if (!rc) FR_HIP_CHECK(hipMemset(h->g_hi, 0, x3_gallery_elems(h->g_cap) * sizeof(bf16_t)));
             if (!rc && !h->match_fb) {
                 rc = dev_alloc((void**)&h->match_fb, sizeof(int));
                 if (!rc) FR_HIP_CHECK(hipMemset(h->match_fb, 0, sizeof(int)));
@@ -1964,8 +1960,7 @@ int fr_gallery_write(fr_handle* h, const float* G, int64_t row0, int64_t n, int 
             s0 = 0;
             sn = rows;
         }
-        FR_HIP_CHECK(launch_split_bf16(h->gallery + (size_t)s0 * D, (size_t)sn * D, h->g_hi + (size_t)s0 * D,
-                                       h->g_lo + (size_t)s0 * D, nullptr));
+        FR_HIP_CHECK(launch_split_x3(h->gallery, s0, sn, h->g_hi, nullptr));
     }
     FR_HIP_CHECK(hipDeviceSynchronize());
     h->g_rows = rows;
@@ -2024,7 +2019,7 @@ static int match_locked(fr_handle* h, const float* P, int B, int k, float* score
         match_x3_plan(B, h->g_rows, &n_split, &rps);
         int rc = ensure_cand(h, (size_t)B * n_split * match_x3_candidates());
         if (rc) return rc;
-        FR_HIP_CHECK(launch_match_x3(P, B, h->gallery, h->g_hi, h->g_lo, h->g_rows, h->g_dim, k, h->g_base, h->cand_s,
+        FR_HIP_CHECK(launch_match_x3(P, B, h->gallery, h->g_hi, h->g_rows, h->g_dim, k, h->g_base, h->cand_s,
                                      h->cand_i, n_split, rps, scores, idx, h->match_fb, s));
         return FR_OK;
     }

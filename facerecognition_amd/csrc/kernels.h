@@ -177,10 +177,13 @@ hipError_t launch_match_topk_large(const float* P, int B, const float* G, int64_
                                    float* S, float* out_s, int32_t* out_i, hipStream_t s);
 // Large-gallery match (match_x3.hip): bf16x3 candidates, exact f32 rescoring with a proof / fallback.
 constexpr int64_t X3_MIN_ROWS = 32768;  // below: the exact f32 kernel is as fast (10k x 256: 0.105 vs 0.16 ms)
-hipError_t launch_split_bf16(const float* G, size_t n, bf16_t* hi, bf16_t* lo, hipStream_t s);
+// bf16 hi/lo copy of gallery rows [row0, row0 + n) of G (f32 [rows][512]) into the candidate pass's
+// chunk-ordered buffer T of x3_gallery_elems(capacity) bf16 (match_x3.hip)
+size_t x3_gallery_elems(int64_t rows);
+hipError_t launch_split_x3(const float* G, int64_t row0, int64_t n, bf16_t* T, hipStream_t s);
 void match_x3_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split);
 int match_x3_candidates();
-hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* Gh, const bf16_t* Gl, int64_t N, int D,
+hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* GT, int64_t N, int D,
                            int k, int64_t index_base, float* cand_s, int32_t* cand_i, int n_split,
                            int64_t rows_per_split, float* out_s, int32_t* out_i, int* n_fallback, hipStream_t s);
 // Choose n_split / rows_per_split for a (B, N) match.

@@ -35,13 +35,7 @@ namespace {
 constexpr int XW = 8;         // waves per block
 constexpr int XP = 16 * XW;   // probes per block
 constexpr int XG = 64;        // gallery rows per tile
-#ifndef FR_X3_ORDER
-#define FR_X3_ORDER 0  // A/B: 1 = a k-step's fragments loaded together, MFMAs product-major
-#endif
-#ifndef FR_X3_XC
-#define FR_X3_XC 64  // dims per LDS chunk (A/B: 128 = 32-KiB chunks, 4-slot ring, half the barriers)
-#endif
-constexpr int XC = FR_X3_XC;  // dims per LDS chunk
+constexpr int XC = 64;        // dims per LDS chunk
 constexpr int XD = 512;       // embedding dim (the kernel is specialised)
 constexpr int KP = 8;         // candidates per (probe, split, sub-lane): 4 sub-lanes per probe
 constexpr int KO = 16;        // candidates written per (probe, split) ...
@@ -91,37 +85,57 @@ __device__ __forceinline__ void insert_s(float (&ls)[KMAX], int (&li)[KMAX], flo
 
 __device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
-// G (f32 [N][D]) -> Gh, Gl (bf16): g = gh + gl + r, |r| <= 2^-16 |g|
-__global__ __launch_bounds__(256) void split_bf16_kernel(const float* __restrict__ G, size_t n, bf16_t* __restrict__ hi,
-                                                         bf16_t* __restrict__ lo) {
-    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        const float g = G[i];
-        const uint16_t h = bf16_bits(g);
-        hi[i] = h;
-        lo[i] = bf16_bits(g - __uint_as_float((uint32_t)h << 16));
+typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
+
+// The candidate pass's gallery copy, in its chunk order: g = gh + gl + r (gh, gl bf16, |r| <= 2^-16 |g|),
+// chunk (tile T = 64 rows, dims 64c ..) = 16 KiB contiguous at (8T + c) x 16 KiB, [gh 64 rows x 128 B][gl
+// 64 rows x 128 B], a row's eight 16-B groups stored at slot group ^ xswz_row(row): the LDS-DMA copies a
+// chunk linearly and the fragment reads stay conflict-free.  (Row-major gh / gl arrays put a chunk's 64
+// rows 1 KiB apart: its 128-B pieces fell on a few HBM / L2 channels, every block of a split on the same
+// ones.)  Rows past the gallery in the last tile are never candidates (the kernel masks them).
+constexpr int XCHUNK_E = 2 * 64 * 64;  // bf16 elements per chunk (16 KiB)
+__device__ __forceinline__ int xswz_row(int row) { return (row >> 1) & 7; }
+
+__global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ G, int64_t row0, int64_t n,
+                                                       bf16_t* __restrict__ T) {
+    // one thread per 8 dims of one row
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n * 64; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = row0 + i / 64;
+        const int grp = (int)(i % 64), c = grp >> 3, g = grp & 7, rr = (int)(r & 63);
+        const float* src = G + r * 512 + 8 * grp;
+        const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint16_t hb[8], lb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            hb[e] = bf16_bits(v[e]);
+            lb[e] = bf16_bits(v[e] - __uint_as_float((uint32_t)hb[e] << 16));
+        }
+        bf16_t* dst = T + ((r >> 6) * 8 + c) * XCHUNK_E + rr * 64 + (g ^ xswz_row(rr)) * 8;
+        uint4 hv, lv;
+        hv.x = hb[0] | (uint32_t)hb[1] << 16; hv.y = hb[2] | (uint32_t)hb[3] << 16;
+        hv.z = hb[4] | (uint32_t)hb[5] << 16; hv.w = hb[6] | (uint32_t)hb[7] << 16;
+        lv.x = lb[0] | (uint32_t)lb[1] << 16; lv.y = lb[2] | (uint32_t)lb[3] << 16;
+        lv.z = lb[4] | (uint32_t)lb[5] << 16; lv.w = lb[6] | (uint32_t)lb[7] << 16;
+        *(uint4*)dst = hv;
+        *(uint4*)(dst + XCHUNK_E / 2) = lv;
     }
 }
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
 
 #ifndef FR_X3_SLOTS
 #define FR_X3_SLOTS 0  // A/B: LDS ring depth override (0: 7 chunks of 16 KiB / 4 of 32 KiB)
 #endif
-constexpr int XSLOT = FR_X3_SLOTS ? FR_X3_SLOTS : (XC == 64 ? 7 : 4);  // LDS ring depth (chunks): XSLOT - 1 in flight
+constexpr int XSLOT = FR_X3_SLOTS ? FR_X3_SLOTS : 7;  // LDS ring depth (chunks): XSLOT - 1 in flight
 constexpr int XCHUNK_B = 2 * XG * XC * 2;      // 16 KiB: [hi 64 rows x 128 B][lo 64 rows x 128 B]
+static_assert(XCHUNK_B == XCHUNK_E * 2, "chunk layout");
 constexpr int XRB = XC * 2;                    // LDS row bytes
-constexpr int XPIECES = XCHUNK_B / 1024;       // 1-KiB DMA pieces per chunk
-constexpr int XPPW = XPIECES / 8;              // pieces per wave per chunk
-constexpr int XRPP = 1024 / XRB;               // rows per piece
-constexpr int XLPR = XRB / 16;                 // lanes (16-B slots) per row
-static_assert(XC == 64 || XC == 128, "chunk width");
+constexpr int XPPW = XCHUNK_B / 1024 / 8;      // 1-KiB DMA pieces per wave per chunk
 typedef __attribute__((address_space(3))) void lds_void;
-constexpr uint32_t XOOB = 0x80000000u;
 
-__device__ __forceinline__ int xswz(int row, int chunk) { return XC == 64 ? chunk ^ ((row >> 1) & 7) : chunk ^ (row & 15); }
+__device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ xswz_row(row); }
 
-__global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__ P, int B, const bf16_t* __restrict__ Gh,
-                                                       const bf16_t* __restrict__ Gl, int64_t N, int64_t index_base,
+__global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__ P, int B, const bf16_t* __restrict__ GT,
+                                                       int64_t N, int64_t index_base,
                                                        int64_t rows_per_split, int n_split, int npb,
                                                        float* __restrict__ cs, int32_t* __restrict__ ci) {
     // ONE LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads)
@@ -164,24 +178,23 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
 #pragma unroll
     for (int q = 0; q < KP; ++q) { ls[q] = -INFINITY; li[q] = INT_MAX; }
 
-    // LDS-DMA of chunk (tile t0, dims 64c..): 16 pieces of 8 rows x 128 B (hi: pieces 0-7, lo: 8-15);
-    // wave w issues pieces 2w, 2w+1; the source 16-B chunk is XOR-swizzled (read side: xswz)
-    const uint32_t g_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)N * XD * 2);
-    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)Gh, 0, g_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)Gl, 0, g_bytes, 0x00020000);
+    // LDS-DMA of chunk (tile t0, dims 64c..): a linear copy of its 16 KiB (split_x3_kernel's layout), 16
+    // pieces of 1 KiB, wave w issues pieces 2w, 2w+1.  The resource starts at the split's first chunk
+    // (32-bit offsets); look-ahead chunks past the gallery read 0, past the split are never used.
+    const size_t g_chunk0 = (size_t)(g_begin / XG) * 8;
+    const size_t g_left = ((size_t)((N + XG - 1) / XG) * 8 - g_chunk0) * XCHUNK_B;
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(GT + g_chunk0 * XCHUNK_E), 0,
+                                                                        (int)min(g_left, (size_t)0x7fffffff), 0x00020000);
     auto issue_chunk = [&](int64_t t0, int c, int slot) {
 #if FR_X3_EXP == 2  // timing experiment: no gallery stream
         return;
 #endif
+        const uint32_t cbase = (uint32_t)((((t0 - g_begin) / XG) * 8 + c) * XCHUNK_B);
 #pragma unroll
         for (int u = 0; u < XPPW; ++u) {
-            const int piece = XPPW * wave + u, half = piece / (XPIECES / 2);
-            const int row = XRPP * (piece % (XPIECES / 2)) + lane / XLPR;
-            const int cl = xswz(row, lane % XLPR);
-            const int64_t gr = t0 + row;
-            const uint32_t off = gr < g_end ? (uint32_t)((gr * XD + XC * c + 8 * cl) * 2) : XOOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(half ? rl : rh, (lds_void*)(smem + slot * XCHUNK_B + piece * 1024),
-                                                     16, off, 0, 0, 0);
+            const int piece = XPPW * wave + u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_void*)(smem + slot * XCHUNK_B + piece * 1024), 16,
+                                                     cbase + piece * 1024 + 16 * lane, 0, 0, 0);
         }
     };
     // prologue: the first XSLOT - 1 chunks (slots are uniform run-time values: one VALU add per chunk)
@@ -213,23 +226,6 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
             for (int tt = 0; tt < XC / 32; ++tt) {
                 const int t = c * (XC / 32) + tt;
                 const int kch = 4 * tt + (lane >> 4);
-#if FR_X3_ORDER == 1  // A/B: the k-step's 8 fragments first, then the MFMAs product-major (same order per accumulator)
-                bf8v gh4[4], gl4[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int row = 16 * j + (lane & 15);
-                    const int o = row * XRB + xswz(row, kch) * 16;
-                    gh4[j] = *(const bf8v*)(ch + o);
-                    gl4[j] = *(const bf8v*)(ch + XCHUNK_B / 2 + o);
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh4[j], ph[t], acc[j], 0, 0, 0);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl4[j], ph[t], acc[j], 0, 0, 0);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh4[j], pl[t], acc[j], 0, 0, 0);
-                continue;
-#endif
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int row = 16 * j + (lane & 15);
@@ -469,10 +465,13 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
 
 }  // namespace
 
-hipError_t launch_split_bf16(const float* G, size_t n, bf16_t* hi, bf16_t* lo, hipStream_t s) {
-    int blocks = (int)((n + 255) / 256);
+size_t x3_gallery_elems(int64_t rows) { return (size_t)((rows + XG - 1) / XG) * 8 * XCHUNK_E; }
+
+hipError_t launch_split_x3(const float* G, int64_t row0, int64_t n, bf16_t* T, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n * 64 + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(split_bf16_kernel, dim3(blocks), dim3(256), 0, s, G, n, hi, lo);
+    hipLaunchKernelGGL(split_x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, G, row0, n, T);
     return hipGetLastError();
 }
 
@@ -489,12 +488,12 @@ void match_x3_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split) {
 
 int match_x3_candidates() { return KS; }
 
-hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* Gh, const bf16_t* Gl, int64_t N, int D,
+hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* GT, int64_t N, int D,
                            int k, int64_t index_base, float* cand_s, int32_t* cand_i, int n_split,
                            int64_t rows_per_split, float* out_s, int32_t* out_i, int* n_fallback, hipStream_t s) {
     if (D != XD || k > KC || k < 1) return hipErrorInvalidValue;
     const int npb = (B + XP - 1) / XP;
-    hipLaunchKernelGGL(match_x3_kernel, dim3(npb * n_split), dim3(512), 0, s, P, B, Gh, Gl, N, index_base,
+    hipLaunchKernelGGL(match_x3_kernel, dim3(npb * n_split), dim3(512), 0, s, P, B, GT, N, index_base,
                        rows_per_split, n_split, npb, cand_s, cand_i);
     hipLaunchKernelGGL(rescore_kernel, dim3((B + 3) / 4), dim3(256), 0, s, P, B, G, N, index_base, cand_s, cand_i,
                        n_split, k, out_s, out_i, n_fallback);
