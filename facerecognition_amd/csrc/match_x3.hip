@@ -122,6 +122,9 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
     }
 }
 
+#ifndef FR_X3_PIPE
+#define FR_X3_PIPE 0  // A/B: 1 = explicitly double-buffered fragment reads within a chunk
+#endif
 #ifndef FR_X3_SLOTS
 #define FR_X3_SLOTS 0  // A/B: LDS ring depth override (0: 7 chunks of 16 KiB / 4 of 32 KiB)
 #endif
@@ -222,6 +225,39 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
             issue_next();
             const char* ch = smem + s_read * XCHUNK_B;
             if (++s_read == XSLOT) s_read = 0;
+#if FR_X3_PIPE
+            // A/B: the chunk's 4 groups (one k-step x two row fragments) double-buffered --
+            // group q + 1's 4 fragments are read before group q's 6 MFMAs (pinned by sched barriers)
+            {
+                bf8v fb[2][4];
+                auto ld = [&](int q, bf8v (&f)[4]) {
+                    const int tt = q >> 1, kch = 4 * tt + (lane >> 4);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int row = 16 * (2 * (q & 1) + h) + (lane & 15);
+                        const int o = row * XRB + xswz(row, kch) * 16;
+                        f[2 * h] = *(const bf8v*)(ch + o);
+                        f[2 * h + 1] = *(const bf8v*)(ch + XCHUNK_B / 2 + o);
+                    }
+                };
+                ld(0, fb[0]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q < 3) ld(q + 1, fb[(q + 1) & 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int t = c * (XC / 32) + (q >> 1);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int j = 2 * (q & 1) + h;
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[q & 1][2 * h], ph[t], acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[q & 1][2 * h + 1], ph[t], acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[q & 1][2 * h], pl[t], acc[j], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            continue;
+#endif
 #pragma unroll
             for (int tt = 0; tt < XC / 32; ++tt) {
                 const int t = c * (XC / 32) + tt;
