@@ -122,6 +122,9 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
     }
 }
 
+#ifndef FR_X3_DEFER
+#define FR_X3_DEFER 0  // A/B: 1 = waves 4-7 run a tile's inserts mid-way through the next tile
+#endif
 #ifndef FR_X3_PIPE
 #define FR_X3_PIPE 0  // A/B: 1 = explicitly double-buffered fragment reads within a chunk
 #endif
@@ -211,6 +214,60 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < XSLOT - 1; ++i) issue_next();
 
+    // the tile's candidate filter and sorted inserts (a = its accumulators, tb = its first row)
+    auto filter_tile = [&](f32x4_t (&a)[4], int64_t tb) {
+        // a[j][r] = s~(probe my_q, row tb + 16*j + 4*my_sub + r).  A row not above the best KP-th score
+        // of the probe's 4 sub-lists (lanes lane ^ 16, ^ 32) is never needed: the floor (>= that score)
+        // covers it in the proof -- ties included, so the scan compares scores only.  The sorted insert
+        // runs once per hit of the wave's busiest lane.
+        if (g_end - tb < XG) {  // last tile of the split: rows past it are zero-filled, never candidates
+            const int lim = (int)(g_end - tb);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (16 * j + 4 * my_sub + r >= lim) a[j][r] = -INFINITY;
+        }
+        // also: when every sub-list holds >= KP/2 entries above x, the probe's top KO = 2 KP (the merge
+        // keeps exactly those) are all above x, so min over the sub-lists of the (KP/2)-th score is a
+        // valid (usually higher) bar too
+        float thr = ls[KP - 1], thr2 = ls[KP / 2 - 1];
+        thr = fmaxf(thr, __shfl_xor(thr, 16));
+        thr2 = fminf(thr2, __shfl_xor(thr2, 16));
+        thr = fmaxf(thr, __shfl_xor(thr, 32));
+        thr2 = fminf(thr2, __shfl_xor(thr2, 32));
+        thr = fmaxf(thr, thr2);
+#if FR_X3_EXP == 3  // timing experiment: no insert (the compares still run)
+        {
+            uint32_t m = 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) m |= (a[e >> 2][e & 3] > thr) << e;
+            asm volatile("" ::"v"(m));
+        }
+        return;
+#endif
+        uint32_t m = 0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) m |= a[e >> 2][e & 3] > thr ? 1u << e : 0u;
+        // one pass per hit of the busiest lane (usually one): pick the score by a select tree
+        while (m) {
+            const int e = __builtin_ctz(m);
+            m &= m - 1;
+            float v8[8], v4[4], v2[2];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v8[q] = (e & 8) ? a[(q + 8) >> 2][(q + 8) & 3] : a[q >> 2][q & 3];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v4[q] = (e & 4) ? v8[q + 4] : v8[q];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) v2[q] = (e & 2) ? v4[q + 2] : v4[q];
+            const float sc = (e & 1) ? v2[1] : v2[0];
+            insert_s<KP>(ls, li, sc, (int)(tb + index_base) + 16 * (e >> 2) + 4 * my_sub + (e & 3));
+        }
+    };
+#if FR_X3_DEFER
+    f32x4_t accp[4];
+    int64_t tp = -1;
+#endif
     for (int64_t t0 = g_begin; t0 < g_end; t0 += XG) {
         f32x4_t acc[4];
 #pragma unroll
@@ -224,6 +281,9 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
             asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(XPPW * (XSLOT - 2)) : "memory");
             issue_next();
             const char* ch = smem + s_read * XCHUNK_B;
+#if FR_X3_DEFER
+            if (c == 4 && wave >= 4 && tp >= 0) filter_tile(accp, tp);  // the previous tile's, mid-way
+#endif
             if (++s_read == XSLOT) s_read = 0;
 #if FR_X3_PIPE
             // A/B: the chunk's 4 groups (one k-step x two row fragments) double-buffered --
@@ -280,54 +340,19 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
                 }
             }
         }
-        // acc[j][r] = s~(probe my_q, row t0 + 16*j + 4*my_sub + r).  A row not above the best KP-th score
-        // of the probe's 4 sub-lists (lanes lane ^ 16, ^ 32) is never needed: the floor (>= that score)
-        // covers it in the proof -- ties included, so the scan compares scores only.  The sorted insert
-        // runs once per hit of the wave's busiest lane.
-        if (g_end - t0 < XG) {  // last tile of the split: rows past it are zero-filled, never candidates
-            const int lim = (int)(g_end - t0);
+#if FR_X3_DEFER
+        if (wave >= 4) {  // waves 4-7 filter this tile during the next one (chunk 4): off their SIMD partner's
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (16 * j + 4 * my_sub + r >= lim) acc[j][r] = -INFINITY;
+            for (int j = 0; j < 4; ++j) accp[j] = acc[j];
+            tp = t0;
+            continue;
         }
-        // also: when every sub-list holds >= KP/2 entries above x, the probe's top KO = 2 KP (the merge
-        // keeps exactly those) are all above x, so min over the sub-lists of the (KP/2)-th score is a
-        // valid (usually higher) bar too
-        float thr = ls[KP - 1], thr2 = ls[KP / 2 - 1];
-        thr = fmaxf(thr, __shfl_xor(thr, 16));
-        thr2 = fminf(thr2, __shfl_xor(thr2, 16));
-        thr = fmaxf(thr, __shfl_xor(thr, 32));
-        thr2 = fminf(thr2, __shfl_xor(thr2, 32));
-        thr = fmaxf(thr, thr2);
-#if FR_X3_EXP == 3  // timing experiment: no insert (the compares still run)
-        {
-            uint32_t m = 0;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) m |= (acc[e >> 2][e & 3] > thr) << e;
-            asm volatile("" ::"v"(m));
-        }
-        continue;
 #endif
-        uint32_t m = 0;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) m |= acc[e >> 2][e & 3] > thr ? 1u << e : 0u;
-        // one pass per hit of the busiest lane (usually one): pick the score by a select tree
-        while (m) {
-            const int e = __builtin_ctz(m);
-            m &= m - 1;
-            float v8[8], v4[4], v2[2];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) v8[q] = (e & 8) ? acc[(q + 8) >> 2][(q + 8) & 3] : acc[q >> 2][q & 3];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v4[q] = (e & 4) ? v8[q + 4] : v8[q];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) v2[q] = (e & 2) ? v4[q + 2] : v4[q];
-            const float sc = (e & 1) ? v2[1] : v2[0];
-            insert_s<KP>(ls, li, sc, (int)(t0 + index_base) + 16 * (e >> 2) + 4 * my_sub + (e & 3));
-        }
+        filter_tile(acc, t0);
     }
+#if FR_X3_DEFER
+    if (wave >= 4 && tp >= 0) filter_tile(accp, tp);
+#endif
     // the look-ahead DMAs (zeros past the split) land everywhere before the ring is reused as scratch
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     // merge the 4 sub-lists of each probe into its top KO: park them in the (drained) ring and let
