@@ -39,6 +39,7 @@ GFLOP_PER_FACE = {"iresnet100": 24.179, "resnet50_arcface": 2.154, "irv1_facenet
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
 FP8_DENSE_PEAK_TFLOPS = 5000.0  # MI355X_MICROARCH.md: ~5 PF dense fp8 (block-scaled f8f6f4 MFMA)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec (about 6.3 TB/s achievable)
+C4_ROWS = 1_000_000  # BASELINE config 4's gallery (the N > 1 default)
 PROF_STRIDE = 8  # roofline: sample every 8th dominant-kernel launch (event overhead ~0.5 % instead of ~4 %)
 
 
@@ -64,7 +65,7 @@ def pmc_passes(args):
     if not shutil.which("rocprofv3"):
         return None, "rocprofv3 not on PATH"
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
-             "--no-prof", "--no-pmc", "--arch", args.arch, "--batch", str(args.batch), "--k", str(args.k)]
+             "--no-prof", "--no-pmc", "--no-n1-1m", "--arch", args.arch, "--batch", str(args.batch), "--k", str(args.k)]
     if args.dtype:
         child += ["--dtype", args.dtype]
     if args.gallery_rows:
@@ -124,6 +125,9 @@ def parse():
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 and the collectives run on gloo "
                          "(staged through host memory); never a measurement")
+    ap.add_argument("--no-n1-1m", action="store_true",
+                    help="N = 1: skip the extra timed run at config 4's 1M-row gallery (the weak-scaling "
+                         "curve's N = 1 point, reported beside the headline as same_workload_as_multi_gpu)")
     ap.add_argument("--host-input", action="store_true",
                     help="crops start in pinned host memory and are copied H2D inside each step "
                          "(PCIe-inclusive rate, DESIGN.md; never the headline value)")
@@ -245,7 +249,7 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.gallery_rows is None:
-        args.gallery_rows = 10000 if world == 1 else 1000000
+        args.gallery_rows = 10000 if world == 1 else C4_ROWS
     pmc, pmc_why = None, "not collected (--no-pmc / --no-prof / N > 1)"
     if world == 1 and not args.no_pmc and not args.no_prof:  # before this process touches the GPU
         pmc, pmc_why = pmc_passes(args)
@@ -280,7 +284,7 @@ def main():
     emb = torch.empty((B, 512), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    matcher = ShardedMatcher(B, 512, K, lambda p: gallery.search_device(p, K), dev)
+    matcher = ShardedMatcher(B, 512, K, lambda p, s, i: gallery.search_device(p, K, s, i), dev)
 
     u8_host = u8.cpu().pin_memory() if args.host_input else None
 
@@ -435,6 +439,36 @@ def main():
                 e["pmc_over_algorithmic"] = round(tb / (by / launches), 2) if by else None
             return e
         result["kernels"] = {k: cls_entry(k, v) for k, v in sorted(kclasses_all.items(), key=lambda kv: -kv[1][0])}
+    if world == 1 and rows != C4_ROWS and not args.no_n1_1m and not args.host_input and \
+            os.environ.get("FR_TIMING_ONLY") != "1":
+        # the N > 1 runs use config 4's 1M-row gallery (per rank: N*256 probes x 1M/N rows, i.e. the match
+        # work of 256 probes x 1M rows whatever N): time that workload at N = 1 too, so the 1 -> 8 curve
+        # has a same-workload N = 1 point (the headline `value` stays config 2's 10k gallery)
+        g1m = DeviceGallery(device=local, index_base=0)
+        g1m.set_device_rows(synthetic_gallery_rows(0, C4_ROWS, dev))
+        m1m = ShardedMatcher(B, 512, K, lambda p, s, i: g1m.search_device(p, K, s, i), dev)
+
+        def step1m():
+            model.embed(u8, out=emb, sync=False)
+            return m1m.search(emb)
+
+        for _ in range(max(2, args.warmup)):
+            step1m()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            _, o_i = step1m()
+        torch.cuda.synchronize(dev)
+        el1 = time.perf_counter() - t1
+        model.sync_check()
+        assert int(o_i[:, 0].min()) >= 0 and int(o_i[:, 0].max()) < C4_ROWS
+        result["same_workload_as_multi_gpu"] = {
+            "gallery_rows": C4_ROWS, "value": round(B * args.steps / el1, 2), "unit": "faces/s",
+            "ms_per_step": round(el1 / args.steps * 1e3, 4), "steps": args.steps,
+            "note": "N = 1 run of the per-rank workload of the N > 1 lines (bs 256 embed + top-k of 256 probes x 1M "
+                    "rows, bf16x3 match): the weak-scaling curve's same-workload N = 1 point"}
+        g1m.close()
+        del g1m, m1m
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.arch, args.cpu_seconds)
     if rank == 0:

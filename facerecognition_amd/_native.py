@@ -74,6 +74,7 @@ _SIGS = {
     "fr_gallery_write": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_int]),
     "fr_match_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "fr_topk_merge": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "fr_topk_merge_ranks": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "fr_embed_match": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "fr_segment_mean_normalize": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),

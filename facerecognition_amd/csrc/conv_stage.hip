@@ -53,9 +53,6 @@ constexpr int SNW = 8;                       // waves per workgroup: 2 pixel hal
 constexpr int FN = 4;                        // 16-channel fragments per wave
 constexpr int NPW = 16 * FN;                 // output channels per wave
 
-#ifndef FR_STAGE_SINGLE
-#define FR_STAGE_SINGLE 1  // 13-fragment kernel: one in-place refilled fragment set (0: two sets, A/B)
-#endif
 // FR_STAGE_TRACE (timing experiments only, tools/stage_trace.py): workgroups 0 and TRACE_WG2 of the
 // 13-fragment kernel record the low 32 bits of the shader clock at four points of each of their first
 // TRACE_CONVS convs per wave (K loop start / end, after the epilogue's entry barrier, after its exit
@@ -77,26 +74,10 @@ __device__ unsigned int g_stage_trace[2][8][TRACE_CONVS][4];
     do {                   \
     } while (0)
 #endif
-#ifndef FR_STAGE_PRIO
-#define FR_STAGE_PRIO 0  // A/B: 1 = the 6-fragment waves at s_setprio 1; 2 = priority alternating between the two
-                         // waves of a SIMD every 18 K-steps
-#endif
-#ifndef FR_STAGE13_RING6
-#define FR_STAGE13_RING6 3  // weight-ring depth of the 6-fragment waves (18 % RING == 0)
-#endif
-#ifndef FR_STAGE13_SPLIT
-#define FR_STAGE13_SPLIT 0  // 1: fragment 6 split between the two waves of a SIMD (26 + 26 MFMAs per K-step instead of
-                            // 28 + 24; A/B: bit-identical, 1 % slower: 5.35-5.39 vs 5.35-5.36 ms)
-#endif
-#ifndef FR_STAGE13_RINGS
-#define FR_STAGE13_RINGS 2  // weight-ring depth of the split variant's waves 4-7 (3 spills 15 VGPRs)
-#endif
-#ifndef FR_STAGE13_RING13
-#define FR_STAGE13_RING13 6  // weight-ring depth of the one-wave-per-SIMD 13-fragment variant (stage13w)
-#endif
-#ifndef FR_STAGE13_RING7
-#define FR_STAGE13_RING7 2  // weight-ring depth of the 13-fragment kernel's 7-fragment waves (3: as the others)
-#endif
+// weight-ring depths (K-steps; loads RING - 1 ahead): the 7-fragment waves of the 13-fragment kernel, which
+// wait ~30 % of each conv at the epilogue barrier for the 6-fragment ones, take 2 and fit 256 VGPRs without
+// epilogue spills; the 6-fragment waves 3; the one-wave-per-SIMD variant 6
+constexpr int RING7 = 2, RING6 = 3, RING13 = 6;
 #ifndef FR_STAGE_EXP
 #define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 8 trivial epilogue (MFMAs kept), 16 no
                         // patch reads in the loop, 32 every weight load reads K-step 0 (stage13), 128
@@ -398,14 +379,10 @@ __device__ __forceinline__ int pix_pos13(int P) {  // patch position of pixel P 
     return (r + 1) * SWP + (P - r * SW) + 1;
 }
 
-// F0 >= 0: the first fragment as a compile-time constant (else the f0 argument); HJ >= 0: fragment HJ of the
-// wave is HALF a fragment -- only n-fragments HI0, HI0 + 1 (the split variant shares one fragment between
-// the two waves of a SIMD); RINGT > 0: the weight-ring depth
-template <bool F16, int FM, int NWV, bool SINGLE, int F0 = -1, int HJ = -1, int HI0 = 0, int RINGT = 0>
+// FM pixel fragments per wave starting at fragment f0, NWV waves per workgroup
+template <bool F16, int FM, int NWV>
 __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, const int wave, const int lane,
-                                             const int wn, const int f0_arg) {
-    const int f0 = F0 >= 0 ? F0 : f0_arg;
-    auto active = [](int i, int j) { return !(j == HJ && (i < HI0 || i >= HI0 + 2)); };
+                                             const int wn, const int f0) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
     const int b = blockIdx.x;
@@ -434,16 +411,13 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     const uint32_t wvo = (uint32_t)((lane >> 4) * 4096 + (wn * NPW + (lane & 15)) * 16);
 
     f32x4_t acc[FN][FM];
-    frag pA[FM], pB[FM];
+    frag pA[FM];
     auto pread = [&](frag (&pf)[FM], int cg, int tap) {
         const char* pa = smem + cg * 4 * PLANE13_B + ((tap / 3 - 1) * SWP + tap % 3 - 1) * 16;
 #pragma unroll
         for (int j = 0; j < FM; ++j) pf[j] = *(const frag*)(pa + aoff[j]);
     };
-    // weight ring depth: 3 K-steps (loads 2 ahead); the 7-fragment waves (which wait ~30 % of each conv at
-    // the epilogue barrier for the 6-fragment ones) take 2 (1 ahead) and 16 VGPRs fewer: their body then
-    // fits 256 VGPRs without the epilogue spills (FR_STAGE13_RING7, A/B)
-    constexpr int RING = RINGT > 0 ? RINGT : (FM == 13 ? FR_STAGE13_RING13 : (FM == 7 ? FR_STAGE13_RING7 : FR_STAGE13_RING6));
+    constexpr int RING = FM == 13 ? RING13 : (FM == 7 ? RING7 : RING6);
     frag wq[RING][FN];
     auto wload = [&](frag (&w)[FN], int g) {
 #pragma unroll
@@ -451,20 +425,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             w[i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wvo + i * 256,
                                                                                   (FR_STAGE_EXP & 32) ? 0u : (uint32_t)g * SLICE_B, 0));
     };
-    auto kstep = [&](int g, int r, frag (&cur)[FM], frag (&nxt)[FM], int cg_n, int tap_n) {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#if !(FR_STAGE_EXP & 16)
-        pread(nxt, cg_n, tap_n);
-#endif
-        wload(wq[(r + RING - 1) % RING], g + RING - 1 < total ? g + RING - 1 : total - 1);
-#pragma unroll
-        for (int i = 0; i < FN; ++i)
-#pragma unroll
-            for (int j = 0; j < FM; ++j)
-                if (active(i, j)) acc[i][j] = T::mfma(wq[r][i], cur[j], acc[i][j]);
-    };
-    // SINGLE: ONE fragment set, refilled in place -- the 4 MFMAs of fragment j (one per weight fragment),
+    // ONE fragment set, refilled in place -- the 4 MFMAs of fragment j (one per weight fragment),
     // then fragment j of the next step is read into the same registers, 4 (FM - 1) MFMAs of this wave
     // before the next step uses it (the order is pinned: left alone, the scheduler sinks every read to
     // the end of the step and the next step waits for them)
@@ -477,7 +438,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         for (int j = 0; j < FM; ++j) {
 #pragma unroll
             for (int i = 0; i < FN; ++i)
-                if (active(i, j)) acc[i][j] = T::mfma(wq[r][i], pf[j], acc[i][j]);
+                acc[i][j] = T::mfma(wq[r][i], pf[j], acc[i][j]);
 #if !(FR_STAGE_EXP & 16)
             pf[j] = *(const frag*)(pa + aoff[j]);
 #endif
@@ -485,8 +446,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         __builtin_amdgcn_sched_group_barrier(0x020, FN, 0);
 #pragma unroll
         for (int q = 0; q < FM; ++q) {
-            if (q == HJ) __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            else __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
     };
@@ -526,7 +486,6 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             const int tr = tab_row(j, ln);
 #pragma unroll
             for (int i = 0; i < FN; ++i) {
-                if (!active(i, j)) continue;
                 const float4 bb = *(const float4*)(t + tr + 64 * i);
                 acc[i][j] = (f32x4_t){bb.x, bb.y, bb.z, bb.w};
             }
@@ -537,7 +496,6 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     __syncthreads();
     wload(wq[0], 0);
     static_assert(18 % RING == 0, "ring slot = K-step % RING must be compile-time in the 18-step body");
-    if (FR_STAGE_PRIO == 1 && FM == 6) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int q = 1; q < RING - 1; ++q) wload(wq[q], q);
 
@@ -554,19 +512,13 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         STAGE_TRACE(cv, 0);
 #pragma unroll 1
         for (int cg = 0; cg < SC / 32; cg += 2) {
-            if (FR_STAGE_PRIO == 2) {
-                if (((cg >> 1) & 1) == (FM == 7 ? 1 : 0)) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
 #pragma unroll
             for (int t = 0; t < 18; ++t) {
                 const int cgl = cg + t / 9, tap = t % 9;
                 const int cgn = t == 8 ? cg + 1 : (t == 17 ? cg + 2 : cgl);
                 const int tapn = t == 8 || t == 17 ? 0 : tap + 1;
                 const int rs = RING == 3 ? tap % 3 : t % RING;  // = global K-step % RING (72, 9 and 18 are multiples)
-                if (SINGLE) kstep1(g0 + cgl * 9 + tap, rs, pA, cgn, tapn);
-                else if (t & 1) kstep(g0 + cgl * 9 + tap, rs, pB, pA, cgn, tapn);
-                else kstep(g0 + cgl * 9 + tap, rs, pA, pB, cgn, tapn);
+                kstep1(g0 + cgl * 9 + tap, rs, pA, cgn, tapn);
             }
         }
         // ---- epilogue (as stage_kernel's): accumulators -> patch; spare-slot lanes write nothing
@@ -587,7 +539,6 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             const int tr = second ? 0 : tab_row(j, ln);
 #pragma unroll
             for (int i = 0; i < FN; ++i) {
-                if (!active(i, j)) continue;
                 const int n = wn * NPW + 16 * i + 4 * g;
                 char* const slot = sj + 2 * i * PLANE13_B;
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
@@ -607,7 +558,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
                     const float4 bb = *(const float4*)(t2 + tr + n * 4);
                     acc[i][j] = (f32x4_t){f[0] + bb.x, f[1] + bb.y, f[2] + bb.z, f[3] + bb.w};
                 }
-                if ((F0 >= 0 ? (F0 + j) * 16 + 15 < SPIX : FM == 7) || (f0 + j) * 16 + 15 < SPIX || P < SPIX)
+                if (FM == 7 || (f0 + j) * 16 + 15 < SPIX || P < SPIX)
                     *(uint2*)slot = make_uint2(pk.x, pk.y);
             }
         }
@@ -655,15 +606,8 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage13_kernel(StageArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if FR_STAGE13_SPLIT
-    // fragment 6 shared: waves 0-3 take fragments 0..5 and n-fragments 0-1 of fragment 6, waves 4-7 n-fragments
-    // 2-3 of fragment 6 and fragments 7..12: 26 MFMAs per K-step for both waves of a SIMD
-    if (wave < 4) stage13_body<F16, 7, SNW, FR_STAGE_SINGLE, 0, 6, 0, FR_STAGE13_RING7>(p, smem, wave, lane, wave, 0);
-    else stage13_body<F16, 7, SNW, FR_STAGE_SINGLE, 6, 0, 2, FR_STAGE13_RINGS>(p, smem, wave, lane, wave - 4, 6);
-#else
-    if (wave < 4) stage13_body<F16, 7, SNW, FR_STAGE_SINGLE>(p, smem, wave, lane, wave, 0);  // fragments 0..6
-    else stage13_body<F16, 6, SNW, FR_STAGE_SINGLE>(p, smem, wave, lane, wave - 4, 7);       // fragments 7..12
-#endif
+    if (wave < 4) stage13_body<F16, 7, SNW>(p, smem, wave, lane, wave, 0);  // fragments 0..6
+    else stage13_body<F16, 6, SNW>(p, smem, wave, lane, wave - 4, 7);       // fragments 7..12
 }
 
 // One wave per SIMD (variant 2): 4 waves, each all 13 pixel fragments x its 64 output channels (52 MFMAs per
@@ -676,7 +620,7 @@ __global__ __launch_bounds__(256, 1) void stage13w_kernel(StageArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    stage13_body<F16, 13, 4, FR_STAGE_SINGLE>(p, smem, wave, lane, wave, 0);
+    stage13_body<F16, 13, 4>(p, smem, wave, lane, wave, 0);
 }
 
 }  // namespace

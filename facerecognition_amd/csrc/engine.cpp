@@ -181,6 +181,8 @@ struct fr_handle {
     bool no_split = false;         // re-run of a failed forward: split stages off
     int64_t stage_reruns = 0;      // forwards re-run on the per-conv path after a run-out wait
     hipEvent_t chk_ev = nullptr;   // completion of the last synchronous-checked forward
+    hipEvent_t async_ev = nullptr; // completion of the last FR_EMBED_ASYNC split-stage forward ...
+    bool async_pending = false;    // ... not yet waited for (its failure is not yet latched)
     bool split_registered = false; // counted in the per-device split-stage handle registry (DevSerial)
     int stage_mode = 1;       // FR_OPT_STAGE: 0 off, 1 auto (stage_runs), 2 always
     int stage_min_fill = 80;  // FR_OPT_STAGE_MIN_FILL (percent)
@@ -1344,24 +1346,41 @@ static bool split_runs(const fr_handle* h, int B) {
 // process) are chained on the GPU: each waits for the previous one's completion event and records its
 // own.  Handles alone on their device pay nothing.  (Other processes on the same device are not seen:
 // their kernels can only delay a wait, which the bounded wait and fr_embed's check then report.)
+// The chain lock is per device (handles on other devices never wait for it); the registry lock only guards
+// the per-device table and is held for a lookup.
 struct DevSerial {
-    static std::mutex& mu() { static std::mutex m; return m; }
-    static std::unordered_map<int, int>& count() { static std::unordered_map<int, int> c; return c; }
-    static std::unordered_map<int, hipEvent_t>& last() { static std::unordered_map<int, hipEvent_t> e; return e; }
+    struct Dev {
+        std::mutex chain;       // held from the wait on `last` until `last` is re-recorded
+        int count = 0;          // handles on the device with split stages
+        hipEvent_t last = nullptr;
+    };
+    static std::mutex& reg_mu() { static std::mutex m; return m; }
+    static Dev& dev(int d) {
+        static std::unordered_map<int, std::unique_ptr<Dev>> m;  // entries are never erased: stable references
+        std::lock_guard<std::mutex> lk(reg_mu());
+        auto& p = m[d];
+        if (!p) p.reset(new Dev());
+        return *p;
+    }
     static void reg(fr_handle* h, bool on) {
-        std::lock_guard<std::mutex> lk(mu());
+        Dev& d = dev(h->device);
+        std::lock_guard<std::mutex> lk(reg_mu());
         if (on == h->split_registered) return;
         h->split_registered = on;
-        count()[h->device] += on ? 1 : -1;
+        d.count += on ? 1 : -1;
     }
     std::unique_lock<std::mutex> lk;
     hipEvent_t ev = nullptr;
     hipStream_t s = nullptr;
-    DevSerial(fr_handle* h, bool split, hipStream_t s_) : lk(mu(), std::defer_lock), s(s_) {
+    DevSerial(fr_handle* h, bool split, hipStream_t s_) : s(s_) {
         if (!split) return;
-        lk.lock();
-        if (count()[h->device] <= 1) { lk.unlock(); return; }
-        hipEvent_t& e = last()[h->device];
+        Dev& d = dev(h->device);
+        {
+            std::lock_guard<std::mutex> rl(reg_mu());
+            if (d.count <= 1) return;
+        }
+        lk = std::unique_lock<std::mutex>(d.chain);
+        hipEvent_t& e = d.last;
         if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
         ev = e;
         if (ev) (void)hipStreamWaitEvent(s, ev, 0);
@@ -1490,6 +1509,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.fail_host = h->fail_dev;
                 a.spin_limit = h->spin_limit;
                 a.variant = h->stage_variant;
+                {
                 ProfScope ps(h, s);
                 ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
                 ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * (r.fp8 ? 1.0 : 2.0);
@@ -1498,10 +1518,25 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                     a.wscale = r.wscale;
                     ps.start("stage8 layer3");
                     FR_HIP_CHECK(launch_stage8(a, s));
-                    break;
+                } else {
+                    ps.start(r.H == 14 ? "stage layer3" : (r.H == 28 ? "stage layer2" : "stage layer1"));
+                    FR_HIP_CHECK(r.parts > 1 ? launch_split_stage(a, r.H, r.C, s) : launch_stage(a, s));
                 }
-                ps.start(r.H == 14 ? "stage layer3" : (r.H == 28 ? "stage layer2" : "stage layer1"));
-                FR_HIP_CHECK(r.parts > 1 ? launch_split_stage(a, r.H, r.C, s) : launch_stage(a, s));
+                }
+                // the stages have no amax epilogue: when a per-conv e4m3 conv reads the stage output (e.g.
+                // layer4.0 under FR_FP8_PLAN=all), its activation scale comes from one reduction pass here
+                if (h->amax && h->need_amax[r.out] &&
+                    std::any_of(h->ops.begin(), h->ops.end(), [&](const Op& c) {  // a per-conv e4m3 reader runs
+                        return c.kind == OP_CONV && c.in == r.out && c.in_off == 0 && c.wi >= 0 && h->convw[c.wi].w8 &&
+                               !op_skipped(c, stage_run);
+                    })) {
+                    const auto& t = h->tensors[r.out];
+                    ProfScope pa(h, s);
+                    pa.bytes = 2.0 * B * t.H * t.W * t.C;
+                    pa.start("amax");
+                    FR_HIP_CHECK(launch_amax(t.dev, (size_t)B * t.H * t.W * t.C, f16 || t.f16,
+                                             h->amax + (size_t)r.out * FR_AMAX_SLOTS, FR_AMAX_SLOTS, s));
+                }
                 break;
             }
             case OP_PRE: {
@@ -1673,8 +1708,10 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     void* fh = nullptr;
     if (hipHostMalloc(&fh, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&h->fail_dev, fh, 0) != hipSuccess ||
-        hipEventCreateWithFlags(&h->chk_ev, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->chk_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->async_ev, hipEventDisableTiming) != hipSuccess) {
         if (fh) (void)hipHostFree(fh);
+        if (h->chk_ev) (void)hipEventDestroy(h->chk_ev);
         set_error("fr_create: host-mapped status word / event allocation failed");
         delete h;
         return FR_ERR_HIP;
@@ -1708,6 +1745,7 @@ void fr_destroy(fr_handle* h) {
     for (auto e : h->ev_free) (void)hipEventDestroy(e);
     DevSerial::reg(h, false);
     if (h->chk_ev) (void)hipEventDestroy(h->chk_ev);
+    if (h->async_ev) (void)hipEventDestroy(h->async_ev);
     if (h->fail_host) (void)hipHostFree(h->fail_host);
     delete h;
 }
@@ -1841,6 +1879,19 @@ static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, 
     const hipStream_t s = (hipStream_t)stream;
     const int fflags = flags & FR_EMBED_RAW;  // what the forward (and its graph key) depends on
     const bool split = split_runs(h, B);
+    if (split && !(flags & FR_EMBED_ASYNC) && h->async_pending) {
+        // a synchronous forward reads the shared failure flag after its own completion: latch the failure
+        // of the FR_EMBED_ASYNC forwards still in flight first, so it is reported as theirs, not taken as
+        // this forward's (and cleared by its re-run)
+        FR_HIP_CHECK(hipEventSynchronize(h->async_ev));
+        h->async_pending = false;
+        if (*(volatile int*)h->fail_host) {
+            *(volatile int*)h->fail_host = 0;
+            set_error("fr_embed: a split stage's halo wait ran out in an earlier FR_EMBED_ASYNC forward on this "
+                      "handle; the affected embeddings are NaN (reported once, see fr_sync_check)");
+            return FR_ERR_STAGE;
+        }
+    }
     int rc;
     {
         DevSerial ser(h, split, s);
@@ -1855,6 +1906,10 @@ static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, 
         } else {
             rc = forward_graph(h, in, in_fmt, B, out, fflags, s);
         }
+    }
+    if (!rc && split && (flags & FR_EMBED_ASYNC)) {
+        FR_HIP_CHECK(hipEventRecord(h->async_ev, s));
+        h->async_pending = true;
     }
     if (rc || !split || (flags & FR_EMBED_ASYNC)) return rc;
     // synchronous check: wait for this forward; if a split stage's halo wait ran out, its images are
@@ -1931,7 +1986,9 @@ int fr_gallery_write(fr_handle* h, const float* G, int64_t row0, int64_t n, int 
     const int64_t rows = std::max(h->g_rows, row0 + n);
     if (rows + h->g_base > INT32_MAX) { set_error("fr_gallery_write: indices must fit int32"); return FR_ERR_ARG; }
     FR_HIP_CHECK(hipSetDevice(h->device));
-    const bool x3 = rows >= h->x3_min_rows && D == 512;
+    // once split, a gallery stays on the bf16x3 path (match_locked takes it whenever g_hi exists), so every
+    // written row must be re-split even if FR_OPT_X3_MIN_ROWS was raised since
+    const bool x3 = (h->g_hi != nullptr || rows >= h->x3_min_rows) && D == 512;
     if (rows > h->g_cap || !h->gallery) {  // grow: 2x, copy the old rows on the device
         const int64_t cap = std::max<int64_t>(rows, std::max<int64_t>(2 * h->g_cap, 1024));
         float* g = nullptr;
@@ -2045,6 +2102,15 @@ int fr_topk_merge(const float* cand_s, const int32_t* cand_i, int B, int n_lists
         return FR_ERR_ARG;
     }
     FR_HIP_CHECK(launch_topk_merge(cand_s, cand_i, B, n_lists, k, scores, idx, (hipStream_t)stream));
+    return FR_OK;
+}
+
+int fr_topk_merge_ranks(const void* xchg, int n_ranks, int B, int k, float* scores, int32_t* idx, void* stream) {
+    if (!xchg || !scores || !idx || B <= 0 || n_ranks <= 0 || k <= 0 || k > 16) {
+        set_error("fr_topk_merge_ranks: bad argument");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_topk_merge_ranks(xchg, n_ranks, B, k, scores, idx, (hipStream_t)stream));
     return FR_OK;
 }
 
@@ -2191,6 +2257,10 @@ int fr_sync_check(fr_handle* h, void* stream) {
     std::lock_guard<std::mutex> lk(h->mu);
     FR_HIP_CHECK(hipSetDevice(h->device));
     FR_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    if (h->async_pending) {  // the async forwards may have been issued on another stream
+        FR_HIP_CHECK(hipEventSynchronize(h->async_ev));
+        h->async_pending = false;
+    }
     if (*(volatile int*)h->fail_host) {
         *(volatile int*)h->fail_host = 0;
         set_error("fr_sync_check: a split stage's halo wait ran out in an FR_EMBED_ASYNC forward on this handle; "

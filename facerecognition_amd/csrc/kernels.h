@@ -65,6 +65,9 @@ size_t rows_packed_elems(int Cout);
 hipError_t rows_pack_weights(const bf16_t* w, int Kpad, int Cout, bf16_t* out, hipStream_t s);
 hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s);
 constexpr int FR_AMAX_SLOTS = 64;  // engine: spreads the producers' atomics over 64 addresses
+// max |x| of n (% 8) bf16/f16 values into amax[0 .. slots) (misc.hip): for tensors an fp8 conv reads whose
+// producer has no amax epilogue (an LDS-resident stage)
+hipError_t launch_amax(const bf16_t* x, size_t n, int f16, float* amax, int slots, hipStream_t s);
 
 // FP8 (e4m3 x e4m3, v_mfma_scale_f32_16x16x128_f8f6f4) implicit GEMM; Cin % 64 == 0.
 int conv_fp8_tile(int M, int Cout);
@@ -171,6 +174,9 @@ hipError_t launch_match_topk(const float* P, int B, const float* G, int64_t N, i
                              int64_t rows_per_split, hipStream_t s);
 hipError_t launch_topk_merge(const float* cs, const int32_t* ci, int B, int n_lists, int k, float* out_s,
                              int32_t* out_i, hipStream_t s);
+// The same merge over the all-gathered exchange block [n_ranks][2][B][k] (scores f32, then indices i32).
+hipError_t launch_topk_merge_ranks(const void* xchg, int n_ranks, int B, int k, float* out_s, int32_t* out_i,
+                                   hipStream_t s);
 // k > 16 (match.hip): exact score rows S [B][N] (the caller's scratch) + a per-probe radix select.
 constexpr int FR_TOPK_LARGE_MAX = 4096;
 hipError_t launch_match_topk_large(const float* P, int B, const float* G, int64_t N, int D, int k, int64_t index_base,

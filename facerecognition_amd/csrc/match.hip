@@ -355,10 +355,14 @@ __global__ __launch_bounds__(256, 1) void match_p512_kernel(const float* __restr
 }
 
 // One wave per probe: lanes insert strided candidates into local lists, then k rounds of a
-// wave-wide (score desc, index asc) argmax pop.
+// wave-wide (score desc, index asc) argmax pop.  Candidate j of list l of probe p is at
+// p * probe_stride + l * list_stride + j (elements) in cs / ci: [P][n_lists][k] for fr_topk_merge
+// (probe_stride = n_lists k, list_stride = k), the all-gathered [rank][2][P][k] exchange block for
+// fr_topk_merge_ranks (probe_stride = k, list_stride = 2 P k, ci = cs + P k).
 template <int KMAX>
 __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ cs, const int32_t* __restrict__ ci,
-                                                         int B, int n_lists, int k, float* __restrict__ out_s,
+                                                         int B, int n_lists, int k, int64_t probe_stride,
+                                                         int64_t list_stride, float* __restrict__ out_s,
                                                          int32_t* __restrict__ out_i) {
     const int lane = threadIdx.x & 63;
     const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -370,8 +374,8 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
     const int n = n_lists * k;
     // 8 candidates per lane in flight per round (their loads issued together, then the inserts): one
     // load at a time exposed the L2 latency per candidate
-    const float* ps = cs + (size_t)p * n;
-    const int32_t* pi = ci + (size_t)p * n;
+    const float* ps = cs + (size_t)p * probe_stride;
+    const int32_t* pi = ci + (size_t)p * probe_stride;
     for (int c0 = 0; c0 < n; c0 += 64 * 8) {
         float sv[8];
         int iv[8];
@@ -379,8 +383,10 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
         for (int u = 0; u < 8; ++u) {
             const int c = c0 + 64 * u + lane;
             const bool ok = c < n;
-            sv[u] = ok ? ps[c] : -INFINITY;
-            iv[u] = ok ? pi[c] : -1;
+            const int l = c / k;
+            const size_t o = (size_t)l * list_stride + (c - l * k);
+            sv[u] = ok ? ps[o] : -INFINITY;
+            iv[u] = ok ? pi[o] : -1;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
@@ -486,14 +492,28 @@ hipError_t launch_match_topk(const float* P, int B, const float* G, int64_t N, i
     return hipGetLastError();
 }
 
-hipError_t launch_topk_merge(const float* cs, const int32_t* ci, int B, int n_lists, int k, float* out_s,
-                             int32_t* out_i, hipStream_t s) {
+static hipError_t merge_strided(const float* cs, const int32_t* ci, int B, int n_lists, int k, int64_t probe_stride,
+                                int64_t list_stride, float* out_s, int32_t* out_i, hipStream_t s) {
     dim3 grid((B + 3) / 4);
     if (k <= 8)
-        hipLaunchKernelGGL(topk_merge_kernel<8>, grid, dim3(256), 0, s, cs, ci, B, n_lists, k, out_s, out_i);
+        hipLaunchKernelGGL(topk_merge_kernel<8>, grid, dim3(256), 0, s, cs, ci, B, n_lists, k, probe_stride, list_stride,
+                           out_s, out_i);
     else
-        hipLaunchKernelGGL(topk_merge_kernel<16>, grid, dim3(256), 0, s, cs, ci, B, n_lists, k, out_s, out_i);
+        hipLaunchKernelGGL(topk_merge_kernel<16>, grid, dim3(256), 0, s, cs, ci, B, n_lists, k, probe_stride,
+                           list_stride, out_s, out_i);
     return hipGetLastError();
+}
+
+hipError_t launch_topk_merge(const float* cs, const int32_t* ci, int B, int n_lists, int k, float* out_s,
+                             int32_t* out_i, hipStream_t s) {
+    return merge_strided(cs, ci, B, n_lists, k, (int64_t)n_lists * k, k, out_s, out_i, s);
+}
+
+hipError_t launch_topk_merge_ranks(const void* xchg, int n_ranks, int B, int k, float* out_s, int32_t* out_i,
+                                   hipStream_t s) {
+    const float* cs = (const float*)xchg;
+    return merge_strided(cs, (const int32_t*)(cs + (size_t)B * k), B, n_ranks, k, k, 2 * (int64_t)B * k, out_s,
+                         out_i, s);
 }
 
 // ---------------------------------------------------------------------------------------------------

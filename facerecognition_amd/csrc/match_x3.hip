@@ -122,16 +122,7 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
     }
 }
 
-#ifndef FR_X3_DEFER
-#define FR_X3_DEFER 0  // A/B: 1 = waves 4-7 run a tile's inserts mid-way through the next tile
-#endif
-#ifndef FR_X3_PIPE
-#define FR_X3_PIPE 0  // A/B: 1 = explicitly double-buffered fragment reads within a chunk
-#endif
-#ifndef FR_X3_SLOTS
-#define FR_X3_SLOTS 0  // A/B: LDS ring depth override (0: 7 chunks of 16 KiB / 4 of 32 KiB)
-#endif
-constexpr int XSLOT = FR_X3_SLOTS ? FR_X3_SLOTS : 7;  // LDS ring depth (chunks): XSLOT - 1 in flight
+constexpr int XSLOT = 7;  // LDS ring depth (chunks): XSLOT - 1 in flight (4, 5, 9, 10 measured slower)
 constexpr int XCHUNK_B = 2 * XG * XC * 2;      // 16 KiB: [hi 64 rows x 128 B][lo 64 rows x 128 B]
 static_assert(XCHUNK_B == XCHUNK_E * 2, "chunk layout");
 constexpr int XRB = XC * 2;                    // LDS row bytes
@@ -264,10 +255,6 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
             insert_s<KP>(ls, li, sc, (int)(tb + index_base) + 16 * (e >> 2) + 4 * my_sub + (e & 3));
         }
     };
-#if FR_X3_DEFER
-    f32x4_t accp[4];
-    int64_t tp = -1;
-#endif
     for (int64_t t0 = g_begin; t0 < g_end; t0 += XG) {
         f32x4_t acc[4];
 #pragma unroll
@@ -281,43 +268,7 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
             asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(XPPW * (XSLOT - 2)) : "memory");
             issue_next();
             const char* ch = smem + s_read * XCHUNK_B;
-#if FR_X3_DEFER
-            if (c == 4 && wave >= 4 && tp >= 0) filter_tile(accp, tp);  // the previous tile's, mid-way
-#endif
             if (++s_read == XSLOT) s_read = 0;
-#if FR_X3_PIPE
-            // A/B: the chunk's 4 groups (one k-step x two row fragments) double-buffered --
-            // group q + 1's 4 fragments are read before group q's 6 MFMAs (pinned by sched barriers)
-            {
-                bf8v fb[2][4];
-                auto ld = [&](int q, bf8v (&f)[4]) {
-                    const int tt = q >> 1, kch = 4 * tt + (lane >> 4);
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int row = 16 * (2 * (q & 1) + h) + (lane & 15);
-                        const int o = row * XRB + xswz(row, kch) * 16;
-                        f[2 * h] = *(const bf8v*)(ch + o);
-                        f[2 * h + 1] = *(const bf8v*)(ch + XCHUNK_B / 2 + o);
-                    }
-                };
-                ld(0, fb[0]);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (q < 3) ld(q + 1, fb[(q + 1) & 1]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    const int t = c * (XC / 32) + (q >> 1);
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int j = 2 * (q & 1) + h;
-                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[q & 1][2 * h], ph[t], acc[j], 0, 0, 0);
-                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[q & 1][2 * h + 1], ph[t], acc[j], 0, 0, 0);
-                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[q & 1][2 * h], pl[t], acc[j], 0, 0, 0);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            continue;
-#endif
 #pragma unroll
             for (int tt = 0; tt < XC / 32; ++tt) {
                 const int t = c * (XC / 32) + tt;
@@ -340,19 +291,8 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
                 }
             }
         }
-#if FR_X3_DEFER
-        if (wave >= 4) {  // waves 4-7 filter this tile during the next one (chunk 4): off their SIMD partner's
-#pragma unroll
-            for (int j = 0; j < 4; ++j) accp[j] = acc[j];
-            tp = t0;
-            continue;
-        }
-#endif
         filter_tile(acc, t0);
     }
-#if FR_X3_DEFER
-    if (wave >= 4 && tp >= 0) filter_tile(accp, tp);
-#endif
     // the look-ahead DMAs (zeros past the split) land everywhere before the ring is reused as scratch
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     // merge the 4 sub-lists of each probe into its top KO: park them in the (drained) ring and let

@@ -8,6 +8,8 @@
 //                   (arcface_model.py:192-196, extract_embeddings.py:381/434)
 //  * segment mean — per-identity mean + renorm (extract_embeddings.py:755-760, :555-592)
 #include "kernels.h"
+
+#include <algorithm>
 #include "../../include/frhip.h"
 
 namespace fr {
@@ -205,7 +207,35 @@ __global__ __launch_bounds__(256) void proj_l2_kernel(const float* x, int K, con
     for (int n = threadIdx.x; n < N; n += 256) out[(size_t)b * N + n] *= inv;
 }
 
+// max |x| of a bf16/f16 NHWC tensor into `slots` partial maxima (atomicMax on the non-negative f32 bit
+// pattern, vector-memory atomics): the amax an fp8 consumer's activation scale needs when its producer is a
+// kernel without an amax epilogue (an LDS-resident stage, engine.cpp forward)
+template <bool F16>
+__global__ __launch_bounds__(256) void amax_kernel(const bf16_t* __restrict__ x, size_t n8, float* __restrict__ amax,
+                                                   int slots) {
+    float m = 0.f;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+        float f[8];
+        Num<F16>::unpack8(*(const uint4*)(x + 8 * i), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(f[e]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)amax + (blockIdx.x % slots), __float_as_uint(m));
+}
+
 }  // namespace
+
+hipError_t launch_amax(const bf16_t* x, size_t n, int f16, float* amax, int slots, hipStream_t s) {
+    if (n % 8 || slots < 1) return hipErrorInvalidValue;
+    const size_t n8 = n / 8;
+    int blocks = (int)std::min<size_t>((n8 + 255) / 256, 1024);
+    if (blocks < 1) blocks = 1;
+    if (f16) hipLaunchKernelGGL(amax_kernel<true>, dim3(blocks), dim3(256), 0, s, x, n8, amax, slots);
+    else hipLaunchKernelGGL(amax_kernel<false>, dim3(blocks), dim3(256), 0, s, x, n8, amax, slots);
+    return hipGetLastError();
+}
 
 hipError_t launch_proj_l2(const float* x, int B, int K, const float* W, const float* bias, int N, int normalize,
                           float* out, hipStream_t s) {

@@ -52,11 +52,27 @@ def native_merge(cand_s: torch.Tensor, cand_i: torch.Tensor, k: int) -> Tuple[to
     return s, i
 
 
-class ShardedMatcher:
-    """Steps 1-4 above with preallocated buffers (no allocation per call).
+def native_merge_ranks(xchg: torch.Tensor, k: int, out_s: torch.Tensor, out_i: torch.Tensor) -> None:
+    """fr_topk_merge_ranks on the device: the all-gathered exchange block xchg [world, 2, P, k] (int32 words:
+    rank r's scores as f32 bits, then its global indices) → out_s / out_i [P, k]."""
+    from . import _native as N
+    W, P = int(xchg.shape[0]), int(xchg.shape[2])
+    N.check(N.lib().fr_topk_merge_ranks(N.ptr(xchg), W, P, k, N.ptr(out_s), N.ptr(out_i), N.stream_ptr(xchg.device)),
+            "fr_topk_merge_ranks")
 
-    local_search(probes [P, D]) -> (scores [P, k] f32, idx [P, k] int32, global indices)
-    merge(cand_s [P, world, k], cand_i [P, world, k], k) -> ([P, k], [P, k])
+
+class ShardedMatcher:
+    """Steps 1-4 above with buffers preallocated at construction: no allocation per call.
+
+    local_search(probes [P, D], out_s [P, k] f32, out_i [P, k] int32) writes the shard's top-k (global
+      indices) into out_s / out_i -- views into this rank's block of the candidate send buffer -- or
+      returns (scores, idx) tensors, which are then copied there;
+    merge(xchg [world, 2, P, k] int32, k, out_s, out_i) merges the all-gathered blocks (default
+      native_merge_ranks, fr_topk_merge_ranks).
+
+    The candidate exchange is ONE all-gather: each rank's block is [2][P][k] 4-byte words (its scores,
+    then its indices), written in place by the shard search, gathered as is and merged as is.
+    search() returns views of buffers owned by the matcher, overwritten by the next call.
     """
 
     def __init__(self, batch: int, dim: int, k: int, local_search: Callable, device: torch.device,
@@ -66,21 +82,30 @@ class ShardedMatcher:
         self.always_exchange = always_exchange  # run steps 1-4 even at world 1 (tests of the collectives)
         self.group, self.k, self.B = group, k, batch
         self.local_search = local_search
-        self.merge = merge or native_merge
-        W = self.world
-        self.all_emb = torch.empty((W * batch, dim), dtype=torch.float32, device=device)
-        self.cand_s = torch.empty((W, W * batch, k), dtype=torch.float32, device=device)
-        self.cand_i = torch.empty((W, W * batch, k), dtype=torch.int32, device=device)
+        self.merge = merge or native_merge_ranks
+        W, P = self.world, self.world * batch
+        self.all_emb = torch.empty((P, dim), dtype=torch.float32, device=device)
+        self.send = torch.empty((2, P, k), dtype=torch.int32, device=device)
+        self.xchg = torch.empty((W, 2, P, k), dtype=torch.int32, device=device)
+        self.out_s = torch.empty((P, k), dtype=torch.float32, device=device)
+        self.out_i = torch.empty((P, k), dtype=torch.int32, device=device)
+        self._send_s, self._send_i = self.send[0].view(torch.float32), self.send[1]
+        self._one_s, self._one_i = self.out_s[:batch], self.out_i[:batch]
+
+    def _local(self, probes, out_s, out_i):
+        r = self.local_search(probes, out_s, out_i)
+        if r is not None:
+            out_s.copy_(r[0])
+            out_i.copy_(r[1])
 
     def search(self, emb: torch.Tensor):
         """emb: this rank's normalized embeddings [B, D] → top-k of every rank's probes, identical on
         all ranks: (scores [world*B, k], idx [world*B, k]); row j*B + b is rank j's probe b."""
         if self.world == 1 and not self.always_exchange:
-            return self.local_search(emb)
+            self._local(emb, self._one_s, self._one_i)
+            return self._one_s, self._one_i
         _all_gather(self.all_emb, emb, self.group)
-        s, i = self.local_search(self.all_emb)
-        _all_gather(self.cand_s.view(-1), s.contiguous().view(-1), self.group)
-        _all_gather(self.cand_i.view(-1), i.contiguous().view(-1), self.group)
-        cs = self.cand_s.permute(1, 0, 2).contiguous()  # [probe][rank][k]
-        ci = self.cand_i.permute(1, 0, 2).contiguous()
-        return self.merge(cs, ci, self.k)
+        self._local(self.all_emb, self._send_s, self._send_i)
+        _all_gather(self.xchg.view(-1), self.send.view(-1), self.group)
+        self.merge(self.xchg, self.k, self.out_s, self.out_i)
+        return self.out_s, self.out_i

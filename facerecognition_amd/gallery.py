@@ -89,14 +89,18 @@ class DeviceGallery:
         """Probes whose bf16x3 candidate proof failed and were rescanned exactly (device sync)."""
         return int(N.lib().fr_debug_match_fallbacks(self._h))
 
-    def search_device(self, probes_dev, k: int):
-        """probes_dev: cuda f32 [B, D] → (scores [B,k] f32, idx [B,k] int32) on the device."""
+    def search_device(self, probes_dev, k: int, out_s=None, out_i=None):
+        """probes_dev: cuda f32 [B, D] → (scores [B,k] f32, idx [B,k] int32) on the device, written into
+        out_s / out_i when given (contiguous [B, k] f32 / int32 device tensors: no allocation)."""
         import torch
 
         p = probes_dev.float().contiguous()
         B = int(p.shape[0])
-        s = torch.empty((B, k), dtype=torch.float32, device=self.device)
-        i = torch.empty((B, k), dtype=torch.int32, device=self.device)
+        s = out_s if out_s is not None else torch.empty((B, k), dtype=torch.float32, device=self.device)
+        i = out_i if out_i is not None else torch.empty((B, k), dtype=torch.int32, device=self.device)
+        if tuple(s.shape) != (B, k) or tuple(i.shape) != (B, k) or not (s.is_contiguous() and i.is_contiguous()) \
+                or s.dtype != torch.float32 or i.dtype != torch.int32:
+            raise ValueError(f"search_device: out_s / out_i must be contiguous [{B}, {k}] float32 / int32")
         N.check(N.lib().fr_match_topk(self._h, N.ptr(p), B, k, N.ptr(s), N.ptr(i), N.stream_ptr(self.device)),
                 "fr_match_topk")
         return s, i

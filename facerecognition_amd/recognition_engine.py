@@ -106,17 +106,38 @@ class _Grow:
 
 class _TrackedDB(dict):
     """dict that counts mutations so the device copy knows when to refresh, and journals plain item
-    assignments (the add_to_db / db[name] = emb pattern) so the device copy can apply them in place
-    instead of rebuilding; any other mutation (del, pop, clear, ...) marks the journal unusable."""
+    assignments (the add_to_db / db[name] = emb pattern) so a device copy can apply them in place
+    instead of rebuilding; any other mutation (del, pop, clear, ...) restarts the journal, so copies
+    synced before it rebuild.  The journal is shared by every consumer (several engines may hold one
+    db): entry i is the key assigned at version journal_base + i + 1, and each consumer replays the
+    entries past the version it synced (journal_since)."""
     version = 0
-    journal = None  # [keys assigned since the device copy synced] or None: rebuild
+    journal_base = 0
+    JOURNAL_MAX = 1 << 16  # past this, the older half is dropped (consumers that far behind rebuild)
+
+    @property
+    def journal(self):
+        if "_journal" not in self.__dict__:
+            self._journal = []
+        return self._journal
+
+    def journal_since(self, version):
+        """Keys assigned after `version` in order, or None when the journal does not reach back to it."""
+        if version < self.journal_base or version > self.version:
+            return None
+        return self.journal[version - self.journal_base:]
 
     def _bump(self, key=None):
         self.version += 1
         if key is None:
-            self.journal = None
-        elif self.journal is not None:
-            self.journal.append(key)
+            self.journal.clear()
+            self.journal_base = self.version
+            return
+        self.journal.append(key)
+        if len(self.journal) > self.JOURNAL_MAX:
+            drop = len(self.journal) // 2
+            del self.journal[:drop]
+            self.journal_base += drop
 
     def __setitem__(self, k, v):
         super().__setitem__(k, v)
@@ -277,8 +298,9 @@ class RecognitionEngine:
         (every fr_embed output) then take one search."""
         from .gallery import DeviceGallery
         key = (id(self._db), self._db.version)
-        if self._g is not None and self._g[0] != key and self._g[0][0] == id(self._db) and self._db.journal is not None:
-            if self._db_apply_journal():
+        if self._g is not None and self._g[0] != key and self._g[0][0] == id(self._db):
+            keys = self._db.journal_since(self._g[0][1])
+            if keys is not None and self._db_apply_journal(keys):
                 self._g = (key, self._g[1], self._g[2])
         if self._g is None or self._g[0] != key:
             names = list(self._db.keys())
@@ -293,16 +315,16 @@ class RecognitionEngine:
                 idx = np.nonzero(mask)[0]
                 parts[tag] = (DeviceGallery(src[idx], dim=rows.shape[1], device=dev), _Grow(idx)) if len(idx) else None
             self._g = (key, parts, names)
-        self._db.journal = []
         return self._g[1], self._g[2]
 
-    def _db_apply_journal(self) -> bool:
-        """Apply the db's journaled assignments to the device copy in place: a new name appends one row
-        to its part (and to the 'all' copy), a re-assigned name overwrites its row when its norm class
-        ('on' / 'off') is unchanged.  False (-> rebuild) for anything else."""
+    def _db_apply_journal(self, keys) -> bool:
+        """Apply the db's journaled assignments since this engine's copy synced (`keys`) to the device
+        copy in place: a new name appends one row to its part (and to the 'all' copy), a re-assigned
+        name overwrites its row when its norm class ('on' / 'off') is unchanged.  False (-> rebuild)
+        for anything else."""
         from .gallery import DeviceGallery
         parts, names = self._g[1], self._g[2]
-        for k in self._db.journal:
+        for k in keys:
             v = np.asarray(self._db[k], dtype=np.float32).reshape(1, -1)
             if v.shape[1] != parts["dim"]:
                 return False

@@ -136,6 +136,15 @@ int fr_match_topk(fr_handle* h, const float* P, int B, int k, float* scores, int
 int fr_topk_merge(const float* cand_s, const int32_t* cand_i, int B, int n_lists, int k,
                   float* scores, int32_t* idx, void* stream);
 
+/* The same merge over the multi-GPU candidate exchange block as all-gathered (SURVEY.md §8e step
+ * 3-4, one collective): xchg = [n_ranks][2][B][k] 4-byte words, rank r's block holding its shard's
+ * top-k scores (f32 [B][k]) followed by their global indices (int32 [B][k]).  Each rank writes its
+ * block with fr_match_topk straight into the send buffer; the all-gather output is merged as is
+ * (no repacking, no permute).  Replaces the per-shard exchange the reference does not have
+ * (single-process recognize_with_db / IndexFlatIP.search, recognition_engine.py:267-326). */
+int fr_topk_merge_ranks(const void* xchg, int n_ranks, int B, int k, float* scores, int32_t* idx,
+                        void* stream);
+
 /* Fused convenience: fr_embed (normalized) then fr_match_topk on the same stream. */
 int fr_embed_match(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, int k,
                    float* emb_out, float* scores, int32_t* idx, void* stream);

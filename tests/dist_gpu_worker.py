@@ -2,7 +2,7 @@
 
 Both ranks share cuda:0 (the test box has one GPU), so the collectives run on gloo staged through host
 memory; the data path is the product one: DeviceGallery.search_device (fr_match_topk with the rank's
-index_base) for the shard-local top-k and native_merge (fr_topk_merge) for the merge."""
+index_base) for the shard-local top-k and native_merge_ranks (fr_topk_merge_ranks) for the merge."""
 import os
 import sys
 
@@ -74,7 +74,7 @@ def main():
             Gs = G[lo:hi].contiguous()
         gal = DeviceGallery(device=0, index_base=lo)
         gal.set_device_rows(Gs)
-        m = ShardedMatcher(b, D, K, lambda p: gal.search_device(p, K), dev)  # merge = native_merge
+        m = ShardedMatcher(b, D, K, lambda p, s, i: gal.search_device(p, K, s, i), dev)  # merge = native_merge_ranks
         s, i = m.search(P[rank * b:(rank + 1) * b].contiguous())
         torch.cuda.synchronize(dev)
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), s=s.cpu().numpy(), i=i.cpu().numpy(),

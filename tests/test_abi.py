@@ -27,6 +27,8 @@ def test_bad_arguments_are_rejected_with_message():
     assert rc == -1 and b"fr_topk_merge" in L.fr_last_error()
     rc = L.fr_topk_merge(None, None, 1, 1, 17, None, None, None)  # k > 16
     assert rc == -1
+    rc = L.fr_topk_merge_ranks(None, 2, 1, 5, None, None, None)
+    assert rc == -1 and b"fr_topk_merge_ranks" in L.fr_last_error()
     d = N.FrConvDesc()
     assert L.fr_op_conv2d(ctypes.byref(d), None) == -1
     assert b"fr_op_conv2d" in L.fr_last_error()

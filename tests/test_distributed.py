@@ -41,17 +41,27 @@ def _worker(rank, world, port, out_dir):
         lo, hi = shard_range(ROWS, rank, world)
         shard = G[lo:hi]
 
-        def local_search(probes):
+        def local_search(probes, out_s, out_i):
             s, i = topk_dot(probes.numpy(), shard, K)
             i = np.where(i >= 0, i + lo, -1)
-            return torch.from_numpy(s), torch.from_numpy(i.astype(np.int32))
+            out_s.copy_(torch.from_numpy(s))
+            out_i.copy_(torch.from_numpy(i.astype(np.int32)))
 
-        def merge(cs, ci, k):
-            s, i = merge_topk(cs.numpy(), ci.numpy(), k)
-            return torch.from_numpy(s), torch.from_numpy(i.astype(np.int32))
+        def merge(xchg, k, out_s, out_i):
+            # the all-gathered exchange block [world, 2, P, k] decoded back into [P, world, k] lists
+            x = xchg.numpy()
+            cs = x[:, 0].view(np.float32).transpose(1, 0, 2)
+            ci = x[:, 1].transpose(1, 0, 2)
+            s, i = merge_topk(np.ascontiguousarray(cs), np.ascontiguousarray(ci), k)
+            out_s.copy_(torch.from_numpy(s))
+            out_i.copy_(torch.from_numpy(i.astype(np.int32)))
 
         m = ShardedMatcher(B, D, K, local_search, torch.device("cpu"), merge=merge)
+        bufs = (m.send.data_ptr(), m.xchg.data_ptr(), m.out_s.data_ptr())
         s, i = m.search(torch.from_numpy(P[rank * B:(rank + 1) * B]))
+        s2, i2 = m.search(torch.from_numpy(P[rank * B:(rank + 1) * B]))  # buffers reused, same answer
+        assert (m.send.data_ptr(), m.xchg.data_ptr(), m.out_s.data_ptr()) == bufs
+        assert torch.equal(s, s2) and torch.equal(i, i2)
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), s=s.numpy(), i=i.numpy())
     finally:
         dist.destroy_process_group()

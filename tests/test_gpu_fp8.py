@@ -248,8 +248,8 @@ def test_iresnet100_fp8_guard_and_top1(gpu):
 
 def test_iresnet100_fp8_bs256(gpu):
     """BASELINE config-5 size (IResNet100 fp8, bs = 256, the autotuner's bs=256 tiles): deterministic replay,
-    finite unit-norm rows, the distribution of 1-cos against bf16 at the same batch (guard bar; the spec
-    bar is test_iresnet100_fp8_meets_config5_bar), an oracle sample, and identical top-1 on a planted 10k gallery."""
+    finite unit-norm rows, every face's 1-cos against bf16 at the same batch within the config-5 bar (1e-3;
+    median / p99 / max printed), an oracle sample, and identical top-1 on a planted 10k gallery."""
     from facerecognition_amd.gallery import DeviceGallery
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
@@ -269,7 +269,7 @@ def test_iresnet100_fp8_bs256(gpu):
     d = 1 - np.sum(a.numpy() * eb, axis=1)
     print(f"\nfp8 vs bf16 at bs=256: 1-cos median {np.median(d):.4g}, p99 {np.quantile(d, 0.99):.4g}, max {d.max():.4g}, "
           f"share <= 1e-3: {np.mean(d <= COS_VS_BF16):.3f}")
-    assert d.max() <= FP8_GUARD
+    assert d.max() <= COS_VS_BF16, f"config-5 bar: {int((d > COS_VS_BF16).sum())} faces above 1e-3, max {d.max():.4g}"
     ref = M.embed(M.build_model("iresnet100", sd), "iresnet100", u8[:3])
     c_o = (a[:3].numpy() * ref).sum(1) / np.linalg.norm(ref, axis=1)
     assert float((1 - c_o).max()) <= FP8_GUARD, 1 - c_o
@@ -301,3 +301,33 @@ def test_iresnet100_fp8_bs256(gpu):
     # a top-1 may only differ where bf16's own top-1 / top-2 margin is within the fp8 drift
     assert np.all(margin[flips] <= 4e-3), margin[flips]
     assert agree >= 0.95
+
+
+def test_iresnet100_fp8_all_plan_guard(gpu, monkeypatch):
+    """FR_FP8_PLAN=all (every eligible conv in e4m3; the A/B plan): the e4m3 layer3 stage's output feeds
+    the per-conv e4m3 layer4.0 convs, whose activation scale needs that tensor's amax -- the stages have
+    no amax epilogue, so the engine runs one reduction pass after the stage.  Bounded by
+    FP8_GUARD against bf16 and the fp32 oracle; without the amax pass layer4 ran unscaled."""
+    import ctypes
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    from facerecognition_amd.weights import synth_state_dict
+    from oracle import models as M
+    monkeypatch.setenv("FR_FP8_PLAN", "all")
+    sd = synth_state_dict("iresnet100")
+    u8 = synthetic_crops(4, 112, seed=44)
+    m8 = FRModel("iresnet100", sd, dtype="fp8")
+    buf = ctypes.create_string_buffer(1 << 16)
+    N.check(N.lib().fr_debug_plan(m8.handle, 4, buf, len(buf)))
+    e8 = m8.embed(torch.from_numpy(u8)).cpu().numpy()
+    m8.close()
+    monkeypatch.delenv("FR_FP8_PLAN")
+    mb = FRModel("iresnet100", sd, dtype="bf16")
+    eb = mb.embed(torch.from_numpy(u8)).cpu().numpy()
+    mb.close()
+    ref = M.embed(M.build_model("iresnet100", sd), "iresnet100", u8)
+    c_b = np.sum(e8 * eb, axis=1)
+    c_o = np.sum(e8 * ref, axis=1) / np.linalg.norm(ref, axis=1)
+    print(f"\nFR_FP8_PLAN=all: 1-cos vs bf16 {1 - c_b}, vs oracle {1 - c_o}")
+    assert np.all(np.isfinite(e8))
+    assert np.all(1 - c_b <= FP8_GUARD) and np.all(1 - c_o <= FP8_GUARD)

@@ -23,6 +23,26 @@ def _probes(arch, n, seed=0):
 _cache = {}
 
 
+def _check_flips(got, ref, G, dev_top1, ref_top1):
+    """Every top-1 flip must be exactly the one the embedding error causes: with a = the device's top-1
+    row and b = the oracle's, the oracle ranks b above a by gap = e_ref.(g_b - g_a) >= 0, and the device
+    ranks a above b, so (e - e_ref).(g_a - g_b) >= gap must hold for that probe (f64, up to the f32
+    rounding of the two scores).  A flip that the error does not explain is a match (or ordering) bug.
+    Returns the per-flip (gap, explained shift) pairs."""
+    flips = np.nonzero(dev_top1 != ref_top1)[0]
+    out = []
+    for q in flips:
+        ga = G[dev_top1[q]].astype(np.float64)
+        gb = G[ref_top1[q]].astype(np.float64)
+        e, er = got[q].astype(np.float64), ref[q].astype(np.float64)
+        gap = float(er @ (gb - ga))
+        shift = float((e - er) @ (ga - gb))
+        out.append((gap, shift))
+        assert gap >= -1e-6, f"probe {q}: the oracle's own top-1 is not its best row (gap {gap:.3e})"
+        assert shift >= gap - 2e-6, f"probe {q}: flip not explained by the embedding error: gap {gap:.3e} > shift {shift:.3e}"
+    return out
+
+
 def _oracle_embed(arch, u8):
     from facerecognition_amd.weights import synth_state_dict
     from oracle import models as M
@@ -157,11 +177,11 @@ def _full_batch_parity(arch, m, a, u8, seed):
     rs, ri = topk_dot(ref, R, 2)
     agree = gi[:, 0] == ri[:, 0]
     gap = rs[:, 0] - rs[:, 1]
-    err = np.linalg.norm(got - ref, axis=1)
     print(f"{arch} {m.dtype} bs={B}: non-planted top-1 agreement {agree.mean():.4f} ({int(agree.sum())}/{B}) on a "
           f"random 10k gallery; oracle top-1/top-2 gap min {gap.min():.2e} median {np.median(gap):.2e}; "
           f"flips at gaps {np.sort(gap[~agree])[:8]}")
-    assert np.all(agree | (gap <= 2 * err)), "a top-1 flip where the oracle's gap exceeds the error bound"
+    fl = _check_flips(got, ref, R, gi[:, 0], ri[:, 0])
+    print(f"{arch} {m.dtype} bs={B}: flips (gap, explained shift) {[(f'{g:.2e}', f'{h:.2e}') for g, h in fl[:8]]}")
     return agree.mean()
 
 
@@ -304,8 +324,8 @@ def test_full_batch_properties_bs256(gpu):
 def test_top1_agreement_random_gallery(gpu):
     """Non-planted top-1 agreement (SURVEY.md §7 'Hard parts'): 64 IResNet100 bf16 embeddings vs the fp32
     oracle's against a random 10k unit gallery.  Reports the agreement rate and the oracle's top-1/top-2
-    gap; a disagreement is only allowed where the oracle's own gap is below the score perturbation that
-    the embedding error can cause (|dg| <= |e - e_ref| * 2, rows being unit)."""
+    gap; a disagreement is only allowed where the embedding error explains it exactly (_check_flips:
+    (e - e_ref).(g_dev - g_ref) >= the oracle's gap between the two rows, per probe)."""
     from facerecognition_amd.gallery import DeviceGallery
     from facerecognition_amd.model import FRModel
     from oracle.match import topk_dot
@@ -323,13 +343,15 @@ def test_top1_agreement_random_gallery(gpu):
     rs, ri = topk_dot(ref, G, 2)
     agree = gi[:, 0] == ri[:, 0]
     gap = rs[:, 0] - rs[:, 1]
-    err = np.linalg.norm(got - ref / np.linalg.norm(ref, axis=1, keepdims=True), axis=1)
+    refn = ref / np.linalg.norm(ref, axis=1, keepdims=True)
+    err = np.linalg.norm(got - refn, axis=1)
     print(f"top-1 agreement {agree.mean():.4f} on 64 probes x 10k random rows; oracle gap median "
           f"{np.median(gap):.2e} min {gap.min():.2e}; embedding error max {err.max():.2e}")
-    # measured 0.94 (4 flips in 64, all inside the bound): a random 10k gallery has top-1/top-2 gaps down
+    # measured 0.94 (4 flips in 64, all explained): a random 10k gallery has top-1/top-2 gaps down
     # to ~3e-4, below what bf16 storage through 100 layers (|e - e_ref| ~ 1e-2) can resolve
     assert agree.mean() >= 0.85
-    assert np.all(agree | (gap <= 2 * err)), "a top-1 flip where the oracle's gap exceeds the error bound"
+    fl = _check_flips(got, refn, G, gi[:, 0], ri[:, 0])
+    print(f"flips (gap, explained shift): {[(f'{g:.2e}', f'{h:.2e}') for g, h in fl]}")
 
 
 @pytest.mark.parametrize("arch", ["irv1_facenet", "resnet50_arcface"])

@@ -476,6 +476,34 @@ def test_topk_merge(gpu):
         assert np.allclose(os_[b].cpu().numpy(), [c[0] for c in cand])
 
 
+@pytest.mark.parametrize("W,B,k", [(8, 2048, 5), (2, 9, 16), (3, 1, 1)])
+def test_topk_merge_ranks_equals_list_merge(gpu, W, B, k):
+    """fr_topk_merge_ranks over the all-gathered exchange block [W][2][B][k] (scores, then indices: the
+    one-collective candidate exchange of ShardedMatcher) equals fr_topk_merge of the same lists in its
+    [B][W][k] layout, bit for bit, including exact ties across ranks and -inf / -1 padding."""
+    rng = np.random.default_rng(W * 100 + k)
+    cs = np.sort(rng.standard_normal((W, B, k)).astype(np.float32), axis=2)[:, :, ::-1].copy()
+    ci = rng.permutation(W * B * k).reshape(W, B, k).astype(np.int32)
+    if W > 1:
+        cs[1, 0, 0] = cs[0, 0, 0] = 9.0  # tie across ranks -> lower index first
+    cs[-1, -1, -1], ci[-1, -1, -1] = -np.inf, -1  # a short shard's padding
+    x = np.empty((W, 2, B, k), np.int32)
+    x[:, 0] = cs.view(np.int32)
+    x[:, 1] = ci
+    tx = torch.from_numpy(x).to(gpu)
+    s1, i1 = torch.empty(B, k, device=gpu), torch.empty(B, k, dtype=torch.int32, device=gpu)
+    N.check(N.lib().fr_topk_merge_ranks(tx.data_ptr(), W, B, k, s1.data_ptr(), i1.data_ptr(), N.stream_ptr()))
+    tcs = torch.from_numpy(np.ascontiguousarray(cs.transpose(1, 0, 2))).to(gpu)
+    tci = torch.from_numpy(np.ascontiguousarray(ci.transpose(1, 0, 2))).to(gpu)
+    s2, i2 = torch.empty(B, k, device=gpu), torch.empty(B, k, dtype=torch.int32, device=gpu)
+    N.check(N.lib().fr_topk_merge(tcs.data_ptr(), tci.data_ptr(), B, W, k, s2.data_ptr(), i2.data_ptr(), N.stream_ptr()))
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s2) and torch.equal(i1, i2)
+    from oracle.match import merge_topk
+    rs, ri = merge_topk(cs.transpose(1, 0, 2), ci.transpose(1, 0, 2), k)
+    assert np.array_equal(i1.cpu().numpy(), ri.astype(np.int32)) and np.array_equal(s1.cpu().numpy(), rs)
+
+
 def test_segment_mean_normalize(gpu):
     rng = np.random.default_rng(2)
     E = _norm(rng.standard_normal((10, 512)))
@@ -688,7 +716,7 @@ def test_nccl_world1_all_gather(gpu):
         G = _norm(rng.standard_normal((40_000, 512)))
         gal = DeviceGallery(G)
         P = torch.from_numpy(_norm(rng.standard_normal((64, 512)))).to(gpu)
-        m = ShardedMatcher(64, 512, 5, lambda p: gal.search_device(p, 5), gpu, always_exchange=True)
+        m = ShardedMatcher(64, 512, 5, lambda p, s, i: gal.search_device(p, 5, s, i), gpu, always_exchange=True)
         s, i = m.search(P)
         s0, i0 = gal.search_device(P, 5)
         torch.cuda.synchronize()
@@ -792,5 +820,31 @@ def test_gallery_write_appends_and_updates_equal_rebuild(gpu):
         rs, ri = ref.search(P, k)
         assert np.array_equal(s, rs) and np.array_equal(i, ri), k
     assert list(gal.search(P[:3], 1)[1][:, 0]) == [7, 2047, 2999]
+    gal.close()
+    ref.close()
+
+
+def test_gallery_write_after_x3_threshold_raised(gpu):
+    """A gallery already split for the bf16x3 path stays on it after FR_OPT_X3_MIN_ROWS is raised, so
+    later appends and updates must be split too (else the candidate pass reads stale hi/lo rows and can
+    miss new rows): the top-k equals a fresh exact-path gallery of the same rows, bit for bit."""
+    from facerecognition_amd import _native as N
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(23)
+    G = _norm(rng.standard_normal((2600, 512)))
+    gal = DeviceGallery(G[:2400], x3_min_rows=2048)  # split now
+    N.check(N.lib().fr_set_option(gal._h, N.FR_OPT_X3_MIN_ROWS, 1 << 30), "fr_set_option")
+    gal.add(G[2400:])  # appends past the (raised) threshold ...
+    G[5] = _norm(rng.standard_normal((1, 512)))[0]
+    gal.update(5, G[5:6])  # ... and an in-place update
+    P = _norm(rng.standard_normal((32, 512)))
+    P[:4] = _norm(G[[5, 2400, 2555, 2599]] + 0.01 * rng.standard_normal((4, 512)))
+    ref = DeviceGallery(G)
+    ref.set_exact(True)
+    for k in (1, 5):
+        s, i = gal.search(P, k)
+        rs, ri = ref.search(P, k)
+        assert np.array_equal(s, rs) and np.array_equal(i, ri), k
+    assert list(gal.search(P[:4], 1)[1][:, 0]) == [5, 2400, 2555, 2599]
     gal.close()
     ref.close()

@@ -192,6 +192,29 @@ def test_split_stage_wait_runout_never_returns_valid_looking_embeddings(gpu):
     m.close()
 
 
+def test_sync_embed_does_not_swallow_async_failure(gpu):
+    """An FR_EMBED_ASYNC forward whose split-stage wait runs out, followed at once (no host sync) by a
+    synchronous fr_embed: the failure belongs to the async forward and is reported as such (FR_ERR_STAGE
+    from the synchronous call, which has not run), never taken by the synchronous call as its own and
+    cleared by its re-run.  The next call then runs normally."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("iresnet100")
+    x = torch.from_numpy(synthetic_crops(6, 112, seed=78)).cuda()
+    m.set_option(N.FR_OPT_STAGE, 2)
+    good = m.embed(x).cpu().numpy()
+    m.set_option(N.FR_OPT_STAGE_SPIN_LIMIT, -1)
+    e_async = m.embed(x, sync=False)
+    with pytest.raises(RuntimeError, match=r"rc=-6"):
+        m.embed(x)
+    assert bool(torch.isnan(e_async).any(dim=1).all())
+    assert m.stage_reruns() == 0  # the synchronous call did not re-run (it did not run at all)
+    m.sync_check()  # reported once
+    m.set_option(N.FR_OPT_STAGE_SPIN_LIMIT, 0)
+    assert np.array_equal(m.embed(x).cpu().numpy(), good)
+    m.close()
+
+
 def test_two_handles_share_a_device(gpu):
     """Two handles on one device, forwards on two streams: their split-stage forwards are chained on
     the GPU (DevSerial), no wait runs out, and each result equals its single-handle result."""

@@ -206,6 +206,42 @@ def test_db_edits_apply_in_place_and_match_a_rebuild(monkeypatch):
     assert eng._g[1] is not parts1
 
 
+def test_shared_db_journal_per_engine(monkeypatch):
+    """Two engines holding ONE db: each replays the journal entries past its own synced version, so an
+    engine that syncs first does not empty the journal the other still needs."""
+    from facerecognition_amd import gallery
+    monkeypatch.setattr(gallery, "DeviceGallery", _NumpyGallery)
+    db, probes = mixed_norm_case()
+    e1 = RE.RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.0)
+    e2 = RE.RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.0)
+    e1.db = dict(db)
+    e2.db = e1.db
+    rng = np.random.default_rng(5)
+
+    def check(eng):
+        for p in probes:
+            name, _, top = eng.recognize_with_db(p)
+            rname, _, rtop = OMT.recognize_with_db(p, dict(eng.db), 0.0)
+            assert name == rname and [t[0] for t in top] == [t[0] for t in rtop]
+
+    check(e1)
+    check(e2)
+    p1, p2 = e1._g[1], e2._g[1]
+    for i in range(3):
+        v = rng.standard_normal(8).astype(np.float32)
+        e1.db[f"n{i}"] = v / np.linalg.norm(v)
+        check(e1)  # e1 syncs after every edit; e2 only at the end, replaying all three
+    e1.db["A"] = probes[0] / np.linalg.norm(probes[0])  # a probe-like row: must win for e2 too
+    check(e1)
+    check(e2)
+    assert e1._g[1] is p1 and e2._g[1] is p2, "journaled edits must not rebuild either device copy"
+    assert e2.recognize_with_db(probes[0])[0] == "A"
+    del e1.db["B"]  # restarts the journal: both rebuild
+    check(e1)
+    check(e2)
+    assert e2._g[1] is not p2
+
+
 def test_extract_batch_empty_and_bad_paths():
     emb, paths = EE.extract_embeddings_batch([], model=None, transform=EE.get_transform())
     assert emb.size == 0 and paths == []
