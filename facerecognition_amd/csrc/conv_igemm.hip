@@ -456,6 +456,7 @@ template <bool F16>
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(ConvArgs p) {
     const int G = p.Cout / 8;
     const size_t total = (size_t)p.M * G;
+    float amax = 0.f;  // as the conv epilogue: max |y| for an fp8 consumer's activation scale
     for (size_t it = blockIdx.x * 256ull + threadIdx.x; it < total; it += (size_t)gridDim.x * 256) {
         const int m = (int)(it / G), n = (int)(it - (size_t)m * G) * 8;
         float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -466,6 +467,14 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(ConvArgs p) {
             v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
         }
         epilogue8<F16>(p, v, m, n);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+    }
+    if (p.y_amax) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+        if ((threadIdx.x & 63) == 0)
+            atomicMax((unsigned int*)p.y_amax + blockIdx.x % max(p.amax_slots, 1), __float_as_uint(amax));
     }
 }
 

@@ -1597,6 +1597,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 if (h->amax && cw.w8 && op.in_off == 0) {
                     a.w8 = cw.w8; a.wscale = cw.wscale; a.Kpad = cw.Kpad8;
                     a.x_amax = h->amax + (size_t)op.in * FR_AMAX_SLOTS;
+                    a.amax_slots = FR_AMAX_SLOTS;  // every producer spreads its maxima over all the slots (read
+                                                   // them all, also when this conv records no amax itself)
                 }
                 int rc = run_conv_args(h, a, s);
                 if (rc) return rc;
@@ -1866,7 +1868,20 @@ static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, 
     if (in_fmt != FR_IN_U8_NHWC && in_fmt != FR_IN_F32_NCHW) { set_error("fr_embed: bad in_fmt"); return FR_ERR_ARG; }
     if (flags & ~(FR_EMBED_RAW | FR_EMBED_ASYNC)) { set_error("fr_embed: unknown flag bits"); return FR_ERR_ARG; }
     FR_HIP_CHECK(hipSetDevice(h->device));
-    if (*(volatile int*)h->fail_host) {  // an earlier FR_EMBED_ASYNC forward's split stage ran out (sticky)
+    // An earlier FR_EMBED_ASYNC forward's split stage ran out (sticky).  The flag is only read once the async
+    // forwards it may come from have completed: a synchronous call waits for them (otherwise it would take their
+    // failure as its own after its own forward, and clear it with its re-run), an async call checks without
+    // blocking and leaves a failure of a forward still in flight to a later call or fr_sync_check (reading the
+    // flag mid-forward would report the layer1 stage's run-out and miss the layer2 stage's, written later).
+    bool flag_final = true;
+    if (h->async_pending) {
+        if (flags & FR_EMBED_ASYNC) {
+            flag_final = hipEventQuery(h->async_ev) == hipSuccess;
+            (void)hipGetLastError();  // hipErrorNotReady must not surface at the next launch check
+        } else FR_HIP_CHECK(hipEventSynchronize(h->async_ev));
+        if (flag_final) h->async_pending = false;
+    }
+    if (flag_final && *(volatile int*)h->fail_host) {
         *(volatile int*)h->fail_host = 0;
         set_error("fr_embed: a split stage's halo wait ran out in an earlier FR_EMBED_ASYNC forward on this "
                   "handle; the affected embeddings are NaN (reported once, see fr_sync_check)");
@@ -1879,19 +1894,6 @@ static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, 
     const hipStream_t s = (hipStream_t)stream;
     const int fflags = flags & FR_EMBED_RAW;  // what the forward (and its graph key) depends on
     const bool split = split_runs(h, B);
-    if (split && !(flags & FR_EMBED_ASYNC) && h->async_pending) {
-        // a synchronous forward reads the shared failure flag after its own completion: latch the failure
-        // of the FR_EMBED_ASYNC forwards still in flight first, so it is reported as theirs, not taken as
-        // this forward's (and cleared by its re-run)
-        FR_HIP_CHECK(hipEventSynchronize(h->async_ev));
-        h->async_pending = false;
-        if (*(volatile int*)h->fail_host) {
-            *(volatile int*)h->fail_host = 0;
-            set_error("fr_embed: a split stage's halo wait ran out in an earlier FR_EMBED_ASYNC forward on this "
-                      "handle; the affected embeddings are NaN (reported once, see fr_sync_check)");
-            return FR_ERR_STAGE;
-        }
-    }
     int rc;
     {
         DevSerial ser(h, split, s);

@@ -8,13 +8,13 @@ for r in $(seq 1 $N); do
   for v in $V; do
     tag=${v//=/_}
     if [ "$v" = base ]; then env_set=""; else env_set="$v"; fi
-    env $env_set timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/${tag}_$r.log 2>&1 || { echo "$v failed"; tail -20 $O/${tag}_$r.log; exit 1; }
+    env $env_set timeout -k 10 200 python bench.py --no-cpu-baseline --no-pmc --no-n1-1m --steps 20 --warmup 5 $AB_ARGS > $O/${tag}_$r.log 2>&1 || { echo "$v failed"; tail -20 $O/${tag}_$r.log; exit 1; }
     python - $O/${tag}_$r.log "$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 ks = d.get("kernels", {})
 print(f"{sys.argv[2]:18s} {d['value']:9.1f} faces/s {d['ms_per_step']:.3f} ms | " +
-      " ".join(f"{k}={v['ms_per_step']}" for k, v in list(ks.items())[:6]), flush=True)
+      " ".join(f"{k}={v['ms_per_step']}" for k, v in list(ks.items())[:8]), flush=True)
 PY
   done
 done
