@@ -156,9 +156,11 @@ struct fr_handle {
     uint64_t tick = 0;
     // per-shape igemm tile autotuning (numerically invisible: every tile accumulates K in the same
     // order; split-K choices stay with the cost model)
-    struct Tuned { int key[10]; int tile; };
+    struct Tuned { int key[13]; int tile, split; };  // the measured kernel choice per conv shape (tune_conv)
     std::vector<Tuned> tuned;
     std::vector<int> tuned_batches;
+    struct StageMeas { int stage, B, run; float t_stage, t_conv; };  // measured stage-vs-per-conv choice per batch
+    std::vector<StageMeas> stage_meas;
     bool tuning = false;
     // LDS-resident stage kernels (fr_set_option FR_OPT_STAGE / FR_OPT_KEEP_INTERMEDIATES)
     std::vector<StageRec> stages;
@@ -1158,20 +1160,28 @@ bool autotune_enabled() {
 }
 
 void shape_key(const ConvArgs& a, int* k) {
-    const int v[10] = {a.M, a.Cout, a.Kpad, a.Cin, a.Kh, a.Kw, a.sh, a.sw, a.res ? 1 : 0, a.y2 ? 1 : 0};
-    for (int i = 0; i < 10; ++i) k[i] = v[i];
+    const int v[13] = {a.M, a.Cout, a.Kpad, a.Cin, a.Kh, a.Kw, a.sh, a.sw, a.res ? 1 : 0, a.y2 ? 1 : 0, a.H, a.W, a.x2 ? 1 : 0};
+    for (int i = 0; i < 13; ++i) k[i] = v[i];
 }
 
-int find_tuned(const fr_handle* h, const ConvArgs& a) {
-    int k[10];
+// A conv's kernel: an FR_TILE_* id (the implicit-GEMM tiles, or one of the specialised kernels: row bands,
+// image bands, weight-resident rows, register weight ring, small-K direct) and a split-K factor (tiles only).
+struct ConvChoice {
+    int tile = -1, split = 1;
+};
+
+static bool find_tuned(const fr_handle* h, const ConvArgs& a, ConvChoice* c) {
+    int k[13];
     shape_key(a, k);
     for (const auto& t : h->tuned)
-        if (std::memcmp(t.key, k, sizeof(k)) == 0) return t.tile;
-    return -1;
+        if (std::memcmp(t.key, k, sizeof(k)) == 0) {
+            c->tile = t.tile;
+            c->split = t.split;
+            return true;
+        }
+    return false;
 }
 
-// Time every applicable tile on this conv (1 warm + 3 timed launches each, HIP events on `s`) and
-// remember the fastest for the shape.  Runs only inside the eager tuning pass of embed_locked.
 static bool wring_enabled() {
     static const bool on = [] {
         const char* e = getenv("FR_NO_WRING");
@@ -1188,31 +1198,128 @@ static bool direct_enabled() {
     return on;
 }
 
+static bool rows_ok(const ConvArgs& a) {
+    if (!rows_enabled() || !a.wrows_ || !a.ep || !a.negf) return false;
+    ConvArgs r = a;
+    r.wimg = a.wrows_;
+    return rows_supported(r);
+}
+
+static bool band_ok(const ConvArgs& a) {
+    int TH, variant;
+    return band_enabled() && !a.y_amax && band_plan(a, &TH, &variant) && variant >= 3;
+}
+
+// the split-K factor the partial workspace allows (reserve() sizes it for conv_plan's splits)
+static int fit_split(const fr_handle* h, const ConvArgs& a, int split) {
+    while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) split /= 2;
+    return split;
+}
+
+// The fixed policy (no measurement: FR_AUTOTUNE=0, a forced FR_CONV_TILE): the specialised kernels where they
+// apply (each measured faster than the implicit GEMM at bs = 256), else conv_plan's cost-model tile and split.
+static ConvChoice default_choice(const fr_handle* h, const ConvArgs& a) {
+    ConvChoice c;
+    if (rows_ok(a)) { c.tile = FR_TILE_ROWS; return c; }
+    if (img28_enabled() && img28_supported(a)) { c.tile = FR_TILE_IMG28; return c; }
+    if (img56_enabled() && img56_supported(a)) { c.tile = FR_TILE_IMG56; return c; }
+    if (band_ok(a)) { c.tile = FR_TILE_BAND; return c; }
+    conv_plan(a.M, a.Cout, a.Kpad, &c.tile, &c.split);
+    c.split = fit_split(h, a, c.split);
+    return c;
+}
+
+// Launches choice c (no timing scope; run_conv_args adds it).
+static hipError_t launch_choice(const fr_handle* h, ConvArgs& a, const ConvChoice& c, hipStream_t s) {
+    a.split_k = 1;
+    a.partial = nullptr;
+    switch (c.tile) {
+        case FR_TILE_ROWS: {
+            ConvArgs r = a;
+            r.wimg = a.wrows_;
+            return launch_conv_rows(r, h->n_cu, s);
+        }
+        case FR_TILE_IMG28: return launch_conv_img28(a, s);
+        case FR_TILE_IMG56: return launch_conv_img56(a, s);
+        case FR_TILE_BAND: {
+            int TH, variant;
+            if (!band_plan(a, &TH, &variant)) return hipErrorInvalidValue;
+            return launch_conv_band(a, TH, variant, s);
+        }
+        default: break;
+    }
+    a.tile = c.tile;
+    if (c.split > 1) {
+        a.split_k = c.split;
+        a.partial = h->partial;
+    }
+    hipError_t e = launch_conv(a, s);
+    if (e == hipSuccess && c.split > 1 && a.y) e = launch_splitk_epilogue(a, s);
+    return e;
+}
+
+static std::string choice_class(const ConvArgs& a, const ConvChoice& c) {
+    switch (c.tile) {
+        case FR_TILE_ROWS: return "conv3x3_rows W" + std::to_string(a.W) + " N" + std::to_string(a.Cout);
+        case FR_TILE_IMG28: return "conv3x3_img W28";
+        case FR_TILE_IMG56: return "conv3x3_img W56";
+        case FR_TILE_BAND: {
+            int TH = 0, variant = 0;
+            band_plan(a, &TH, &variant);
+            return "conv3x3_band W" + std::to_string(a.W) + " v" + std::to_string(variant);
+        }
+        case FR_TILE_WRING: return "conv_wring";
+        case FR_TILE_DIRECT: return "conv_direct";
+        default: return "conv_igemm tile" + std::to_string(c.tile) + (c.split > 1 ? " splitk" : "");
+    }
+}
+
+// Time every applicable kernel on this conv (1 warm + 3 timed launches each, three interleaved passes, the
+// best time per candidate, HIP events on `s`) and remember the fastest for the shape.  Candidates: the
+// specialised kernels that apply, every implicit-GEMM tile unsplit, the register-weight-ring and small-K
+// direct kernels, and conv_plan's split-K plan when it splits (small M: a few tiles over a long K).  Runs
+// only inside the eager tuning pass of embed_locked, so a batch size's choice is measured at that size
+// (bs = 1 and bs = 256 pick differently).  Every candidate sums K in the same order except split-K, whose
+// partial sums differ in f32 rounding only.
 int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
-    int cand[16];
-    int nc = conv_tile_candidates(a.Cout, cand);
+    std::vector<ConvChoice> cand;
+    auto add = [&](int tile, int split) {
+        ConvChoice c;
+        c.tile = tile;
+        c.split = split;
+        cand.push_back(c);
+    };
+    if (rows_ok(a)) add(FR_TILE_ROWS, 1);
+    if (img28_enabled() && img28_supported(a)) add(FR_TILE_IMG28, 1);
+    if (img56_enabled() && img56_supported(a)) add(FR_TILE_IMG56, 1);
+    if (band_ok(a)) add(FR_TILE_BAND, 1);
+    int tiles[16];
+    const int nt = conv_tile_candidates(a.Cout, tiles);
+    for (int i = 0; i < nt; ++i) add(tiles[i], 1);
     if (wring_enabled() && a.wring_) {  // the register-weight-ring kernel competes per shape
         ConvArgs w = a;
         w.wimg = a.wring_;
         w.partial = nullptr;
-        if (wring_supported(w)) cand[nc++] = TILE_WRING;
+        if (wring_supported(w)) add(TILE_WRING, 1);
     }
-    if (direct_enabled() && direct_supported(a)) cand[nc++] = TILE_DIRECT;  // small-K direct conv
+    if (direct_enabled() && direct_supported(a)) add(TILE_DIRECT, 1);  // small-K direct conv
+    {
+        int tile, split;
+        conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
+        split = fit_split(h, a, split);
+        if (split > 1) add(tile, split);
+    }
     hipEvent_t e0, e1;
     FR_HIP_CHECK(hipEventCreate(&e0));
     FR_HIP_CHECK(hipEventCreate(&e1));
-    a.split_k = 1;
-    a.partial = nullptr;
     // three interleaved passes, best time per candidate: one pass in candidate order let clock ramps
     // and neighbours' cache state pick different tiles from run to run (profiles/r01_bench_runs.jsonl)
-    float cand_ms[16];
-    for (int c = 0; c < nc; ++c) cand_ms[c] = 1e30f;
+    std::vector<float> cand_ms(cand.size(), 1e30f);
     for (int pass = 0; pass < 3; ++pass) {
-        for (int c = 0; c < nc; ++c) {
-            a.tile = cand[c];
-            FR_HIP_CHECK(launch_conv(a, s));
+        for (size_t c = 0; c < cand.size(); ++c) {
+            FR_HIP_CHECK(launch_choice(h, a, cand[c], s));
             FR_HIP_CHECK(hipEventRecord(e0, s));
-            for (int r = 0; r < 3; ++r) FR_HIP_CHECK(launch_conv(a, s));
+            for (int r = 0; r < 3; ++r) FR_HIP_CHECK(launch_choice(h, a, cand[c], s));
             FR_HIP_CHECK(hipEventRecord(e1, s));
             FR_HIP_CHECK(hipEventSynchronize(e1));
             float ms = 0.f;
@@ -1220,17 +1327,42 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
             cand_ms[c] = std::min(cand_ms[c], ms);
         }
     }
-    int best = -1;
-    float best_ms = 1e30f;
-    for (int c = 0; c < nc; ++c)
-        if (cand_ms[c] < best_ms * 0.99f) { best_ms = cand_ms[c]; best = cand[c]; }
+    size_t best = 0;
+    for (size_t c = 1; c < cand.size(); ++c)
+        if (cand_ms[c] < cand_ms[best] * 0.99f) best = c;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     fr_handle::Tuned t;
     shape_key(a, t.key);
-    t.tile = best;
+    t.tile = cand[best].tile;
+    t.split = cand[best].split;
     h->tuned.push_back(t);
     return FR_OK;
+}
+
+// The kernel choice of a conv launch: the measured one for its shape (tuned in the eager tuning forward of
+// the batch size), else the fixed policy; then the launch inside its timing scope.
+static bool choice_ok(const ConvArgs& a, const ConvChoice& c) {
+    switch (c.tile) {
+        case FR_TILE_ROWS: return rows_ok(a);
+        case FR_TILE_IMG28: return img28_enabled() && img28_supported(a);
+        case FR_TILE_IMG56: return img56_enabled() && img56_supported(a);
+        case FR_TILE_BAND: return band_ok(a);
+        case FR_TILE_WRING: {
+            ConvArgs w = a;
+            w.wimg = a.wring_;
+            w.partial = nullptr;
+            return a.wring_ && wring_supported(w);
+        }
+        case FR_TILE_DIRECT: return direct_supported(a);
+        default: return c.tile >= 0;
+    }
+}
+
+static ConvChoice conv_choice(const fr_handle* h, const ConvArgs& a) {
+    ConvChoice c;
+    if (autotune_enabled() && !conv_tile_forced() && find_tuned(h, a, &c) && choice_ok(a, c)) return c;
+    return default_choice(h, a);
 }
 
 int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
@@ -1245,54 +1377,21 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
         FR_HIP_CHECK(launch_conv_fp8(a, s));
         return FR_OK;
     }
-    if (rows_enabled() && a.wrows_ && a.ep && a.negf) {  // 64-channel 3x3/s1 convs: weight-resident rows
+    ConvChoice c;
+    if (autotune_enabled() && !conv_tile_forced() && !find_tuned(h, a, &c) && h->tuning) {
+        const int rc = tune_conv(h, a, s);
+        if (rc) return rc;
+    }
+    c = conv_choice(h, a);
+    if (c.tile == FR_TILE_ROWS) {  // the event pair rides on the launched args
         ConvArgs r = a;
         r.wimg = a.wrows_;
-        if (rows_supported(r)) {
-            ps.start("conv3x3_rows W" + std::to_string(a.W) + " N" + std::to_string(a.Cout), &r);
-            FR_HIP_CHECK(launch_conv_rows(r, h->n_cu, s));
-            return FR_OK;
-        }
-    }
-    if (img28_enabled() && img28_supported(a)) {  // layer2 3x3 128->128 @28x28: quarter-image bands
-        ps.start("conv3x3_img W28", &a);
-        FR_HIP_CHECK(launch_conv_img28(a, s));
+        ps.start(choice_class(a, c), &r);
+        FR_HIP_CHECK(launch_conv_rows(r, h->n_cu, s));
         return FR_OK;
     }
-    if (img56_enabled() && img56_supported(a)) {  // layer1 3x3 64->64 @56x56: 4-row bands
-        ps.start("conv3x3_img W56", &a);
-        FR_HIP_CHECK(launch_conv_img56(a, s));
-        return FR_OK;
-    }
-    int TH, variant;
-    // auto policy (measured, profiles/r01_tile_sweep.txt): the software-pipelined row-band variants
-    // (3: 14x14, 4: 28x28) beat the implicit GEMM; the legacy 8-wave variants do not
-    if (band_enabled() && !a.y_amax && band_plan(a, &TH, &variant) && variant >= 3) {
-        ps.start("conv3x3_band W" + std::to_string(a.W) + " v" + std::to_string(variant), &a);
-        FR_HIP_CHECK(launch_conv_band(a, TH, variant, s));
-        return FR_OK;
-    }
-    int tile, split;
-    conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
-    if (split == 1 && autotune_enabled() && !conv_tile_forced()) {
-        int t = find_tuned(h, a);
-        if (t < 0 && h->tuning) {
-            int rc = tune_conv(h, a, s);
-            if (rc) return rc;
-            t = find_tuned(h, a);
-        }
-        if (t >= 0) tile = t;
-    }
-    a.tile = tile;
-    while (split > 1 && (size_t)split * a.M * a.Npad > h->partial_floats) split /= 2;
-    if (split > 1) a.partial = h->partial;
-    a.split_k = split;
-    ps.start(tile == TILE_WRING ? std::string("conv_wring")
-             : tile == TILE_DIRECT ? std::string("conv_direct")
-                                   : "conv_igemm tile" + std::to_string(tile) + (split > 1 ? " splitk" : ""),
-             &a);
-    FR_HIP_CHECK(launch_conv(a, s));
-    if (split > 1 && a.y) FR_HIP_CHECK(launch_splitk_epilogue(a, s));
+    ps.start(choice_class(a, c), &a);
+    FR_HIP_CHECK(launch_choice(h, a, c, s));
     return FR_OK;
 }
 
@@ -1312,9 +1411,15 @@ static bool split_stage_enabled(int H) {
     return !(off == 1 || off == H);
 }
 
-static bool stage_runs(const fr_handle* h, int B, const StageRec& r) {
+static int stage_choice(const fr_handle* h, int st, int B);
+
+static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     if (h->stage_mode == 0) return false;
     if (r.parts > 1 && (h->no_split || !split_stage_enabled(r.H))) return false;
+    if (h->stage_mode == 1) {  // measured at this batch size (measure_stage)
+        const int c = stage_choice(h, st, B);
+        if (c >= 0) return c == 1;
+    }
     const int cap = std::max(1, h->n_cu / r.parts);
     if (h->stage_mode == 2 || B <= cap) return true;
     const int64_t rounds = (B + cap - 1) / cap;
@@ -1324,7 +1429,7 @@ static bool stage_runs(const fr_handle* h, int B, const StageRec& r) {
 // Per-op skip rule: a stage op runs when its stage runs; its member convs run when it does not.
 static std::vector<char> stage_plan(const fr_handle* h, int B) {
     std::vector<char> run(h->stages.size());
-    for (size_t i = 0; i < run.size(); ++i) run[i] = stage_runs(h, B, h->stages[i]);
+    for (size_t i = 0; i < run.size(); ++i) run[i] = stage_runs(h, B, h->stages[i], (int)i);
     return run;
 }
 
@@ -1335,8 +1440,8 @@ static bool op_skipped(const Op& op, const std::vector<char>& run) {
 
 // Whether a forward at batch B runs a split stage (its parts wait for each other).
 static bool split_runs(const fr_handle* h, int B) {
-    for (const auto& r : h->stages)
-        if (r.parts > 1 && stage_runs(h, B, r)) return true;
+    for (size_t i = 0; i < h->stages.size(); ++i)
+        if (h->stages[i].parts > 1 && stage_runs(h, B, h->stages[i], (int)i)) return true;
     return false;
 }
 
@@ -1421,6 +1526,143 @@ static bool ms_enabled() {
     return e && e[0] == '1';
 }
 
+// One LDS-resident stage launch (+ the amax pass an e4m3 reader of its output needs).
+static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vector<char>& stage_run, hipStream_t s) {
+    const StageRec& r = h->stages[op.stage];
+    StageArgs a{};
+    a.x = h->tensors[r.in].dev;
+    a.y = h->tensors[r.out].dev;
+    a.w = r.w;
+    a.conv = r.table;
+    a.ep = r.ep;
+    a.slope = r.slope;
+    if (h->keep_inter) { a.dbg_x = r.dbg; a.dbg_t = r.dbg + r.nblk; }
+    a.B = B;
+    a.nblk = r.nblk;
+    a.f16 = f16;
+    a.dbg = stage_dbg();
+    a.xchg = h->stage_xchg;
+    a.flags = h->stage_flags + (size_t)h->max_batch * 4 * op.stage;  // the stage's own counter region
+    a.spin_timeouts = h->stage_spin;
+    a.fail_host = h->fail_dev;
+    a.spin_limit = h->spin_limit;
+    a.variant = h->stage_variant;
+    {
+        ProfScope ps(h, s);
+        ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
+        ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * (r.fp8 ? 1.0 : 2.0);
+        if (r.fp8) {
+            a.w = (const bf16_t*)r.w8;
+            a.wscale = r.wscale;
+            ps.start("stage8 layer3");
+            FR_HIP_CHECK(launch_stage8(a, s));
+        } else {
+            ps.start(r.H == 14 ? "stage layer3" : (r.H == 28 ? "stage layer2" : "stage layer1"));
+            FR_HIP_CHECK(r.parts > 1 ? launch_split_stage(a, r.H, r.C, s) : launch_stage(a, s));
+        }
+    }
+    // the stages have no amax epilogue: when a per-conv e4m3 conv reads the stage output (e.g.
+    // layer4.0 under FR_FP8_PLAN=all), its activation scale comes from one reduction pass here
+    if (h->amax && h->need_amax[r.out] &&
+        std::any_of(h->ops.begin(), h->ops.end(), [&](const Op& c) {  // a per-conv e4m3 reader runs
+            return c.kind == OP_CONV && c.in == r.out && c.in_off == 0 && c.wi >= 0 && h->convw[c.wi].w8 &&
+                   !op_skipped(c, stage_run);
+        })) {
+        const auto& t = h->tensors[r.out];
+        ProfScope pa(h, s);
+        pa.bytes = 2.0 * B * t.H * t.W * t.C;
+        pa.start("amax");
+        FR_HIP_CHECK(launch_amax(t.dev, (size_t)B * t.H * t.W * t.C, f16 || t.f16,
+                                 h->amax + (size_t)r.out * FR_AMAX_SLOTS, FR_AMAX_SLOTS, s));
+    }
+    return FR_OK;
+}
+
+// One conv op: its ConvArgs from the plan's tensors and weights, then the kernel choice (run_conv_args).
+static int run_conv_op(fr_handle* h, const Op& op, int B, int f16, hipStream_t s) {
+    const auto& cw = h->convw[op.wi];
+    const auto& ti = h->tensors[op.in];
+    const auto& to = h->tensors[op.out];
+    ConvArgs a{};
+    a.f16 = f16 || ti.f16;
+    a.y_bf16 = ti.f16 && !to.f16;  // f16 section -> bf16 plan boundary
+    a.x = ti.dev; a.B = B; a.H = ti.H; a.W = ti.W; a.Cx = ti.C; a.x_off = op.in_off; a.Cin = op.cin;
+    a.w = cw.w; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
+    a.K = cw.K; a.Kpad = cw.Kpad;
+    a.Ho = to.H; a.Wo = to.W; a.M = B * to.H * to.W; a.Cout = cw.Cout; a.Npad = cw.Npad;
+    a.bias = cw.bias; a.slope = cw.slope; a.act = op.act; a.bias9 = cw.bias9; a.wimg = cw.wimg;
+    a.negf = cw.negf; a.ep = cw.ep;
+    a.wrows_ = cw.wrows;
+    a.wring_ = cw.wring;
+    if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
+    if (op.x2 >= 0) {
+        const auto& t2 = h->tensors[op.x2];
+        a.x2 = t2.dev; a.H2 = t2.H; a.W2 = t2.W; a.Cx2 = t2.C; a.x2_off = op.x2_off;
+        a.C2 = cw.C2; a.st2 = op.st2; a.K1 = cw.K1;
+    }
+    a.y = to.dev; a.Cy = to.C; a.y_off = op.out_off;
+    if (op.out2 >= 0) {
+        a.y2 = h->tensors[op.out2].dev; a.Cy2 = h->tensors[op.out2].C; a.y2_off = 0;
+        a.aff_s = cw.aff_s; a.aff_b = cw.aff_b;
+    }
+    if (h->amax && h->need_amax[op.out]) {
+        a.y_amax = h->amax + (size_t)op.out * FR_AMAX_SLOTS;
+        a.amax_slots = FR_AMAX_SLOTS;
+    }
+    if (h->amax && cw.w8 && op.in_off == 0) {
+        a.w8 = cw.w8; a.wscale = cw.wscale; a.Kpad = cw.Kpad8;
+        a.x_amax = h->amax + (size_t)op.in * FR_AMAX_SLOTS;
+        a.amax_slots = FR_AMAX_SLOTS;  // every producer spreads its maxima over all the slots (read
+                                       // them all, also when this conv records no amax itself)
+    }
+    return run_conv_args(h, a, s);
+}
+
+// Stage or per-conv launches for a stage's blocks at batch B, measured (FR_OPT_STAGE = 1, the default): in the
+// eager tuning forward of a new batch size the member convs run (and tune their kernels), then the member
+// sequence and the stage are timed with HIP events, and the faster is kept for B (-1: not measured yet).  The
+// winner runs last, so the tuning forward's output equals every later forward's.
+static int stage_choice(const fr_handle* h, int st, int B) {
+    for (const auto& m : h->stage_meas)
+        if (m.stage == st && m.B == B) return m.run;
+    return -1;
+}
+
+static int measure_stage(fr_handle* h, const Op& op, int B, int f16, const std::vector<char>& stage_run, hipStream_t s) {
+    const StageRec& r = h->stages[op.stage];
+    auto members = [&]() {
+        for (int oi : r.conv_ops) {
+            const int rc = run_conv_op(h, h->ops[oi], B, f16, s);
+            if (rc) return rc;
+        }
+        return (int)FR_OK;
+    };
+    int rc = members();  // tunes the member convs' kernels
+    if (!rc) rc = run_stage(h, op, B, f16, stage_run, s);  // warm
+    if (rc) return rc;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (auto& e : ev) FR_HIP_CHECK(hipEventCreate(&e));
+    float t_conv = 1e30f, t_stage = 1e30f;
+    for (int pass = 0; pass < 2 && !rc; ++pass) {  // best of two, interleaved
+        FR_HIP_CHECK(hipEventRecord(ev[0], s));
+        rc = members();
+        FR_HIP_CHECK(hipEventRecord(ev[1], s));
+        if (!rc) rc = run_stage(h, op, B, f16, stage_run, s);
+        FR_HIP_CHECK(hipEventRecord(ev[2], s));
+        FR_HIP_CHECK(hipEventSynchronize(ev[2]));
+        float a = 0.f, b = 0.f;
+        FR_HIP_CHECK(hipEventElapsedTime(&a, ev[0], ev[1]));
+        FR_HIP_CHECK(hipEventElapsedTime(&b, ev[1], ev[2]));
+        t_conv = std::min(t_conv, a);
+        t_stage = std::min(t_stage, b);
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    if (rc) return rc;
+    const int run = t_stage <= t_conv ? 1 : 0;
+    h->stage_meas.push_back({op.stage, B, run, t_stage, t_conv});
+    return run ? FR_OK : members();  // the stage's output is in place; else the per-conv one replaces it
+}
+
 int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int flags, hipStream_t s_main) {
     const int f16 = h->dtype == FR_DTYPE_F16;
     const std::vector<char> stage_run = stage_plan(h, B);
@@ -1490,53 +1732,10 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
         const hipStream_t s = strm[target];
         switch (op.kind) {
             case OP_STAGE: {
-                const StageRec& r = h->stages[op.stage];
-                StageArgs a{};
-                a.x = h->tensors[r.in].dev;
-                a.y = h->tensors[r.out].dev;
-                a.w = r.w;
-                a.conv = r.table;
-                a.ep = r.ep;
-                a.slope = r.slope;
-                if (h->keep_inter) { a.dbg_x = r.dbg; a.dbg_t = r.dbg + r.nblk; }
-                a.B = B;
-                a.nblk = r.nblk;
-                a.f16 = f16;
-                a.dbg = stage_dbg();
-                a.xchg = h->stage_xchg;
-                a.flags = h->stage_flags + (size_t)h->max_batch * 4 * op.stage;  // the stage's own counter region
-                a.spin_timeouts = h->stage_spin;
-                a.fail_host = h->fail_dev;
-                a.spin_limit = h->spin_limit;
-                a.variant = h->stage_variant;
-                {
-                ProfScope ps(h, s);
-                ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
-                ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * (r.fp8 ? 1.0 : 2.0);
-                if (r.fp8) {
-                    a.w = (const bf16_t*)r.w8;
-                    a.wscale = r.wscale;
-                    ps.start("stage8 layer3");
-                    FR_HIP_CHECK(launch_stage8(a, s));
-                } else {
-                    ps.start(r.H == 14 ? "stage layer3" : (r.H == 28 ? "stage layer2" : "stage layer1"));
-                    FR_HIP_CHECK(r.parts > 1 ? launch_split_stage(a, r.H, r.C, s) : launch_stage(a, s));
-                }
-                }
-                // the stages have no amax epilogue: when a per-conv e4m3 conv reads the stage output (e.g.
-                // layer4.0 under FR_FP8_PLAN=all), its activation scale comes from one reduction pass here
-                if (h->amax && h->need_amax[r.out] &&
-                    std::any_of(h->ops.begin(), h->ops.end(), [&](const Op& c) {  // a per-conv e4m3 reader runs
-                        return c.kind == OP_CONV && c.in == r.out && c.in_off == 0 && c.wi >= 0 && h->convw[c.wi].w8 &&
-                               !op_skipped(c, stage_run);
-                    })) {
-                    const auto& t = h->tensors[r.out];
-                    ProfScope pa(h, s);
-                    pa.bytes = 2.0 * B * t.H * t.W * t.C;
-                    pa.start("amax");
-                    FR_HIP_CHECK(launch_amax(t.dev, (size_t)B * t.H * t.W * t.C, f16 || t.f16,
-                                             h->amax + (size_t)r.out * FR_AMAX_SLOTS, FR_AMAX_SLOTS, s));
-                }
+                const bool measure = h->tuning && h->stage_mode == 1 && !h->keep_inter && !h->prof &&
+                                     stage_choice(h, op.stage, B) < 0;
+                const int rc = measure ? measure_stage(h, op, B, f16, stage_run, s) : run_stage(h, op, B, f16, stage_run, s);
+                if (rc) return rc;
                 break;
             }
             case OP_PRE: {
@@ -1565,42 +1764,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 break;
             }
             case OP_CONV: {
-                const auto& cw = h->convw[op.wi];
-                const auto& ti = h->tensors[op.in];
-                const auto& to = h->tensors[op.out];
-                ConvArgs a{};
-                a.f16 = f16 || ti.f16;
-                a.y_bf16 = ti.f16 && !to.f16;  // f16 section -> bf16 plan boundary
-                a.x = ti.dev; a.B = B; a.H = ti.H; a.W = ti.W; a.Cx = ti.C; a.x_off = op.in_off; a.Cin = op.cin;
-                a.w = cw.w; a.Kh = op.kh; a.Kw = op.kw; a.sh = op.sh; a.sw = op.sw; a.ph = op.ph; a.pw = op.pw;
-                a.K = cw.K; a.Kpad = cw.Kpad;
-                a.Ho = to.H; a.Wo = to.W; a.M = B * to.H * to.W; a.Cout = cw.Cout; a.Npad = cw.Npad;
-                a.bias = cw.bias; a.slope = cw.slope; a.act = op.act; a.bias9 = cw.bias9; a.wimg = cw.wimg;
-                a.negf = cw.negf; a.ep = cw.ep;
-                a.wrows_ = cw.wrows;
-                a.wring_ = cw.wring;
-                if (op.res >= 0) { a.res = h->tensors[op.res].dev; a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
-                if (op.x2 >= 0) {
-                    const auto& t2 = h->tensors[op.x2];
-                    a.x2 = t2.dev; a.H2 = t2.H; a.W2 = t2.W; a.Cx2 = t2.C; a.x2_off = op.x2_off;
-                    a.C2 = cw.C2; a.st2 = op.st2; a.K1 = cw.K1;
-                }
-                a.y = to.dev; a.Cy = to.C; a.y_off = op.out_off;
-                if (op.out2 >= 0) {
-                    a.y2 = h->tensors[op.out2].dev; a.Cy2 = h->tensors[op.out2].C; a.y2_off = 0;
-                    a.aff_s = cw.aff_s; a.aff_b = cw.aff_b;
-                }
-                if (h->amax && h->need_amax[op.out]) {
-                    a.y_amax = h->amax + (size_t)op.out * FR_AMAX_SLOTS;
-                    a.amax_slots = FR_AMAX_SLOTS;
-                }
-                if (h->amax && cw.w8 && op.in_off == 0) {
-                    a.w8 = cw.w8; a.wscale = cw.wscale; a.Kpad = cw.Kpad8;
-                    a.x_amax = h->amax + (size_t)op.in * FR_AMAX_SLOTS;
-                    a.amax_slots = FR_AMAX_SLOTS;  // every producer spreads its maxima over all the slots (read
-                                                   // them all, also when this conv records no amax itself)
-                }
-                int rc = run_conv_args(h, a, s);
+                const int rc = run_conv_op(h, op, B, f16, s);
                 if (rc) return rc;
                 break;
             }
@@ -2163,15 +2327,12 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
             a.Npad = cw.Npad; a.B = B; a.wimg = cw.wimg; a.f16 = h->dtype == FR_DTYPE_F16; a.bias9 = cw.bias9;
             a.Cx = h->tensors[op.in].C; a.x_off = op.in_off; a.Cy = h->tensors[op.out].C; a.y_off = op.out_off;
             if (op.res >= 0) { a.Cres = h->tensors[op.res].C; a.res_off = op.res_off; }
-            int TH, variant;
-            ConvArgs rr = a;
-            rr.wimg = cw.wrows;
-            rr.y2 = a.y2; rr.partial = nullptr;
-            if (rows_enabled() && cw.wrows && rows_supported(rr)) tile = FR_TILE_ROWS;
-            else if (img28_enabled() && img28_supported(a)) tile = FR_TILE_IMG28;
-            else if (img56_enabled() && img56_supported(a)) tile = FR_TILE_IMG56;
-            else if (band_enabled() && band_plan(a, &TH, &variant) && variant >= 3) tile = FR_TILE_BAND;
-            else if (sp == 1 && autotune_enabled() && !conv_tile_forced() && find_tuned(h, a) >= 0) tile = find_tuned(h, a);
+            a.wrows_ = cw.wrows; a.wring_ = cw.wring; a.ep = cw.ep; a.negf = cw.negf; a.K = cw.K;
+            if (op.x2 >= 0) { a.x2 = (const bf16_t*)1; a.C2 = cw.C2; a.K1 = cw.K1; a.st2 = op.st2; }
+            if (h->amax && h->need_amax[op.out]) a.y_amax = (float*)1;
+            const ConvChoice c = conv_choice(h, a);  // the measured kernel (after a forward at B), else the policy
+            tile = c.tile;
+            sp = c.split;
         }
         const std::string nm = op.kind == OP_HEAD ? "head" : h->tensors[op.out].name;
         out += (op.kind == OP_HEAD ? "head " : "conv ") + std::to_string(M) + " " + std::to_string(cw.Cout) + " " +
