@@ -159,6 +159,7 @@ struct fr_handle {
     struct Tuned { int key[13]; int tile, split; };  // the measured kernel choice per conv shape (tune_conv)
     std::vector<Tuned> tuned;
     std::vector<int> tuned_batches;
+    void* blas = nullptr;  // hipBLASLt state of the FR_TILE_BLAS choice (blas.cpp), created on first use
     struct StageMeas { int stage, B, run; float t_stage, t_conv; };  // measured stage-vs-per-conv choice per batch
     std::vector<StageMeas> stage_meas;
     bool tuning = false;
@@ -1218,6 +1219,14 @@ static int fit_split(const fr_handle* h, const ConvArgs& a, int split) {
 
 // The fixed policy (no measurement: FR_AUTOTUNE=0, a forced FR_CONV_TILE): the specialised kernels where they
 // apply (each measured faster than the implicit GEMM at bs = 256), else conv_plan's cost-model tile and split.
+static bool blas_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_BLAS");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 static ConvChoice default_choice(const fr_handle* h, const ConvArgs& a) {
     ConvChoice c;
     if (rows_ok(a)) { c.tile = FR_TILE_ROWS; return c; }
@@ -1230,10 +1239,13 @@ static ConvChoice default_choice(const fr_handle* h, const ConvArgs& a) {
 }
 
 // Launches choice c (no timing scope; run_conv_args adds it).
-static hipError_t launch_choice(const fr_handle* h, ConvArgs& a, const ConvChoice& c, hipStream_t s) {
+static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, hipStream_t s) {
     a.split_k = 1;
     a.partial = nullptr;
     switch (c.tile) {
+        case FR_TILE_BLAS:
+            if (!h->blas) h->blas = blas_create();
+            return launch_conv_blas(h->blas, a, s);
         case FR_TILE_ROWS: {
             ConvArgs r = a;
             r.wimg = a.wrows_;
@@ -1270,6 +1282,7 @@ static std::string choice_class(const ConvArgs& a, const ConvChoice& c) {
         }
         case FR_TILE_WRING: return "conv_wring";
         case FR_TILE_DIRECT: return "conv_direct";
+        case FR_TILE_BLAS: return "blas gemm";
         default: return "conv_igemm tile" + std::to_string(c.tile) + (c.split > 1 ? " splitk" : "");
     }
 }
@@ -1303,6 +1316,7 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
         if (wring_supported(w)) add(TILE_WRING, 1);
     }
     if (direct_enabled() && direct_supported(a)) add(TILE_DIRECT, 1);  // small-K direct conv
+    if (blas_enabled() && blas_supported(a)) add(FR_TILE_BLAS, 1);       // 1x1 conv as a library GEMM
     {
         int tile, split;
         conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
@@ -1317,7 +1331,12 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     std::vector<float> cand_ms(cand.size(), 1e30f);
     for (int pass = 0; pass < 3; ++pass) {
         for (size_t c = 0; c < cand.size(); ++c) {
-            FR_HIP_CHECK(launch_choice(h, a, cand[c], s));
+            if (cand_ms[c] < 0.f) continue;  // failed to launch (a library candidate without an algorithm)
+            if (launch_choice(h, a, cand[c], s) != hipSuccess) {
+                (void)hipGetLastError();
+                cand_ms[c] = -1.f;
+                continue;
+            }
             FR_HIP_CHECK(hipEventRecord(e0, s));
             for (int r = 0; r < 3; ++r) FR_HIP_CHECK(launch_choice(h, a, cand[c], s));
             FR_HIP_CHECK(hipEventRecord(e1, s));
@@ -1328,8 +1347,9 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
         }
     }
     size_t best = 0;
-    for (size_t c = 1; c < cand.size(); ++c)
-        if (cand_ms[c] < cand_ms[best] * 0.99f) best = c;
+    while (best + 1 < cand.size() && cand_ms[best] < 0.f) ++best;
+    for (size_t c = best + 1; c < cand.size(); ++c)
+        if (cand_ms[c] >= 0.f && cand_ms[c] < cand_ms[best] * 0.99f) best = c;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     fr_handle::Tuned t;
@@ -1355,6 +1375,7 @@ static bool choice_ok(const ConvArgs& a, const ConvChoice& c) {
             return a.wring_ && wring_supported(w);
         }
         case FR_TILE_DIRECT: return direct_supported(a);
+        case FR_TILE_BLAS: return blas_enabled() && blas_supported(a);
         default: return c.tile >= 0;
     }
 }
@@ -1912,6 +1933,7 @@ void fr_destroy(fr_handle* h) {
     DevSerial::reg(h, false);
     if (h->chk_ev) (void)hipEventDestroy(h->chk_ev);
     if (h->async_ev) (void)hipEventDestroy(h->async_ev);
+    if (h->blas) blas_destroy(h->blas);
     if (h->fail_host) (void)hipHostFree(h->fail_host);
     delete h;
 }

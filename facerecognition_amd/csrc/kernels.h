@@ -64,6 +64,12 @@ bool rows_supported(const ConvArgs& a);
 size_t rows_packed_elems(int Cout);
 hipError_t rows_pack_weights(const bf16_t* w, int Kpad, int Cout, bf16_t* out, hipStream_t s);
 hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s);
+// 1x1 stride-1 convs as hipBLASLt GEMMs (blas.cpp): bias + ReLU epilogue, residual as beta * C.  The state (library
+// handle, 32-MiB workspace, per-conv descriptors and algorithm) lives per fr_handle.
+bool blas_supported(const ConvArgs& a);
+void* blas_create();
+void blas_destroy(void* state);
+hipError_t launch_conv_blas(void* state, const ConvArgs& a, hipStream_t s);
 constexpr int FR_AMAX_SLOTS = 64;  // engine: spreads the producers' atomics over 64 addresses
 // max |x| of n (% 8) bf16/f16 values into amax[0 .. slots) (misc.hip): for tensors an fp8 conv reads whose
 // producer has no amax epilogue (an LDS-resident stage)

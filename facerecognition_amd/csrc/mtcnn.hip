@@ -8,7 +8,8 @@
 //     regions -- whole images for the PNet pyramid, box crops for RNet (24x24) / ONet (48x48) -- with
 //     the (x - 127.5) * 0.0078125 normalisation; window sums of u8 values are exact in f32 and the
 //     division is torch's sum / kh / kw, so the result is bit-identical to the CPU reference;
-//   * conv_kernel: valid 3x3 / 2x2 / 1x1 conv, stride 1, bias + PReLU;
+//   * conv_kernel: valid 3x3 / 2x2 / 1x1 conv, stride 1, bias + PReLU; a thread per output pixel and
+//     output-channel block, weights through the scalar cache;
 //   * maxpool_ceil_kernel: MaxPool2d(k, 2, ceil_mode=True);
 //   * dense_kernel: Linear (+ PReLU); weights pre-permuted on the host to the NHWC flatten order;
 //   * head_kernel: the classification / regression heads: softmax of the first two outputs, the rest raw.
@@ -44,28 +45,58 @@ __global__ __launch_bounds__(256) void area_resample_kernel(const uint8_t* __res
     o[2] = (s2 / kh / kw - 127.5f) * 0.0078125f;
 }
 
-// one thread per (output pixel, output channel); weights [Cout][kh][kw][Cin]
+// One thread per output pixel and CB output channels (blockIdx.y), accumulators in registers: the weights of
+// a (tap, input channel) step are the same for every lane of the workgroup, so they come through the scalar
+// cache (s_load, 4 input channels per load when Cin % 4 == 0) and each input value loaded feeds CB FMAs (the
+// one-thread-per-output kernel loaded an input and a weight per FMA).  Each output still sums its taps in the
+// same (r, s, c) order with fmaf.  Weights [Cout][kh][kw][Cin].
+template <int CB, bool V4>
 __global__ __launch_bounds__(256) void conv_kernel(const float* __restrict__ x, int B, int H, int W, int Cin,
                                                    const float* __restrict__ wt, const float* __restrict__ bias,
                                                    const float* __restrict__ slope, int Cout, int kh, int kw,
                                                    float* __restrict__ y) {
     const int Ho = H - kh + 1, Wo = W - kw + 1;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)B * Ho * Wo * Cout) return;
-    const int co = (int)(i % Cout);
-    const int64_t pix = i / Cout;
-    const int ox = (int)(pix % Wo), oy = (int)((pix / Wo) % Ho), b = (int)(pix / ((int64_t)Wo * Ho));
-    float acc = 0.f;
-    const float* wc = wt + (size_t)co * kh * kw * Cin;
+    const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int co0 = blockIdx.y * CB;
+    const bool live = pix < (int64_t)B * Ho * Wo;
+    const int64_t pc = live ? pix : 0;  // dead lanes compute pixel 0 and store nothing (uniform loops)
+    const int ox = (int)(pc % Wo), oy = (int)((pc / Wo) % Ho), b = (int)(pc / ((int64_t)Wo * Ho));
+    const int KK = kh * kw * Cin;
+    float acc[CB];
+#pragma unroll
+    for (int j = 0; j < CB; ++j) acc[j] = 0.f;
     for (int r = 0; r < kh; ++r)
         for (int s = 0; s < kw; ++s) {
             const float* xp = x + (((size_t)b * H + oy + r) * W + ox + s) * Cin;
-            const float* wp = wc + (r * kw + s) * Cin;
-            for (int c = 0; c < Cin; ++c) acc = fmaf(xp[c], wp[c], acc);
+            const float* wp = wt + (size_t)co0 * KK + (r * kw + s) * Cin;
+            if (V4) {
+                for (int c = 0; c < Cin; c += 4) {
+                    const float4 xv = *(const float4*)(xp + c);
+#pragma unroll
+                    for (int j = 0; j < CB; ++j) {
+                        const float4 wv = *(const float4*)(wp + (size_t)j * KK + c);  // wave-uniform: scalar load
+                        acc[j] = fmaf(xv.x, wv.x, acc[j]);
+                        acc[j] = fmaf(xv.y, wv.y, acc[j]);
+                        acc[j] = fmaf(xv.z, wv.z, acc[j]);
+                        acc[j] = fmaf(xv.w, wv.w, acc[j]);
+                    }
+                }
+            } else {
+                for (int c = 0; c < Cin; ++c) {
+                    const float xv = xp[c];
+#pragma unroll
+                    for (int j = 0; j < CB; ++j) acc[j] = fmaf(xv, wp[(size_t)j * KK + c], acc[j]);
+                }
+            }
         }
-    float v = acc + (bias ? bias[co] : 0.f);
-    if (slope) v = v >= 0.f ? v : v * slope[co];
-    y[i] = v;
+    if (!live) return;
+    float* yp = y + (size_t)pix * Cout + co0;
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+        float v = acc[j] + (bias ? bias[co0 + j] : 0.f);
+        if (slope) v = v >= 0.f ? v : v * slope[co0 + j];
+        yp[j] = v;
+    }
 }
 
 __global__ __launch_bounds__(256) void maxpool_ceil_kernel(const float* __restrict__ x, int B, int H, int W, int C,
@@ -145,12 +176,24 @@ hipError_t launch_area_resample(const uint8_t* img, int H, int W, const int32_t*
     return hipGetLastError();
 }
 
+template <int CB>
+static hipError_t conv_cb(const float* x, int B, int H, int W, int Cin, const float* w, const float* bias,
+                          const float* slope, int Cout, int kh, int kw, float* y, hipStream_t s) {
+    const dim3 grid(blocks((int64_t)B * (H - kh + 1) * (W - kw + 1), 256), Cout / CB);
+    auto k = Cin % 4 == 0 ? conv_kernel<CB, true> : conv_kernel<CB, false>;
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, s, x, B, H, W, Cin, w, bias, slope, Cout, kh, kw, y);
+    return hipGetLastError();
+}
+
+// CB output channels per thread: the largest of 16, 8, 5, 4, 2, 1 dividing Cout (PNet conv1's 10 -> 5)
 hipError_t launch_mtcnn_conv(const float* x, int B, int H, int W, int Cin, const float* w, const float* bias,
                              const float* slope, int Cout, int kh, int kw, float* y, hipStream_t s) {
-    const int64_t n = (int64_t)B * (H - kh + 1) * (W - kw + 1) * Cout;
-    hipLaunchKernelGGL(conv_kernel, dim3(blocks(n, 256)), dim3(256), 0, s, x, B, H, W, Cin, w, bias, slope, Cout, kh,
-                       kw, y);
-    return hipGetLastError();
+    if (Cout % 16 == 0) return conv_cb<16>(x, B, H, W, Cin, w, bias, slope, Cout, kh, kw, y, s);
+    if (Cout % 8 == 0) return conv_cb<8>(x, B, H, W, Cin, w, bias, slope, Cout, kh, kw, y, s);
+    if (Cout % 5 == 0) return conv_cb<5>(x, B, H, W, Cin, w, bias, slope, Cout, kh, kw, y, s);
+    if (Cout % 4 == 0) return conv_cb<4>(x, B, H, W, Cin, w, bias, slope, Cout, kh, kw, y, s);
+    if (Cout % 2 == 0) return conv_cb<2>(x, B, H, W, Cin, w, bias, slope, Cout, kh, kw, y, s);
+    return conv_cb<1>(x, B, H, W, Cin, w, bias, slope, Cout, kh, kw, y, s);
 }
 
 hipError_t launch_mtcnn_maxpool(const float* x, int B, int H, int W, int C, int k, int st, int Ho, int Wo, float* y,

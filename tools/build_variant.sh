@@ -10,12 +10,12 @@ C=$S/facerecognition_amd/csrc
 B=$R/facerecognition_amd/csrc/build_$N
 mkdir -p $B $R/facerecognition_amd/lib/variants
 objs=""
-for s in conv_igemm.hip conv_fp8.hip conv_band.hip conv_stage.hip conv_stage8.hip conv_split_stage.hip conv_wring.hip conv_direct.hip conv_img.hip conv_rows.hip conv_stem.hip misc.hip match.hip match_x3.hip preprocess.hip mtcnn.hip engine.cpp; do
+for s in conv_igemm.hip conv_fp8.hip conv_band.hip conv_stage.hip conv_stage8.hip conv_split_stage.hip conv_wring.hip conv_direct.hip conv_img.hip conv_rows.hip conv_stem.hip misc.hip match.hip match_x3.hip preprocess.hip mtcnn.hip blas.cpp engine.cpp; do
   o=$B/${s%.*}.o; objs="$objs $o"
   x=""; [ "${s##*.}" = cpp ] && x="-x hip"
   [ "$s" = conv_rows.hip ] && x="-mllvm -amdgpu-mfma-vgpr-form"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -I$S/include $F $x -c $C/$s -o $o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o $R/facerecognition_amd/lib/variants/libfrhip_$N.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o $R/facerecognition_amd/lib/variants/libfrhip_$N.so -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
 echo "built facerecognition_amd/lib/variants/libfrhip_$N.so"

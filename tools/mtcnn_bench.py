@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""MTCNN detector throughput on the device (reference preprocessing/face_detector.py:144-210):
+FaceDetector.detect on a synthetic 1080p frame (synthetic weights -- no MTCNN weights ship with the reference),
+end to end with its host pyramid / NMS logic, plus the device nets alone: PNet on the largest pyramid level,
+RNet on 256 24x24 crops, ONet on 256 48x48 crops (HIP events around each call).
+
+    python tools/mtcnn_bench.py [--iters 20] [--out profiles/r04_mtcnn.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def frame(H=1080, W=1920, seed=0):
+    rng = np.random.default_rng(seed)
+    a = torch.tensor(rng.standard_normal((H // 8 + 2, W // 8 + 2, 3)))
+    a = F.interpolate(a.permute(2, 0, 1)[None], size=(H, W), mode="bicubic", align_corners=False)[0].permute(1, 2, 0)
+    a = a.numpy()
+    return ((a - a.min()) / (a.max() - a.min()) * 255).clip(0, 255).astype(np.uint8)
+
+
+def timed(fn, iters):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    from facerecognition_amd import face_detector as FD
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    img = frame()
+    fd = FD.FaceDetector(mtcnn_state=FD.synth_mtcnn_state(7))
+    m = fd.mtcnn if hasattr(fd, "mtcnn") else fd.detector
+    bgr = np.ascontiguousarray(img[..., ::-1])
+    fd.detect(bgr)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        det = fd.detect(bgr)
+    torch.cuda.synchronize()
+    t_detect = (time.perf_counter() - t0) / a.iters * 1e3
+    H, W = img.shape[:2]
+    scales = FD.pyramid_scales(H, W)
+    dev_img = torch.as_tensor(img[None]).cuda()
+    hs, ws = int(H * scales[0] + 1), int(W * scales[0] + 1)
+    x0 = m.resample(dev_img, np.array([[0, 0, 0, H, W]]), hs, ws)
+    t_pnet0 = timed(lambda: m.pnet(x0), a.iters)
+    t_pyr = timed(lambda: [m.pnet(m.resample(dev_img, np.array([[0, 0, 0, H, W]]), int(H * s + 1), int(W * s + 1)))
+                           for s in scales], max(3, a.iters // 4))
+    xr = torch.randn(256, 24, 24, 3, device="cuda")
+    xo = torch.randn(256, 48, 48, 3, device="cuda")
+    t_rnet = timed(lambda: m.rnet(xr), a.iters)
+    t_onet = timed(lambda: m.onet(xo), a.iters)
+    res = {"frame": f"{W}x{H} synthetic RGB u8", "weights": "synthetic (synth_mtcnn_state(7))",
+           "pyramid_levels": len(scales), "detect_ms": round(t_detect, 3),
+           "detected": det is not None, "pnet_level0_ms": round(t_pnet0, 3), "pnet_level0_shape": [hs, ws],
+           "pnet_all_levels_with_resample_ms": round(t_pyr, 3), "rnet_256_crops_ms": round(t_rnet, 3),
+           "onet_256_crops_ms": round(t_onet, 3)}
+    print(json.dumps(res), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
