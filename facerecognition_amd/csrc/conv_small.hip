@@ -1,0 +1,153 @@
+// Small-M implicit GEMM (CDNA4 / gfx950): the convs of small batches (bs = 1 is the reference's online path,
+// recognition_engine.py:328-381 -> extract_embedding_single), where M = B*Ho*Wo is a few hundred pixels.  The
+// LDS-resident stages put one image on one CU (layer3 at bs = 1: 1.7 ms on one CU) and the implicit-GEMM tiles
+// leave most CUs idle while one block walks a long K; split-K needs a second (epilogue) launch per conv.
+// Here one WAVE computes a 16-pixel x 64-channel output tile over the whole K with no LDS and no barrier: every
+// K-step (32 deep) it loads its 4 weight fragments (16 B per lane, the [Npad][Kpad] rows) and its pixel fragment
+// (16 B per lane: the im2col gather, zero by out-of-range buffer offsets at the padding) straight from global
+// memory into registers, PF steps ahead, and issues 4 v_mfma_f32_16x16x32.  A 3x3 256->256 conv of one 14x14
+// image is 13 x 4 = 52 waves, ~2-3 us.  The K-concatenated 1x1 projection (a transition block's downsample,
+// ConvArgs::x2) continues the K loop.  Per output the 32-deep MFMA chain runs over k in order and the epilogue
+// is conv_igemm's (acc + bias, + the border-class bias, + residual, activation), so the result equals
+// conv_igemm tile 0 bit for bit: an autotuner candidate (FR_TILE_SMALL) that changes nothing numerically.
+#include "kernels.h"
+
+#include <hip/hip_ext.h>
+
+namespace fr {
+namespace {
+
+constexpr int NFR = 4;   // 16-channel fragments per wave (64 output channels)
+constexpr int PF = 4;    // K-steps of loads in flight
+constexpr uint32_t OOB = 0x80000000u;
+
+template <bool F16>
+__global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, int n_units) {
+    typedef Num<F16> T;
+    typedef typename T::frag frag;
+    const int lane = threadIdx.x & 63;
+    const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave-uniform
+    if (unit >= n_units) return;
+    const int mf = unit % n_mf, ng = unit / n_mf;  // pixel fragment, 64-channel group
+    const int n0 = ng * 16 * NFR;
+    const int g = lane >> 4;                       // k-group: k = 32 s + 8 g .. + 7
+    const int m = 16 * mf + (lane & 15);           // the lane's pixel (B operand row)
+    const bool mv = m < p.M;
+    const int HoWo = p.Ho * p.Wo;
+    const int mb = mv ? m / HoWo : 0, mr = mv ? m - mb * HoWo : 0, oh = mr / p.Wo, ow = mr - oh * p.Wo;
+    const int ih0 = oh * p.sh - p.ph, iw0 = ow * p.sw - p.pw;
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * p.H * p.W * p.Cx * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.x2 ? p.x2 : p.x), 0,
+        (uint32_t)min((size_t)0x7fffffff, p.x2 ? (size_t)p.B * p.H2 * p.W2 * p.Cx2 * 2 : (size_t)0), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.w, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2), 0x00020000);
+    const int K1 = p.x2 ? p.K1 : p.K;          // the conv's own K; the projection K-steps follow
+    const int nks = p.Kpad / 32;
+    const uint32_t wbase = (uint32_t)(((n0 + (lane & 15)) * p.Kpad + 8 * g) * 2);
+    const uint32_t x2base = (mv && p.x2)
+                                ? (uint32_t)((((mb * p.H2 + oh * p.st2) * p.W2 + ow * p.st2) * p.Cx2 + p.x2_off + 8 * g) * 2)
+                                : OOB;
+
+    // operand offsets of K-step s (k0 = 32 s): a 32-deep step lies inside one tap (Cin % 32 == 0)
+    auto xoff = [&](int s) -> uint32_t {
+        const int k0 = 32 * s;
+        if (k0 >= K1) {  // projection K-steps (or the zero padding past K)
+            const int c = k0 - K1;
+            return (p.x2 && c < p.C2 && x2base != OOB) ? x2base + (uint32_t)(c * 2) : OOB;
+        }
+        const int tap = k0 / p.Cin, c0 = k0 - tap * p.Cin;
+        const int r = tap / p.Kw, t = tap - r * p.Kw;
+        const int ih = ih0 + r, iw = iw0 + t;
+        if (!mv || (unsigned)ih >= (unsigned)p.H || (unsigned)iw >= (unsigned)p.W) return OOB;
+        return (uint32_t)((((mb * p.H + ih) * p.W + iw) * p.Cx + p.x_off + c0 + 8 * g) * 2);
+    };
+    frag wa[PF][NFR], xb[PF];
+    auto load_step = [&](int s, int slot) {
+        const bool proj = 32 * s >= K1;
+        const uint32_t xo = xoff(s);
+        xb[slot] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(proj ? x2r : xr, xo, 0, 0));
+#pragma unroll
+        for (int i = 0; i < NFR; ++i)
+            wa[slot][i] = __builtin_bit_cast(
+                frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wbase + (uint32_t)(i * 16 * p.Kpad * 2), (uint32_t)(s * 64), 0));
+    };
+    f32x4_t acc[NFR];
+#pragma unroll
+    for (int i = 0; i < NFR; ++i) acc[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+        if (q < nks) load_step(q, q);
+    // PF steps per iteration: the ring slot of step s is s % PF, compile-time inside the unrolled body
+    for (int s0 = 0; s0 < nks; s0 += PF) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+            const int s = s0 + q;
+            if (s >= nks) break;
+#pragma unroll
+            for (int i = 0; i < NFR; ++i) acc[i] = T::mfma(wa[q][i], xb[q], acc[i]);
+            if (s + PF < nks) load_step(s + PF, q);
+        }
+    }
+    if (!mv) return;
+    // epilogue (conv_igemm's arithmetic): lane holds channels n .. n + 3 of fragment i of pixel m
+#pragma unroll
+    for (int i = 0; i < NFR; ++i) {
+        const int n = n0 + 16 * i + 4 * g;
+        if (n >= p.Cout) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][e] + ((p.bias && !p.bias9) ? p.bias[n + e] : 0.f);
+        if (p.bias9) {
+            const float* bb = p.bias9 + (size_t)border_class(oh, ow, p.Ho, p.Wo) * p.Npad + n;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += bb[e];
+        }
+        if (p.res) {
+            const uint2 r = *(const uint2*)(p.res + (size_t)m * p.Cres + p.res_off + n);
+            float f[8];
+            T::unpack8(make_uint4(r.x, r.y, 0u, 0u), f);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += f[e];
+        }
+        if (p.act == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        } else if (p.act == 2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope[n + e];
+        }
+        float o8[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
+        const uint4 pk = F16 && p.y_bf16 ? Num<false>::pack8(o8) : T::pack8(o8);
+        *(uint2*)(p.y + (size_t)m * p.Cy + p.y_off + n) = make_uint2(pk.x, pk.y);
+    }
+}
+
+}  // namespace
+
+bool small_supported(const ConvArgs& a) {
+    const bool kcat = a.x2 != nullptr;
+    return a.B > 0 && a.M > 0 && a.Cin % 32 == 0 && a.Cout % 64 == 0 && a.Npad >= a.Cout && a.Kpad % 32 == 0 &&
+           a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.Cy % 4 == 0 && a.y_off % 4 == 0 && !a.y2 && !a.partial && !a.w8 &&
+           !a.y_amax && (!a.res || (a.Cres % 4 == 0 && a.res_off % 4 == 0)) &&
+           (kcat ? (a.C2 % 32 == 0 && a.Cx2 % 8 == 0 && a.x2_off % 8 == 0 && a.K1 == a.Kh * a.Kw * a.Cin &&
+                    a.K1 + a.C2 <= a.Kpad && a.K == a.K1 + a.C2)
+                 : a.K == a.Kh * a.Kw * a.Cin) &&
+           (!a.y_bf16 || (a.f16 && !a.res));
+}
+
+hipError_t launch_conv_small(const ConvArgs& a, hipStream_t s) {
+    if (!small_supported(a)) return hipErrorInvalidValue;
+    const int n_mf = (a.M + 15) / 16, n_units = n_mf * (a.Cout / 64);
+    const dim3 grid((unsigned)((n_units + 3) / 4));
+    auto k = a.f16 ? conv_small_kernel<true> : conv_small_kernel<false>;
+    if (a.ev0)
+        hipExtLaunchKernelGGL(k, grid, dim3(256), 0, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, n_mf, n_units);
+    else
+        hipLaunchKernelGGL(k, grid, dim3(256), 0, s, a, n_mf, n_units);
+    return hipGetLastError();
+}
+
+}  // namespace fr

@@ -1246,6 +1246,7 @@ static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, 
         case FR_TILE_BLAS:
             if (!h->blas) h->blas = blas_create();
             return launch_conv_blas(h->blas, a, s);
+        case FR_TILE_SMALL: return launch_conv_small(a, s);
         case FR_TILE_ROWS: {
             ConvArgs r = a;
             r.wimg = a.wrows_;
@@ -1283,6 +1284,7 @@ static std::string choice_class(const ConvArgs& a, const ConvChoice& c) {
         case FR_TILE_WRING: return "conv_wring";
         case FR_TILE_DIRECT: return "conv_direct";
         case FR_TILE_BLAS: return "blas gemm";
+        case FR_TILE_SMALL: return "conv_small";
         default: return "conv_igemm tile" + std::to_string(c.tile) + (c.split > 1 ? " splitk" : "");
     }
 }
@@ -1317,6 +1319,8 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     }
     if (direct_enabled() && direct_supported(a)) add(TILE_DIRECT, 1);  // small-K direct conv
     if (blas_enabled() && blas_supported(a)) add(FR_TILE_BLAS, 1);       // 1x1 conv as a library GEMM
+    // small M (a few hundred pixels: small batches): one wave per 16 px x 64 ch, no LDS, no second launch
+    if (a.M <= 8192 && small_supported(a)) add(FR_TILE_SMALL, 1);
     {
         int tile, split;
         conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
@@ -1376,6 +1380,7 @@ static bool choice_ok(const ConvArgs& a, const ConvChoice& c) {
         }
         case FR_TILE_DIRECT: return direct_supported(a);
         case FR_TILE_BLAS: return blas_enabled() && blas_supported(a);
+        case FR_TILE_SMALL: return small_supported(a);
         default: return c.tile >= 0;
     }
 }
@@ -2644,6 +2649,20 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         a.wimg = (const bf16_t*)tw;
         FR_HIP_CHECK(launch_conv_wring(a, st));
         FR_HIP_CHECK(hipFreeAsync(tw, st));
+        return FR_OK;
+    }
+    if (d->tile == FR_TILE_SMALL + 1) {
+        if (!small_supported(a)) { set_error("fr_op_conv2d: small-M kernel not applicable"); return FR_ERR_ARG; }
+        FR_HIP_CHECK(launch_conv_small(a, (hipStream_t)stream));
+        return FR_OK;
+    }
+    if (d->tile == FR_TILE_BLAS + 1) {  // a per-call library state: the op API holds no handle
+        if (!blas_supported(a)) { set_error("fr_op_conv2d: library GEMM not applicable (1x1 / stride 1 / ReLU)"); return FR_ERR_ARG; }
+        void* st = blas_create();
+        const hipError_t e = launch_conv_blas(st, a, (hipStream_t)stream);
+        (void)hipStreamSynchronize((hipStream_t)stream);
+        blas_destroy(st);
+        FR_HIP_CHECK(e);
         return FR_OK;
     }
     if (d->tile == FR_TILE_DIRECT + 1) {

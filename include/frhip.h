@@ -251,6 +251,7 @@ typedef struct fr_conv_desc {
 #define FR_TILE_DIRECT 14    /* persistent small-K direct conv (conv_direct.hip): Cin % 8 == 0, Kpad <= 384, Cout % 32 == 0,
                                 bias + activation epilogue; autotuned per shape (env FR_NO_DIRECT=1: off) */
 #define FR_TILE_BLAS 15      /* 1x1 stride-1 conv as a hipBLASLt GEMM (bias + ReLU / residual epilogue); an autotuner candidate */
+#define FR_TILE_SMALL 16     /* small-M implicit GEMM, one wave per 16 px x 64 ch over the whole K (conv_small.hip); bit-identical to tile 0 */
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 

@@ -848,3 +848,60 @@ def test_gallery_write_after_x3_threshold_raised(gpu):
     assert list(gal.search(P[:4], 1)[1][:, 0]) == [5, 2400, 2555, 2599]
     gal.close()
     ref.close()
+
+
+SMALL_CASES = [
+    # B, H, W, Cin, Cout, stride   (small-batch shapes: bs = 1 layer3 / layer4 / layer2, a transition, bs = 3)
+    (1, 14, 14, 256, 256, 1), (1, 7, 7, 512, 512, 1), (1, 28, 28, 128, 256, 2), (1, 28, 28, 128, 128, 1),
+    (3, 14, 14, 256, 512, 2), (1, 56, 56, 64, 64, 1)]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("case", SMALL_CASES)
+def test_conv_small(gpu, case, dtype):
+    """Small-M implicit GEMM (conv_small.hip, forced): one wave per 16 px x 64 ch over the whole K with the
+    igemm's 32-deep MFMA order and epilogue arithmetic, so bias + residual, border-class bias + PReLU and ReLU
+    all equal tile 0 bit for bit; a shape it cannot take is refused, never silently run elsewhere."""
+    B, H, W, Cin, Cout, st = case
+    g = torch.Generator().manual_seed(B + H + Cin + Cout + st + 7)
+    x = torch.randn(B, H, W, Cin, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    slope = torch.rand(Cout, generator=g) * 0.5
+    Ho = (H + 2 - 3) // st + 1
+    res = torch.randn(B, Ho, Ho, Cout, generator=g).to(TORCH_DT[dtype]).to(gpu)
+    kw = dict(stride=(st, st), pad=(1, 1), dtype=dtype)
+    y = conv_op(x, w, bias=bias, res=res, tile=N.FR_TILE_SMALL, **kw)
+    _close(y, conv_ref(x, w, bias=bias, res=res, **kw), tol=1e-2 if dtype == "bf16" else 2e-3)
+    assert torch.equal(y, conv_op(x, w, bias=bias, res=res, tile=0, **kw))
+    b9 = torch.randn(9, Cout, generator=g) * 0.1
+    y = conv_op(x, w, act=2, slope=slope, bias9=b9, tile=N.FR_TILE_SMALL, **kw)
+    assert torch.equal(y, conv_op(x, w, act=2, slope=slope, bias9=b9, tile=0, **kw))
+    y = conv_op(x, w, bias=bias, act=1, tile=N.FR_TILE_SMALL, **kw)
+    assert torch.equal(y, conv_op(x, w, bias=bias, act=1, tile=0, **kw))
+    with pytest.raises(RuntimeError, match="small"):  # Cout % 64 != 0
+        conv_op(x, torch.randn(32, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_SMALL, dtype=dtype)
+
+
+BLAS_CASES = [
+    # B, H, W, Cin, Cout, act, residual   (IRV1 / ResNet-50 1x1 shapes, smaller batches)
+    (4, 8, 8, 896, 256, 1, False), (4, 8, 8, 256, 896, 1, True), (2, 17, 17, 256, 96, 1, False),
+    (2, 3, 3, 1792, 384, 0, False), (2, 28, 28, 512, 128, 1, False), (2, 14, 14, 256, 1024, 1, True)]
+
+
+@pytest.mark.parametrize("case", BLAS_CASES)
+def test_conv_blas(gpu, case):
+    """1x1 convs as hipBLASLt GEMMs (blas.cpp, forced): the library's bias + ReLU epilogue and the residual as
+    beta * C, against the fp32 reference (only the f32 summation order differs from the implicit GEMM)."""
+    B, H, W, Cin, Cout, act, with_res = case
+    g = torch.Generator().manual_seed(B + H + Cin + Cout)
+    x = torch.randn(B, H, W, Cin, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(Cout, Cin, 1, 1, generator=g) / np.sqrt(Cin)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    res = torch.randn(B, H, W, Cout, generator=g).to(torch.bfloat16).to(gpu) if with_res else None
+    y = conv_op(x, w, bias=bias, act=act, res=res, tile=N.FR_TILE_BLAS)
+    _close(y, conv_ref(x, w, bias=bias, act=act, res=res))
+    y0 = conv_op(x, w, bias=bias, act=act, res=res, tile=0)
+    assert float((y.float() - y0.float()).abs().max()) <= 2e-2 * float(y0.float().abs().max())
+    with pytest.raises(RuntimeError, match="library GEMM"):  # a 3x3 conv is not a plain GEMM
+        conv_op(x, torch.randn(Cout, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_BLAS)

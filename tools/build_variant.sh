@@ -10,7 +10,8 @@ C=$S/facerecognition_amd/csrc
 B=$R/facerecognition_amd/csrc/build_$N
 mkdir -p $B $R/facerecognition_amd/lib/variants
 objs=""
-for s in conv_igemm.hip conv_fp8.hip conv_band.hip conv_stage.hip conv_stage8.hip conv_split_stage.hip conv_wring.hip conv_direct.hip conv_img.hip conv_rows.hip conv_stem.hip misc.hip match.hip match_x3.hip preprocess.hip mtcnn.hip blas.cpp engine.cpp; do
+for s in conv_igemm.hip conv_fp8.hip conv_band.hip conv_stage.hip conv_stage8.hip conv_split_stage.hip conv_wring.hip conv_direct.hip conv_small.hip conv_img.hip conv_rows.hip conv_stem.hip misc.hip match.hip match_x3.hip preprocess.hip mtcnn.hip blas.cpp engine.cpp; do
+  [ -f $C/$s ] || continue  # an older checkout (SRC_ROOT) may predate a source
   o=$B/${s%.*}.o; objs="$objs $o"
   x=""; [ "${s##*.}" = cpp ] && x="-x hip"
   [ "$s" = conv_rows.hip ] && x="-mllvm -amdgpu-mfma-vgpr-form"
