@@ -1,0 +1,233 @@
+// LDS-resident Inception-ResNet blocks (CDNA4 / gfx950): FaceNet IRV1's Block35 (17x17), Block17 (8x8) and
+// Block8 (3x3) as one launch each (reference: facenet_model.py:28-36 -> facenet-pytorch InceptionResnetV1).
+// Per conv the per-conv path writes the branch tensors to HBM and reads them back, and the 32-128-channel
+// branch convs are small GEMMs that leave most of the chip idle (profiles/r03_final_irv1_layer_profile.txt:
+// Block35 75 us, Block17 65 us, 11-18 % of the bf16 peak).  Here one workgroup owns G images (G = 1 for
+// Block35 / Block17) and runs the block's convs as a short program: the block input is read from global
+// memory, every branch intermediate (the concatenation and the second-stage tensors) stays in LDS, and only
+// the block output goes back to HBM.  The weights stream from L2 (one XCD's 32 CUs share them).
+//
+// A conv is an implicit GEMM over the workgroup's pixels: 8 waves take units of MF pixel fragments x NF
+// 16-channel fragments; per 32-deep K-step a unit loads MF activation fragments (ds_read_b128 from LDS, or a
+// buffer load from the block input) and NF weight fragments (buffer loads, PF steps ahead) and issues MF*NF
+// v_mfma_f32_16x16x32.  Convs of one program step are independent (Block35's two 3x3 branches) and share the
+// waves; a barrier separates the steps.  LDS rows are the workgroup's pixels, ld % 32 == 16 elements so the 16
+// consecutive pixels of a fragment hit 16 distinct 16-byte bank groups; out-of-image taps read a zeroed
+// 64-byte area.  Per output the MFMA chain runs over k in order and the epilogue is conv_igemm's (acc + bias,
+// + residual, activation), so every conv equals conv_igemm tile 0 bit for bit (the padded K-steps beyond
+// K, which add 0 * 0, are skipped).
+#include "kernels.h"
+
+#include <hip/hip_ext.h>
+
+namespace fr {
+namespace {
+
+constexpr int WAVES = 8;
+constexpr int PF = 2;  // K-steps of operand loads in flight per unit
+constexpr uint32_t OOB = 0x80000000u;
+
+__device__ __forceinline__ uint4 lds_read16(const char* lds, uint32_t byte) {
+    return *(const uint4*)(lds + byte);
+}
+
+template <bool F16, int MF, int NF, bool GSRC>
+__device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& c, int mu, int nu, char* lds,
+                                           uint32_t zoff, int lane, int npx, int img0) {
+    typedef Num<F16> T;
+    typedef typename T::frag frag;
+    const int g = lane >> 4;
+    const int HW = p.H * p.W;
+    int orow[MF], oh[MF], ow[MF];
+    bool pv[MF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+        const int q = 16 * (mu * MF + i) + (lane & 15);
+        pv[i] = q < npx;
+        const int qq = pv[i] ? q : 0;
+        const int im = qq / HW, r = qq - im * HW;
+        oh[i] = r / p.W;
+        ow[i] = r - oh[i] * p.W;
+        orow[i] = im * HW;  // the pixel's image base row
+    }
+    const int K = c.kh * c.kw * c.Cin;
+    const int nks = (K + 31) / 32;
+    const int n0 = nu * NF * 16;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)c.w, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)c.Npad * c.Kpad * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.x + (size_t)img0 * HW * p.Cx), 0, (uint32_t)min((size_t)0x7fffffff, (size_t)npx * p.Cx * 2),
+        0x00020000);
+    const uint32_t wbase = (uint32_t)(((n0 + (lane & 15)) * c.Kpad + 8 * g) * 2);
+    const int ld = GSRC ? p.Cx : p.ld;
+    const int cbase = c.src_off + 8 * g;
+
+    frag wa[PF][NF], xb[PF][MF];
+    // the next K-step to load, as (kernel row, kernel column, channel) counters
+    int lr = 0, lt = 0, lc = 0;
+    auto load_step = [&](int s, int slot) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+            const int ih = oh[i] + lr - c.ph, iw = ow[i] + lt - c.pw;
+            const bool ok = pv[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            const int row = orow[i] + ih * p.W + iw;
+            if (GSRC) {
+                const uint32_t off = ok ? (uint32_t)((row * ld + cbase + lc) * 2) : OOB;
+                xb[slot][i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+            } else {
+                const uint32_t off = ok ? (uint32_t)((row * ld + cbase + lc) * 2) : zoff + 16u * g;
+                xb[slot][i] = __builtin_bit_cast(frag, lds_read16(lds, off));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+            wa[slot][j] = __builtin_bit_cast(
+                frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wbase + (uint32_t)(j * 16 * c.Kpad * 2), (uint32_t)(s * 64), 0));
+        lc += 32;
+        if (lc == c.Cin) {
+            lc = 0;
+            if (++lt == c.kw) { lt = 0; ++lr; }
+        }
+    };
+    f32x4_t acc[MF][NF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+        if (q < nks) load_step(q, q);
+    for (int s0 = 0; s0 < nks; s0 += PF) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+            const int s = s0 + q;
+            if (s >= nks) break;
+#pragma unroll
+            for (int i = 0; i < MF; ++i)
+#pragma unroll
+                for (int j = 0; j < NF; ++j) acc[i][j] = T::mfma(wa[q][j], xb[q][i], acc[i][j]);
+            if (s + PF < nks) load_step(s + PF, q);
+        }
+    }
+    // epilogue (conv_igemm's arithmetic): lane holds channels n .. n + 3 of fragment j for pixel q of fragment i
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+        if (!pv[i]) continue;
+        const int q = 16 * (mu * MF + i) + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            const int n = n0 + 16 * j + 4 * g;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + (c.bias ? c.bias[n + e] : 0.f);
+            if (c.res) {
+                const uint2 r = *(const uint2*)(p.x + ((size_t)img0 * HW + q) * p.Cx + c.res_off + n);
+                float f[8];
+                T::unpack8(make_uint4(r.x, r.y, 0u, 0u), f);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += f[e];
+            }
+            if (c.act == 1) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+            } else if (c.act == 2) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * c.slope[n + e];
+            }
+            float o8[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
+            const uint4 pk = T::pack8(o8);
+            if (c.dst_lds)
+                *(uint2*)(lds + (size_t)(q * p.ld + c.dst_off + n) * 2) = make_uint2(pk.x, pk.y);
+            else
+                *(uint2*)(p.y + ((size_t)img0 * HW + q) * p.Cy + c.dst_off + n) = make_uint2(pk.x, pk.y);
+        }
+    }
+}
+
+template <bool F16, bool GSRC>
+__device__ __forceinline__ void block_unit_shape(const BlockArgs& p, const BlockConv& c, int mu, int nu, char* lds,
+                                                 uint32_t zoff, int lane, int npx, int img0) {
+    switch (c.mf * 8 + c.nf) {
+        case 8 + 1: block_unit<F16, 1, 1, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        case 8 + 2: block_unit<F16, 1, 2, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        case 8 + 4: block_unit<F16, 1, 4, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        case 16 + 1: block_unit<F16, 2, 1, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        case 16 + 2: block_unit<F16, 2, 2, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        case 16 + 4: block_unit<F16, 2, 4, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        case 32 + 1: block_unit<F16, 4, 1, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        case 32 + 2: block_unit<F16, 4, 2, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        default: block_unit<F16, 4, 4, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+    }
+}
+
+template <bool F16>
+__global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int img0 = blockIdx.x * p.G;
+    const int G = min(p.G, p.B - img0);
+    const int npx = G * p.H * p.W, n_mf = (npx + 15) / 16;
+    const uint32_t zoff = (uint32_t)npx * p.ld * 2;  // 64 zero bytes after the pixel rows
+    if (threadIdx.x < 16) *(uint32_t*)(lds + zoff + 4 * threadIdx.x) = 0u;
+    __syncthreads();
+    for (int st = 0; st < p.nstep; ++st) {
+        int base = 0;  // the step's units, numbered across its convs; unit u goes to wave u % WAVES
+        for (int ci = 0; ci < p.nconv; ++ci) {
+            const BlockConv& c = p.c[ci];
+            if (c.step != st) continue;
+            const int mus = (n_mf + c.mf - 1) / c.mf, nus = c.Cout / (16 * c.nf), n = mus * nus;
+            for (int u = (wave - base % WAVES + WAVES) % WAVES; u < n; u += WAVES) {
+                const int mu = u % mus, nu = u / mus;
+                if (c.src_lds)
+                    block_unit_shape<F16, false>(p, c, mu, nu, lds, zoff, lane, npx, img0);
+                else
+                    block_unit_shape<F16, true>(p, c, mu, nu, lds, zoff, lane, npx, img0);
+            }
+            base += n;
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+size_t block_lds_bytes(int G, int H, int W, int ld) { return (size_t)G * H * W * ld * 2 + 64; }
+
+bool block_supported(const BlockArgs& a) {
+    if (a.nconv < 1 || a.nconv > FR_BLOCK_MAX_CONVS || a.nstep < 1 || a.G < 1 || a.B < 1 || a.ld % 32 != 16 ||
+        a.Cx % 4 != 0 || a.Cy % 4 != 0 || block_lds_bytes(a.G, a.H, a.W, a.ld) > 160 * 1024)
+        return false;
+    for (int i = 0; i < a.nconv; ++i) {
+        const BlockConv& c = a.c[i];
+        const int nfr = c.Cout / 16;
+        if (c.Cin % 32 != 0 || c.Cout % 16 != 0 || c.Kpad % 32 != 0 || c.Kpad < c.kh * c.kw * c.Cin ||
+            c.Npad < c.Cout || c.step < 0 || c.step >= a.nstep || (c.mf != 1 && c.mf != 2 && c.mf != 4) ||
+            (c.nf != 1 && c.nf != 2 && c.nf != 4) || nfr % c.nf != 0 || c.src_off % 8 != 0 || c.dst_off % 4 != 0 ||
+            (c.act == 2 && !c.slope) || c.act < 0 || c.act > 2)
+            return false;
+        if (c.src_lds ? c.src_off + c.Cin > a.ld : c.src_off + c.Cin > a.Cx) return false;
+        if (c.dst_lds ? c.dst_off + c.Cout > a.ld : c.dst_off + c.Cout > a.Cy) return false;
+        if (c.res && (c.res_off % 4 != 0 || c.res_off + c.Cout > a.Cx)) return false;
+    }
+    return true;
+}
+
+hipError_t launch_block(const BlockArgs& a, hipStream_t s) {
+    if (!block_supported(a)) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((a.B + a.G - 1) / a.G));
+    const size_t lds = block_lds_bytes(a.G, a.H, a.W, a.ld);
+    auto k = a.f16 ? block_kernel<true> : block_kernel<false>;
+    static bool attr[2] = {false, false};
+    if (!attr[a.f16 ? 1 : 0]) {
+        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr[a.f16 ? 1 : 0] = true;
+    }
+    if (a.ev0)
+        hipExtLaunchKernelGGL(k, grid, dim3(WAVES * 64), lds, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);
+    else
+        hipLaunchKernelGGL(k, grid, dim3(WAVES * 64), lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace fr
