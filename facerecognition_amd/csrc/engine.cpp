@@ -1353,10 +1353,13 @@ static int fit_split(const fr_handle* h, const ConvArgs& a, int split) {
 
 // The fixed policy (no measurement: FR_AUTOTUNE=0, a forced FR_CONV_TILE): the specialised kernels where they
 // apply (each measured faster than the implicit GEMM at bs = 256), else conv_plan's cost-model tile and split.
+// hipBLASLt (FR_TILE_BLAS) is an autotuner candidate only with FR_BLAS=1: its f32 summation order differs from
+// the implicit GEMM's, so with it an embedding could depend on the batch it was computed in (the kernel choice
+// is per batch size); every default candidate accumulates K in the igemm order.
 static bool blas_enabled() {
     static const bool on = [] {
-        const char* e = getenv("FR_NO_BLAS");
-        return !(e && e[0] == '1');
+        const char* e = getenv("FR_BLAS");
+        return e && e[0] == '1';
     }();
     return on;
 }
