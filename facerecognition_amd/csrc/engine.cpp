@@ -1353,9 +1353,8 @@ static int fit_split(const fr_handle* h, const ConvArgs& a, int split) {
 
 // The fixed policy (no measurement: FR_AUTOTUNE=0, a forced FR_CONV_TILE): the specialised kernels where they
 // apply (each measured faster than the implicit GEMM at bs = 256), else conv_plan's cost-model tile and split.
-// hipBLASLt (FR_TILE_BLAS) is an autotuner candidate only with FR_BLAS=1: its f32 summation order differs from
-// the implicit GEMM's, so with it an embedding could depend on the batch it was computed in (the kernel choice
-// is per batch size); every default candidate accumulates K in the igemm order.
+// hipBLASLt (FR_TILE_BLAS) is an autotuner candidate only with FR_BLAS=1 (not yet measured faster on a whole
+// forward; its f32 summation order differs from the implicit GEMM's in every conv it takes).
 static bool blas_enabled() {
     static const bool on = [] {
         const char* e = getenv("FR_BLAS");

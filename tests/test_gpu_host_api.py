@@ -98,7 +98,11 @@ def test_recognize_batch_end_to_end(gold, r50, names_db):
     assert [r["identity"] for r in res[:8]] == [str(n) for n in gold["best_name"]]
     assert res[8]["status"] == "error" and res[8]["embedding"] is None
     single = eng.recognize(imgs[2])
-    assert single["identity"] == res[2]["identity"] and abs(single["confidence"] - res[2]["confidence"]) < 1e-6
+    # bs = 1 and bs = 9 run the kernels measured fastest at each batch size (e.g. split-K at bs = 1), whose f32
+    # summation orders differ, so the two embeddings agree to bf16 rounding, not bit for bit; both stay at the
+    # oracle bar (as the reference's own single and batched paths may differ in their last bits on a GPU)
+    assert single["identity"] == res[2]["identity"] and abs(single["confidence"] - res[2]["confidence"]) < 1e-3
+    assert _cos_dist(single["embedding"], gold["emb_single"][2]) <= COS_TOL
     assert _cos_dist(res[2]["embedding"], gold["emb_single"][2]) <= COS_TOL
     # in-place db edit is picked up by the device copy
     eng.db["zz_probe2"] = res[2]["embedding"]
