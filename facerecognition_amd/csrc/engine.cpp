@@ -2508,6 +2508,17 @@ int fr_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, i
     return FR_OK;
 }
 
+// " <fused ms> <per-conv ms>" of a stage / block measured at batch B (measure_stage), else ""
+static std::string meas_note(const fr_handle* h, int grp, int B) {
+    for (const auto& m : h->stage_meas)
+        if (m.stage == grp && m.B == B) {
+            char t[64];
+            std::snprintf(t, sizeof t, " %.4f %.4f", m.t_stage, m.t_conv);
+            return t;
+        }
+    return "";
+}
+
 int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
     if (!h || !buf || n == 0 || B <= 0) { set_error("fr_debug_plan: bad argument"); return FR_ERR_ARG; }
     std::string out;
@@ -2518,14 +2529,14 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
             const StageRec& r = h->stages[op.stage];
             const std::string K = std::to_string(9 * r.C);
             out += std::string(r.fp8 ? "stage8 " : "stage ") + std::to_string(B * r.H * r.H) + " " + std::to_string(r.C) + " " + K + " " + K + " " +
-                   std::to_string(2 * r.nblk) + " 1 3x3 " + h->tensors[r.out].name + "\n";
+                   std::to_string(2 * r.nblk) + " 1 3x3 " + h->tensors[r.out].name + meas_note(h, op.grp, B) + "\n";
             continue;
         }
         if (op.kind == OP_BLOCK) {  // M, 1, MACs per pixel (x 2 = FLOPs), -, 1 launch
             const BlockRec& r = h->blocks[op.block];
             const std::string K = std::to_string((long long)r.flops_px);
             out += "block " + std::to_string(B * r.H * r.W) + " 1 " + K + " " + K + " 1 1 " + std::to_string(r.nstep) +
-                   "step " + (h->tensors[r.out].name.empty() ? r.name : h->tensors[r.out].name) + "\n";
+                   "step " + (h->tensors[r.out].name.empty() ? r.name : h->tensors[r.out].name) + meas_note(h, op.grp, B) + "\n";
             continue;
         }
         if (op.kind != OP_CONV && op.kind != OP_HEAD) {

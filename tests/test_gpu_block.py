@@ -65,6 +65,11 @@ def test_irv1_blocks_equal_member_convs(gpu, B):
     m.set_option(N.FR_OPT_STAGE, 2)          # blocks always on
     x = torch.from_numpy(synthetic_crops(B, 160, seed=11))
     e_blk = m.embed(x).cpu().numpy()
+    import ctypes
+    buf = ctypes.create_string_buffer(1 << 16)
+    N.check(N.lib().fr_debug_plan(m.handle, B, buf, len(buf)), "fr_debug_plan")
+    plan = buf.value.decode().splitlines()
+    assert sum(l.startswith("block ") for l in plan) == 21, "the 21 blocks did not all run as conv_block launches"
     M = "model."
     pairs = [("conv2d_4b", "repeat_1.0"), ("repeat_1.3", "repeat_1.4"), ("mixed_6a", "repeat_2.0"),
              ("repeat_2.8", "repeat_2.9"), ("mixed_7a", "repeat_3.0"), ("repeat_3.4", "block8")]

@@ -43,33 +43,44 @@ def main():
     from facerecognition_amd import face_detector as FD
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--detect-iters", type=int, default=3)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     img = frame()
     fd = FD.FaceDetector(mtcnn_state=FD.synth_mtcnn_state(7))
     m = fd.mtcnn if hasattr(fd, "mtcnn") else fd.detector
-    bgr = np.ascontiguousarray(img[..., ::-1])
-    fd.detect(bgr)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.iters):
-        det = fd.detect(bgr)
-    torch.cuda.synchronize()
-    t_detect = (time.perf_counter() - t0) / a.iters * 1e3
     H, W = img.shape[:2]
     scales = FD.pyramid_scales(H, W)
+    # the device nets first (each line printed as it completes: detect() below can be slow with synthetic
+    # weights, whose near-random scores pass many boxes through the host NMS)
     dev_img = torch.as_tensor(img[None]).cuda()
     hs, ws = int(H * scales[0] + 1), int(W * scales[0] + 1)
     x0 = m.resample(dev_img, np.array([[0, 0, 0, H, W]]), hs, ws)
     t_pnet0 = timed(lambda: m.pnet(x0), a.iters)
+    print(f"pnet level 0 {hs}x{ws}: {t_pnet0:.3f} ms", flush=True)
     t_pyr = timed(lambda: [m.pnet(m.resample(dev_img, np.array([[0, 0, 0, H, W]]), int(H * s + 1), int(W * s + 1)))
                            for s in scales], max(3, a.iters // 4))
+    print(f"pnet all {len(scales)} levels + resample: {t_pyr:.3f} ms", flush=True)
     xr = torch.randn(256, 24, 24, 3, device="cuda")
     xo = torch.randn(256, 48, 48, 3, device="cuda")
     t_rnet = timed(lambda: m.rnet(xr), a.iters)
     t_onet = timed(lambda: m.onet(xo), a.iters)
+    print(f"rnet 256 crops: {t_rnet:.3f} ms, onet 256 crops: {t_onet:.3f} ms", flush=True)
+    bgr = np.ascontiguousarray(img[..., ::-1])
+    t = time.perf_counter()
+    fd.detect(bgr)
+    torch.cuda.synchronize()
+    print(f"detect (first call): {(time.perf_counter() - t) * 1e3:.1f} ms", flush=True)
+    t_each = []
+    for _ in range(a.detect_iters):
+        t = time.perf_counter()
+        det = fd.detect(bgr)
+        torch.cuda.synchronize()
+        t_each.append((time.perf_counter() - t) * 1e3)
+        print(f"detect: {t_each[-1]:.1f} ms", flush=True)
+    t_detect = float(np.median(t_each))
     res = {"frame": f"{W}x{H} synthetic RGB u8", "weights": "synthetic (synth_mtcnn_state(7))",
-           "pyramid_levels": len(scales), "detect_ms": round(t_detect, 3),
+           "pyramid_levels": len(scales), "detect_ms_median": round(t_detect, 3), "detect_iters": a.detect_iters,
            "detected": det is not None, "pnet_level0_ms": round(t_pnet0, 3), "pnet_level0_shape": [hs, ws],
            "pnet_all_levels_with_resample_ms": round(t_pyr, 3), "rnet_256_crops_ms": round(t_rnet, 3),
            "onet_256_crops_ms": round(t_onet, 3)}
