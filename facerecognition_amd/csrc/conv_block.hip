@@ -9,7 +9,7 @@
 //
 // A conv is an implicit GEMM over the workgroup's pixels: 8 waves take units of MF pixel fragments x NF
 // 16-channel fragments; per 32-deep K-step a unit loads MF activation fragments (ds_read_b128 from LDS, or a
-// buffer load from the block input) and NF weight fragments (buffer loads, PF steps ahead) and issues MF*NF
+// buffer load from the block input) and NF weight fragments (buffer loads, D steps ahead) and issues MF*NF
 // v_mfma_f32_16x16x32.  Convs of one program step are independent (Block35's two 3x3 branches) and share the
 // waves; a barrier separates the steps.  LDS rows are the workgroup's pixels, ld % 32 == 16 elements so the 16
 // consecutive pixels of a fragment hit 16 distinct 16-byte bank groups; out-of-image taps read a zeroed
@@ -24,7 +24,6 @@ namespace fr {
 namespace {
 
 constexpr int WAVES = 8;
-constexpr int PF = 2;  // K-steps of operand loads in flight per unit
 constexpr uint32_t OOB = 0x80000000u;
 
 __device__ __forceinline__ uint4 lds_read16(const char* lds, uint32_t byte) {
@@ -38,51 +37,65 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
     typedef typename T::frag frag;
     const int g = lane >> 4;
     const int HW = p.H * p.W;
-    int orow[MF], oh[MF], ow[MF];
-    bool pv[MF];
-#pragma unroll
-    for (int i = 0; i < MF; ++i) {
-        const int q = 16 * (mu * MF + i) + (lane & 15);
-        pv[i] = q < npx;
-        const int qq = pv[i] ? q : 0;
-        const int im = qq / HW, r = qq - im * HW;
-        oh[i] = r / p.W;
-        ow[i] = r - oh[i] * p.W;
-        orow[i] = im * HW;  // the pixel's image base row
-    }
     const int K = c.kh * c.kw * c.Cin;
     const int nks = (K + 31) / 32;
     const int n0 = nu * NF * 16;
+    const int ld = GSRC ? p.Cx : p.ld;
+    // per pixel fragment: the lane's pixel byte offset (tap (ph, pw), channel 8 g) and a mask of the taps that
+    // land inside its image (0 for a pixel past the workgroup's last), so a K-step costs a scalar tap offset plus
+    // a bit test per fragment
+    uint32_t base[MF], vmask[MF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+        const int q = 16 * (mu * MF + i) + (lane & 15);
+        const bool pv = q < npx;
+        const int qq = pv ? q : 0;
+        const int im = qq / HW, r = qq - im * HW;
+        const int oh = r / p.W, ow = r - oh * p.W;
+        base[i] = (uint32_t)((qq * ld + c.src_off + 8 * g) * 2);
+        uint32_t m = 0;
+        for (int tr = 0; tr < c.kh; ++tr)
+            for (int tc = 0; tc < c.kw; ++tc) {
+                const int ih = oh + tr - c.ph, iw = ow + tc - c.pw;
+                if (pv && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) m |= 1u << (tr * c.kw + tc);
+            }
+        vmask[i] = m;
+    }
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)c.w, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)c.Npad * c.Kpad * 2), 0x00020000);
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.x + (size_t)img0 * HW * p.Cx), 0, (uint32_t)min((size_t)0x7fffffff, (size_t)npx * p.Cx * 2),
         0x00020000);
     const uint32_t wbase = (uint32_t)(((n0 + (lane & 15)) * c.Kpad + 8 * g) * 2);
-    const int ld = GSRC ? p.Cx : p.ld;
-    const int cbase = c.src_off + 8 * g;
+    const uint32_t zaddr = zoff + 16u * g;
 
-    frag wa[PF][NF], xb[PF][MF];
-    // the next K-step to load, as (kernel row, kernel column, channel) counters
+    // Operand ring of D K-steps.  The steady-state loop issues the loads of step s + D right after the MFMAs of
+    // step s, unconditionally (steps past the end read zeros: an out-of-range buffer offset / the LDS zero
+    // area), so the loop body has no branch and the compiler waits for exactly the loads each step consumes.
+    constexpr int D = MF * NF <= 8 ? 4 : 2;
+    frag wa[D][NF], xb[D][MF];
+    // the next K-step to load, as (kernel row, kernel column, channel) counters (wave-uniform)
     int lr = 0, lt = 0, lc = 0;
     auto load_step = [&](int s, int slot) {
+        const bool live = s < nks;
+        const int tap = live ? lr * c.kw + lt : 31;  // bit 31 is never set (kh * kw <= 31)
+        const int soff = (((lr - c.ph) * p.W + (lt - c.pw)) * ld + lc) * 2;
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
-            const int ih = oh[i] + lr - c.ph, iw = ow[i] + lt - c.pw;
-            const bool ok = pv[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-            const int row = orow[i] + ih * p.W + iw;
+            const bool ok = (vmask[i] >> tap) & 1u;
             if (GSRC) {
-                const uint32_t off = ok ? (uint32_t)((row * ld + cbase + lc) * 2) : OOB;
+                const uint32_t off = ok ? base[i] + (uint32_t)soff : OOB;
                 xb[slot][i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
             } else {
-                const uint32_t off = ok ? (uint32_t)((row * ld + cbase + lc) * 2) : zoff + 16u * g;
+                const uint32_t off = ok ? base[i] + (uint32_t)soff : zaddr;
                 xb[slot][i] = __builtin_bit_cast(frag, lds_read16(lds, off));
             }
         }
+        const uint32_t so = live ? (uint32_t)(s * 64) : OOB;
 #pragma unroll
         for (int j = 0; j < NF; ++j)
             wa[slot][j] = __builtin_bit_cast(
-                frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wbase + (uint32_t)(j * 16 * c.Kpad * 2), (uint32_t)(s * 64), 0));
+                frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wbase + (uint32_t)(j * 16 * c.Kpad * 2), so, 0));
         lc += 32;
         if (lc == c.Cin) {
             lc = 0;
@@ -94,26 +107,30 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
     for (int i = 0; i < MF; ++i)
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    auto mfmas = [&](int q) {
 #pragma unroll
-    for (int q = 0; q < PF; ++q)
-        if (q < nks) load_step(q, q);
-    for (int s0 = 0; s0 < nks; s0 += PF) {
+        for (int i = 0; i < MF; ++i)
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-            const int s = s0 + q;
-            if (s >= nks) break;
+            for (int j = 0; j < NF; ++j) acc[i][j] = T::mfma(wa[q][j], xb[q][i], acc[i][j]);
+    };
 #pragma unroll
-            for (int i = 0; i < MF; ++i)
+    for (int q = 0; q < D; ++q) load_step(q, q);
+    int s0 = 0;
+    for (; s0 + D <= nks; s0 += D) {
 #pragma unroll
-                for (int j = 0; j < NF; ++j) acc[i][j] = T::mfma(wa[q][j], xb[q][i], acc[i][j]);
-            if (s + PF < nks) load_step(s + PF, q);
+        for (int q = 0; q < D; ++q) {
+            mfmas(q);
+            load_step(s0 + q + D, q);
         }
     }
+#pragma unroll
+    for (int q = 0; q < D - 1; ++q)
+        if (s0 + q < nks) mfmas(q);
     // epilogue (conv_igemm's arithmetic): lane holds channels n .. n + 3 of fragment j for pixel q of fragment i
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
-        if (!pv[i]) continue;
         const int q = 16 * (mu * MF + i) + (lane & 15);
+        if (q >= npx) continue;
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
             const int n = n0 + 16 * j + 4 * g;
@@ -200,7 +217,7 @@ bool block_supported(const BlockArgs& a) {
     for (int i = 0; i < a.nconv; ++i) {
         const BlockConv& c = a.c[i];
         const int nfr = c.Cout / 16;
-        if (c.Cin % 32 != 0 || c.Cout % 16 != 0 || c.Kpad % 32 != 0 || c.Kpad < c.kh * c.kw * c.Cin ||
+        if (c.Cin % 32 != 0 || c.Cout % 16 != 0 || c.kh * c.kw > 31 || c.Kpad % 32 != 0 || c.Kpad < c.kh * c.kw * c.Cin ||
             c.Npad < c.Cout || c.step < 0 || c.step >= a.nstep || (c.mf != 1 && c.mf != 2 && c.mf != 4) ||
             (c.nf != 1 && c.nf != 2 && c.nf != 4) || nfr % c.nf != 0 || c.src_off % 8 != 0 || c.dst_off % 4 != 0 ||
             (c.act == 2 && !c.slope) || c.act < 0 || c.act > 2)
