@@ -50,47 +50,63 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
     const uint32_t x2base = (mv && p.x2)
                                 ? (uint32_t)((((mb * p.H2 + oh * p.st2) * p.W2 + ow * p.st2) * p.Cx2 + p.x2_off + 8 * g) * 2)
                                 : OOB;
+    // the lane's pixel at tap (0, 0) and the mask of the taps inside the image (0 past M), so a K-step costs a
+    // scalar tap offset plus a bit test (a 32-deep step lies inside one tap: Cin % 32 == 0)
+    const uint32_t xbase = (uint32_t)((((mb * p.H + ih0) * p.W + iw0) * p.Cx + p.x_off + 8 * g) * 2);
+    uint32_t vmask = 0;
+    for (int r = 0; r < p.Kh; ++r)
+        for (int t = 0; t < p.Kw; ++t)
+            if (mv && (unsigned)(ih0 + r) < (unsigned)p.H && (unsigned)(iw0 + t) < (unsigned)p.W) vmask |= 1u << (r * p.Kw + t);
 
-    // operand offsets of K-step s (k0 = 32 s): a 32-deep step lies inside one tap (Cin % 32 == 0)
-    auto xoff = [&](int s) -> uint32_t {
-        const int k0 = 32 * s;
-        if (k0 >= K1) {  // projection K-steps (or the zero padding past K)
-            const int c = k0 - K1;
-            return (p.x2 && c < p.C2 && x2base != OOB) ? x2base + (uint32_t)(c * 2) : OOB;
-        }
-        const int tap = k0 / p.Cin, c0 = k0 - tap * p.Cin;
-        const int r = tap / p.Kw, t = tap - r * p.Kw;
-        const int ih = ih0 + r, iw = iw0 + t;
-        if (!mv || (unsigned)ih >= (unsigned)p.H || (unsigned)iw >= (unsigned)p.W) return OOB;
-        return (uint32_t)((((mb * p.H + ih) * p.W + iw) * p.Cx + p.x_off + c0 + 8 * g) * 2);
-    };
+    // Operand ring of PF K-steps: the steady-state loop issues the loads of step s + PF right after the MFMAs of
+    // step s, unconditionally (steps past the end read zeros by out-of-range offsets), so the loop body has no
+    // branch around a load and the compiler waits for exactly the loads each step consumes.
     frag wa[PF][NFR], xb[PF];
+    int lr = 0, lt = 0, lc = 0;  // the next main-conv K-step as (kernel row, kernel column, channel), wave-uniform
     auto load_step = [&](int s, int slot) {
-        const bool proj = 32 * s >= K1;
-        const uint32_t xo = xoff(s);
+        const int k0 = 32 * s;
+        const bool proj = k0 >= K1;  // projection K-steps (or the zero padding past K)
+        uint32_t xo;
+        if (!proj) {
+            const int tap = lr * p.Kw + lt;
+            const int soff = ((lr * p.W + lt) * p.Cx + lc) * 2;
+            xo = ((vmask >> tap) & 1u) ? xbase + (uint32_t)soff : OOB;
+            lc += 32;
+            if (lc == p.Cin) {
+                lc = 0;
+                if (++lt == p.Kw) { lt = 0; ++lr; }
+            }
+        } else {
+            const int c = k0 - K1;
+            xo = (s < nks && p.x2 && c < p.C2) ? x2base + (uint32_t)(c * 2) : OOB;
+        }
         xb[slot] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(proj ? x2r : xr, xo, 0, 0));
+        const uint32_t so = s < nks ? (uint32_t)(s * 64) : OOB;
 #pragma unroll
         for (int i = 0; i < NFR; ++i)
             wa[slot][i] = __builtin_bit_cast(
-                frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wbase + (uint32_t)(i * 16 * p.Kpad * 2), (uint32_t)(s * 64), 0));
+                frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wbase + (uint32_t)(i * 16 * p.Kpad * 2), so, 0));
     };
     f32x4_t acc[NFR];
 #pragma unroll
     for (int i = 0; i < NFR; ++i) acc[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    auto mfmas = [&](int q) {
 #pragma unroll
-    for (int q = 0; q < PF; ++q)
-        if (q < nks) load_step(q, q);
-    // PF steps per iteration: the ring slot of step s is s % PF, compile-time inside the unrolled body
-    for (int s0 = 0; s0 < nks; s0 += PF) {
+        for (int i = 0; i < NFR; ++i) acc[i] = T::mfma(wa[q][i], xb[q], acc[i]);
+    };
+#pragma unroll
+    for (int q = 0; q < PF; ++q) load_step(q, q);
+    int s0 = 0;
+    for (; s0 + PF <= nks; s0 += PF) {
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
-            const int s = s0 + q;
-            if (s >= nks) break;
-#pragma unroll
-            for (int i = 0; i < NFR; ++i) acc[i] = T::mfma(wa[q][i], xb[q], acc[i]);
-            if (s + PF < nks) load_step(s + PF, q);
+            mfmas(q);
+            load_step(s0 + q + PF, q);
         }
     }
+#pragma unroll
+    for (int q = 0; q < PF - 1; ++q)
+        if (s0 + q < nks) mfmas(q);
     if (!mv) return;
     // epilogue (conv_igemm's arithmetic): lane holds channels n .. n + 3 of fragment i of pixel m
 #pragma unroll
@@ -129,7 +145,7 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
 
 bool small_supported(const ConvArgs& a) {
     const bool kcat = a.x2 != nullptr;
-    return a.B > 0 && a.M > 0 && a.Cin % 32 == 0 && a.Cout % 64 == 0 && a.Npad >= a.Cout && a.Kpad % 32 == 0 &&
+    return a.B > 0 && a.M > 0 && a.Cin % 32 == 0 && a.Kh * a.Kw <= 32 && a.Cout % 64 == 0 && a.Npad >= a.Cout && a.Kpad % 32 == 0 &&
            a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.Cy % 4 == 0 && a.y_off % 4 == 0 && !a.y2 && !a.partial && !a.w8 &&
            !a.y_amax && (!a.res || (a.Cres % 4 == 0 && a.res_off % 4 == 0)) &&
            (kcat ? (a.C2 % 32 == 0 && a.Cx2 % 8 == 0 && a.x2_off % 8 == 0 && a.K1 == a.Kh * a.Kw * a.Cin &&
