@@ -20,6 +20,10 @@
 
 #include <hip/hip_ext.h>
 
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 namespace fr {
 namespace {
 
@@ -113,6 +117,25 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
 #pragma unroll
             for (int j = 0; j < NF; ++j) acc[i][j] = T::mfma(wa[q][j], xb[q][i], acc[i][j]);
     };
+    // the epilogue's global operands (bias, residual), loaded before the K loop: issued after the block's output
+    // stores they could alias, each would be a full memory round trip per fragment
+    float4 bz[NF];
+    uint2 rz[MF][NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+        const int n = n0 + 16 * j + 4 * g;
+        bz[j] = c.bias ? *(const float4*)(c.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (c.res) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+            const int q = 16 * (mu * MF + i) + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+                rz[i][j] = q < npx ? *(const uint2*)(p.x + ((size_t)img0 * HW + q) * p.Cx + c.res_off + n0 + 16 * j + 4 * g)
+                                   : make_uint2(0u, 0u);
+        }
+    }
 #pragma unroll
     for (int q = 0; q < D; ++q) load_step(q, q);
     int s0 = 0;
@@ -134,13 +157,10 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
             const int n = n0 + 16 * j + 4 * g;
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + (c.bias ? c.bias[n + e] : 0.f);
+            float v[4] = {acc[i][j][0] + bz[j].x, acc[i][j][1] + bz[j].y, acc[i][j][2] + bz[j].z, acc[i][j][3] + bz[j].w};
             if (c.res) {
-                const uint2 r = *(const uint2*)(p.x + ((size_t)img0 * HW + q) * p.Cx + c.res_off + n);
                 float f[8];
-                T::unpack8(make_uint4(r.x, r.y, 0u, 0u), f);
+                T::unpack8(make_uint4(rz[i][j].x, rz[i][j].y, 0u, 0u), f);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] += f[e];
             }
@@ -186,6 +206,15 @@ __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
     const int npx = G * p.H * p.W, n_mf = (npx + 15) / 16;
     const uint32_t zoff = (uint32_t)npx * p.ld * 2;  // 64 zero bytes after the pixel rows
     if (threadIdx.x < 16) *(uint32_t*)(lds + zoff + 4 * threadIdx.x) = 0u;
+    int ns = 0;  // timing stamps (FR_BLOCK_STAMPS): [wave][64][2] = (clock, code) of workgroup 0, lane 0 stores
+    auto stamp = [&](unsigned long long code) {
+        if (p.stamps && blockIdx.x == 0 && lane == 0 && ns < 64) {
+            p.stamps[(wave * 64 + ns) * 2] = __builtin_amdgcn_s_memtime();
+            p.stamps[(wave * 64 + ns) * 2 + 1] = code;
+            ++ns;
+        }
+    };
+    stamp(0);
     __syncthreads();
     for (int st = 0; st < p.nstep; ++st) {
         int base = 0;  // the step's units, numbered across its convs; unit u goes to wave u % WAVES
@@ -195,6 +224,7 @@ __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
             const int mus = (n_mf + c.mf - 1) / c.mf, nus = c.Cout / (16 * c.nf), n = mus * nus;
             for (int u = (wave - base % WAVES + WAVES) % WAVES; u < n; u += WAVES) {
                 const int mu = u % mus, nu = u / mus;
+                stamp(1000 + 100 * ci + u);
                 if (c.src_lds)
                     block_unit_shape<F16, false>(p, c, mu, nu, lds, zoff, lane, npx, img0);
                 else
@@ -202,7 +232,9 @@ __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
             }
             base += n;
         }
+        stamp(10 + st);
         __syncthreads();
+        stamp(20 + st);
     }
 }
 
@@ -239,6 +271,27 @@ hipError_t launch_block(const BlockArgs& a, hipStream_t s) {
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr[a.f16 ? 1 : 0] = true;
+    }
+    static const bool stamps = getenv("FR_BLOCK_STAMPS") != nullptr;  // timing experiment: print WG 0's stamps
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (stamps && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+        static unsigned long long* buf = nullptr;
+        if (!buf && hipMalloc(&buf, WAVES * 64 * 2 * 8) != hipSuccess) return hipErrorOutOfMemory;
+        (void)hipMemsetAsync(buf, 0, WAVES * 64 * 2 * 8, s);
+        BlockArgs b = a;
+        b.stamps = buf;
+        hipLaunchKernelGGL(k, grid, dim3(WAVES * 64), lds, s, b);
+        std::vector<unsigned long long> h(WAVES * 64 * 2);
+        (void)hipMemcpyAsync(h.data(), buf, h.size() * 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        const unsigned long long t0 = h[0];
+        for (int w = 0; w < WAVES; ++w) {
+            fprintf(stderr, "block H%d w%d:", a.H, w);
+            for (int i = 0; i < 64 && h[(w * 64 + i) * 2]; ++i)
+                fprintf(stderr, " %llu@%llu", h[(w * 64 + i) * 2 + 1], h[(w * 64 + i) * 2] - t0);
+            fprintf(stderr, "\n");
+        }
+        return hipGetLastError();
     }
     if (a.ev0)
         hipExtLaunchKernelGGL(k, grid, dim3(WAVES * 64), lds, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);

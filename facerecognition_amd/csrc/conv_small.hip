@@ -94,6 +94,21 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
 #pragma unroll
         for (int i = 0; i < NFR; ++i) acc[i] = T::mfma(wa[q][i], xb[q], acc[i]);
     };
+    // the epilogue's global operands (bias, residual), loaded before the K loop: issued after the output stores
+    // they could alias, each would be a full memory round trip per fragment
+    float4 bz[NFR], b9z[NFR], sz[NFR];
+    uint2 rz[NFR];
+    const int bcls = border_class(oh, ow, p.Ho, p.Wo);
+#pragma unroll
+    for (int i = 0; i < NFR; ++i) {
+        const int n = n0 + 16 * i + 4 * g;
+        const bool nv = n < p.Cout;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        bz[i] = (p.bias && !p.bias9 && nv) ? *(const float4*)(p.bias + n) : z;
+        b9z[i] = (p.bias9 && nv) ? *(const float4*)(p.bias9 + (size_t)bcls * p.Npad + n) : z;
+        sz[i] = (p.act == 2 && nv) ? *(const float4*)(p.slope + n) : z;
+        rz[i] = (p.res && mv && nv) ? *(const uint2*)(p.res + (size_t)m * p.Cres + p.res_off + n) : make_uint2(0u, 0u);
+    }
 #pragma unroll
     for (int q = 0; q < PF; ++q) load_step(q, q);
     int s0 = 0;
@@ -113,18 +128,13 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
     for (int i = 0; i < NFR; ++i) {
         const int n = n0 + 16 * i + 4 * g;
         if (n >= p.Cout) continue;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][e] + ((p.bias && !p.bias9) ? p.bias[n + e] : 0.f);
+        float v[4] = {acc[i][0] + bz[i].x, acc[i][1] + bz[i].y, acc[i][2] + bz[i].z, acc[i][3] + bz[i].w};
         if (p.bias9) {
-            const float* bb = p.bias9 + (size_t)border_class(oh, ow, p.Ho, p.Wo) * p.Npad + n;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += bb[e];
+            v[0] += b9z[i].x; v[1] += b9z[i].y; v[2] += b9z[i].z; v[3] += b9z[i].w;
         }
         if (p.res) {
-            const uint2 r = *(const uint2*)(p.res + (size_t)m * p.Cres + p.res_off + n);
             float f[8];
-            T::unpack8(make_uint4(r.x, r.y, 0u, 0u), f);
+            T::unpack8(make_uint4(rz[i].x, rz[i].y, 0u, 0u), f);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += f[e];
         }
@@ -133,7 +143,7 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
             for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
         } else if (p.act == 2) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * p.slope[n + e];
+            for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * (&sz[i].x)[e];
         }
         float o8[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
         const uint4 pk = F16 && p.y_bf16 ? Num<false>::pack8(o8) : T::pack8(o8);
