@@ -30,13 +30,18 @@ namespace {
 constexpr int WAVES = 8;
 constexpr uint32_t OOB = 0x80000000u;
 
-__device__ __forceinline__ uint4 lds_read16(const char* lds, uint32_t byte) {
-    return *(const uint4*)(lds + byte);
+typedef __attribute__((address_space(3))) char lds_char;
+
+typedef unsigned int u32x4_v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u32x4_v lds_read16(const lds_char* lds, uint32_t byte) {
+    return *(const __attribute__((address_space(3))) u32x4_v*)(lds + byte);
 }
 
 template <bool F16, int MF, int NF, bool GSRC>
-__device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& c, int mu, int nu, char* lds,
-                                           uint32_t zoff, int lane, int npx, int img0) {
+__device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& c, int mu, int nu, lds_char* lds,
+                                           uint32_t zoff, uint32_t ptab, int lane, int npx, int img0) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
     const int g = lane >> 4;
@@ -45,25 +50,25 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
     const int nks = (K + 31) / 32;
     const int n0 = nu * NF * 16;
     const int ld = GSRC ? p.Cx : p.ld;
-    // per pixel fragment: the lane's pixel byte offset (tap (ph, pw), channel 8 g) and a mask of the taps that
-    // land inside its image (0 for a pixel past the workgroup's last), so a K-step costs a scalar tap offset plus
-    // a bit test per fragment
+    // per pixel fragment: the lane's pixel byte offset (channel 8 g) and a mask of the taps that land inside its
+    // image (0 for a pixel past the workgroup's last), so a K-step costs the step table's scalar tap offset plus
+    // a bit test per fragment.  The pixel's (row, column) comes from the workgroup's LDS table.
     uint32_t base[MF], vmask[MF];
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
         const int q = 16 * (mu * MF + i) + (lane & 15);
         const bool pv = q < npx;
         const int qq = pv ? q : 0;
-        const int im = qq / HW, r = qq - im * HW;
-        const int oh = r / p.W, ow = r - oh * p.W;
+        const uint32_t pc = *(const __attribute__((address_space(3))) uint32_t*)(lds + ptab + 4 * qq);
+        const int oh = pc & 0xffff, ow = pc >> 16;
         base[i] = (uint32_t)((qq * ld + c.src_off + 8 * g) * 2);
+        // taps (tr, tc) inside the image: tr in [r0, r1], tc in [c0, c1]
+        const int r0 = max(0, c.ph - oh), r1 = min(c.kh - 1, p.H - 1 + c.ph - oh);
+        const int c0 = max(0, c.pw - ow), c1 = min(c.kw - 1, p.W - 1 + c.pw - ow);
+        const uint32_t cols = c1 >= c0 ? (2u << c1) - (1u << c0) : 0u;
         uint32_t m = 0;
-        for (int tr = 0; tr < c.kh; ++tr)
-            for (int tc = 0; tc < c.kw; ++tc) {
-                const int ih = oh + tr - c.ph, iw = ow + tc - c.pw;
-                if (pv && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) m |= 1u << (tr * c.kw + tc);
-            }
-        vmask[i] = m;
+        for (int tr = 0; tr < c.kh; ++tr) m |= (tr >= r0 && tr <= r1) ? cols << (tr * c.kw) : 0u;
+        vmask[i] = pv ? m : 0u;
     }
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)c.w, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)c.Npad * c.Kpad * 2), 0x00020000);
@@ -78,20 +83,19 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
     // area), so the loop body has no branch and the compiler waits for exactly the loads each step consumes.
     constexpr int D = MF * NF <= 8 ? 4 : 2;
     frag wa[D][NF], xb[D][MF];
-    // the next K-step to load, as (kernel row, kernel column, channel) counters (wave-uniform)
-    int lr = 0, lt = 0, lc = 0;
     auto load_step = [&](int s, int slot) {
         const bool live = s < nks;
-        const int tap = live ? lr * c.kw + lt : 31;  // bit 31 is never set (kh * kw <= 31)
-        const int soff = (((lr - c.ph) * p.W + (lt - c.pw)) * ld + lc) * 2;
+        const int2 st = c.steps[s];  // {tap offset, tap} (tap 31 past the end: no mask bit), wave-uniform
+        const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane(st.x);
+        const uint32_t bit = 1u << __builtin_amdgcn_readfirstlane(st.y);
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
-            const bool ok = (vmask[i] >> tap) & 1u;
+            const bool ok = (vmask[i] & bit) != 0u;
             if (GSRC) {
-                const uint32_t off = ok ? base[i] + (uint32_t)soff : OOB;
+                const uint32_t off = ok ? base[i] + toff : OOB;
                 xb[slot][i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
             } else {
-                const uint32_t off = ok ? base[i] + (uint32_t)soff : zaddr;
+                const uint32_t off = ok ? base[i] + toff : zaddr;
                 xb[slot][i] = __builtin_bit_cast(frag, lds_read16(lds, off));
             }
         }
@@ -100,11 +104,6 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
         for (int j = 0; j < NF; ++j)
             wa[slot][j] = __builtin_bit_cast(
                 frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wbase + (uint32_t)(j * 16 * c.Kpad * 2), so, 0));
-        lc += 32;
-        if (lc == c.Cin) {
-            lc = 0;
-            if (++lt == c.kw) { lt = 0; ++lr; }
-        }
     };
     f32x4_t acc[MF][NF];
 #pragma unroll
@@ -174,7 +173,7 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
             float o8[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
             const uint4 pk = T::pack8(o8);
             if (c.dst_lds)
-                *(uint2*)(lds + (size_t)(q * p.ld + c.dst_off + n) * 2) = make_uint2(pk.x, pk.y);
+                *(__attribute__((address_space(3))) u32x2_v*)(lds + (q * p.ld + c.dst_off + n) * 2) = (u32x2_v){pk.x, pk.y};
             else
                 *(uint2*)(p.y + ((size_t)img0 * HW + q) * p.Cy + c.dst_off + n) = make_uint2(pk.x, pk.y);
         }
@@ -182,30 +181,36 @@ __device__ __forceinline__ void block_unit(const BlockArgs& p, const BlockConv& 
 }
 
 template <bool F16, bool GSRC>
-__device__ __forceinline__ void block_unit_shape(const BlockArgs& p, const BlockConv& c, int mu, int nu, char* lds,
-                                                 uint32_t zoff, int lane, int npx, int img0) {
+__device__ __forceinline__ void block_unit_shape(const BlockArgs& p, const BlockConv& c, int mu, int nu, lds_char* lds,
+                                                 uint32_t zoff, uint32_t ptab, int lane, int npx, int img0) {
     switch (c.mf * 8 + c.nf) {
-        case 8 + 1: block_unit<F16, 1, 1, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
-        case 8 + 2: block_unit<F16, 1, 2, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
-        case 8 + 4: block_unit<F16, 1, 4, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
-        case 16 + 1: block_unit<F16, 2, 1, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
-        case 16 + 2: block_unit<F16, 2, 2, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
-        case 16 + 4: block_unit<F16, 2, 4, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
-        case 32 + 1: block_unit<F16, 4, 1, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
-        case 32 + 2: block_unit<F16, 4, 2, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
-        default: block_unit<F16, 4, 4, GSRC>(p, c, mu, nu, lds, zoff, lane, npx, img0); break;
+        case 8 + 1: block_unit<F16, 1, 1, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
+        case 8 + 2: block_unit<F16, 1, 2, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
+        case 8 + 4: block_unit<F16, 1, 4, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
+        case 16 + 1: block_unit<F16, 2, 1, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
+        case 16 + 2: block_unit<F16, 2, 2, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
+        case 16 + 4: block_unit<F16, 2, 4, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
+        case 32 + 1: block_unit<F16, 4, 1, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
+        case 32 + 2: block_unit<F16, 4, 2, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
+        default: block_unit<F16, 4, 4, GSRC>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0); break;
     }
 }
 
 template <bool F16>
 __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
+    extern __shared__ __attribute__((aligned(16))) char lds_generic[];
+    lds_char* lds = (lds_char*)lds_generic;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int img0 = blockIdx.x * p.G;
     const int G = min(p.G, p.B - img0);
     const int npx = G * p.H * p.W, n_mf = (npx + 15) / 16;
     const uint32_t zoff = (uint32_t)npx * p.ld * 2;  // 64 zero bytes after the pixel rows
-    if (threadIdx.x < 16) *(uint32_t*)(lds + zoff + 4 * threadIdx.x) = 0u;
+    if (threadIdx.x < 16) *(__attribute__((address_space(3))) uint32_t*)(lds + zoff + 4 * threadIdx.x) = 0u;
+    const uint32_t ptab = zoff + 64;  // per pixel: row | column << 16
+    for (int q = threadIdx.x; q < npx; q += WAVES * 64) {
+        const int r = q % (p.H * p.W), oh = r / p.W;
+        *(__attribute__((address_space(3))) uint32_t*)(lds + ptab + 4 * q) = (uint32_t)oh | (uint32_t)(r - oh * p.W) << 16;
+    }
     int ns = 0;  // timing stamps (FR_BLOCK_STAMPS): [wave][64][2] = (clock, code) of workgroup 0, lane 0 stores
     auto stamp = [&](unsigned long long code) {
         if (p.stamps && blockIdx.x == 0 && lane == 0 && ns < 64) {
@@ -226,9 +231,9 @@ __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
                 const int mu = u % mus, nu = u / mus;
                 stamp(1000 + 100 * ci + u);
                 if (c.src_lds)
-                    block_unit_shape<F16, false>(p, c, mu, nu, lds, zoff, lane, npx, img0);
+                    block_unit_shape<F16, false>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0);
                 else
-                    block_unit_shape<F16, true>(p, c, mu, nu, lds, zoff, lane, npx, img0);
+                    block_unit_shape<F16, true>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0);
             }
             base += n;
         }
@@ -240,7 +245,7 @@ __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
 
 }  // namespace
 
-size_t block_lds_bytes(int G, int H, int W, int ld) { return (size_t)G * H * W * ld * 2 + 64; }
+size_t block_lds_bytes(int G, int H, int W, int ld) { return (size_t)G * H * W * (ld * 2 + 4) + 64; }
 
 bool block_supported(const BlockArgs& a) {
     if (a.nconv < 1 || a.nconv > FR_BLOCK_MAX_CONVS || a.nstep < 1 || a.G < 1 || a.B < 1 || a.ld % 32 != 16 ||
@@ -250,7 +255,7 @@ bool block_supported(const BlockArgs& a) {
         const BlockConv& c = a.c[i];
         const int nfr = c.Cout / 16;
         if (c.Cin % 32 != 0 || c.Cout % 16 != 0 || c.kh * c.kw > 31 || c.Kpad % 32 != 0 || c.Kpad < c.kh * c.kw * c.Cin ||
-            c.Npad < c.Cout || c.step < 0 || c.step >= a.nstep || (c.mf != 1 && c.mf != 2 && c.mf != 4) ||
+            c.Npad < c.Cout || !c.steps || c.step < 0 || c.step >= a.nstep || (c.mf != 1 && c.mf != 2 && c.mf != 4) ||
             (c.nf != 1 && c.nf != 2 && c.nf != 4) || nfr % c.nf != 0 || c.src_off % 8 != 0 || c.dst_off % 4 != 0 ||
             (c.act == 2 && !c.slope) || c.act < 0 || c.act > 2)
             return false;

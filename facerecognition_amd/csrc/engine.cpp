@@ -400,6 +400,19 @@ static void plan_block(fr_handle* h, int bo, int x, int y, const std::string& na
         c.res_off = op.res_off;
         c.step = st;
         block_unit_shape(n_mf, cw.Cout / 16, cw.K / 32, cw.K, cw.Cout, &c.mf, &c.nf);
+        {  // K-step table: the tap and channel block's byte offset from the pixel, the tap index (31 past the end)
+            const int ld = c.src_lds ? r.ld : h->tensors[x].C;
+            std::vector<int2> tab;
+            const int nks = cw.K / 32;
+            for (int s2 = 0; s2 < nks + 4; ++s2) {
+                if (s2 >= nks || op.cin % 32) { tab.push_back(make_int2(0, 31)); continue; }
+                const int k0 = 32 * s2, tap = k0 / op.cin, cc = k0 - tap * op.cin, tr = tap / op.kw, tc = tap - tr * op.kw;
+                tab.push_back(make_int2((((tr - op.ph) * r.W + (tc - op.pw)) * ld + cc) * 2, tap));
+            }
+            int2* dev = nullptr;
+            if (upload(h, &dev, tab)) return;
+            c.steps = dev;
+        }
         r.conv.push_back(c);
         r.flops_px += (double)cw.Cout * cw.K;
     }

@@ -166,6 +166,8 @@ struct BlockConv {
     int res, res_off;          // add block-input channels [res_off, + Cout) before the activation
     int step;                  // program step (a barrier after each); convs of one step are independent
     int mf, nf;                // unit shape: pixel fragments (1, 2, 4) x 16-channel fragments (1, 2, 4)
+    const int2* steps;         // per K-step (+ 4 past the end): {source byte offset of the tap and channel
+                               //   block relative to the pixel, tap index (31 past the end)}
 };
 struct BlockArgs {
     const bf16_t* x; int Cx;   // block input [B][H][W][Cx]
