@@ -10,6 +10,10 @@
 // ConvArgs::x2) continues the K loop.  Per output the 32-deep MFMA chain runs over k in order and the epilogue
 // is conv_igemm's (acc + bias, + the border-class bias, + residual, activation), so the result equals
 // conv_igemm tile 0 bit for bit: an autotuner candidate (FR_TILE_SMALL) that changes nothing numerically.
+// KS = 4 / 8 (the candidate's split): KS waves share one tile, each over a contiguous K chunk, and sum their
+// partials through LDS in wave order before the epilogue (deterministic, but the f32 summation order of a
+// split-K plan): at bs = 1 a 3x3 256->256 conv has 52 tiles, and one wave walking K = 2304 alone waits on
+// 72 steps of weight loads.
 #include "kernels.h"
 
 #include <hip/hip_ext.h>
@@ -21,12 +25,12 @@ constexpr int NFR = 4;   // 16-channel fragments per wave (64 output channels)
 constexpr int PF = 4;    // K-steps of loads in flight
 constexpr uint32_t OOB = 0x80000000u;
 
-template <bool F16>
-__global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, int n_units) {
+template <bool F16, int KS>
+__global__ __launch_bounds__(KS == 1 ? 256 : 64 * KS) void conv_small_kernel(ConvArgs p, int n_mf, int n_units) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
-    const int lane = threadIdx.x & 63;
-    const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave-uniform
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int unit = KS == 1 ? blockIdx.x * 4 + wv : blockIdx.x;  // KS > 1: one tile per workgroup
     if (unit >= n_units) return;
     const int mf = unit % n_mf, ng = unit / n_mf;  // pixel fragment, 64-channel group
     const int n0 = ng * 16 * NFR;
@@ -45,7 +49,10 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)p.w, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)p.Npad * p.Kpad * 2), 0x00020000);
     const int K1 = p.x2 ? p.K1 : p.K;          // the conv's own K; the projection K-steps follow
-    const int nks = p.Kpad / 32;
+    const int nks_all = p.Kpad / 32;
+    // this wave's K chunk [s_beg, s_end) (all of K for KS = 1)
+    const int s_beg = KS == 1 ? 0 : nks_all * wv / KS, s_end = KS == 1 ? nks_all : nks_all * (wv + 1) / KS;
+    const int nks = s_end - s_beg;
     const uint32_t wbase = (uint32_t)(((n0 + (lane & 15)) * p.Kpad + 8 * g) * 2);
     const uint32_t x2base = (mv && p.x2)
                                 ? (uint32_t)((((mb * p.H2 + oh * p.st2) * p.W2 + ow * p.st2) * p.Cx2 + p.x2_off + 8 * g) * 2)
@@ -62,8 +69,11 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
     // step s, unconditionally (steps past the end read zeros by out-of-range offsets), so the loop body has no
     // branch around a load and the compiler waits for exactly the loads each step consumes.
     frag wa[PF][NFR], xb[PF];
-    int lr = 0, lt = 0, lc = 0;  // the next main-conv K-step as (kernel row, kernel column, channel), wave-uniform
-    auto load_step = [&](int s, int slot) {
+    // the next main-conv K-step as (kernel row, kernel column, channel), wave-uniform
+    int lc = (32 * s_beg) % p.Cin, lt = (32 * s_beg) / p.Cin, lr = lt / p.Kw;
+    lt -= lr * p.Kw;
+    auto load_step = [&](int si, int slot) {  // si: the step's index inside the chunk
+        const int s = s_beg + si;
         const int k0 = 32 * s;
         const bool proj = k0 >= K1;  // projection K-steps (or the zero padding past K)
         uint32_t xo;
@@ -78,10 +88,11 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
             }
         } else {
             const int c = k0 - K1;
-            xo = (s < nks && p.x2 && c < p.C2) ? x2base + (uint32_t)(c * 2) : OOB;
+            xo = (s < s_end && p.x2 && c < p.C2) ? x2base + (uint32_t)(c * 2) : OOB;
         }
+        if (s >= s_end) xo = OOB;
         xb[slot] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(proj ? x2r : xr, xo, 0, 0));
-        const uint32_t so = s < nks ? (uint32_t)(s * 64) : OOB;
+        const uint32_t so = s < s_end ? (uint32_t)(s * 64) : OOB;
 #pragma unroll
         for (int i = 0; i < NFR; ++i)
             wa[slot][i] = __builtin_bit_cast(
@@ -102,7 +113,7 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
 #pragma unroll
     for (int i = 0; i < NFR; ++i) {
         const int n = n0 + 16 * i + 4 * g;
-        const bool nv = n < p.Cout;
+        const bool nv = n < p.Cout && (KS == 1 || i == wv);  // KS > 1: wave i runs fragment i's epilogue
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         bz[i] = (p.bias && !p.bias9 && nv) ? *(const float4*)(p.bias + n) : z;
         b9z[i] = (p.bias9 && nv) ? *(const float4*)(p.bias9 + (size_t)bcls * p.Npad + n) : z;
@@ -122,12 +133,27 @@ __global__ __launch_bounds__(256) void conv_small_kernel(ConvArgs p, int n_mf, i
 #pragma unroll
     for (int q = 0; q < PF - 1; ++q)
         if (s0 + q < nks) mfmas(q);
+    if (KS > 1) {  // partials through LDS, summed in wave order by wave i for fragment i
+        __shared__ f32x4_t part[KS > 1 ? KS : 1][NFR][64];
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) part[wv][i][lane] = acc[i];
+        __syncthreads();
+        if (wv >= NFR) return;
+#pragma unroll
+        for (int i = 0; i < NFR; ++i)
+            if (i == wv) {
+                f32x4_t t = part[0][i][lane];
+#pragma unroll
+                for (int k = 1; k < KS; ++k) t += part[k][i][lane];
+                acc[i] = t;
+            }
+    }
     if (!mv) return;
     // epilogue (conv_igemm's arithmetic): lane holds channels n .. n + 3 of fragment i of pixel m
 #pragma unroll
     for (int i = 0; i < NFR; ++i) {
         const int n = n0 + 16 * i + 4 * g;
-        if (n >= p.Cout) continue;
+        if (n >= p.Cout || (KS > 1 && i != wv)) continue;
         float v[4] = {acc[i][0] + bz[i].x, acc[i][1] + bz[i].y, acc[i][2] + bz[i].z, acc[i][3] + bz[i].w};
         if (p.bias9) {
             v[0] += b9z[i].x; v[1] += b9z[i].y; v[2] += b9z[i].z; v[3] += b9z[i].w;
@@ -164,15 +190,17 @@ bool small_supported(const ConvArgs& a) {
            (!a.y_bf16 || (a.f16 && !a.res));
 }
 
-hipError_t launch_conv_small(const ConvArgs& a, hipStream_t s) {
-    if (!small_supported(a)) return hipErrorInvalidValue;
+hipError_t launch_conv_small(const ConvArgs& a, int ks, hipStream_t s) {
+    if (!small_supported(a) || (ks != 1 && ks != 4 && ks != 8)) return hipErrorInvalidValue;
     const int n_mf = (a.M + 15) / 16, n_units = n_mf * (a.Cout / 64);
-    const dim3 grid((unsigned)((n_units + 3) / 4));
-    auto k = a.f16 ? conv_small_kernel<true> : conv_small_kernel<false>;
+    const dim3 grid((unsigned)(ks == 1 ? (n_units + 3) / 4 : n_units)), block(ks == 1 ? 256 : 64 * ks);
+    auto k = ks == 1 ? (a.f16 ? conv_small_kernel<true, 1> : conv_small_kernel<false, 1>)
+           : ks == 4 ? (a.f16 ? conv_small_kernel<true, 4> : conv_small_kernel<false, 4>)
+                     : (a.f16 ? conv_small_kernel<true, 8> : conv_small_kernel<false, 8>);
     if (a.ev0)
-        hipExtLaunchKernelGGL(k, grid, dim3(256), 0, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, n_mf, n_units);
+        hipExtLaunchKernelGGL(k, grid, block, 0, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, n_mf, n_units);
     else
-        hipLaunchKernelGGL(k, grid, dim3(256), 0, s, a, n_mf, n_units);
+        hipLaunchKernelGGL(k, grid, block, 0, s, a, n_mf, n_units);
     return hipGetLastError();
 }
 

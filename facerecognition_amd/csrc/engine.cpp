@@ -1395,7 +1395,7 @@ static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, 
         case FR_TILE_BLAS:
             if (!h->blas) h->blas = blas_create();
             return launch_conv_blas(h->blas, a, s);
-        case FR_TILE_SMALL: return launch_conv_small(a, s);
+        case FR_TILE_SMALL: return launch_conv_small(a, c.split, s);
         case FR_TILE_ROWS: {
             ConvArgs r = a;
             r.wimg = a.wrows_;
@@ -1469,7 +1469,9 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     if (direct_enabled() && direct_supported(a)) add(TILE_DIRECT, 1);  // small-K direct conv
     if (blas_enabled() && blas_supported(a)) add(FR_TILE_BLAS, 1);       // 1x1 conv as a library GEMM
     // small M (a few hundred pixels: small batches): one wave per 16 px x 64 ch, no LDS, no second launch
-    if (a.M <= 8192 && small_supported(a)) add(FR_TILE_SMALL, 1);
+    // (split 4 / 8: that many waves share a tile's K, summed through LDS)
+    if (a.M <= 8192 && small_supported(a))
+        for (int ks : {1, 4, 8}) add(FR_TILE_SMALL, ks);
     {
         int tile, split;
         conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
@@ -1529,7 +1531,7 @@ static bool choice_ok(const ConvArgs& a, const ConvChoice& c) {
         }
         case FR_TILE_DIRECT: return direct_supported(a);
         case FR_TILE_BLAS: return blas_enabled() && blas_supported(a);
-        case FR_TILE_SMALL: return small_supported(a);
+        case FR_TILE_SMALL: return small_supported(a) && (c.split == 1 || c.split == 4 || c.split == 8);
         default: return c.tile >= 0;
     }
 }
@@ -2870,7 +2872,7 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
     }
     if (d->tile == FR_TILE_SMALL + 1) {
         if (!small_supported(a)) { set_error("fr_op_conv2d: small-M kernel not applicable"); return FR_ERR_ARG; }
-        FR_HIP_CHECK(launch_conv_small(a, (hipStream_t)stream));
+        FR_HIP_CHECK(launch_conv_small(a, d->split_k > 1 ? d->split_k : 1, (hipStream_t)stream));
         return FR_OK;
     }
     if (d->tile == FR_TILE_BLAS + 1) {  // a per-call library state: the op API holds no handle

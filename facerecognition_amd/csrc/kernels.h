@@ -65,9 +65,10 @@ size_t rows_packed_elems(int Cout);
 hipError_t rows_pack_weights(const bf16_t* w, int Kpad, int Cout, bf16_t* out, hipStream_t s);
 hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s);
 // Small-M implicit GEMM (conv_small.hip): one wave per 16 pixels x 64 channels over the whole K, operands straight
-// from global memory (no LDS); Cin % 32 == 0, Cout % 64 == 0; equal to conv_igemm tile 0 bit for bit.
+// from global memory (no LDS); Cin % 32 == 0, Cout % 64 == 0; ks = 1: equal to conv_igemm tile 0 bit for bit;
+// ks = 4 / 8: that many waves split each tile's K and sum through LDS (a split-K summation order).
 bool small_supported(const ConvArgs& a);
-hipError_t launch_conv_small(const ConvArgs& a, hipStream_t s);
+hipError_t launch_conv_small(const ConvArgs& a, int ks, hipStream_t s);
 // 1x1 stride-1 convs as hipBLASLt GEMMs (blas.cpp): bias + ReLU epilogue, residual as beta * C.  The state (library
 // handle, 32-MiB workspace, per-conv descriptors and algorithm) lives per fr_handle.
 bool blas_supported(const ConvArgs& a);

@@ -879,6 +879,12 @@ def test_conv_small(gpu, case, dtype):
     assert torch.equal(y, conv_op(x, w, act=2, slope=slope, bias9=b9, tile=0, **kw))
     y = conv_op(x, w, bias=bias, act=1, tile=N.FR_TILE_SMALL, **kw)
     assert torch.equal(y, conv_op(x, w, bias=bias, act=1, tile=0, **kw))
+    for ks in (4, 8):  # K split over 4 / 8 waves of a workgroup, summed through LDS in wave order
+        y = conv_op(x, w, bias=bias, res=res, tile=N.FR_TILE_SMALL, split_k=ks, **kw)
+        _close(y, conv_ref(x, w, bias=bias, res=res, **kw), tol=1e-2 if dtype == "bf16" else 2e-3)
+        assert torch.equal(y, conv_op(x, w, bias=bias, res=res, tile=N.FR_TILE_SMALL, split_k=ks, **kw))
+        y = conv_op(x, w, act=2, slope=slope, bias9=b9, tile=N.FR_TILE_SMALL, split_k=ks, **kw)
+        _close(y, conv_op(x, w, act=2, slope=slope, bias9=b9, tile=0, **kw), tol=1e-2 if dtype == "bf16" else 2e-3)
     with pytest.raises(RuntimeError, match="small"):  # Cout % 64 != 0
         conv_op(x, torch.randn(32, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_SMALL, dtype=dtype)
 

@@ -58,7 +58,7 @@ def analyse(trace, plan_path):
         d = 0
         r = seq[i]; i += 1
         d += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        if split > 1 or p[0] == "head":
+        if (split > 1 and tile != 16) or p[0] == "head":  # (tile 16 = conv_small: its split is in-kernel)
             r = seq[i]; i += 1  # split-K epilogue / head finalize
             d += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         flop = 2.0 * M * Nn * K * (tile if p[0] == "stage" else 1)  # stage line: tile = its conv count
