@@ -20,10 +20,6 @@
 
 #include <hip/hip_ext.h>
 
-#include <cstdio>
-#include <cstdlib>
-#include <vector>
-
 namespace fr {
 namespace {
 
@@ -211,15 +207,6 @@ __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
         const int r = q % (p.H * p.W), oh = r / p.W;
         *(__attribute__((address_space(3))) uint32_t*)(lds + ptab + 4 * q) = (uint32_t)oh | (uint32_t)(r - oh * p.W) << 16;
     }
-    int ns = 0;  // timing stamps (FR_BLOCK_STAMPS): [wave][64][2] = (clock, code) of workgroup 0, lane 0 stores
-    auto stamp = [&](unsigned long long code) {
-        if (p.stamps && blockIdx.x == 0 && lane == 0 && ns < 64) {
-            p.stamps[(wave * 64 + ns) * 2] = __builtin_amdgcn_s_memtime();
-            p.stamps[(wave * 64 + ns) * 2 + 1] = code;
-            ++ns;
-        }
-    };
-    stamp(0);
     __syncthreads();
     for (int st = 0; st < p.nstep; ++st) {
         int base = 0;  // the step's units, numbered across its convs; unit u goes to wave u % WAVES
@@ -229,7 +216,6 @@ __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
             const int mus = (n_mf + c.mf - 1) / c.mf, nus = c.Cout / (16 * c.nf), n = mus * nus;
             for (int u = (wave - base % WAVES + WAVES) % WAVES; u < n; u += WAVES) {
                 const int mu = u % mus, nu = u / mus;
-                stamp(1000 + 100 * ci + u);
                 if (c.src_lds)
                     block_unit_shape<F16, false>(p, c, mu, nu, lds, zoff, ptab, lane, npx, img0);
                 else
@@ -237,9 +223,7 @@ __global__ __launch_bounds__(WAVES * 64) void block_kernel(BlockArgs p) {
             }
             base += n;
         }
-        stamp(10 + st);
         __syncthreads();
-        stamp(20 + st);
     }
 }
 
@@ -276,27 +260,6 @@ hipError_t launch_block(const BlockArgs& a, hipStream_t s) {
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr[a.f16 ? 1 : 0] = true;
-    }
-    static const bool stamps = getenv("FR_BLOCK_STAMPS") != nullptr;  // timing experiment: print WG 0's stamps
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (stamps && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
-        static unsigned long long* buf = nullptr;
-        if (!buf && hipMalloc(&buf, WAVES * 64 * 2 * 8) != hipSuccess) return hipErrorOutOfMemory;
-        (void)hipMemsetAsync(buf, 0, WAVES * 64 * 2 * 8, s);
-        BlockArgs b = a;
-        b.stamps = buf;
-        hipLaunchKernelGGL(k, grid, dim3(WAVES * 64), lds, s, b);
-        std::vector<unsigned long long> h(WAVES * 64 * 2);
-        (void)hipMemcpyAsync(h.data(), buf, h.size() * 8, hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
-        const unsigned long long t0 = h[0];
-        for (int w = 0; w < WAVES; ++w) {
-            fprintf(stderr, "block H%d w%d:", a.H, w);
-            for (int i = 0; i < 64 && h[(w * 64 + i) * 2]; ++i)
-                fprintf(stderr, " %llu@%llu", h[(w * 64 + i) * 2 + 1], h[(w * 64 + i) * 2] - t0);
-            fprintf(stderr, "\n");
-        }
-        return hipGetLastError();
     }
     if (a.ev0)
         hipExtLaunchKernelGGL(k, grid, dim3(WAVES * 64), lds, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);

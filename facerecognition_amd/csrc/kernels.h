@@ -178,7 +178,6 @@ struct BlockArgs {
     BlockConv c[FR_BLOCK_MAX_CONVS];
     void* ev0;
     void* ev1;
-    unsigned long long* stamps;  // timing experiments only (FR_BLOCK_STAMPS): per-wave clock stamps of workgroup 0
 };
 size_t block_lds_bytes(int G, int H, int W, int ld);
 bool block_supported(const BlockArgs& a);

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--pad", type=int, default=-1, help="default: kernel // 2")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--act", type=int, default=0)
+    ap.add_argument("--split", type=int, default=1, help="split_k (igemm partials, or conv_small's in-kernel split)")
     a = ap.parse_args()
     from tests.helpers import TORCH_DT, conv_op
     g = torch.Generator().manual_seed(0)
@@ -41,12 +42,12 @@ def main():
     res = torch.randn(a.batch, Ho, Wo, a.cout, generator=g).to(dt).cuda() if a.res else None
     y = torch.empty(a.batch, Ho, Wo, a.cout, dtype=dt, device="cuda")
     tile = None if a.tile < 0 else a.tile
-    kw = dict(stride=(a.stride, a.stride), pad=(ph, pw), bias=bias, res=res, y=y, tile=tile, dtype=a.dtype, act=a.act)
+    kw = dict(stride=(a.stride, a.stride), pad=(ph, pw), bias=bias, res=res, y=y, tile=tile, dtype=a.dtype, act=a.act, split_k=a.split)
     conv_op(x, w, timed_iters=3, **kw)
     _, ms = conv_op(x, w, timed_iters=a.iters, **kw)
     us = float(np.median(ms)) * 1e3
     flop = 2.0 * a.batch * Ho * Wo * a.cout * a.kh * a.kw * a.cin
-    print(json.dumps({"hw": a.hw, "cin": a.cin, "cout": a.cout, "k": [a.kh, a.kw], "stride": a.stride, "tile": a.tile,
+    print(json.dumps({"hw": a.hw, "cin": a.cin, "cout": a.cout, "k": [a.kh, a.kw], "stride": a.stride, "tile": a.tile, "split": a.split, "batch": a.batch,
                       "us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}))
 
 
