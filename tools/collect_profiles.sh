@@ -12,4 +12,7 @@ cp $O/pmc_traffic.json profiles/${R}_pmc_traffic.json
 grep -v "^\s*$" $O/tests.log | tail -40 > profiles/${R}_gpu_tests.txt
 grep -E "1-cos|agreement|rel err|bs=256" $O/tests.log > profiles/${R}_parity_stats.txt || true
 [ -f $O/layer_profile.txt ] && cp $O/layer_profile.txt profiles/${R}_layer_profile.txt
+[ -f $O/layer_profile_irv1.txt ] && cp $O/layer_profile_irv1.txt profiles/${R}_irv1_layer_profile.txt
+[ -f $O/layer_profile_bs1.txt ] && cp $O/layer_profile_bs1.txt profiles/${R}_bs1_layer_profile.txt
+[ -f $O/mtcnn.json ] && cp $O/mtcnn.json profiles/${R}_mtcnn.json
 echo "collected $T -> profiles/${R}_*"

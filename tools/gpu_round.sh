@@ -39,4 +39,7 @@ cd $R
 python tools/pmc_traffic.py --fetch $O/pf --write $O/pw --out $O/pmc_traffic.json
 find $O/prof -name "*kernel_stats.csv" | head -1 | xargs -r head -12
 cd $R && bash tools/gpu_layer_profile.sh ${T}_iresnet100 > $O/layer_profile.log 2>&1 && cp gpurun_out/lp_${T}_iresnet100/summary.txt $O/layer_profile.txt
+bash tools/gpu_layer_profile.sh ${T}_irv1 --arch irv1_facenet > $O/layer_profile_irv1.log 2>&1 && cp gpurun_out/lp_${T}_irv1/summary.txt $O/layer_profile_irv1.txt
+bash tools/gpu_layer_profile.sh ${T}_bs1 --batch 1 > $O/layer_profile_bs1.log 2>&1 && cp gpurun_out/lp_${T}_bs1/summary.txt $O/layer_profile_bs1.txt
+step mtcnn 300 python -u tools/mtcnn_bench.py --out $O/mtcnn.json
 echo "[$(date +%T)] done"
