@@ -401,6 +401,50 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
             *(float4*)dst = v0;
             *(float4*)(dst + 4) = v1;
         }
+        if (!p.splitk_cnt) return;
+        // In-launch split-K reduction (cdna_hip_programming.md §6 Guideline 16, counter hand-off): every slice
+        // publishes its partial tile (agent-scope release before the ticket); the slice that draws the last
+        // ticket acquires, sums the tile's partials in split order and runs the split-K epilogue's arithmetic
+        // (splitk_epilogue_kernel: the same bits), one kernel boundary per split conv fewer.
+        wait_vmn<0>();
+        __syncthreads();  // every wave's partial stores issued and waited; sE no longer read
+        volatile int* flag = (volatile int*)smem;
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            wait_vmn<0>();
+            const int t = __hip_atomic_fetch_add(p.splitk_cnt + lid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = t == (int)gridDim.y - 1;
+            if (last) {
+                __hip_atomic_store(p.splitk_cnt + lid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                wait_vmn<0>();
+            }
+            *flag = last;
+        }
+        __syncthreads();
+        if (!*flag) return;
+        float amax = 0.f;
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+            const int m = m0 + ml0 + it * RS;
+            if (m >= p.M || !nv) continue;
+            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int s2 = 0; s2 < (int)gridDim.y; ++s2) {
+                const float* src = p.partial + ((size_t)s2 * p.M + m) * p.Npad + n;
+                const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+                v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+                v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+            }
+            epilogue8<F16>(p, v, m, n);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+        }
+        if (p.y_amax) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+            if ((tid & 63) == 0)
+                atomicMax((unsigned int*)p.y_amax + blockIdx.x % max(p.amax_slots, 1), __float_as_uint(amax));
+        }
         return;
     }
     float amax = 0.f;  // max |y| of this thread's stores (fp8 consumers' dynamic activation scale)

@@ -112,6 +112,7 @@ struct BlockRec {
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 constexpr size_t FR_MAX_SPLIT_STAGES = 4;  // stage ops per plan (at most one per residual layer)
+constexpr int FR_SPLITK_TILES = 1 << 16;   // in-launch split-K tile counters per handle
 
 }  // namespace
 
@@ -128,6 +129,7 @@ struct fr_handle {
     std::vector<void*> act_allocs;
     float* partial = nullptr;
     size_t partial_floats = 0;
+    int* splitk_cnt = nullptr;  // [FR_SPLITK_TILES] in-launch split-K arrival counters (conv_igemm), zero between launches
     // gallery
     float* gallery = nullptr;
     int64_t g_rows = 0;
@@ -248,6 +250,7 @@ void free_acts(fr_handle* h) {
     for (auto& t : h->tensors) t.dev = nullptr;
     h->partial = nullptr;
     h->partial_floats = 0;
+    h->splitk_cnt = nullptr;
     h->emb_pre = nullptr;
     h->amax = nullptr;
     h->max_batch = 0;
@@ -1152,6 +1155,13 @@ int reserve(fr_handle* h, int maxB) {
     h->act_allocs.push_back(p);
     h->partial = (float*)p;
     h->partial_floats = need;
+    {
+        void* q = nullptr;
+        if ((rc = dev_alloc(&q, FR_SPLITK_TILES * sizeof(int)))) { free_acts(h); return rc; }
+        h->act_allocs.push_back(q);
+        FR_HIP_CHECK(hipMemset(q, 0, FR_SPLITK_TILES * sizeof(int)));
+        h->splitk_cnt = (int*)q;
+    }
     h->max_batch = maxB;
     if (std::any_of(h->need_amax.begin(), h->need_amax.end(), [](char c) { return c != 0; })) {
         void* q = nullptr;
@@ -1387,6 +1397,16 @@ static ConvChoice default_choice(const fr_handle* h, const ConvArgs& a) {
     return c;
 }
 
+// FR_SPLITK_EPILOGUE=1: split-K convs reduce in a second launch (splitk_epilogue_kernel) instead of in-launch
+// (A/B timing; the same bits either way).
+static bool inlaunch_splitk_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_SPLITK_EPILOGUE");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 // Launches choice c (no timing scope; run_conv_args adds it).
 static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, hipStream_t s) {
     a.split_k = 1;
@@ -1411,12 +1431,18 @@ static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, 
         default: break;
     }
     a.tile = c.tile;
+    a.splitk_cnt = nullptr;
     if (c.split > 1) {
         a.split_k = c.split;
         a.partial = h->partial;
+        // the last of each tile's split workgroups reduces in the same launch (conv_igemm.hip), where the tile
+        // counters fit; else the separate split-K epilogue launch
+        const int64_t tiles = (int64_t)((a.M + conv_tile_bm(c.tile) - 1) / conv_tile_bm(c.tile)) *
+                              ((a.Cout + conv_tile_bn(c.tile) - 1) / conv_tile_bn(c.tile));
+        if (a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && inlaunch_splitk_enabled()) a.splitk_cnt = h->splitk_cnt;
     }
     hipError_t e = launch_conv(a, s);
-    if (e == hipSuccess && c.split > 1 && a.y) e = launch_splitk_epilogue(a, s);
+    if (e == hipSuccess && c.split > 1 && a.y && !a.splitk_cnt) e = launch_splitk_epilogue(a, s);
     return e;
 }
 
@@ -1889,6 +1915,9 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
     const int f16 = h->dtype == FR_DTYPE_F16;
     const std::vector<char> stage_run = stage_plan(h, B);
     if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s_main));
+    // the split-K tile counters return to zero after every launch; re-zeroed per forward all the same, so an
+    // aborted earlier launch cannot leave a count behind
+    if (h->splitk_cnt) FR_HIP_CHECK(hipMemsetAsync(h->splitk_cnt, 0, FR_SPLITK_TILES * sizeof(int), s_main));
     h->slot_done = false;
     const bool ms = h->ms_on;
     const size_t nops = h->ops.size();

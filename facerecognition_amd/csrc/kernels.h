@@ -47,6 +47,9 @@ struct ConvArgs {
     int H2, W2, Cx2, x2_off, C2, st2, K1;
     int y_bf16;                   // f16 input / MFMA, bf16 output (igemm; the end of an f16 plan section)
     const bf16_t* wring_;         // engine: the conv's conv_wring weight image when it has one (else null)
+    // split-K (partial != null): per-tile arrival counters (zero between launches).  Non-null: the last of a tile's
+    // split workgroups sums the partials and runs the epilogue in the same launch (no launch_splitk_epilogue)
+    int* splitk_cnt;
 };
 // Implicit GEMM with the weights streamed from L2 into a register ring (conv_wring.hip): Cin % 64 == 0,
 // Cout % 256 == 0, Kpad = K (+ the K-concatenated projection) % 128 == 0; a.wimg = the packed image.
