@@ -130,6 +130,7 @@ struct fr_handle {
     float* partial = nullptr;
     size_t partial_floats = 0;
     int* splitk_cnt = nullptr;  // [FR_SPLITK_TILES] in-launch split-K arrival counters (conv_igemm), zero between launches
+    bool splitk_inlaunch = true;  // FR_OPT_SPLITK_INLAUNCH
     // gallery
     float* gallery = nullptr;
     int64_t g_rows = 0;
@@ -1397,16 +1398,6 @@ static ConvChoice default_choice(const fr_handle* h, const ConvArgs& a) {
     return c;
 }
 
-// FR_SPLITK_EPILOGUE=1: split-K convs reduce in a second launch (splitk_epilogue_kernel) instead of in-launch
-// (A/B timing; the same bits either way).
-static bool inlaunch_splitk_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_SPLITK_EPILOGUE");
-        return !(e && e[0] == '1');
-    }();
-    return on;
-}
-
 // Launches choice c (no timing scope; run_conv_args adds it).
 static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, hipStream_t s) {
     a.split_k = 1;
@@ -1439,7 +1430,7 @@ static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, 
         // counters fit; else the separate split-K epilogue launch
         const int64_t tiles = (int64_t)((a.M + conv_tile_bm(c.tile) - 1) / conv_tile_bm(c.tile)) *
                               ((a.Cout + conv_tile_bn(c.tile) - 1) / conv_tile_bn(c.tile));
-        if (a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && inlaunch_splitk_enabled()) a.splitk_cnt = h->splitk_cnt;
+        if (a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && h->splitk_inlaunch) a.splitk_cnt = h->splitk_cnt;
     }
     hipError_t e = launch_conv(a, s);
     if (e == hipSuccess && c.split > 1 && a.y && !a.splitk_cnt) e = launch_splitk_epilogue(a, s);
@@ -2118,6 +2109,7 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->dtype = dtype;
     h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
     h->stage_mode = stage_default();
+    if (const char* e = getenv("FR_SPLITK_EPILOGUE")) h->splitk_inlaunch = e[0] != '1';  // A/B timing
     if (const char* e = getenv("FR_STAGE_VARIANT")) {  // A/B timing
         const int v = atoi(e);
         h->stage_variant = v == 1 || v == 2 ? v : 0;
@@ -2642,6 +2634,7 @@ int fr_set_option(fr_handle* h, int option, int value) {
             if (value < 0 || value > 2) { set_error("fr_set_option: FR_OPT_STAGE_VARIANT is 0, 1 or 2"); return FR_ERR_ARG; }
             h->stage_variant = value;
             break;
+        case FR_OPT_SPLITK_INLAUNCH: h->splitk_inlaunch = value != 0; break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;
     }
     drop_graphs(h);  // captured replays bake in the plan
@@ -2658,6 +2651,7 @@ int fr_get_option(const fr_handle* h, int option) {
         case FR_OPT_X3_MIN_ROWS: return (int)h->x3_min_rows;
         case FR_OPT_STAGE_SPIN_LIMIT: return h->spin_limit;
         case FR_OPT_STAGE_VARIANT: return h->stage_variant;
+        case FR_OPT_SPLITK_INLAUNCH: return h->splitk_inlaunch ? 1 : 0;
         default: return FR_ERR_ARG;
     }
 }

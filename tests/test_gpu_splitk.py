@@ -1,0 +1,36 @@
+"""In-launch split-K reduction (conv_igemm.hip): the last workgroup of each tile sums the tile's partials in split
+order and runs the split-K epilogue's arithmetic, replacing the second (splitk_epilogue_kernel) launch.  Same
+bits either way: a model forward with FR_OPT_SPLITK_INLAUNCH on equals the one with it off, at the small
+batches whose plans take split-K convs (the reference's online path, recognition_engine.py:328-381)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from facerecognition_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("arch,B", [("iresnet100", 1), ("iresnet100", 3), ("resnet50_arcface", 2)])
+def test_splitk_inlaunch_equals_epilogue_launch(gpu, arch, B):
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic(arch)
+    assert m.get_option(N.FR_OPT_SPLITK_INLAUNCH) == 1
+    x = torch.from_numpy(synthetic_crops(B, m.input_size, seed=5 + B))
+    a = m.embed(x).cpu().numpy()  # tuning forward (kernel choice per conv measured at this batch size)
+    a = m.embed(x).cpu().numpy()
+    buf = ctypes.create_string_buffer(1 << 16)
+    N.check(N.lib().fr_debug_plan(m.handle, B, buf, len(buf)), "fr_debug_plan")
+    splits = [l for l in buf.value.decode().splitlines()
+              if l.startswith("conv ") and int(l.split()[6]) > 1 and int(l.split()[5]) != N.FR_TILE_SMALL]
+    m.set_option(N.FR_OPT_SPLITK_INLAUNCH, 0)
+    b = m.embed(x).cpu().numpy()
+    m.set_option(N.FR_OPT_SPLITK_INLAUNCH, 1)
+    c = m.embed(x).cpu().numpy()
+    m.close()
+    assert np.array_equal(a, b) and np.array_equal(a, c), f"max |diff| {np.abs(a - b).max():.3g}"
+    if not splits:
+        pytest.skip(f"{arch} bs={B}: the measured plan took no igemm split-K conv")
