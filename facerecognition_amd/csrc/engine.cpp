@@ -1423,17 +1423,19 @@ static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, 
     }
     a.tile = c.tile;
     a.splitk_cnt = nullptr;
-    if (c.split > 1) {
-        a.split_k = c.split;
+    const int split = c.split < 0 ? -c.split : c.split;  // negative: reduced in-launch
+    if (split > 1) {
+        a.split_k = split;
         a.partial = h->partial;
-        // the last of each tile's split workgroups reduces in the same launch (conv_igemm.hip), where the tile
-        // counters fit; else the separate split-K epilogue launch
+        // in-launch: the last of each tile's split workgroups reduces (conv_igemm.hip), where the tile counters
+        // fit; else the separate split-K epilogue launch
         const int64_t tiles = (int64_t)((a.M + conv_tile_bm(c.tile) - 1) / conv_tile_bm(c.tile)) *
                               ((a.Cout + conv_tile_bn(c.tile) - 1) / conv_tile_bn(c.tile));
-        if (a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && h->splitk_inlaunch) a.splitk_cnt = h->splitk_cnt;
+        if (c.split < 0 && a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && h->splitk_inlaunch)
+            a.splitk_cnt = h->splitk_cnt;
     }
     hipError_t e = launch_conv(a, s);
-    if (e == hipSuccess && c.split > 1 && a.y && !a.splitk_cnt) e = launch_splitk_epilogue(a, s);
+    if (e == hipSuccess && split > 1 && a.y && !a.splitk_cnt) e = launch_splitk_epilogue(a, s);
     return e;
 }
 
@@ -1451,7 +1453,8 @@ static std::string choice_class(const ConvArgs& a, const ConvChoice& c) {
         case FR_TILE_DIRECT: return "conv_direct";
         case FR_TILE_BLAS: return "blas gemm";
         case FR_TILE_SMALL: return "conv_small";
-        default: return "conv_igemm tile" + std::to_string(c.tile) + (c.split > 1 ? " splitk" : "");
+        default:
+            return "conv_igemm tile" + std::to_string(c.tile) + (c.split > 1 ? " splitk" : c.split < -1 ? " splitk-inlaunch" : "");
     }
 }
 
@@ -1493,7 +1496,10 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
         int tile, split;
         conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
         split = fit_split(h, a, split);
-        if (split > 1) add(tile, split);
+        if (split > 1) {
+            add(tile, split);
+            if (h->splitk_inlaunch) add(tile, -split);  // the same split reduced in-launch (negative split)
+        }
     }
     hipEvent_t e0, e1;
     FR_HIP_CHECK(hipEventCreate(&e0));

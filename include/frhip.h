@@ -304,9 +304,10 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * discarded per row), 2: the 13-fragment layout at one wave per SIMD (each weight fragment loaded once per
  * CU).  All give the same bits (A/B and regression tests). */
 #define FR_OPT_STAGE_VARIANT 7
-/* FR_OPT_SPLITK_INLAUNCH (default 1; env FR_SPLITK_EPILOGUE=1 starts at 0): a split-K implicit-GEMM conv reduces
- * its partials in the same launch (the last workgroup of each tile sums them in split order), 0 = a second
- * launch does.  The same bits either way. */
+/* FR_OPT_SPLITK_INLAUNCH (default 1; env FR_SPLITK_EPILOGUE=1 starts at 0): a split-K implicit-GEMM conv may reduce
+ * its partials in the same launch (the last workgroup of each tile sums them in split order) where the
+ * per-shape tuning measured that faster than a second launch; 0 = always the second launch.  The same bits
+ * either way.  fr_debug_plan prints an in-launch split as a negative split count. */
 #define FR_OPT_SPLITK_INLAUNCH 8
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);

@@ -25,7 +25,7 @@ def test_splitk_inlaunch_equals_epilogue_launch(gpu, arch, B):
     buf = ctypes.create_string_buffer(1 << 16)
     N.check(N.lib().fr_debug_plan(m.handle, B, buf, len(buf)), "fr_debug_plan")
     splits = [l for l in buf.value.decode().splitlines()
-              if l.startswith("conv ") and int(l.split()[6]) > 1 and int(l.split()[5]) != N.FR_TILE_SMALL]
+              if l.startswith("conv ") and abs(int(l.split()[6])) > 1 and int(l.split()[5]) != N.FR_TILE_SMALL]
     m.set_option(N.FR_OPT_SPLITK_INLAUNCH, 0)
     b = m.embed(x).cpu().numpy()
     m.set_option(N.FR_OPT_SPLITK_INLAUNCH, 1)
@@ -34,3 +34,4 @@ def test_splitk_inlaunch_equals_epilogue_launch(gpu, arch, B):
     assert np.array_equal(a, b) and np.array_equal(a, c), f"max |diff| {np.abs(a - b).max():.3g}"
     if not splits:
         pytest.skip(f"{arch} bs={B}: the measured plan took no igemm split-K conv")
+    print(f"{arch} bs={B}: {len(splits)} split-K convs, {sum(int(l.split()[6]) < 0 for l in splits)} reduced in-launch")
