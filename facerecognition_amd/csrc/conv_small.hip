@@ -10,10 +10,14 @@
 // ConvArgs::x2) continues the K loop.  Per output the 32-deep MFMA chain runs over k in order and the epilogue
 // is conv_igemm's (acc + bias, + the border-class bias, + residual, activation), so the result equals
 // conv_igemm tile 0 bit for bit: an autotuner candidate (FR_TILE_SMALL) that changes nothing numerically.
-// KS = 4 / 8 (the candidate's split): KS waves share one tile, each over a contiguous K chunk, and sum their
+// KS = 4 / 8 / 16 (the candidate's split): KS waves share one tile, each over a contiguous K chunk, and sum their
 // partials through LDS in wave order before the epilogue (deterministic, but the f32 summation order of a
 // split-K plan): at bs = 1 a 3x3 256->256 conv has 52 tiles, and one wave walking K = 2304 alone waits on
 // 72 steps of weight loads.
+// NF = 4 / 2 / 1: 16-channel fragments per tile (64 / 32 / 16 output channels).  A narrower tile spreads a small
+// conv over more CUs: at bs = 1 layer3's 52 tiles of 64 channels used 52 of 256 CUs, each pulling its whole 64 x K
+// weight slab and 16 x K patch through one CU's L2 port (~290 KB, 2+ us); 16-channel tiles are 208 workgroups of
+// ~150 KB each.  The narrower tiles keep PF = 8 steps of loads in flight (their ring is smaller).
 #include "kernels.h"
 
 #include <hip/hip_ext.h>
@@ -21,12 +25,11 @@
 namespace fr {
 namespace {
 
-constexpr int NFR = 4;   // 16-channel fragments per wave (64 output channels)
-constexpr int PF = 4;    // K-steps of loads in flight
 constexpr uint32_t OOB = 0x80000000u;
 
-template <bool F16, int KS>
+template <bool F16, int KS, int NFR>
 __global__ __launch_bounds__(KS == 1 ? 256 : 64 * KS) void conv_small_kernel(ConvArgs p, int n_mf, int n_units) {
+    constexpr int PF = NFR == 4 ? 4 : 8;  // K-steps of loads in flight
     typedef Num<F16> T;
     typedef typename T::frag frag;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -179,9 +182,10 @@ __global__ __launch_bounds__(KS == 1 ? 256 : 64 * KS) void conv_small_kernel(Con
 
 }  // namespace
 
-bool small_supported(const ConvArgs& a) {
+bool small_supported(const ConvArgs& a, int nf) {
     const bool kcat = a.x2 != nullptr;
-    return a.B > 0 && a.M > 0 && a.Cin % 32 == 0 && a.Kh * a.Kw <= 32 && a.Cout % 64 == 0 && a.Npad >= a.Cout && a.Kpad % 32 == 0 &&
+    return a.B > 0 && a.M > 0 && a.Cin % 32 == 0 && a.Kh * a.Kw <= 32 && a.Cout % (16 * nf) == 0 && a.Npad >= a.Cout &&
+           a.Kpad % 32 == 0 &&
            a.Cx % 8 == 0 && a.x_off % 8 == 0 && a.Cy % 4 == 0 && a.y_off % 4 == 0 && !a.y2 && !a.partial && !a.w8 &&
            !a.y_amax && (!a.res || (a.Cres % 4 == 0 && a.res_off % 4 == 0)) &&
            (kcat ? (a.C2 % 32 == 0 && a.Cx2 % 8 == 0 && a.x2_off % 8 == 0 && a.K1 == a.Kh * a.Kw * a.Cin &&
@@ -190,18 +194,34 @@ bool small_supported(const ConvArgs& a) {
            (!a.y_bf16 || (a.f16 && !a.res));
 }
 
-hipError_t launch_conv_small(const ConvArgs& a, int ks, hipStream_t s) {
-    if (!small_supported(a) || (ks != 1 && ks != 4 && ks != 8)) return hipErrorInvalidValue;
-    const int n_mf = (a.M + 15) / 16, n_units = n_mf * (a.Cout / 64);
+// split = KS | NF << 8 (NF field 0: the 64-channel tile)
+hipError_t launch_conv_small(const ConvArgs& a, int split, hipStream_t s) {
+    const int ks = split & 0xff, nf = (split >> 8) ? (split >> 8) : 4;
+    if (!small_supported(a, nf) || !small_split_ok(split)) return hipErrorInvalidValue;
+    const int n_mf = (a.M + 15) / 16, n_units = n_mf * (a.Cout / (16 * nf));
     const dim3 grid((unsigned)(ks == 1 ? (n_units + 3) / 4 : n_units)), block(ks == 1 ? 256 : 64 * ks);
-    auto k = ks == 1 ? (a.f16 ? conv_small_kernel<true, 1> : conv_small_kernel<false, 1>)
-           : ks == 4 ? (a.f16 ? conv_small_kernel<true, 4> : conv_small_kernel<false, 4>)
-                     : (a.f16 ? conv_small_kernel<true, 8> : conv_small_kernel<false, 8>);
+    void (*k)(ConvArgs, int, int) = nullptr;
+#define FR_SMALL_K(KS, NF) \
+    if (ks == KS && nf == NF) k = a.f16 ? conv_small_kernel<true, KS, NF> : conv_small_kernel<false, KS, NF>;
+    FR_SMALL_K(1, 4) FR_SMALL_K(4, 4) FR_SMALL_K(8, 4) FR_SMALL_K(4, 2) FR_SMALL_K(8, 2) FR_SMALL_K(4, 1)
+    FR_SMALL_K(8, 1) FR_SMALL_K(16, 1)
+#undef FR_SMALL_K
+    if (!k) return hipErrorInvalidValue;
     if (a.ev0)
         hipExtLaunchKernelGGL(k, grid, block, 0, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a, n_mf, n_units);
     else
         hipLaunchKernelGGL(k, grid, block, 0, s, a, n_mf, n_units);
     return hipGetLastError();
+}
+
+bool small_split_ok(int split) {
+    const int ks = split & 0xff, nf = split >> 8;
+    switch (nf) {
+        case 0: return ks == 1 || ks == 4 || ks == 8;
+        case 2: return ks == 4 || ks == 8;
+        case 1: return ks == 4 || ks == 8 || ks == 16;
+        default: return false;
+    }
 }
 
 }  // namespace fr

@@ -130,7 +130,8 @@ struct fr_handle {
     float* partial = nullptr;
     size_t partial_floats = 0;
     int* splitk_cnt = nullptr;  // [FR_SPLITK_TILES] in-launch split-K arrival counters (conv_igemm), zero between launches
-    bool splitk_inlaunch = true;  // FR_OPT_SPLITK_INLAUNCH
+    bool splitk_inlaunch = false;  // FR_OPT_SPLITK_INLAUNCH (opt-in: wrong results in graph replays)
+    bool inlaunch_used = false;   // an in-launch split-K conv has run (the per-forward counter memset is needed)
     // gallery
     float* gallery = nullptr;
     int64_t g_rows = 0;
@@ -1431,8 +1432,10 @@ static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, 
         // fit; else the separate split-K epilogue launch
         const int64_t tiles = (int64_t)((a.M + conv_tile_bm(c.tile) - 1) / conv_tile_bm(c.tile)) *
                               ((a.Cout + conv_tile_bn(c.tile) - 1) / conv_tile_bn(c.tile));
-        if (c.split < 0 && a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && h->splitk_inlaunch)
+        if (c.split < 0 && a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && h->splitk_inlaunch) {
             a.splitk_cnt = h->splitk_cnt;
+            h->inlaunch_used = true;
+        }
     }
     hipError_t e = launch_conv(a, s);
     if (e == hipSuccess && split > 1 && a.y && !a.splitk_cnt) e = launch_splitk_epilogue(a, s);
@@ -1490,8 +1493,13 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     if (blas_enabled() && blas_supported(a)) add(FR_TILE_BLAS, 1);       // 1x1 conv as a library GEMM
     // small M (a few hundred pixels: small batches): one wave per 16 px x 64 ch, no LDS, no second launch
     // (split 4 / 8: that many waves share a tile's K, summed through LDS)
-    if (a.M <= 8192 && small_supported(a))
-        for (int ks : {1, 4, 8}) add(FR_TILE_SMALL, ks);
+    static const bool small_nf4 = [] {  // FR_SMALL_NF4=1: only the 64-channel tiles (A/B)
+        const char* e = getenv("FR_SMALL_NF4");
+        return e && e[0] == '1';
+    }();
+    if (a.M <= 8192)
+        for (int sp : {1, 4, 8, 4 | 2 << 8, 8 | 2 << 8, 4 | 1 << 8, 8 | 1 << 8, 16 | 1 << 8})
+            if ((!small_nf4 || sp < 256) && small_supported(a, (sp >> 8) ? (sp >> 8) : 4)) add(FR_TILE_SMALL, sp);
     {
         int tile, split;
         conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
@@ -1554,7 +1562,7 @@ static bool choice_ok(const ConvArgs& a, const ConvChoice& c) {
         }
         case FR_TILE_DIRECT: return direct_supported(a);
         case FR_TILE_BLAS: return blas_enabled() && blas_supported(a);
-        case FR_TILE_SMALL: return small_supported(a) && (c.split == 1 || c.split == 4 || c.split == 8);
+        case FR_TILE_SMALL: return small_split_ok(c.split) && small_supported(a, (c.split >> 8) ? (c.split >> 8) : 4);
         default: return c.tile >= 0;
     }
 }
@@ -1744,6 +1752,15 @@ bool rgn_hit(const std::vector<Rgn>& a, const std::vector<Rgn>& b) {
 // 3 same-box pairs) and ResNet-50 (157.0-157.9k vs 157.8-158.5k): the branches' kernels size their grids
 // for the whole GPU (persistent conv_direct / conv_rows, full igemm tile grids), so two of them at once
 // share the CUs instead of filling idle ones.
+// FR_NO_HEAD_GEMV=1: the small-batch head runs on the implicit-GEMM tiles too (A/B timing)
+static bool head_gemv_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_HEAD_GEMV");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 static bool ms_enabled() {
     const char* e = getenv("FR_BRANCH_STREAMS");
     return e && e[0] == '1';
@@ -1912,9 +1929,10 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
     const int f16 = h->dtype == FR_DTYPE_F16;
     const std::vector<char> stage_run = stage_plan(h, B);
     if (h->amax) FR_HIP_CHECK(hipMemsetAsync(h->amax, 0, h->tensors.size() * FR_AMAX_SLOTS * sizeof(float), s_main));
-    // the split-K tile counters return to zero after every launch; re-zeroed per forward all the same, so an
-    // aborted earlier launch cannot leave a count behind
-    if (h->splitk_cnt) FR_HIP_CHECK(hipMemsetAsync(h->splitk_cnt, 0, FR_SPLITK_TILES * sizeof(int), s_main));
+    // the split-K tile counters return to zero after every launch; re-zeroed per forward all the same (once an
+    // in-launch split has run on this handle: zeroed at fr_reserve before that), so an aborted earlier launch
+    // cannot leave a count behind.  The memset node is ~6 us of a 1 ms bs = 1 forward that may have no such split.
+    if (h->splitk_cnt && h->inlaunch_used) FR_HIP_CHECK(hipMemsetAsync(h->splitk_cnt, 0, FR_SPLITK_TILES * sizeof(int), s_main));
     h->slot_done = false;
     const bool ms = h->ms_on;
     const size_t nops = h->ops.size();
@@ -2053,13 +2071,21 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 int tile, split;
                 head_plan(B, cw.Cout, cw.Kpad, &tile, &split);
                 while (split > 1 && (size_t)split * B * cw.Npad > h->partial_floats) split /= 2;
+                // B <= 4 (the online bs = 1 path): a GEMV over 8 K chunks instead of 128-row MFMA tiles
+                const bool gemv = B <= 4 && head_gemv_enabled() && head_gemv_supported(B, cw.K, cw.Kpad, cw.Npad) &&
+                                  (size_t)8 * B * cw.Npad <= h->partial_floats;
+                if (gemv) split = 8;
                 a.tile = tile;
                 a.split_k = split;
                 a.partial = h->partial;
                 // input, weights, the f32 split-K partials written and read back, the f32 embeddings
                 ps.bytes = (double)B * cw.K * 2.0 + (double)cw.K * cw.Cout * 2.0 + 2.0 * split * B * cw.Npad * 4.0 +
                            (double)B * cw.Cout * 4.0;
-                FR_HIP_CHECK(launch_conv(a, s));
+                if (gemv)
+                    FR_HIP_CHECK(launch_head_gemv(ti.dev, B, cw.K, cw.w, cw.Kpad, cw.Cout, cw.Npad, split, f16 || ti.f16,
+                                                  h->partial, s));
+                else
+                    FR_HIP_CHECK(launch_conv(a, s));
                 if (h->proj_d) {  // IRV1 L2 (always: InceptionResnetV1 classify=False) -> projection -> L2
                     FR_HIP_CHECK(launch_head_finalize(h->partial, split, B, cw.Cout, cw.Npad, cw.bias, 1, h->emb_pre, s));
                     FR_HIP_CHECK(launch_proj_l2(h->emb_pre, B, cw.Cout, h->proj_w, h->proj_b, h->proj_d,
@@ -2115,7 +2141,7 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->dtype = dtype;
     h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
     h->stage_mode = stage_default();
-    if (const char* e = getenv("FR_SPLITK_EPILOGUE")) h->splitk_inlaunch = e[0] != '1';  // A/B timing
+    if (const char* e = getenv("FR_SPLITK_INLAUNCH")) h->splitk_inlaunch = e[0] == '1';  // A/B timing
     if (const char* e = getenv("FR_STAGE_VARIANT")) {  // A/B timing
         const int v = atoi(e);
         h->stage_variant = v == 1 || v == 2 ? v : 0;
@@ -2463,6 +2489,15 @@ static int ensure_cand(fr_handle* h, size_t need) {
     return FR_OK;
 }
 
+// FR_NO_MATCH_ROWS=1: small batches take the MFMA match kernels too (A/B timing)
+static bool match_rows_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_MATCH_ROWS");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 static int match_locked(fr_handle* h, const float* P, int B, int k, float* scores, int32_t* idx, void* stream) {
     if (!P || !scores || !idx || B <= 0 || k <= 0 || k > FR_TOPK_LARGE_MAX) {
         set_error("fr_match_topk: bad argument (1 <= k <= " + std::to_string(FR_TOPK_LARGE_MAX) + ")");
@@ -2490,6 +2525,17 @@ static int match_locked(fr_handle* h, const float* P, int B, int k, float* score
     }
     int n_split;
     int64_t rps;
+    // B <= 4 (the online bs = 1 path): one wave per 64 rows, exact f32 scores in the f32 kernels' order
+    if (match_rows_enabled() && match_rows_supported(B, h->g_dim, k)) {
+        int n_lists, R;
+        match_rows_plan(h->g_rows, &n_lists, &R);
+        int rc = ensure_cand(h, (size_t)B * n_lists * k);
+        if (rc) return rc;
+        FR_HIP_CHECK(launch_match_rows(P, B, h->gallery, h->g_rows, h->g_dim, k, h->g_base, h->cand_s, h->cand_i,
+                                       n_lists, R, s));
+        FR_HIP_CHECK(launch_topk_merge(h->cand_s, h->cand_i, B, n_lists, k, scores, idx, s));
+        return FR_OK;
+    }
     // bf16x3 candidates + exact f32 rescoring (match_x3.hip).  Its proof needs the k-th exact score to
     // clear the 16th candidate by 2 eps, which a k close to 16 almost never does (every probe would be
     // rescanned by one wave), so k > 8 takes the exact kernel.
@@ -2900,8 +2946,12 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         return FR_OK;
     }
     if (d->tile == FR_TILE_SMALL + 1) {
-        if (!small_supported(a)) { set_error("fr_op_conv2d: small-M kernel not applicable"); return FR_ERR_ARG; }
-        FR_HIP_CHECK(launch_conv_small(a, d->split_k > 1 ? d->split_k : 1, (hipStream_t)stream));
+        const int sp = d->split_k > 1 ? d->split_k : 1;  // KS | NF << 8 (conv_small.hip)
+        if (!small_split_ok(sp) || !small_supported(a, (sp >> 8) ? (sp >> 8) : 4)) {
+            set_error("fr_op_conv2d: small-M kernel not applicable");
+            return FR_ERR_ARG;
+        }
+        FR_HIP_CHECK(launch_conv_small(a, sp, (hipStream_t)stream));
         return FR_OK;
     }
     if (d->tile == FR_TILE_BLAS + 1) {  // a per-call library state: the op API holds no handle

@@ -70,8 +70,10 @@ hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s);
 // Small-M implicit GEMM (conv_small.hip): one wave per 16 pixels x 64 channels over the whole K, operands straight
 // from global memory (no LDS); Cin % 32 == 0, Cout % 64 == 0; ks = 1: equal to conv_igemm tile 0 bit for bit;
 // ks = 4 / 8: that many waves split each tile's K and sum through LDS (a split-K summation order).
-bool small_supported(const ConvArgs& a);
-hipError_t launch_conv_small(const ConvArgs& a, int ks, hipStream_t s);
+// conv_small.hip: split = KS (waves sharing a tile's K) | NF << 8 (16-channel fragments per tile; 0 = 4)
+bool small_supported(const ConvArgs& a, int nf = 4);
+bool small_split_ok(int split);
+hipError_t launch_conv_small(const ConvArgs& a, int split, hipStream_t s);
 // 1x1 stride-1 convs as hipBLASLt GEMMs (blas.cpp): bias + ReLU epilogue, residual as beta * C.  The state (library
 // handle, 32-MiB workspace, per-conv descriptors and algorithm) lives per fr_handle.
 bool blas_supported(const ConvArgs& a);
@@ -202,6 +204,9 @@ hipError_t launch_maxpool(const bf16_t* x, int B, int H, int W, int Cx, int x_of
                           int pad, bf16_t* y, int Cy, int y_off, int Ho, int Wo, int f16, hipStream_t s);
 hipError_t launch_avgpool(const bf16_t* x, int B, int H, int W, int C, bf16_t* y, int f16, hipStream_t s);
 // Sum split-K partials [split][B][Npad] + bias, optional L2 normalize → out [B][N] f32.
+bool head_gemv_supported(int B, int K, int Kpad, int Npad);
+hipError_t launch_head_gemv(const bf16_t* x, int B, int K, const bf16_t* w, int Kpad, int N, int Npad, int S, int f16,
+                            float* partial, hipStream_t s);
 hipError_t launch_head_finalize(const float* partial, int split, int B, int N, int Npad, const float* bias,
                                 int normalize, float* out, hipStream_t s);
 // FaceNet projection: out = x W^T + bias (f32), optional F.normalize (eps 1e-12).  K <= 1024.
@@ -230,6 +235,10 @@ constexpr int64_t X3_MIN_ROWS = 32768;  // below: the exact f32 kernel is as fas
 size_t x3_gallery_elems(int64_t rows);
 hipError_t launch_split_x3(const float* G, int64_t row0, int64_t n, bf16_t* T, hipStream_t s);
 void match_x3_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split);
+bool match_rows_supported(int B, int D, int k);
+void match_rows_plan(int64_t N, int* n_lists, int* R);
+hipError_t launch_match_rows(const float* P, int B, const float* G, int64_t N, int D, int k, int64_t index_base,
+                             float* cand_s, int32_t* cand_i, int n_lists, int R, hipStream_t s);
 int match_x3_candidates();
 hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* GT, int64_t N, int D,
                            int k, int64_t index_base, float* cand_s, int32_t* cand_i, int n_split,

@@ -21,6 +21,7 @@
 // splits from HBM once and the other probe blocks hit its L2.
 #include "kernels.h"
 
+#include <algorithm>
 #include <float.h>
 #include <stdlib.h>
 #include <limits.h>
@@ -464,6 +465,103 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
     }
 }
 
+// Small-batch exact match (B <= 4 probes: the reference's online recognize path at bs = 1,
+// recognition_engine.py:328-381).  match_p512_kernel keeps 64 probes per block in MFMA fragments, so at B = 1 a
+// block scores 63 padding probes and the split plan leaves ~80 blocks each walking 128 rows through an LDS ring
+// (32 us for 10k rows).  Here each lane scores one row at a time (R rows per lane, WPB waves per block) for every
+// probe with exact_dot's k-ordered fmaf chain (the f32 kernels' order: the scores are theirs bit for bit; 8 16-dim
+// steps of loads in flight measured 15.7 vs 13.9 us for 1 x 10k), and keeps per-lane sorted lists; each wave's top-k per probe goes to LDS, wave 0
+// merges the block's WPB lists and writes one candidate list per block for topk_merge_kernel.  WPB = 1 while the
+// waves fit the CUs (each CU then streams one wave's 128 KiB of rows), more waves per block (fewer lists) beyond.
+template <int NB, int KL, int WPB>
+__global__ __launch_bounds__(64 * WPB) void match_rows_kernel(const float* __restrict__ P, int B, const float* __restrict__ G,
+                                                         int64_t N, int64_t index_base, int k, int R,
+                                                         float* __restrict__ cand_s, int32_t* __restrict__ cand_i) {
+    __shared__ float xs[NB][WPB][KL];
+    __shared__ int xi[NB][WPB][KL];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t r0 = ((int64_t)blockIdx.x * WPB + wave) * 64 * R;
+    float ls[NB][KL];
+    int li[NB][KL];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int q = 0; q < KL; ++q) { ls[b][q] = -INFINITY; li[b][q] = INT_MAX; }
+    for (int j = 0; j < R; ++j) {
+        const int64_t r = r0 + 64 * j + lane;
+        if (r >= N) break;
+        const float* g = G + (size_t)r * XD;
+        float acc[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[b] = 0.f;
+#pragma unroll 2
+        for (int t16 = 0; t16 < XD / 16; ++t16) {
+            float4 gv[4];
+#pragma unroll
+            for (int kq = 0; kq < 4; ++kq) gv[kq] = *(const float4*)(g + 16 * t16 + 4 * kq);
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                if (b >= B) break;
+                float4 pv[4];
+#pragma unroll
+                for (int kq = 0; kq < 4; ++kq) pv[kq] = *(const float4*)(P + (size_t)b * XD + 16 * t16 + 4 * kq);
+                // exact_dot's order: k = 16 t + 4 kq + c, c outer
+#pragma unroll
+                for (int kq = 0; kq < 4; ++kq) acc[b] = fmaf(pv[kq].x, gv[kq].x, acc[b]);
+#pragma unroll
+                for (int kq = 0; kq < 4; ++kq) acc[b] = fmaf(pv[kq].y, gv[kq].y, acc[b]);
+#pragma unroll
+                for (int kq = 0; kq < 4; ++kq) acc[b] = fmaf(pv[kq].z, gv[kq].z, acc[b]);
+#pragma unroll
+                for (int kq = 0; kq < 4; ++kq) acc[b] = fmaf(pv[kq].w, gv[kq].w, acc[b]);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+            if (b < B) insert<KL>(ls[b], li[b], acc[b], (int)(r + index_base));
+    }
+    // each wave's top-k per probe -> LDS
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b >= B) break;
+        int head = 0;
+        for (int q = 0; q < k; ++q) {
+            float ws;
+            int wi;
+            wave_pop<KL>(ls[b], li[b], head, ws, wi);
+            if (lane == 0) { xs[b][wave][q] = ws; xi[b][wave][q] = wi; }
+        }
+    }
+    __syncthreads();
+    if (wave) return;
+    // wave 0: lane 16 w + q holds entry q of wave w's list; k pops give the block's top-k
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b >= B) break;
+        float ms[1] = {-INFINITY};
+        int mi[1] = {INT_MAX};
+        const int w = lane >> 4, q = lane & 15;
+        if (w < WPB && q < k) { ms[0] = xs[b][w][q]; mi[0] = xi[b][w][q]; }
+        int head = 0;
+        float outs = -INFINITY;
+        int outi = -1;
+        for (int q2 = 0; q2 < k; ++q2) {
+            float ws;
+            int wi;
+            wave_pop<1>(ms, mi, head, ws, wi);
+            if (lane == q2) {
+                outs = wi == INT_MAX ? -INFINITY : ws;
+                outi = wi == INT_MAX ? -1 : wi;
+            }
+        }
+        if (lane < k) {
+            const size_t o = ((size_t)b * gridDim.x + blockIdx.x) * k + lane;
+            cand_s[o] = outs;
+            cand_i[o] = outi;
+        }
+    }
+}
+
 }  // namespace
 
 size_t x3_gallery_elems(int64_t rows) { return (size_t)((rows + XG - 1) / XG) * 8 * XCHUNK_E; }
@@ -485,6 +583,34 @@ void match_x3_plan(int B, int64_t N, int* n_split, int64_t* rows_per_split) {
     const int64_t rps = ((tiles + want - 1) / want) * XG;
     *rows_per_split = rps;
     *n_split = (int)((N + rps - 1) / rps);
+}
+
+// match_rows_kernel's plan: R rows per lane so that at most ~1024 blocks run (one list each), WPB waves per block
+bool match_rows_supported(int B, int D, int k) { return B >= 1 && B <= 4 && D == XD && k >= 1 && k <= 8; }
+
+static int rows_wpb(int64_t N) {
+    const int64_t waves = (N + 63) / 64;
+    return waves <= 256 ? 1 : waves <= 512 ? 2 : 4;
+}
+
+void match_rows_plan(int64_t N, int* n_lists, int* R) {
+    const int64_t per = 64LL * rows_wpb(N) * 1024;
+    *R = (int)std::max<int64_t>(1, (N + per - 1) / per);
+    *n_lists = (int)((N + 64LL * rows_wpb(N) * *R - 1) / (64LL * rows_wpb(N) * *R));
+}
+
+hipError_t launch_match_rows(const float* P, int B, const float* G, int64_t N, int D, int k, int64_t index_base,
+                             float* cand_s, int32_t* cand_i, int n_lists, int R, hipStream_t s) {
+    if (!match_rows_supported(B, D, k) || n_lists < 1) return hipErrorInvalidValue;
+    typedef void (*Kern)(const float*, int, const float*, int64_t, int64_t, int, int, float*, int32_t*);
+    const int wpb = rows_wpb(N);
+    const Kern tab[3][4] = {
+        {match_rows_kernel<1, 5, 1>, match_rows_kernel<1, 8, 1>, match_rows_kernel<4, 5, 1>, match_rows_kernel<4, 8, 1>},
+        {match_rows_kernel<1, 5, 2>, match_rows_kernel<1, 8, 2>, match_rows_kernel<4, 5, 2>, match_rows_kernel<4, 8, 2>},
+        {match_rows_kernel<1, 5, 4>, match_rows_kernel<1, 8, 4>, match_rows_kernel<4, 5, 4>, match_rows_kernel<4, 8, 4>}};
+    const Kern kern = tab[wpb == 1 ? 0 : wpb == 2 ? 1 : 2][(B == 1 ? 0 : 2) + (k <= 5 ? 0 : 1)];
+    hipLaunchKernelGGL(kern, dim3(n_lists), dim3(64 * wpb), 0, s, P, B, G, N, index_base, k, R, cand_s, cand_i);
+    return hipGetLastError();
 }
 
 int match_x3_candidates() { return KS; }

@@ -140,6 +140,51 @@ __global__ __launch_bounds__(256) void head_finalize_kernel(const float* __restr
     if (own) *(float4*)(out + (size_t)b * N + n) = v;
 }
 
+// Head GEMV for small batches (bs = 1 is the reference's online path, recognition_engine.py:328-381): the
+// 25088 -> 512 head as split-K partials [S][B][Npad] for head_finalize_kernel, like the implicit-GEMM head, but
+// with no 128-row MFMA tile of which one row is real.  Grid (Npad / 16, S): each wave owns 4 output rows over
+// the block's K chunk, lanes stride K by 8 elements (one 16-B load of each weight row and of each input row
+// per step), f32 FMAs, a wave reduction per (row, probe).  The weight matrix (25.7 MB) is read once in total.
+template <bool F16, int NB>
+__global__ __launch_bounds__(256) void head_gemv_kernel(const bf16_t* __restrict__ x, int B, int K,
+                                                        const bf16_t* __restrict__ w, int Kpad, int N, int Npad,
+                                                        int kchunk, float* __restrict__ partial) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n0 = blockIdx.x * 16 + wave * 4, s = blockIdx.y;
+    const int k0 = s * kchunk, k1 = min(K, k0 + kchunk);
+    float acc[4][NB];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[j][b] = 0.f;
+    for (int k = k0 + 8 * lane; k < k1; k += 512) {
+        float xf[NB][8];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const uint4 v = b < B ? *(const uint4*)(x + (size_t)b * K + k) : make_uint4(0u, 0u, 0u, 0u);
+            Num<F16>::unpack8(v, xf[b]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float wf[8];
+            Num<F16>::unpack8(*(const uint4*)(w + (size_t)(n0 + j) * Kpad + k), wf);
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[j][b] = fmaf(wf[e], xf[b][e], acc[j][b]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            float v = acc[j][b];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+            if (lane == 0 && b < B) partial[((size_t)s * B + b) * Npad + n0 + j] = v;
+        }
+}
+
 __global__ __launch_bounds__(256) void l2norm_rows_kernel(float* __restrict__ x, int D) {
     __shared__ float red[4];
     float* row = x + (size_t)blockIdx.x * D;
@@ -285,6 +330,22 @@ hipError_t launch_head_finalize(const float* partial, int split, int B, int N, i
     if (N % 4 || N > 1024 || Npad % 4) return hipErrorInvalidValue;
     hipLaunchKernelGGL(head_finalize_kernel, dim3(B), dim3(256), 0, s, partial, split, B, N, Npad, bias, normalize,
                        out);
+    return hipGetLastError();
+}
+
+// S split-K partials of the head for B <= 8 probes (head_gemv_kernel); head_finalize_kernel sums them
+bool head_gemv_supported(int B, int K, int Kpad, int Npad) { return B >= 1 && B <= 8 && K % 8 == 0 && Kpad >= K && Npad % 16 == 0; }
+
+hipError_t launch_head_gemv(const bf16_t* x, int B, int K, const bf16_t* w, int Kpad, int N, int Npad, int S, int f16,
+                            float* partial, hipStream_t s) {
+    if (!head_gemv_supported(B, K, Kpad, Npad) || S < 1) return hipErrorInvalidValue;
+    const int kchunk = (K + 8 * S - 1) / (8 * S) * 8;
+    void (*k)(const bf16_t*, int, int, const bf16_t*, int, int, int, int, float*) =
+        B == 1   ? (f16 ? head_gemv_kernel<true, 1> : head_gemv_kernel<false, 1>)
+        : B == 2 ? (f16 ? head_gemv_kernel<true, 2> : head_gemv_kernel<false, 2>)
+        : B <= 4 ? (f16 ? head_gemv_kernel<true, 4> : head_gemv_kernel<false, 4>)
+                 : (f16 ? head_gemv_kernel<true, 8> : head_gemv_kernel<false, 8>);
+    hipLaunchKernelGGL(k, dim3(Npad / 16, S), dim3(256), 0, s, x, B, K, w, Kpad, N, Npad, kchunk, partial);
     return hipGetLastError();
 }
 

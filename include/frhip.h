@@ -251,7 +251,9 @@ typedef struct fr_conv_desc {
 #define FR_TILE_DIRECT 14    /* persistent small-K direct conv (conv_direct.hip): Cin % 8 == 0, Kpad <= 384, Cout % 32 == 0,
                                 bias + activation epilogue; autotuned per shape (env FR_NO_DIRECT=1: off) */
 #define FR_TILE_BLAS 15      /* 1x1 stride-1 conv as a hipBLASLt GEMM (bias + ReLU / residual epilogue); an autotuner candidate */
-#define FR_TILE_SMALL 16     /* small-M implicit GEMM, one wave per 16 px x 64 ch over the whole K (conv_small.hip); bit-identical to tile 0 */
+#define FR_TILE_SMALL 16     /* small-M implicit GEMM, one wave per 16 px x 64 ch over the whole K (conv_small.hip); bit-identical to tile 0.
+                                split_k = KS | NF << 8: KS (4 / 8 / 16) waves share a tile's K (split-K summation order), NF
+                                (2 / 1; 0 = 4) 16-channel fragments per tile: 1, 4, 8, 4|2<<8, 8|2<<8, 4|1<<8, 8|1<<8, 16|1<<8 */
 
 int fr_op_conv2d(const fr_conv_desc* d, void* stream);
 
@@ -304,10 +306,12 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * discarded per row), 2: the 13-fragment layout at one wave per SIMD (each weight fragment loaded once per
  * CU).  All give the same bits (A/B and regression tests). */
 #define FR_OPT_STAGE_VARIANT 7
-/* FR_OPT_SPLITK_INLAUNCH (default 1; env FR_SPLITK_EPILOGUE=1 starts at 0): a split-K implicit-GEMM conv may reduce
+/* FR_OPT_SPLITK_INLAUNCH (default 0; env FR_SPLITK_INLAUNCH=1 starts at 1): a split-K implicit-GEMM conv may reduce
  * its partials in the same launch (the last workgroup of each tile sums them in split order) where the
  * per-shape tuning measured that faster than a second launch; 0 = always the second launch.  The same bits
- * either way.  fr_debug_plan prints an in-launch split as a negative split count. */
+ * either way in eager forwards; opt-in because replays of a captured forward gave wrong embeddings once forwards
+ * at other batch sizes had run.  fr_debug_plan prints an in-launch split as a negative
+ * split count. */
 #define FR_OPT_SPLITK_INLAUNCH 8
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);

@@ -444,6 +444,31 @@ def test_match_ties_across_splits_multi_tile(gpu):
     assert np.allclose(s, rs, atol=1e-5)
 
 
+@pytest.mark.parametrize("Ng,k", [(10000, 5), (777, 8), (40000, 5), (70000, 1)])
+def test_match_small_batch_rows_kernel(gpu, Ng, k):
+    """B <= 4 takes match_rows_kernel (one wave per 64 rows, exact_dot's fmaf order): its scores equal the
+    MFMA kernels' (B = 9 runs match_p512 below 32768 rows, the bf16x3 path + exact rescoring above) bit for bit,
+    ties keep (score desc, index asc) across waves (recognition_engine.py:277-289 order), and the indices match
+    the numpy oracle."""
+    from facerecognition_amd.gallery import DeviceGallery
+    rng = np.random.default_rng(Ng + k)
+    G = _norm(rng.standard_normal((Ng, 512)))
+    for r in (Ng // 3, Ng // 2, Ng - 1):  # exact ties with row 7 in other waves / lists
+        G[r] = G[7]
+    P = _norm(rng.standard_normal((9, 512)))
+    P[0] = _norm(G[7:8] + 0.02 * rng.standard_normal((1, 512)))[0]
+    P[2] = _norm(G[100:101] + 0.05 * rng.standard_normal((1, 512)))[0]
+    gal = DeviceGallery(G)
+    s9, i9 = gal.search(P, k)
+    for B in (1, 2, 3, 4):
+        s, i = gal.search(P[:B], k)
+        assert np.array_equal(s, s9[:B]) and np.array_equal(i, i9[:B]), B
+    rs, ri = _np_topk(P, G, k)
+    assert np.array_equal(i9[:, 0], ri[:, 0])
+    assert np.allclose(s9, rs, atol=1e-5)
+    assert list(i9[0, : min(k, 4)]) == [7, Ng // 3, Ng // 2, Ng - 1][: min(k, 4)]
+
+
 def test_match_unnormalized_rows_cosine(gpu):
     """cosine_similarity semantics: non-unit rows are divided by their norm, zero rows score 0."""
     from facerecognition_amd.gallery import DeviceGallery
@@ -587,6 +612,7 @@ def test_match_x3_fallback_on_ties(gpu):
     G = _norm(rng.standard_normal((6000, 512)))
     G[100:140] = G[7]
     P = _norm(G[[7, 11]] + 0.01 * rng.standard_normal((2, 512)))
+    P = np.concatenate([P, _norm(rng.standard_normal((4, 512)))])  # B > 4: the bf16x3 path, not match_rows
     gal = DeviceGallery(G, x3_min_rows=4096)
     s3, i3 = gal.search(P, 5)
     assert gal.fallbacks() >= 1
@@ -606,7 +632,7 @@ def test_match_x3_sublist_overflow_floor(gpu):
     from facerecognition_amd.gallery import DeviceGallery
     rng = np.random.default_rng(9)
     G = _norm(rng.standard_normal((8192, 512)))
-    P = _norm(rng.standard_normal((3, 512)))
+    P = _norm(rng.standard_normal((6, 512)))  # B > 4: the bf16x3 path, not match_rows
     rows = [16 * (i // 4) + i % 4 for i in range(12)]
     for i, r in enumerate(rows):
         G[r] = _norm(P[:1] + (0.1 + 0.05 * i) * _norm(rng.standard_normal((1, 512))))[0]
@@ -885,8 +911,22 @@ def test_conv_small(gpu, case, dtype):
         assert torch.equal(y, conv_op(x, w, bias=bias, res=res, tile=N.FR_TILE_SMALL, split_k=ks, **kw))
         y = conv_op(x, w, act=2, slope=slope, bias9=b9, tile=N.FR_TILE_SMALL, split_k=ks, **kw)
         _close(y, conv_op(x, w, act=2, slope=slope, bias9=b9, tile=0, **kw), tol=1e-2 if dtype == "bf16" else 2e-3)
-    with pytest.raises(RuntimeError, match="small"):  # Cout % 64 != 0
+        # the narrower tiles (32 / 16 output channels, split_k = KS | NF << 8) chunk K by KS alone: the same bits
+        for nf in (2, 1):
+            yn = conv_op(x, w, bias=bias, res=res, tile=N.FR_TILE_SMALL, split_k=ks | nf << 8, **kw)
+            assert torch.equal(yn, conv_op(x, w, bias=bias, res=res, tile=N.FR_TILE_SMALL, split_k=ks, **kw))
+            yn = conv_op(x, w, act=2, slope=slope, bias9=b9, tile=N.FR_TILE_SMALL, split_k=ks | nf << 8, **kw)
+            assert torch.equal(yn, y)
+    y16 = conv_op(x, w, bias=bias, act=1, tile=N.FR_TILE_SMALL, split_k=16 | 1 << 8, **kw)
+    _close(y16, conv_op(x, w, bias=bias, act=1, tile=0, **kw), tol=1e-2 if dtype == "bf16" else 2e-3)
+    with pytest.raises(RuntimeError, match="small"):  # Cout % 64 != 0 for the 64-channel tile
         conv_op(x, torch.randn(32, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_SMALL, dtype=dtype)
+    with pytest.raises(RuntimeError, match="small"):  # no 16-wave split of the 64-channel tile
+        conv_op(x, w, pad=(1, 1), tile=N.FR_TILE_SMALL, split_k=16, dtype=dtype)
+    w32 = torch.randn(32, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)  # 32 channels: the 32 / 16-channel tiles
+    y32 = conv_op(x, w32, bias=bias[:32], act=1, tile=N.FR_TILE_SMALL, split_k=8 | 2 << 8, **kw)
+    assert torch.equal(y32, conv_op(x, w32, bias=bias[:32], act=1, tile=N.FR_TILE_SMALL, split_k=8 | 1 << 8, **kw))
+    _close(y32, conv_ref(x, w32, bias=bias[:32], act=1, **kw), tol=1e-2 if dtype == "bf16" else 2e-3)
 
 
 BLAS_CASES = [

@@ -18,7 +18,8 @@ def test_splitk_inlaunch_equals_epilogue_launch(gpu, arch, B):
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
     m = FRModel.synthetic(arch)
-    assert m.get_option(N.FR_OPT_SPLITK_INLAUNCH) == 1
+    assert m.get_option(N.FR_OPT_SPLITK_INLAUNCH) == 0  # opt-in
+    m.set_option(N.FR_OPT_SPLITK_INLAUNCH, 1)
     x = torch.from_numpy(synthetic_crops(B, m.input_size, seed=5 + B))
     a = m.embed(x).cpu().numpy()  # tuning forward (kernel choice per conv measured at this batch size)
     a = m.embed(x).cpu().numpy()

@@ -52,7 +52,8 @@ if __name__ == "__main__":
     ap.add_argument("--exact", action="store_true", help="force the f32-MFMA kernel (FR_OPT_MATCH_EXACT)")
     ap.add_argument("--x3-min-rows", type=int, default=None, help="FR_OPT_X3_MIN_ROWS for the galleries")
     ap.add_argument("--only-rows", type=int, default=None, help="run only the shape with this many rows")
+    ap.add_argument("--probes", type=int, default=None, help="override the probe count of the shapes run")
     a = ap.parse_args()
     for rows, probes in ((10000, 256), (125000, 2048), (1000000, 256)):
         if a.only_rows is None or rows == a.only_rows:
-            print(json.dumps(run(rows, probes, a.k, a.iters, a.exact, a.x3_min_rows)), flush=True)
+            print(json.dumps(run(rows, a.probes or probes, a.k, a.iters, a.exact, a.x3_min_rows)), flush=True)
