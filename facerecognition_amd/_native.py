@@ -113,6 +113,7 @@ _SIGS = {
     "fr_mtcnn_maxpool": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "fr_mtcnn_dense": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "fr_mtcnn_head": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "fr_nms_host": (c_int, [c_void_p, c_int64, c_void_p, ctypes.c_float, c_int, c_void_p, c_void_p]),
     "fr_op_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "fr_op_maxpool": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                               c_int, c_int, c_int, c_int, c_int, c_void_p]),

@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 namespace fr {
+typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -391,15 +392,24 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
         }
     __syncthreads();
     if (p.partial) {
+        // in-launch reduction: the partial slabs go through sc1 (write-through, coherent across XCDs) buffer stores
+        // and loads (cdna_hip_programming.md §6 Guideline 16 R1), besides the release / acquire pair below
+        const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)p.partial, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)gridDim.y * p.M * p.Npad * 4), 0x00020000);
 #pragma unroll
         for (int it = 0; it < ITER; ++it) {
             const int ml = ml0 + it * RS, m = m0 + ml;
             if (m >= p.M || !nv) continue;
             const float4 v0 = *(const float4*)(sE + ml * EPI_LD + g * 8);
             const float4 v1 = *(const float4*)(sE + ml * EPI_LD + g * 8 + 4);
-            float* dst = p.partial + ((size_t)split * p.M + m) * p.Npad + n;
-            *(float4*)dst = v0;
-            *(float4*)(dst + 4) = v1;
+            const size_t e = ((size_t)split * p.M + m) * p.Npad + n;
+            if (p.splitk_cnt) {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, v0), pr, (uint32_t)(e * 4), 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, v1), pr, (uint32_t)(e * 4 + 16), 0, 16);
+            } else {
+                *(float4*)(p.partial + e) = v0;
+                *(float4*)(p.partial + e + 4) = v1;
+            }
         }
         if (!p.splitk_cnt) return;
         // In-launch split-K reduction (cdna_hip_programming.md §6 Guideline 16, counter hand-off): every slice
@@ -430,8 +440,9 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
             if (m >= p.M || !nv) continue;
             float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             for (int s2 = 0; s2 < (int)gridDim.y; ++s2) {
-                const float* src = p.partial + ((size_t)s2 * p.M + m) * p.Npad + n;
-                const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+                const uint32_t o = (uint32_t)((((size_t)s2 * p.M + m) * p.Npad + n) * 4);
+                const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, o, 0, 16));
+                const float4 b = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, o + 16, 0, 16));
                 v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
                 v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
             }

@@ -130,7 +130,7 @@ struct fr_handle {
     float* partial = nullptr;
     size_t partial_floats = 0;
     int* splitk_cnt = nullptr;  // [FR_SPLITK_TILES] in-launch split-K arrival counters (conv_igemm), zero between launches
-    bool splitk_inlaunch = false;  // FR_OPT_SPLITK_INLAUNCH (opt-in: wrong results in graph replays)
+    bool splitk_inlaunch = true;  // FR_OPT_SPLITK_INLAUNCH
     bool inlaunch_used = false;   // an in-launch split-K conv has run (the per-forward counter memset is needed)
     // gallery
     float* gallery = nullptr;
@@ -2141,7 +2141,7 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->dtype = dtype;
     h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
     h->stage_mode = stage_default();
-    if (const char* e = getenv("FR_SPLITK_INLAUNCH")) h->splitk_inlaunch = e[0] == '1';  // A/B timing
+    if (const char* e = getenv("FR_SPLITK_INLAUNCH")) h->splitk_inlaunch = e[0] != '0';  // A/B timing
     if (const char* e = getenv("FR_STAGE_VARIANT")) {  // A/B timing
         const int v = atoi(e);
         h->stage_variant = v == 1 || v == 2 ? v : 0;

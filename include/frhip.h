@@ -195,6 +195,14 @@ int fr_mtcnn_dense(const float* x, int B, int K, const float* w, const float* bi
 int fr_mtcnn_head(const float* x, int64_t M, int C, const float* w, const float* bias, int n_out, float* out,
                   void* stream);
 
+/* Greedy NMS on the host (detect_face's batched_nms / batched_nms_numpy): boxes [n][4] (x1, y1, x2, y2) float32,
+ * order = the candidates' score order; a box is dropped when a kept box earlier in the order overlaps it with
+ * IoU > thresh (min_mode = 0: torchvision's areas and test, a 0 / 0 IoU keeps) or unless intersection / min
+ * area <= thresh (min_mode = 1: nms_numpy's 'Min', +1-pixel extents), float32 arithmetic as numpy's.  keep [n] receives the kept indices in
+ * order, *n_keep their count.  Grid-bucketed: O(n) for boxes of bounded size. */
+int fr_nms_host(const float* boxes, int64_t n, const int64_t* order, float thresh, int min_mode, int64_t* keep,
+                int64_t* n_keep);
+
 /* ---- op-level entry points (kernel parity tests and custom graphs) ---- */
 
 /* Implicit-GEMM convolution on NHWC bf16 with fused epilogue:
@@ -306,12 +314,10 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * discarded per row), 2: the 13-fragment layout at one wave per SIMD (each weight fragment loaded once per
  * CU).  All give the same bits (A/B and regression tests). */
 #define FR_OPT_STAGE_VARIANT 7
-/* FR_OPT_SPLITK_INLAUNCH (default 0; env FR_SPLITK_INLAUNCH=1 starts at 1): a split-K implicit-GEMM conv may reduce
+/* FR_OPT_SPLITK_INLAUNCH (default 1; env FR_SPLITK_INLAUNCH=0 starts at 0): a split-K implicit-GEMM conv may reduce
  * its partials in the same launch (the last workgroup of each tile sums them in split order) where the
  * per-shape tuning measured that faster than a second launch; 0 = always the second launch.  The same bits
- * either way in eager forwards; opt-in because replays of a captured forward gave wrong embeddings once forwards
- * at other batch sizes had run.  fr_debug_plan prints an in-launch split as a negative
- * split count. */
+ * either way.  fr_debug_plan prints an in-launch split as a negative split count. */
 #define FR_OPT_SPLITK_INLAUNCH 8
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);

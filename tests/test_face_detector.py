@@ -100,6 +100,25 @@ def test_nms_modes_against_oracle():
         assert np.array_equal(FD.nms(boxes, scores, t, "min"), OM.nms_numpy(boxes, scores, t, "Min"))
 
 
+def test_nms_grid_windows_against_oracle():
+    """PNet-like windows (a dense 12-px grid at stride 2, scaled boxes of several pyramid levels, near-equal
+    scores) and degenerate boxes (zero / negative extent: numpy's 0 / 0 drops them regardless of distance):
+    the grid-bucketed fr_nms_host keeps exactly the numpy greedy pass's boxes, in its order."""
+    rng = np.random.default_rng(4)
+    parts = []
+    for s in (1.0, 0.7, 0.49):
+        yy, xx = np.mgrid[0:30, 0:40].astype(np.float32)
+        q1 = np.floor((2 * np.stack([xx.ravel(), yy.ravel()], 1) + 1) / s)
+        q2 = np.floor((2 * np.stack([xx.ravel(), yy.ravel()], 1) + 12) / s)
+        parts.append(np.concatenate([q1, q2], 1))
+    boxes = np.concatenate(parts + [np.array([[5, 5, 5, 9], [50, 50, 50, 50], [80, 10, 70, 20], [7, 7, 7, 7]], np.float32)])
+    boxes = boxes.astype(np.float32)
+    scores = np.round(rng.uniform(0.6, 1.0, len(boxes)), 2).astype(np.float32)  # many exact ties
+    for t in (0.5, 0.7):
+        assert np.array_equal(FD.nms(boxes, scores, t, "iou"), OM.nms_iou(boxes, scores, t))
+        assert np.array_equal(FD.nms(boxes, scores, t, "min"), OM.nms_numpy(boxes, scores, t, "Min"))
+
+
 def test_pyramid_and_pool_shapes():
     assert FD.pyramid_scales(150, 190) == OM.pyramid_scales(150, 190)
     for n in range(2, 60):

@@ -18,8 +18,7 @@ def test_splitk_inlaunch_equals_epilogue_launch(gpu, arch, B):
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
     m = FRModel.synthetic(arch)
-    assert m.get_option(N.FR_OPT_SPLITK_INLAUNCH) == 0  # opt-in
-    m.set_option(N.FR_OPT_SPLITK_INLAUNCH, 1)
+    assert m.get_option(N.FR_OPT_SPLITK_INLAUNCH) == 1
     x = torch.from_numpy(synthetic_crops(B, m.input_size, seed=5 + B))
     a = m.embed(x).cpu().numpy()  # tuning forward (kernel choice per conv measured at this batch size)
     a = m.embed(x).cpu().numpy()
@@ -36,3 +35,33 @@ def test_splitk_inlaunch_equals_epilogue_launch(gpu, arch, B):
     if not splits:
         pytest.skip(f"{arch} bs={B}: the measured plan took no igemm split-K conv")
     print(f"{arch} bs={B}: {len(splits)} split-K convs, {sum(int(l.split()[6]) < 0 for l in splits)} reduced in-launch")
+
+
+@pytest.mark.parametrize("inlaunch", [0, 1])
+def test_graph_replay_after_other_batch_sizes(gpu, inlaunch):
+    """A bs = 1 forward captured as a hipGraph and replayed after forwards at other batch sizes (tuning passes,
+    their own captures) returns the embeddings it returned before (tests/test_gpu_host_api.py's call order:
+    recognize_batch, then recognize).  In-launch split-K failed exactly this (1-cos 0.15, deterministic) while its
+    partial slabs went through plain stores and loads behind the agent-scope release / acquire pair; with sc1
+    stores and loads it passes."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("resnet50_arcface")
+    m.set_option(N.FR_OPT_SPLITK_INLAUNCH, inlaunch)
+    x = torch.from_numpy(synthetic_crops(9, m.input_size, seed=21)).to(gpu)
+    x1 = x[:1].clone()
+    out = torch.empty((1, 512), dtype=torch.float32, device=gpu)
+    first = []
+    for _ in range(4):  # tuning forward, first sighting, capture + replay, replay
+        m.embed(x1, out=out)
+        first.append(out.cpu().numpy().copy())
+    m.embed(x[:8])
+    m.embed(x)
+    m.embed(x[:8])
+    later = []
+    for _ in range(3):
+        m.embed(x1, out=out)
+        later.append(out.cpu().numpy().copy())
+    m.close()
+    for e in first[1:] + later:
+        assert np.array_equal(e, first[0]), f"max |diff| {np.abs(e - first[0]).max():.3g}"
