@@ -17,7 +17,9 @@
 // NF = 4 / 2 / 1: 16-channel fragments per tile (64 / 32 / 16 output channels).  A narrower tile spreads a small
 // conv over more CUs: at bs = 1 layer3's 52 tiles of 64 channels used 52 of 256 CUs, each pulling its whole 64 x K
 // weight slab and 16 x K patch through one CU's L2 port (~290 KB, 2+ us); 16-channel tiles are 208 workgroups of
-// ~150 KB each.  The narrower tiles keep PF = 8 steps of loads in flight (their ring is smaller).
+// ~150 KB each.  The narrower tiles keep PF = 8 steps of loads in flight (their ring is smaller).  KS = 1 with
+// NF = 2 / 1 (one wave per 16 px x 32 / 16 ch) is also a candidate at large M: the N = 32 / 96 convs of FaceNet's
+// Block35 at bs = 256 fill half of an implicit-GEMM tile's 64 or 128 columns.
 #include "kernels.h"
 
 #include <hip/hip_ext.h>
@@ -203,8 +205,8 @@ hipError_t launch_conv_small(const ConvArgs& a, int split, hipStream_t s) {
     void (*k)(ConvArgs, int, int) = nullptr;
 #define FR_SMALL_K(KS, NF) \
     if (ks == KS && nf == NF) k = a.f16 ? conv_small_kernel<true, KS, NF> : conv_small_kernel<false, KS, NF>;
-    FR_SMALL_K(1, 4) FR_SMALL_K(4, 4) FR_SMALL_K(8, 4) FR_SMALL_K(4, 2) FR_SMALL_K(8, 2) FR_SMALL_K(4, 1)
-    FR_SMALL_K(8, 1) FR_SMALL_K(16, 1)
+    FR_SMALL_K(1, 4) FR_SMALL_K(4, 4) FR_SMALL_K(8, 4) FR_SMALL_K(1, 2) FR_SMALL_K(4, 2) FR_SMALL_K(8, 2)
+    FR_SMALL_K(1, 1) FR_SMALL_K(4, 1) FR_SMALL_K(8, 1) FR_SMALL_K(16, 1)
 #undef FR_SMALL_K
     if (!k) return hipErrorInvalidValue;
     if (a.ev0)
@@ -218,8 +220,8 @@ bool small_split_ok(int split) {
     const int ks = split & 0xff, nf = split >> 8;
     switch (nf) {
         case 0: return ks == 1 || ks == 4 || ks == 8;
-        case 2: return ks == 4 || ks == 8;
-        case 1: return ks == 4 || ks == 8 || ks == 16;
+        case 2: return ks == 1 || ks == 4 || ks == 8;
+        case 1: return ks == 1 || ks == 4 || ks == 8 || ks == 16;
         default: return false;
     }
 }

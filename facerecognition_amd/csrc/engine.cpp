@@ -1500,6 +1500,11 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     if (a.M <= 8192)
         for (int sp : {1, 4, 8, 4 | 2 << 8, 8 | 2 << 8, 4 | 1 << 8, 8 | 1 << 8, 16 | 1 << 8})
             if ((!small_nf4 || sp < 256) && small_supported(a, (sp >> 8) ? (sp >> 8) : 4)) add(FR_TILE_SMALL, sp);
+    // one wave per 16 px x 32 / 16 channels at any M: narrow-N convs (FaceNet Block35's N = 32 / 96) waste half of
+    // every implicit-GEMM tile
+    if (!small_nf4 && a.Cout <= 96)
+        for (int sp : {1 | 2 << 8, 1 | 1 << 8})
+            if (small_supported(a, sp >> 8)) add(FR_TILE_SMALL, sp);
     {
         int tile, split;
         conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);

@@ -926,6 +926,11 @@ def test_conv_small(gpu, case, dtype):
     w32 = torch.randn(32, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)  # 32 channels: the 32 / 16-channel tiles
     y32 = conv_op(x, w32, bias=bias[:32], act=1, tile=N.FR_TILE_SMALL, split_k=8 | 2 << 8, **kw)
     assert torch.equal(y32, conv_op(x, w32, bias=bias[:32], act=1, tile=N.FR_TILE_SMALL, split_k=8 | 1 << 8, **kw))
+    for sp in (1 | 2 << 8, 1 | 1 << 8):  # one wave per 16 px x 32 / 16 ch over the whole K: tile 0's bits
+        assert torch.equal(conv_op(x, w32, bias=bias[:32], act=1, tile=N.FR_TILE_SMALL, split_k=sp, **kw),
+                           conv_op(x, w32, bias=bias[:32], act=1, tile=0, **kw))
+        assert torch.equal(conv_op(x, w, act=2, slope=slope, bias9=b9, tile=N.FR_TILE_SMALL, split_k=sp, **kw),
+                           conv_op(x, w, act=2, slope=slope, bias9=b9, tile=0, **kw))
     _close(y32, conv_ref(x, w32, bias=bias[:32], act=1, **kw), tol=1e-2 if dtype == "bf16" else 2e-3)
 
 
