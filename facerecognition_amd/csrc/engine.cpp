@@ -1432,7 +1432,9 @@ static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, 
         // fit; else the separate split-K epilogue launch
         const int64_t tiles = (int64_t)((a.M + conv_tile_bm(c.tile) - 1) / conv_tile_bm(c.tile)) *
                               ((a.Cout + conv_tile_bn(c.tile) - 1) / conv_tile_bn(c.tile));
-        if (c.split < 0 && a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && h->splitk_inlaunch) {
+        // (the in-launch slabs are addressed by 32-bit buffer offsets)
+        if (c.split < 0 && a.y && h->splitk_cnt && tiles <= FR_SPLITK_TILES && h->splitk_inlaunch &&
+            (size_t)split * a.M * a.Npad * sizeof(float) < 0x7fffffffull) {
             a.splitk_cnt = h->splitk_cnt;
             h->inlaunch_used = true;
         }
