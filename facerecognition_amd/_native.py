@@ -32,7 +32,6 @@ FR_TILE_IMG56 = 11
 FR_TILE_ROWS = 12
 FR_TILE_WRING = 13
 FR_TILE_DIRECT = 14
-FR_TILE_BLAS = 15
 FR_TILE_SMALL = 16
 FR_OPT_STAGE = 1
 FR_OPT_KEEP_INTERMEDIATES = 2

@@ -310,9 +310,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_band_kernel(ConvArgs 
     }
 
     const int npw = __builtin_amdgcn_readfirstlane((PI - wave + NW - 1) / NW);  // this wave's patch instrs
-    const int dbg = p.dbg;
     auto issue_patch = [&](int chunk, int pb) {
-        if ((dbg & 2) && chunk > 0) return;
         const uint32_t cadd = (uint32_t)(chunk * 64 * 2);
         char* dst = smem + pb * PATCH;
 #pragma unroll
@@ -323,7 +321,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_band_kernel(ConvArgs 
             }
     };
     auto issue_w = [&](int step, int wb) {
-        if ((dbg & 1) && step >= WS) return;
         const int chunk = step / 9, tap = step - chunk * 9;
         const uint32_t kadd = (uint32_t)((tap * p.Cin + chunk * 64) * 2);
         char* dst = smem + 2 * PATCH + wb * WSL;
@@ -496,7 +493,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
         boff1[i] = boff[i] ^ 64;
     }
 
-    const int dbg = p.dbg;  // timing-only experiment switches (FR_CONV_DBG), 0 in production
     // one 1-KiB DMA piece of the next chunk's patch / of a weight slice (u < NPW / NWI); the pieces are
     // issued one per 7-MFMA group inside the k-halves so their issue cost hides behind MFMAs
     auto patch_piece = [&](int chunk, int pb, int u) {
@@ -611,8 +607,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
             if (tap == 0) wait_vmn<NPW>();
             else wait_vmn<0>();
         }
-        if (dbg & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         // k-half 1: prefetch k-half 0 of the next step; this step's slot (read-complete before the
         // barrier) receives slice step+WS (clamped to the last slice at the tail)
         const bool nxt = tap < 8 || !last_chunk;
@@ -642,15 +637,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_bandp_kernel(ConvArgs
     }
     wait_vmn<0>();  // the tail re-fetches must land before the workgroup's LDS is released
 
-    if (dbg & 4) {  // timing-only: keep the accumulators live without the epilogue's traffic
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < FN; ++i)
-#pragma unroll
-            for (int j = 0; j < FM; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-        if (t == 1234.5f) p.y[0] = 0;
-        return;
-    }
     __syncthreads();  // every wave is past its last LDS read before the staging overwrites the ring
     band_epilogue_lds<T, W, Wp, Mv, FM, FN, WM, WN>(p, acc, smem, threadIdx.x, lane, wm, wn,
                                                      (size_t)(b * H + oh0) * W, n0);

@@ -31,9 +31,6 @@ typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr int BK = 64;
-#ifndef FR_IGEMM_SCHED
-#define FR_IGEMM_SCHED 1  // K-step fragment reads pinned between MFMAs (A/B: 0 = the compiler's order)
-#endif
 constexpr uint32_t OOB = 0x80000000u;  // buffer offset past num_records → the DMA writes zeros
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -183,16 +180,14 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
     }
     int k_cur = kt0 * BK + 8 * cl;
 
-    const int dbg = p.dbg;  // timing-only experiment switches (FR_CONV_DBG), 0 in production
     auto issue = [&](int kt, int buf) {
         const char* sA = smem + buf * STAGE;
         const char* sB = sA + STAGE_A;
-        const bool skipA = (dbg & 32) && kt > kt0 + 1, skipB = (dbg & 64) && kt > kt0 + 1;
         if (FASTK && kt >= kt_x2) {  // projection K-steps: x2 at the output's stride-st2 position
             const uint32_t c2 = (uint32_t)((kt - kt_x2) * BK * 2);
 #pragma unroll
             for (int i = 0; i < NA; ++i)
-                if (!skipA) dma16(x2r, sA + (wave + NW * i) * 1024, a_base2[i] == OOB ? OOB : a_base2[i] + c2);
+                dma16(x2r, sA + (wave + NW * i) * 1024, a_base2[i] == OOB ? OOB : a_base2[i] + c2);
         } else {
             const int soff = ((r_cur * p.W + s_cur) * p.Cx + c_cur) * 2;
 #pragma unroll
@@ -201,12 +196,12 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
                 bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
                 if (!FASTK) ok = ok && k_cur < p.K;
                 const uint32_t off = ok ? a_base[i] + (uint32_t)soff : OOB;
-                if (!skipA) dma16(xr, sA + (wave + NW * i) * 1024, off);
+                dma16(xr, sA + (wave + NW * i) * 1024, off);
             }
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j)
-            if (!skipB) dma16(wr, sB + (wave + NW * j) * 1024, b_base[j] + (uint32_t)(kt * BK * 2));
+            dma16(wr, sB + (wave + NW * j) * 1024, b_base[j] + (uint32_t)(kt * BK * 2));
         // advance one K-step
         if (FASTK) {
             c_cur += BK;
@@ -247,7 +242,6 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
                 bfr[kk][j] = *(const frag*)(sA + row * BK + swz(row, ch) * 8);
             }
         };
-#if FR_IGEMM_SCHED
         // pinned order: the first half-step's fragments, then its MFMAs with the second half-step's
         // fragment reads spread between them (left to itself the scheduler issues each read just before
         // its use and waits on it there)
@@ -271,16 +265,6 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
         for (int i = 0; i < FN; ++i)
 #pragma unroll
             for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[1][i], bfr[1][j], acc[i][j]);
-#else
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            rd(kk);
-#pragma unroll
-            for (int i = 0; i < FN; ++i)
-#pragma unroll
-                for (int j = 0; j < FM; ++j) acc[i][j] = T::mfma(af[kk][i], bfr[kk][j], acc[i][j]);
-        }
-#endif
     };
 
     constexpr int G = BN / 8;            // 8-channel groups per tile row
@@ -312,7 +296,7 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
     }
     uint4 rr[ITER];
     const bool want_res = p.res && !p.partial;
-    const bool pre_res = want_res && !(p.dbg & 128);  // A/B switch: 128 = load the residual in the epilogue
+    const bool pre_res = want_res;  // the residual rides behind the last K-steps' DMA
     auto load_res = [&]() {
 #pragma unroll
         for (int it = 0; it < ITER; ++it) {
@@ -370,15 +354,6 @@ void conv_igemm_kernel(ConvArgs p, int tiles_n, int kt_per_split) {
         __syncthreads();
     }
 
-    if (dbg & 16) {  // timing-only: keep the accumulators live without the epilogue
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < FN; ++i)
-#pragma unroll
-            for (int j = 0; j < FM; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-        if (t == 1234.5f) p.y[0] = 0;
-        return;
-    }
     if (want_res && (STAGES != 2 || !pre_res)) load_res();
     // Epilogue: accumulators → LDS f32 tile [BM][EPI_LD] → coalesced 8-channel groups.
     float* sE = (float*)smem;

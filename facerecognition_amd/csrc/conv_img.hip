@@ -25,9 +25,6 @@
 namespace fr {
 namespace {
 
-#ifndef FR_IMG_EXP
-#define FR_IMG_EXP 0  // timing experiments only (tools/img_exp.sh: 1 no weight DMA, 2 no patch DMA, 4 neither); 0 in every shipped build
-#endif
 
 // Geometry of one instance: IW x IW images with IC input = output channels; a workgroup owns QR output
 // rows x all IC channels, laid out as QR rows x PCOL virtual columns (IW valid + pad) = 16-pixel frags;
@@ -95,9 +92,6 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
     // [PC positions][16 B]; halo, pad and spare pieces read out of range (zeros).  Offsets recomputed
     // per chunk (no live registers); the chunk's channel offset in the scalar offset.
     auto issue_patch = [&](int cc, int buf) {
-#if FR_IMG_EXP == 2
-        if (cc > 0) return;
-#endif
         int ln = lane;
         asm volatile("" : "+v"(ln));  // opaque copy: the offsets are not hoisted (registers for the MFMAs)
 #pragma unroll
@@ -146,9 +140,6 @@ __global__ __launch_bounds__(256, 2) void conv_img_kernel(ConvArgs p) {
     // weight slice of K-step s: pre-packed in the LDS image [g][n][16 B] (img_pack_weights), so each
     // of the WP pieces per wave is 1 KiB contiguous; the step in soffset
     auto issue_w = [&](int s, int slot) {
-#if FR_IMG_EXP == 1
-        if (s > 2) return;
-#endif
 #pragma unroll
         for (int u = 0; u < G::WP; ++u) {
             const int piece = G::WP * wave + u;

@@ -45,19 +45,6 @@ constexpr int NKS = 18;                                        // K-steps (2 cha
 constexpr int W_B = NKS * WSLICE_B;                            // 73728
 constexpr int ROWS_LDS = W_B + 2 * PATCH_B;                    // 163840 = all of the CU's LDS
 constexpr uint32_t OOB = 0x80000000u;
-#ifndef FR_ROWS_SEED_EARLY
-#define FR_ROWS_SEED_EARLY 0  // issue the next unit's seed loads before the K loop instead of after it
-#endif
-#ifndef FR_ROWS_SCHED
-#define FR_ROWS_SCHED 1  // K-step instruction order pinned with sched_group_barrier (A/B: 0 = compiler's)
-#endif
-#ifndef FR_ROWS_DRAIN
-#define FR_ROWS_DRAIN 0  // A/B: 1 = drain the unit's output stores before the next unit starts
-#endif
-#ifndef FR_ROWS_EXP
-#define FR_ROWS_EXP 0  // timing-only experiments (WRONG results): 1 trivial epilogue, 2 no K-loop MFMAs,
-                       // 4 no next-patch DMA, 8 no fragment reads in the K loop
-#endif
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -204,27 +191,20 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
     for (int k = k0; k < units; k += kstride) {
         const bool has_next = k + kstride < units;
         Unit nxt = has_next ? unit_of(k + kstride, H, W) : cur;
-        if (has_next && !(FR_ROWS_EXP & 4)) issue_patch(nxt, buf ^ 1);
-#if FR_ROWS_SEED_EARLY
-        if (has_next) load_seeds(nxt);  // a whole K loop of latency cover (registers spill to AGPRs)
-#endif
+        if (has_next) issue_patch(nxt, buf ^ 1);
         // ---- K loop: 18 steps, the next step's 9 fragments read during this step's 14 MFMAs
         read_step(0, buf, 0);
 #pragma unroll
         for (int s = 0; s < NKS; ++s) {
-#if FR_ROWS_SCHED
             __builtin_amdgcn_sched_barrier(0);
-#endif
-            if (s + 1 < NKS && !(FR_ROWS_EXP & 8)) read_step(s + 1, buf, (s + 1) & 1);
-#if !(FR_ROWS_EXP & 2)
+            if (s + 1 < NKS) read_step(s + 1, buf, (s + 1) & 1);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(fa[s & 1][i], fb[s & 1][j], acc[i][j]);
-#if FR_ROWS_SCHED
             // pinned order: one next-step fragment read behind each of the first 9 MFMAs (left to
             // itself the scheduler sinks each read to just before its use and waits on it there)
-            if (s + 1 < NKS && !(FR_ROWS_EXP & 8)) {
+            if (s + 1 < NKS) {
 #pragma unroll
                 for (int q = 0; q < 9; ++q) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -232,27 +212,10 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
                 }
                 __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
             }
-#endif
-#else
-            acc[s & 1][s % 7][0] += (float)fa[s & 1][0][0] + (float)fb[s & 1][s % 7][0];
-#endif
         }
         // ---- epilogue: the next unit's seeds load meanwhile
-#if FR_ROWS_EXP & 1
         {
-            float t = 0.f;
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 7; ++j) t += acc[i][j][0];
-            if (t == 1.2345f) p.y[lane] = 0;
-        }
-        if (false)
-#endif
-        {
-#if !FR_ROWS_SEED_EARLY
             if (has_next) load_seeds(nxt);
-#endif
             const size_t base = ((size_t)cur.b * H + cur.r0) * W + cur.c0;
             // every wave is past its K-loop reads of `buf`: it becomes the unit's output staging tile
             // [224 pixels][64 channels] (128-B rows, 16-B chunks swizzled with the pixel: conflict-free
@@ -295,12 +258,7 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
         }
         // every wave is past its copy-out reads of `buf`, which the next iteration's DMA overwrites (the
         // next patch landed before the copy-out; its stores stay in flight)
-#if FR_ROWS_DRAIN || (FR_ROWS_EXP & 1)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-#else
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
         cur = nxt;
         buf ^= 1;
     }
@@ -310,7 +268,7 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
 // processing alternate units of the workgroup's list, synchronised by LDS-counter group barriers instead of
 // s_barrier.  A SIMD then holds one wave of each group: while one group waits for its patch DMA or runs
 // its epilogue and copy-out, the other group's K loop keeps the MFMA pipe busy (the single-group kernel
-// above issues all of them from one wave per SIMD, so they add up: FR_ROWS_EXP timings).  No patch
+// above issues all of them from one wave per SIMD, so they add up, per the timing builds of round 2).  No patch
 // prefetch within a group (the other group covers the DMA); the group counters live in the unused tail
 // of each patch buffer (its DMA lanes past PSLOTS are masked off).
 constexpr int PP_SPIN_LIMIT = 1 << 22;  // group-barrier spins (x s_sleep 1) before giving up (a bug, not a wait)
@@ -434,15 +392,12 @@ __global__ __launch_bounds__(512, 1) void conv_rows_pp_kernel(ConvArgs p, int NG
         read_step(0, 0);
 #pragma unroll
         for (int s = 0; s < NKS; ++s) {
-#if FR_ROWS_SCHED
             __builtin_amdgcn_sched_barrier(0);
-#endif
             if (s + 1 < NKS) read_step(s + 1, (s + 1) & 1);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 7; ++j) acc[i][j] = T::mfma(fa[s & 1][i], fb[s & 1][j], acc[i][j]);
-#if FR_ROWS_SCHED
             if (s + 1 < NKS) {
 #pragma unroll
                 for (int q = 0; q < 9; ++q) {
@@ -451,7 +406,6 @@ __global__ __launch_bounds__(512, 1) void conv_rows_pp_kernel(ConvArgs p, int NG
                 }
                 __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
             }
-#endif
         }
         gbar(false);  // every wave of the group is past its patch reads: the buffer becomes the output tile
         const size_t base = ((size_t)cur.b * H + cur.r0) * W + cur.c0;

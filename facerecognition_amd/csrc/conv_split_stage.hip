@@ -83,10 +83,6 @@ constexpr uint32_t OOB = 0x80000000u;
 constexpr int SPIN_LIMIT = 1 << 21;       // default: x s_sleep 1 (64 cycles): ~0.1 s, then the wait has run out
 constexpr int SC1 = 16;                   // buffer-load cache policy: sc1 (L1 bypass; gfx940+ cpol bit 4)
 
-#ifndef FR_SPLIT_EXP
-#define FR_SPLIT_EXP 0  // timing-only experiments (WRONG results): 1 exchange rows without the counter
-                        // synchronisation, 2 no exchange at all, 4 trivial epilogue (MFMAs kept)
-#endif
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -273,7 +269,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     // Positions 2 and 3 leave those DMAs in flight (kstep's halo slack); position 4's wait and barrier
     // complete them before position 5 reads position 6, the first halo tap.
     auto import_halo = [&](int cv) {
-        if (wave == 0 && lane < 2 && !(FR_SPLIT_EXP & 1) && (lane == 0 ? has_up : has_dn)) {
+        if (wave == 0 && lane < 2 && (lane == 0 ? has_up : has_dn)) {
             const int* nf = my_flag + (lane == 0 ? -1 : 1);
             int it = 0;
             while (p.spin_limit < 0 ||
@@ -330,7 +326,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         for (int cg = 0; cg < C / 32; cg += 2) {
 #pragma unroll
             for (int t = 0; t < 18; ++t) {
-                if (t == HALO_POS && cg == 0 && pending >= 0 && !(FR_SPLIT_EXP & 2)) {
+                if (t == HALO_POS && cg == 0 && pending >= 0) {
                     halo = import_halo(pending);
                     pending = -1;
                 }
@@ -342,8 +338,8 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
                 // publish the previous conv's boundary rows: step 1's wait (vmcnt(1): everything but the
                 // step-0 weight DMA) and barrier have completed every wave's row stores, so the counter can
                 // go out without a drain of its own (a vmcnt(0) + barrier after the epilogue also drained
-                // the weight ring and cost ~6 % of the stage, FR_SPLIT_EXP 2 timing)
-                if (t == 1 && cg == 0 && pending >= 0 && !(FR_SPLIT_EXP & 2) && threadIdx.x == 0 && !(FR_SPLIT_EXP & 1))
+                // the weight ring and cost ~6 % of the stage in a timing build)
+                if (t == 1 && cg == 0 && pending >= 0 && threadIdx.x == 0)
                     __hip_atomic_store(my_flag, (int)((unsigned)f0 + (unsigned)(pending + 1)), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -352,17 +348,6 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         // ---- epilogue (every wave is past its last patch read): accumulators -> patch only; the global
         // copies (boundary rows, stage output, intermediates) are read back from the patch afterwards
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#if FR_SPLIT_EXP & 4
-        {  // timing-only: trivial epilogue (the accumulators stay live, nothing is written)
-            float sum = 0.f;
-#pragma unroll
-            for (int i = 0; i < FN; ++i)
-#pragma unroll
-                for (int j = 0; j < FM; ++j) sum += acc[i][j][0] + acc[i][j][3];
-            if (sum == 1.2345f) p.y[lane] = 0;
-        }
-        if (false)
-#endif
         {
             int ln = lane;
             asm volatile("" : "+v"(ln));
@@ -417,7 +402,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         // the conv's output is in the patch for every wave (the next conv's reads, the copies below)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const bool exch = cv < nconv - 1;
-        if (exch && !(FR_SPLIT_EXP & 2)) {
+        if (exch) {
             // boundary rows for the neighbours, plane-major [NPL][IW][8] per row (16-B chunks, positions
             // fastest: conflict-free LDS reads, contiguous stores), sc1 stores (the hand-off rule, header)
             for (int c = opaque_tid(); c < 2 * NPL * IW; c += 64 * NW) {
@@ -450,7 +435,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
                 }
             }
         }
-        if (exch && !(FR_SPLIT_EXP & 2)) {
+        if (exch) {
             // the rows are published at the next conv's K-step 1 (above), once every wave's stores are
             // complete; the neighbours' rows are imported at its K-step 2 (import_halo)
             pending = cv;

@@ -53,36 +53,10 @@ constexpr int SNW = 8;                       // waves per workgroup: 2 pixel hal
 constexpr int FN = 4;                        // 16-channel fragments per wave
 constexpr int NPW = 16 * FN;                 // output channels per wave
 
-// FR_STAGE_TRACE (timing experiments only, tools/stage_trace.py): workgroups 0 and TRACE_WG2 of the
-// 13-fragment kernel record the low 32 bits of the shader clock at four points of each of their first
-// TRACE_CONVS convs per wave (K loop start / end, after the epilogue's entry barrier, after its exit
-// barrier) into 2 KiB of LDS past the kernel's own (uniform ds_write: no registers held, no spills),
-// copied to g_stage_trace at the end and read back by fr_stage_trace_read.
-#ifdef FR_STAGE_TRACE
-constexpr int TRACE_CONVS = 16, TRACE_WG2 = 200, TRACE_LDS = 151552, TRACE_B = 8 * TRACE_CONVS * 4 * 4;
-__device__ unsigned int g_stage_trace[2][8][TRACE_CONVS][4];
-#define STAGE_TRACE(cv, k)                                                                              \
-    do {                                                                                                \
-        if ((blockIdx.x == 0 || blockIdx.x == TRACE_WG2) && (cv) < TRACE_CONVS) {                       \
-            const unsigned t_ = (unsigned)__builtin_readcyclecounter();                                  \
-            *(volatile __attribute__((address_space(3))) unsigned*)(uintptr_t)(                        \
-                TRACE_LDS + ((wave * TRACE_CONVS + (cv)) * 4 + (k)) * 4) = t_;                           \
-        }                                                                                               \
-    } while (0)
-#else
-#define STAGE_TRACE(cv, k) \
-    do {                   \
-    } while (0)
-#endif
 // weight-ring depths (K-steps; loads RING - 1 ahead): the 7-fragment waves of the 13-fragment kernel, which
 // wait ~30 % of each conv at the epilogue barrier for the 6-fragment ones, take 2 and fit 256 VGPRs without
 // epilogue spills; the 6-fragment waves 3; the one-wave-per-SIMD variant 6
 constexpr int RING7 = 2, RING6 = 3, RING13 = 6;
-#ifndef FR_STAGE_EXP
-#define FR_STAGE_EXP 0  // timing-only experiments (WRONG results): 8 trivial epilogue (MFMAs kept), 16 no
-                        // patch reads in the loop, 32 every weight load reads K-step 0 (stage13), 128
-                        // epilogue tables replaced by constants (no loads)
-#endif
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -163,9 +137,7 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
     auto kstep = [&](int g, int r, frag (&cur)[7], frag (&nxt)[7], int cg_n, int tap_n) {
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-#if !(FR_STAGE_EXP & 16)
         pread(nxt, cg_n, tap_n);
-#endif
         wload(wq[(r + 2) % 3], g + 2 < total ? g + 2 : total - 1);
 #pragma unroll
         for (int i = 0; i < FN; ++i)
@@ -262,22 +234,6 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
         // the weight stream and the small epilogue tables).  The barrier only needs every wave's patch
         // reads drained (the weight loads in flight go to registers).
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#if FR_STAGE_EXP & 8
-        {
-            float sum = 0.f;
-#pragma unroll
-            for (int i = 0; i < FN; ++i)
-#pragma unroll
-                for (int j = 0; j < 7; ++j) sum += acc[i][j][0] + acc[i][j][3];
-            if (sum == 1.2345f) p.y[lane] = 0;
-            if (!second) {
-#pragma unroll
-                for (int i = 0; i < FN; ++i)
-#pragma unroll
-                    for (int j = 0; j < 7; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-            }
-        }
-#else
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int cc = ln & 15;
@@ -323,7 +279,6 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage_kernel(StageArgs p) {
                 *(uint2*)slot = pk2;
             }
         }
-#endif
         // the new activation is visible to every wave before the next conv reads it (and the copies below)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         bf16_t* dbg = nullptr;
@@ -423,7 +378,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 #pragma unroll
         for (int i = 0; i < FN; ++i)
             w[i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wvo + i * 256,
-                                                                                  (FR_STAGE_EXP & 32) ? 0u : (uint32_t)g * SLICE_B, 0));
+                                                                                  (uint32_t)g * SLICE_B, 0));
     };
     // ONE fragment set, refilled in place -- the 4 MFMAs of fragment j (one per weight fragment),
     // then fragment j of the next step is read into the same registers, 4 (FM - 1) MFMAs of this wave
@@ -439,9 +394,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 #pragma unroll
             for (int i = 0; i < FN; ++i)
                 acc[i][j] = T::mfma(wq[r][i], pf[j], acc[i][j]);
-#if !(FR_STAGE_EXP & 16)
             pf[j] = *(const frag*)(pa + aoff[j]);
-#endif
         }
         __builtin_amdgcn_sched_group_barrier(0x020, FN, 0);
 #pragma unroll
@@ -509,7 +462,6 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         }
         pread(pA, 0, 0);
         const int g0 = cv * KSTEPS;
-        STAGE_TRACE(cv, 0);
 #pragma unroll 1
         for (int cg = 0; cg < SC / 32; cg += 2) {
 #pragma unroll
@@ -522,9 +474,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             }
         }
         // ---- epilogue (as stage_kernel's): accumulators -> patch; spare-slot lanes write nothing
-        STAGE_TRACE(cv, 1);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        STAGE_TRACE(cv, 2);
         // Fragment-major: the lane's slot for (j, i) is its B-fragment base aoff[j] moved to the output
         // channel plane (n >> 3 = 8 wn + 2 i + (g >> 1), byte (n & 7) * 2 = (g & 1) * 8), and x (conv1) is
         // read right where it is consumed (preloaded per n-fragment, the 7 x were spilled to scratch)
@@ -563,7 +513,6 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        STAGE_TRACE(cv, 3);
         bf16_t* dbg = nullptr;
         if (p.dbg_x) dbg = second ? p.dbg_x[cv >> 1] : p.dbg_t[cv >> 1];
         bf16_t* const yo = second && cv == nconv - 1 ? p.y : dbg;
@@ -591,13 +540,6 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         run_conv(2 * blk, std::false_type{});
         run_conv(2 * blk + 1, std::true_type{});
     }
-#ifdef FR_STAGE_TRACE
-    __syncthreads();
-    if (blockIdx.x == 0 || blockIdx.x == TRACE_WG2) {
-        const int c = opaque_tid();
-        if (c < 512) ((unsigned*)g_stage_trace)[(blockIdx.x == 0 ? 0 : 512) + c] = ((const unsigned*)(smem + TRACE_LDS))[c];
-    }
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -625,13 +567,6 @@ __global__ __launch_bounds__(256, 1) void stage13w_kernel(StageArgs p) {
 
 }  // namespace
 
-#ifdef FR_STAGE_TRACE
-extern "C" int fr_stage_trace_read(unsigned int* out, int n) {
-    const int all = (int)(sizeof(g_stage_trace) / sizeof(unsigned int));
-    if (n < all) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_trace), sizeof(g_stage_trace)) == hipSuccess ? all : -2;
-}
-#endif
 
 bool stage_supported(int B, int H, int W, int C) { return B > 0 && H == SW && W == SW && C == SC; }
 
@@ -658,12 +593,7 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t s) {
     auto k = v == 1   ? (a.f16 ? stage_kernel<true> : stage_kernel<false>)
              : v == 2 ? (a.f16 ? stage13w_kernel<true> : stage13w_kernel<false>)
                       : (a.f16 ? stage13_kernel<true> : stage13_kernel<false>);
-#ifdef FR_STAGE_TRACE
-    static_assert(TRACE_LDS == STAGE13_LDS, "trace area");
-    const int lds = v == 1 ? STAGE_LDS : STAGE13_LDS + TRACE_B;
-#else
     const int lds = v == 1 ? STAGE_LDS : STAGE13_LDS;
-#endif
     const int threads = v == 2 ? 256 : 64 * SNW;
     static bool attr[6] = {false, false, false, false, false, false};
     const int ai = 2 * v + (a.f16 ? 1 : 0);

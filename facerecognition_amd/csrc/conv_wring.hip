@@ -64,35 +64,9 @@ __device__ __forceinline__ void wait_vm() {
 }
 constexpr uint32_t OOB = 0x80000000u;
 
-#ifndef FR_WRING_EXP
-#define FR_WRING_EXP 0  // timing-only experiments (WRONG results): 1 every weight load reads substep 0,
-                        // 2 every stage DMA reads K-step 0
-#endif
-#ifndef FR_WRING_SCHED
-#define FR_WRING_SCHED 1  // substep order pinned with sched_group_barrier (A/B: 0 = the compiler's)
-#endif
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-// FR_WRING_TRACE (timing experiments only, tools/wring_trace.py): blocks 0 and WTRACE_B2 stamp the low 32
-// bits of the shader clock per wave at kernel start (0), after the prologue (1), before each of the first
-// WTRACE_ST stage-boundary waits (2 + 2t) and after its barrier (3 + 2t), at the main loop's end and at the
-// kernel's end, into LDS past the kernel's own; copied to g_wring_trace at the end (the last launch wins).
-#ifdef FR_WRING_TRACE
-constexpr int WTRACE_ST = 40, WTRACE_N = 4 + 2 * WTRACE_ST, WTRACE_B2 = 100;
-__device__ unsigned int g_wring_trace[2][8][WTRACE_N];
-#define WTRACE(ldsb, k)                                                                                     \
-    do {                                                                                                    \
-        if ((blockIdx.x == 0 || blockIdx.x == WTRACE_B2) && (k) < WTRACE_N) {                               \
-            const unsigned t_ = (unsigned)__builtin_readcyclecounter();                                      \
-            *(volatile __attribute__((address_space(3))) unsigned*)(uintptr_t)((ldsb) + (wave * WTRACE_N + (k)) * 4) = t_; \
-        }                                                                                                   \
-    } while (0)
-#else
-#define WTRACE(ldsb, k) \
-    do {                \
-    } while (0)
-#endif
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const char* lds, uint32_t voff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
@@ -109,7 +83,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    WTRACE(Gm::LDS, 0);
     const int lid = xcd_remap(blockIdx.x, gridDim.x);
     const int tn = lid / tiles_m, tm = lid - tn * tiles_m;  // pixels fastest: an XCD keeps one weight half
     const int m0 = tm * BM, n0 = tn * BN;
@@ -164,7 +137,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
             const uint32_t o2 = a_base2[i] == OOB ? OOB : a_base2[i] + c2;
             d_off[i] = d_x2 ? o2 : o1;
         }
-        if (FR_WRING_EXP & 2) return;
         k_cur += CH;
         c_cur += CH;
         if (c_cur == p.Cin) {
@@ -194,7 +166,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
 #pragma unroll
         for (int i = 0; i < 2; ++i)
             w[i] = __builtin_bit_cast(frag, __builtin_amdgcn_raw_buffer_load_b128(wr, wvo + i * 256,
-                                                                                  (FR_WRING_EXP & 1) ? 0u : (uint32_t)s * wstep, 0));
+                                                                                  (uint32_t)s * wstep, 0));
     };
 
     // B fragment j, substep kk of a stage: row 16 j + (lane & 15), logical chunk 4 kk + (lane >> 4)
@@ -225,7 +197,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
     for (int q = 0; q < WD - 1; ++q) wload(wq[q], q);
     wait_vm<3 * PPW + Gm::WP>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    WTRACE(Gm::LDS, 1);
     bread(bq[0], 0, 0);
 
     auto mfmas = [&](int slot_w, frag (&b)[FM]) {
@@ -260,39 +231,32 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
                 if (kk + 1 < KSS) {
                     bread(bq[(kk + 1) & 1], slot, kk + 1);
                     mfmas(w, bq[kk & 1]);
-#if FR_WRING_SCHED
 #pragma unroll
                     for (int q = 0; q < FM; ++q) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     }
-#endif
                 } else {
                     prep();  // stage t + 4's offsets while the previous substep's MFMAs run
-                    WTRACE(Gm::LDS, 2 + 2 * t);
                     if (t >= 2) wait_vm<Gm::Yb>();
                     else if (t == 1) wait_vm<Gm::Yb1>();
                     else wait_vm<Gm::Yb0>();
                     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                    WTRACE(Gm::LDS, 3 + 2 * t);
                     __builtin_amdgcn_sched_barrier(0);
                     fire(slot);  // stage t + 4 into stage t's slot
                     bread(bq[(kk + 1) & 1], nslot, 0);
                     mfmas(w, bq[kk & 1]);
-#if FR_WRING_SCHED
 #pragma unroll
                     for (int q = 0; q < FM; ++q) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     }
-#endif
                 }
             }
         }
     }
 
     // ---- epilogue: accumulators -> f32 LDS tile [BM][EPI_LD] -> coalesced 8-channel groups
-    WTRACE(Gm::LDS, WTRACE_N - 2);
     constexpr int G = BN / 8, RS = 64 * NW / G, ITER = BM / RS;  // 32 groups, 16 rows per pass, 7 passes
     static_assert(RS * G == 64 * NW && ITER * RS == BM, "epilogue mapping");
     const int g = tid % G, ml0 = tid / G, n = n0 + g * 8;
@@ -355,14 +319,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wring_kernel(ConvArgs p,
         }
         *(uint4*)(p.y + (size_t)m * p.Cy + p.y_off + n) = F16 && p.y_bf16 ? Num<false>::pack8(v) : T::pack8(v);
     }
-#ifdef FR_WRING_TRACE
-    WTRACE(Gm::LDS, WTRACE_N - 1);
-    __syncthreads();
-    if (blockIdx.x == 0 || blockIdx.x == WTRACE_B2)
-        for (int c = tid; c < NW * WTRACE_N; c += 64 * NW)
-            ((unsigned*)g_wring_trace)[(blockIdx.x == 0 ? 0 : 8 * WTRACE_N) + c] =
-                *(volatile __attribute__((address_space(3))) unsigned*)(uintptr_t)(Gm::LDS + c * 4);
-#endif
 }
 
 // out[s][g][n][e] = w[n][32 s + 8 g + e]: one 32-deep substep image per s
@@ -403,11 +359,7 @@ hipError_t launch_kss(const ConvArgs& a, hipStream_t s) {
     typedef WGeo<KSS, NW> Gm;
     const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.Cout / Gm::BN;
     auto k = a.f16 ? conv_wring_kernel<true, KSS, NW> : conv_wring_kernel<false, KSS, NW>;
-#ifdef FR_WRING_TRACE
-    const int lds = Gm::LDS + 8 * WTRACE_N * 4;
-#else
     const int lds = Gm::LDS;
-#endif
     static bool attr[2] = {false, false};
     if (!attr[a.f16 ? 1 : 0]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -431,13 +383,6 @@ static bool use_kss4(const ConvArgs& a) {
     return ok && force != 2;
 }
 
-#ifdef FR_WRING_TRACE
-extern "C" int fr_wring_trace_read(unsigned int* out, int n) {
-    const int all = (int)(sizeof(g_wring_trace) / sizeof(unsigned int));
-    if (n < all) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wring_trace), sizeof(g_wring_trace)) == hipSuccess ? all : -2;
-}
-#endif
 
 hipError_t launch_conv_wring(const ConvArgs& a, hipStream_t s) {
     if (!wring_supported(a) || !a.wimg) return hipErrorInvalidValue;

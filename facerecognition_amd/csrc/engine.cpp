@@ -96,6 +96,13 @@ struct StageRec {
     bool fp8 = false;                     // e4m3 stage (conv_stage8.hip): the members carry .wscale
     uint8_t* w8 = nullptr;                // fp8: stage8_pack_weights images of all convs
     float* wscale = nullptr;              // fp8: [2*nblk][256] per-channel weight scales
+    // fused transition block (conv_trans.hip, IResNet100 layer1.0): conv_ops = {conv1, conv2 + downsample}
+    bool trans = false;
+    bf16_t* tw1 = nullptr;                // trans_pack_weights images of conv1 / conv2 + downsample
+    bf16_t* tw2 = nullptr;
+    float* tep1 = nullptr;                // [9][64] conv1 bias per border class
+    float* tsl1 = nullptr;                // [64] conv1 PReLU slopes
+    float* tb2 = nullptr;                 // [64] conv2 + downsample bias
 };
 
 // One LDS-resident Inception-ResNet block (conv_block.hip): its member convs as a program of steps over
@@ -111,7 +118,7 @@ struct BlockRec {
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
-constexpr size_t FR_MAX_SPLIT_STAGES = 4;  // stage ops per plan (at most one per residual layer)
+constexpr size_t FR_MAX_SPLIT_STAGES = 6;  // stage ops per plan (at most one per residual layer + the transition)
 constexpr int FR_SPLITK_TILES = 1 << 16;   // in-launch split-K tile counters per handle
 
 }  // namespace
@@ -176,7 +183,6 @@ struct fr_handle {
     struct Tuned { int key[13]; int tile, split; };  // the measured kernel choice per conv shape (tune_conv)
     std::vector<Tuned> tuned;
     std::vector<int> tuned_batches;
-    void* blas = nullptr;  // hipBLASLt state of the FR_TILE_BLAS choice (blas.cpp), created on first use
     struct StageMeas { int stage, B, run; float t_stage, t_conv; };  // measured stage-vs-per-conv choice per batch
     std::vector<StageMeas> stage_meas;
     bool tuning = false;
@@ -810,6 +816,7 @@ int build_stage(fr_handle* h, StageRec& r) {
 // Device pointer table of a stage's intermediate tensors (filled after every activation reserve).
 int fill_stage_dbg(fr_handle* h) {
     for (auto& r : h->stages) {
+        if (r.trans) continue;  // no intermediates: the member convs run when they are kept
         std::vector<bf16_t*> p(2 * r.nblk);
         for (int i = 0; i < r.nblk; ++i) {
             p[i] = h->tensors[r.x_tensors[i]].dev;
@@ -818,6 +825,41 @@ int fill_stage_dbg(fr_handle* h) {
         FR_HIP_CHECK(hipMemcpy(r.dbg, p.data(), p.size() * sizeof(bf16_t*), hipMemcpyHostToDevice));
     }
     return FR_OK;
+}
+
+// Packs a fused transition block (conv_trans.hip) from its member convs' device weights.
+int build_trans(fr_handle* h, StageRec& r) {
+    const DevConvW& c1 = h->convw[h->ops[r.conv_ops[0]].wi];
+    const DevConvW& c2 = h->convw[h->ops[r.conv_ops[1]].wi];
+    if (c1.K != 576 || c2.K != 640 || c2.K1 != 576 || c2.C2 != 64 || c1.Cout != 64 || c2.Cout != 64 || !c1.slope ||
+        (!c1.bias9 && !c1.bias) || !c2.bias) {
+        set_error("plan: transition block members do not match the fused kernel");
+        return FR_ERR_ARG;
+    }
+    void* q = nullptr;
+    int rc = dev_alloc(&q, trans_packed_elems(c1.K) * sizeof(bf16_t));
+    if (rc) return rc;
+    h->weight_allocs.push_back(q);
+    r.tw1 = (bf16_t*)q;
+    if ((rc = dev_alloc(&q, trans_packed_elems(c2.K) * sizeof(bf16_t)))) return rc;
+    h->weight_allocs.push_back(q);
+    r.tw2 = (bf16_t*)q;
+    FR_HIP_CHECK(trans_pack_weights(c1.w, c1.Kpad, c1.K, r.tw1, 0));
+    FR_HIP_CHECK(trans_pack_weights(c2.w, c2.Kpad, c2.K, r.tw2, 0));
+    FR_HIP_CHECK(hipDeviceSynchronize());
+    std::vector<float> ep(9 * 64), sl(64), b2(64);
+    if (c1.bias9) {
+        for (int k = 0; k < 9; ++k)
+            FR_HIP_CHECK(hipMemcpy(ep.data() + k * 64, c1.bias9 + (size_t)k * c1.Npad, 64 * sizeof(float), hipMemcpyDeviceToHost));
+    } else {
+        FR_HIP_CHECK(hipMemcpy(ep.data(), c1.bias, 64 * sizeof(float), hipMemcpyDeviceToHost));
+        for (int k = 1; k < 9; ++k) std::copy(ep.begin(), ep.begin() + 64, ep.begin() + k * 64);
+    }
+    FR_HIP_CHECK(hipMemcpy(sl.data(), c1.slope, 64 * sizeof(float), hipMemcpyDeviceToHost));
+    FR_HIP_CHECK(hipMemcpy(b2.data(), c2.bias, 64 * sizeof(float), hipMemcpyDeviceToHost));
+    if ((rc = upload(h, &r.tep1, ep))) return rc;
+    if ((rc = upload(h, &r.tsl1, sl))) return rc;
+    return upload(h, &r.tb2, b2);
 }
 
 std::string L(int l, int i) { return "layer" + std::to_string(l) + "." + std::to_string(i); }
@@ -875,10 +917,21 @@ void build_iresnet100(Builder& b) {
                 h->ops.push_back(op);
             }
             const int Hin = i == 0 ? H : Ho, st = i == 0 ? 2 : 1;
+            const bool fuse = i == 0 && b.fuse_ds(P, C, pre);
+            // layer1.0 as one fused launch (conv_trans.hip) beside its member convs (measured per batch size)
+            const bool tr = i == 0 && fuse && !b.is_fp8(pre + ".conv1") && !b.is_fp8(pre + ".conv2") &&
+                            trans_supported(1, H, H, C, P, P, 9 * C, 9 * P + C);
+            int tr_op = -1;
+            if (tr) {
+                tr_op = (int)h->ops.size();
+                Op op;
+                op.kind = OP_STAGE;
+                op.stage = (int)h->stages.size();
+                h->ops.push_back(op);
+            }
             const int hmid = b.tensor(Hin, Hin, P, pre + ".prelu");
             b.conv({pre + ".conv1"}, x, 0, C, hmid, 0, 3, 3, 1, 1, 1, 1, 2);
             int res = x;
-            const bool fuse = i == 0 && b.fuse_ds(P, C, pre);
             if (i == 0 && !fuse) {
                 res = b.tensor(Ho, Ho, P, pre + ".downsample");
                 b.conv({pre + ".downsample"}, x, 0, C, res, 0, 1, 1, 2, 2, 0, 0, 0);
@@ -889,6 +942,17 @@ void build_iresnet100(Builder& b) {
                           x, C, 2);
             else
                 b.conv({pre + ".conv2"}, hmid, 0, P, y, 0, 3, 3, st, st, 1, 1, 0, res, 0);
+            if (tr && !b.rc) {
+                StageRec t;
+                t.trans = true;
+                t.in = x; t.out = y; t.nblk = 1; t.H = H; t.C = P;
+                t.conv_ops = {(int)h->ops.size() - 2, (int)h->ops.size() - 1};
+                t.t_tensors = {hmid};
+                t.x_tensors = {y};
+                for (int oi : t.conv_ops) h->ops[oi].stage = h->ops[tr_op].stage;
+                b.rc = build_trans(h, t);
+                h->stages.push_back(t);
+            }
             if (st_op >= 0 && !b.rc) {
                 rec.conv_ops.push_back((int)h->ops.size() - 2);
                 rec.conv_ops.push_back((int)h->ops.size() - 1);
@@ -1239,22 +1303,6 @@ bool band_enabled() {
     return on;
 }
 
-int conv_dbg() {
-    static const int d = [] {
-        const char* e = getenv("FR_CONV_DBG");
-        return e ? atoi(e) : 0;
-    }();
-    return d;
-}
-
-int stage_dbg() {
-    static const int d = [] {
-        const char* e = getenv("FR_STAGE_DBG");
-        return e ? atoi(e) : 0;
-    }();
-    return d;
-}
-
 hipEvent_t prof_event(fr_handle* h) {
     if (!h->ev_free.empty()) { hipEvent_t e = h->ev_free.back(); h->ev_free.pop_back(); return e; }
     hipEvent_t e = nullptr;
@@ -1378,15 +1426,6 @@ static int fit_split(const fr_handle* h, const ConvArgs& a, int split) {
 
 // The fixed policy (no measurement: FR_AUTOTUNE=0, a forced FR_CONV_TILE): the specialised kernels where they
 // apply (each measured faster than the implicit GEMM at bs = 256), else conv_plan's cost-model tile and split.
-// hipBLASLt (FR_TILE_BLAS) is an autotuner candidate only with FR_BLAS=1 (not yet measured faster on a whole
-// forward; its f32 summation order differs from the implicit GEMM's in every conv it takes).
-static bool blas_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_BLAS");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
 
 static ConvChoice default_choice(const fr_handle* h, const ConvArgs& a) {
     ConvChoice c;
@@ -1404,9 +1443,6 @@ static hipError_t launch_choice(fr_handle* h, ConvArgs& a, const ConvChoice& c, 
     a.split_k = 1;
     a.partial = nullptr;
     switch (c.tile) {
-        case FR_TILE_BLAS:
-            if (!h->blas) h->blas = blas_create();
-            return launch_conv_blas(h->blas, a, s);
         case FR_TILE_SMALL: return launch_conv_small(a, c.split, s);
         case FR_TILE_ROWS: {
             ConvArgs r = a;
@@ -1456,7 +1492,6 @@ static std::string choice_class(const ConvArgs& a, const ConvChoice& c) {
         }
         case FR_TILE_WRING: return "conv_wring";
         case FR_TILE_DIRECT: return "conv_direct";
-        case FR_TILE_BLAS: return "blas gemm";
         case FR_TILE_SMALL: return "conv_small";
         default:
             return "conv_igemm tile" + std::to_string(c.tile) + (c.split > 1 ? " splitk" : c.split < -1 ? " splitk-inlaunch" : "");
@@ -1492,7 +1527,6 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
         if (wring_supported(w)) add(TILE_WRING, 1);
     }
     if (direct_enabled() && direct_supported(a)) add(TILE_DIRECT, 1);  // small-K direct conv
-    if (blas_enabled() && blas_supported(a)) add(FR_TILE_BLAS, 1);       // 1x1 conv as a library GEMM
     // small M (a few hundred pixels: small batches): one wave per 16 px x 64 ch, no LDS, no second launch
     // (split 4 / 8: that many waves share a tile's K, summed through LDS)
     static const bool small_nf4 = [] {  // FR_SMALL_NF4=1: only the 64-channel tiles (A/B)
@@ -1568,7 +1602,6 @@ static bool choice_ok(const ConvArgs& a, const ConvChoice& c) {
             return a.wring_ && wring_supported(w);
         }
         case FR_TILE_DIRECT: return direct_supported(a);
-        case FR_TILE_BLAS: return blas_enabled() && blas_supported(a);
         case FR_TILE_SMALL: return small_split_ok(c.split) && small_supported(a, (c.split >> 8) ? (c.split >> 8) : 4);
         default: return c.tile >= 0;
     }
@@ -1581,7 +1614,6 @@ static ConvChoice conv_choice(const fr_handle* h, const ConvArgs& a) {
 }
 
 int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
-    a.dbg = conv_dbg();
     ProfScope ps(h, s);
     ps.flops = conv_flops(a);
     ps.bytes = conv_bytes(a);
@@ -1628,8 +1660,19 @@ static bool split_stage_enabled(int H) {
 
 static int stage_choice(const fr_handle* h, int st, int B);
 
+// FR_NO_TRANS=1: IResNet100 layer1.0 always runs as its two member convs (A/B timing)
+static bool trans_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FR_NO_TRANS");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     if (h->stage_mode == 0) return false;
+    // the fused transition keeps no t tensor and records no amax
+    if (r.trans && (h->keep_inter || (h->amax && h->need_amax[r.out]) || !trans_enabled())) return false;
     if (r.parts > 1 && (h->no_split || !split_stage_enabled(r.H))) return false;
     if (h->stage_mode == 1) {  // measured at this batch size (measure_stage)
         const int c = stage_choice(h, st, B);
@@ -1776,6 +1819,20 @@ static bool ms_enabled() {
 // One LDS-resident stage launch (+ the amax pass an e4m3 reader of its output needs).
 static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vector<char>& stage_run, hipStream_t s) {
     const StageRec& r = h->stages[op.stage];
+    if (r.trans) {
+        TransArgs t{};
+        t.x = h->tensors[r.in].dev;
+        t.y = h->tensors[r.out].dev;
+        t.w1 = r.tw1; t.w2 = r.tw2; t.ep1 = r.tep1; t.slope1 = r.tsl1; t.b2 = r.tb2;
+        t.B = B; t.f16 = f16;
+        ProfScope ps(h, s);
+        // conv1 (B x 112^2 x 64 x 576) + conv2 with the downsample (B x 56^2 x 64 x 640)
+        ps.flops = 2.0 * B * (12544.0 * 64 * 576 + 3136.0 * 64 * 640);
+        ps.bytes = 2.0 * B * (12544.0 + 3136.0) * 64 + 2.0 * 64 * (576 + 640);
+        ps.start("trans layer1.0");
+        FR_HIP_CHECK(launch_trans(t, s));
+        return FR_OK;
+    }
     StageArgs a{};
     a.x = h->tensors[r.in].dev;
     a.y = h->tensors[r.out].dev;
@@ -1787,7 +1844,6 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
     a.B = B;
     a.nblk = r.nblk;
     a.f16 = f16;
-    a.dbg = stage_dbg();
     a.xchg = h->stage_xchg;
     a.flags = h->stage_flags + (size_t)h->max_batch * 4 * op.stage;  // the stage's own counter region
     a.spin_timeouts = h->stage_spin;
@@ -2197,7 +2253,6 @@ void fr_destroy(fr_handle* h) {
     DevSerial::reg(h, false);
     if (h->chk_ev) (void)hipEventDestroy(h->chk_ev);
     if (h->async_ev) (void)hipEventDestroy(h->async_ev);
-    if (h->blas) blas_destroy(h->blas);
     if (h->fail_host) (void)hipHostFree(h->fail_host);
     delete h;
 }
@@ -2620,6 +2675,12 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
     const std::vector<char> stage_run = stage_plan(h, B);
     for (const auto& op : h->ops) {
         if (op_skipped(op, stage_run)) continue;
+        if (op.kind == OP_STAGE && h->stages[op.stage].trans) {  // M x 64 x 2944 MACs = conv1 + conv2 + downsample
+            const StageRec& r = h->stages[op.stage];
+            out += "trans " + std::to_string(B * 3136) + " 64 2944 2944 1 1 3x3 " + h->tensors[r.out].name +
+                   meas_note(h, op.grp, B) + "\n";
+            continue;
+        }
         if (op.kind == OP_STAGE) {
             const StageRec& r = h->stages[op.stage];
             const std::string K = std::to_string(9 * r.C);
@@ -2959,15 +3020,6 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
             return FR_ERR_ARG;
         }
         FR_HIP_CHECK(launch_conv_small(a, sp, (hipStream_t)stream));
-        return FR_OK;
-    }
-    if (d->tile == FR_TILE_BLAS + 1) {  // a per-call library state: the op API holds no handle
-        if (!blas_supported(a)) { set_error("fr_op_conv2d: library GEMM not applicable (1x1 / stride 1 / ReLU)"); return FR_ERR_ARG; }
-        void* st = blas_create();
-        const hipError_t e = launch_conv_blas(st, a, (hipStream_t)stream);
-        (void)hipStreamSynchronize((hipStream_t)stream);
-        blas_destroy(st);
-        FR_HIP_CHECK(e);
         return FR_OK;
     }
     if (d->tile == FR_TILE_DIRECT + 1) {

@@ -26,7 +26,6 @@ struct ConvArgs {
     float* partial; int split_k;  // partial != null: raw f32 partials [split][M][Npad], no epilogue
     int f16;                      // 0: bf16 storage + bf16 MFMA; 1: f16 storage + f16 MFMA
     int tile;                     // TILE_* variant (conv_plan)
-    int dbg;                      // experiment switches (FR_CONV_DBG env; 0 in production)
     void* ev0;                    // optional hipEvent_t pair stamped by the dispatch itself
     void* ev1;                    //   (hipExtLaunchKernel; fr_prof_* timing), null normally
     // fp8 path (conv_fp8.hip): e4m3 weights [Npad][Kpad] (Kpad = bytes per row, % 128), per-channel
@@ -74,12 +73,6 @@ hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s);
 bool small_supported(const ConvArgs& a, int nf = 4);
 bool small_split_ok(int split);
 hipError_t launch_conv_small(const ConvArgs& a, int split, hipStream_t s);
-// 1x1 stride-1 convs as hipBLASLt GEMMs (blas.cpp): bias + ReLU epilogue, residual as beta * C.  The state (library
-// handle, 32-MiB workspace, per-conv descriptors and algorithm) lives per fr_handle.
-bool blas_supported(const ConvArgs& a);
-void* blas_create();
-void blas_destroy(void* state);
-hipError_t launch_conv_blas(void* state, const ConvArgs& a, hipStream_t s);
 constexpr int FR_AMAX_SLOTS = 64;  // engine: spreads the producers' atomics over 64 addresses
 // max |x| of n (% 8) bf16/f16 values into amax[0 .. slots) (misc.hip): for tensors an fp8 conv reads whose
 // producer has no amax epilogue (an LDS-resident stage)
@@ -138,7 +131,7 @@ struct StageArgs {
     int* fail_host;            // host-mapped flag: set to 1 (plain vector store) by any part whose wait ran out
     int spin_limit;            // sleeps before a wait counts as run out; < 0: every wait runs out (debug)
     int variant;               // kernel variant (FR_OPT_STAGE_VARIANT): 0 default, 1 the legacy layout
-    int B, nblk, f16, dbg;     // dbg: timing-only experiment switches (FR_STAGE_DBG), 0 in production
+    int B, nblk, f16;
     void* ev0;
     void* ev1;
 };
@@ -187,6 +180,25 @@ struct BlockArgs {
 size_t block_lds_bytes(int G, int H, int W, int ld);
 bool block_supported(const BlockArgs& a);
 hipError_t launch_block(const BlockArgs& a, hipStream_t s);
+// Fused IResNet100 transition block layer1.0 (conv_trans.hip): conv1 3x3/s1 + PReLU (t rows kept in LDS) ->
+// conv2 3x3/s2 + the K-concatenated 1x1/s2 downsample + bias, one workgroup per image; x [B][112][112][64] ->
+// y [B][56][56][64].  w1 / w2 = trans_pack_weights images of conv1 (K 576) and conv2 + downsample (K 640).
+struct TransArgs {
+    const bf16_t* x;
+    bf16_t* y;
+    const bf16_t* w1;
+    const bf16_t* w2;
+    const float* ep1;     // [9][64] conv1 bias per border class (bn1 folded)
+    const float* slope1;  // [64] conv1 PReLU slopes
+    const float* b2;      // [64] conv2 + downsample bias
+    int B, f16;
+    void* ev0;
+    void* ev1;
+};
+bool trans_supported(int B, int H, int W, int Cin, int Cmid, int Cout, int K1, int K2);
+size_t trans_packed_elems(int K);
+hipError_t trans_pack_weights(const bf16_t* w, int Kpad, int K, bf16_t* out, hipStream_t s);
+hipError_t launch_trans(const TransArgs& a, hipStream_t s);
 // Split-K reduction + the same fused epilogue as the conv kernel.
 hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
 // Number of K-tiles of 64 (for split-k planning).

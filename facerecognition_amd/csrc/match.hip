@@ -170,9 +170,6 @@ __global__ __launch_bounds__(256) void match_partial_kernel(const float* __restr
 // waits and one LDS-only barrier per chunk.  (The old kernel staged both operands per chunk through
 // registers behind full barriers; register prefetch one chunk ahead left each block one 16-KB load in
 // flight and ran 74 us at 256 x 10k, latency bound.)
-#ifndef FR_MATCH_EXP
-#define FR_MATCH_EXP 0  // timing-only experiments (WRONG results): 1 no MFMAs, 2 no top-k filter, 4 no chunk DMA
-#endif
 constexpr int D512 = 512;
 constexpr int NBUF = 4;                    // chunk ring depth (3 chunks in flight)
 constexpr int CHUNK_B = MG * KC * 4;       // 16384
@@ -257,11 +254,9 @@ __global__ __launch_bounds__(256, 1) void match_p512_kernel(const float* __restr
         for (int ch = 0; ch < D512 / KC; ++ch) {
             // chunk 8 tl + ch landed: only the two chunks issued after it (8 DMAs) may be in flight
             __builtin_amdgcn_sched_barrier(0);
-            if (FR_MATCH_EXP & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             lds_barrier();
-            if (!(FR_MATCH_EXP & 4)) issue_chunk(8 * tl + ch + NBUF - 1);  // into the buffer read last chunk
-            else asm volatile("s_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0" ::: "memory");
+            issue_chunk(8 * tl + ch + NBUF - 1);  // into the buffer read last chunk
             const char* buf = smem + (ch % NBUF) * CHUNK_B;
             // all 16 B fragments of the chunk first, one LDS wait (left alone the compiler waits before every
             // 4 MFMAs, and one wave per SIMD cannot hide that), then the MFMAs with the 4 accumulators
@@ -279,11 +274,6 @@ __global__ __launch_bounds__(256, 1) void match_p512_kernel(const float* __restr
 #pragma unroll
             for (int t16 = 0; t16 < KC / 16; ++t16) {
                 const float4 a4 = pa[(KC / 16) * ch + t16];
-                if (FR_MATCH_EXP & 1) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[j][0] += a4.x * b4[t16][j].x + b4[t16][j].w;
-                    continue;
-                }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4[t16][j].x, acc[j], 0, 0, 0);
 #pragma unroll
@@ -301,7 +291,7 @@ __global__ __launch_bounds__(256, 1) void match_p512_kernel(const float* __restr
             for (int r = 0; r < 4; ++r)
                 sS[(16 * wave + 4 * (lane >> 4) + r) * (MG + 1) + 16 * j + (lane & 15)] = acc[j][r];
         lds_barrier();
-        if (!(FR_MATCH_EXP & 2)) {
+        {
             // filter (no branches: all 16 scores read, 32-bit indices), then the few inserts.  Threshold:
             // the best of the probe's 4 sub-lists' last entries (lanes 4p .. 4p+3): that sub-list holds
             // KMAX >= k entries at least that good, so nothing worse can reach the split's top k

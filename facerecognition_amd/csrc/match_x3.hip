@@ -29,9 +29,6 @@
 namespace fr {
 namespace {
 
-#ifndef FR_X3_EXP
-#define FR_X3_EXP 0  // timing experiments only (tools/x3_exp.sh); 0 in every shipped build
-#endif
 
 constexpr int XW = 8;         // waves per block
 constexpr int XP = 16 * XW;   // probes per block
@@ -184,9 +181,6 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
     const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(GT + g_chunk0 * XCHUNK_E), 0,
                                                                         (int)min(g_left, (size_t)0x7fffffff), 0x00020000);
     auto issue_chunk = [&](int64_t t0, int c, int slot) {
-#if FR_X3_EXP == 2  // timing experiment: no gallery stream
-        return;
-#endif
         const uint32_t cbase = (uint32_t)((((t0 - g_begin) / XG) * 8 + c) * XCHUNK_B);
 #pragma unroll
         for (int u = 0; u < XPPW; ++u) {
@@ -229,15 +223,6 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
         thr = fmaxf(thr, __shfl_xor(thr, 32));
         thr2 = fminf(thr2, __shfl_xor(thr2, 32));
         thr = fmaxf(thr, thr2);
-#if FR_X3_EXP == 3  // timing experiment: no insert (the compares still run)
-        {
-            uint32_t m = 0;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) m |= (a[e >> 2][e & 3] > thr) << e;
-            asm volatile("" ::"v"(m));
-        }
-        return;
-#endif
         uint32_t m = 0;
 #pragma unroll
         for (int e = 0; e < 16; ++e) m |= a[e >> 2][e & 3] > thr ? 1u << e : 0u;
@@ -282,13 +267,9 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
                     const bf8v gl = *(const bf8v*)(ch + XCHUNK_B / 2 + o);
                     // gallery rows as the A operand: D[row][probe], so each lane's accumulators belong to
                     // ONE probe (its own candidate sub-list) and the filter never leaves the registers
-#if FR_X3_EXP == 1  // timing experiment: no MFMA
-                    acc[j][0] += (float)gh[t & 7] + (float)gl[t & 7];
-#else
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, ph[t], acc[j], 0, 0, 0);
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl, ph[t], acc[j], 0, 0, 0);
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, pl[t], acc[j], 0, 0, 0);
-#endif
                 }
             }
         }

@@ -258,7 +258,7 @@ typedef struct fr_conv_desc {
                                 autotuned per shape against the igemm tiles (env FR_NO_WRING=1: off) */
 #define FR_TILE_DIRECT 14    /* persistent small-K direct conv (conv_direct.hip): Cin % 8 == 0, Kpad <= 384, Cout % 32 == 0,
                                 bias + activation epilogue; autotuned per shape (env FR_NO_DIRECT=1: off) */
-#define FR_TILE_BLAS 15      /* 1x1 stride-1 conv as a hipBLASLt GEMM (bias + ReLU / residual epilogue); an autotuner candidate */
+/* 15: retired (round 5; a hipBLASLt candidate that never won a whole forward) */
 #define FR_TILE_SMALL 16     /* small-M implicit GEMM, one wave per 16 px x 64 ch over the whole K (conv_small.hip); bit-identical to tile 0.
                                 split_k = KS | NF << 8: KS (4 / 8 / 16) waves share a tile's K (split-K summation order), NF
                                 (2 / 1; 0 = 4) 16-channel fragments per tile: 1, 4, 8, 1|2<<8, 4|2<<8, 8|2<<8, 1|1<<8, 4|1<<8,

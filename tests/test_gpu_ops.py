@@ -932,27 +932,3 @@ def test_conv_small(gpu, case, dtype):
         assert torch.equal(conv_op(x, w, act=2, slope=slope, bias9=b9, tile=N.FR_TILE_SMALL, split_k=sp, **kw),
                            conv_op(x, w, act=2, slope=slope, bias9=b9, tile=0, **kw))
     _close(y32, conv_ref(x, w32, bias=bias[:32], act=1, **kw), tol=1e-2 if dtype == "bf16" else 2e-3)
-
-
-BLAS_CASES = [
-    # B, H, W, Cin, Cout, act, residual   (IRV1 / ResNet-50 1x1 shapes, smaller batches)
-    (4, 8, 8, 896, 256, 1, False), (4, 8, 8, 256, 896, 1, True), (2, 17, 17, 256, 96, 1, False),
-    (2, 3, 3, 1792, 384, 0, False), (2, 28, 28, 512, 128, 1, False), (2, 14, 14, 256, 1024, 1, True)]
-
-
-@pytest.mark.parametrize("case", BLAS_CASES)
-def test_conv_blas(gpu, case):
-    """1x1 convs as hipBLASLt GEMMs (blas.cpp, forced): the library's bias + ReLU epilogue and the residual as
-    beta * C, against the fp32 reference (only the f32 summation order differs from the implicit GEMM)."""
-    B, H, W, Cin, Cout, act, with_res = case
-    g = torch.Generator().manual_seed(B + H + Cin + Cout)
-    x = torch.randn(B, H, W, Cin, generator=g).to(torch.bfloat16).to(gpu)
-    w = torch.randn(Cout, Cin, 1, 1, generator=g) / np.sqrt(Cin)
-    bias = torch.randn(Cout, generator=g) * 0.1
-    res = torch.randn(B, H, W, Cout, generator=g).to(torch.bfloat16).to(gpu) if with_res else None
-    y = conv_op(x, w, bias=bias, act=act, res=res, tile=N.FR_TILE_BLAS)
-    _close(y, conv_ref(x, w, bias=bias, act=act, res=res))
-    y0 = conv_op(x, w, bias=bias, act=act, res=res, tile=0)
-    assert float((y.float() - y0.float()).abs().max()) <= 2e-2 * float(y0.float().abs().max())
-    with pytest.raises(RuntimeError, match="library GEMM"):  # a 3x3 conv is not a plain GEMM
-        conv_op(x, torch.randn(Cout, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_BLAS)
