@@ -374,7 +374,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, embed_ms = float(t[0]), float(t[1])
     # sanity: top-1 indices are valid global gallery rows (FR_TIMING_ONLY=1: timing-only experiment
-    # libraries, tools/build_variant.sh, whose results are wrong by construction)
+    # libraries, tools/variant.sh, whose results are wrong by construction)
     if os.environ.get("FR_TIMING_ONLY") != "1":
         assert int(out_i[:, 0].min()) >= 0 and int(out_i[:, 0].max()) < rows
 

@@ -14,6 +14,9 @@ namespace fr {
 
 // Thread-local last-error plumbing (defined in engine.cpp).
 void set_error(const std::string& msg);
+// A/B switches from the FR_AB environment variable (engine.cpp): "key" or "key=value", comma separated
+const char* ab_str(const char* key);
+int ab_int(const char* key, int dflt);
 
 #define FR_HIP_CHECK(expr)                                                        \
     do {                                                                          \

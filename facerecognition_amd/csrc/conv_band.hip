@@ -694,10 +694,7 @@ static hipError_t launch_band_k(const ConvArgs& a, hipStream_t s) {
 // Applicability: 3x3 / stride 1 / pad 1, Cin % 64 == 0, a supported (W, TH) band, Cout a multiple of
 // the variant's BN.  Returns the band config id (see launch_conv_band).
 static bool band_legacy() {
-    static const bool on = [] {
-        const char* e = getenv("FR_BAND_LEGACY");
-        return e && e[0] == '1';
-    }();
+    static const bool on = [] { return ab_int("band_legacy", 0) != 0; }();
     return on;
 }
 

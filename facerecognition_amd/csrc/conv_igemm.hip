@@ -568,12 +568,9 @@ static int tile_blocks_per_cu(int tile) {
 
 // Tile + split-K choice: minimise rounds-of-resident-blocks x per-block work / tile efficiency,
 // plus a charge for split-K (partials round trip + reduce kernel + prologue/epilogue amortised over
-// fewer K-steps).  A forced variant via FR_CONV_TILE=<id> (env) is honoured for experiments.
+// fewer K-steps).  A forced variant via FR_AB conv_tile=<id> (env) is honoured for experiments.
 static int env_tile_id() {
-    static const int t = [] {
-        const char* e = getenv("FR_CONV_TILE");
-        return e ? atoi(e) : -1;
-    }();
+    static const int t = [] { return ab_int("conv_tile", -1); }();
     return t;
 }
 
@@ -630,15 +627,15 @@ void conv_plan(int M, int Cout, int Kpad, int* tile, int* split) {
 
 // The embedding head (M = batch, N = 512, K = 25,088 at 7x7x512): a few output tiles over a very long K, so
 // split-K wide enough to give every CU a block (conv_plan stopped at 16 splits of the 2-stage tile: 256 blocks
-// of 24 K-steps at bs = 256, 43 us); splits that divide the K-steps evenly, >= 4 K-steps each.  FR_HEAD_PLAN=tile,split
+// of 24 K-steps at bs = 256, 43 us); splits that divide the K-steps evenly, >= 4 K-steps each.  FR_AB head_plan=tile:split
 // overrides (experiments).
 void head_plan(int M, int Cout, int Kpad, int* tile, int* split) {
     struct EnvPlan { int tile = -1, split = -1; };
     static const EnvPlan env = [] {
         EnvPlan e;
-        const char* v = getenv("FR_HEAD_PLAN");
+        const char* v = ab_str("head_plan");  // "tile:split"
         int t = -1, sp = -1;
-        if (v && sscanf(v, "%d,%d", &t, &sp) == 2 && t >= 0 && sp >= 1) { e.tile = t; e.split = sp; }
+        if (v && sscanf(v, "%d:%d", &t, &sp) == 2 && t >= 0 && sp >= 1) { e.tile = t; e.split = sp; }
         return e;
     }();
     if (env.tile >= 0) {

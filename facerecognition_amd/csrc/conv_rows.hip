@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256, 1) void conv_rows_kernel(ConvArgs p, int NG, i
     }
 }
 
-// Ping-pong variant (FR_ROWS_PP, default): 8 waves = two groups of 4, each with its own patch buffer,
+// Ping-pong variant (FR_AB rows_pp, default): 8 waves = two groups of 4, each with its own patch buffer,
 // processing alternate units of the workgroup's list, synchronised by LDS-counter group barriers instead of
 // s_barrier.  A SIMD then holds one wave of each group: while one group waits for its patch DMA or runs
 // its epilogue and copy-out, the other group's K loop keeps the MFMA pipe busy (the single-group kernel
@@ -479,10 +479,7 @@ hipError_t launch_conv_rows(const ConvArgs& a, int n_cu, hipStream_t s) {
     int grid = (n_cu / NG) * NG;                       // every workgroup owns one n-group
     if (grid > units * NG) grid = units * NG;
     const bool act = a.act != 0;
-    static const bool pp = [] {
-        const char* e = getenv("FR_ROWS_PP");
-        return !(e && e[0] == '0');
-    }();
+    static const bool pp = [] { return ab_int("rows_pp", 1) != 0; }();
     auto k = pp ? (a.res ? (act ? conv_rows_pp_kernel<true, 2> : conv_rows_pp_kernel<true, 0>)
                          : (act ? conv_rows_pp_kernel<false, 2> : conv_rows_pp_kernel<false, 0>))
                 : (a.res ? (act ? conv_rows_kernel<true, 2> : conv_rows_kernel<true, 0>)

@@ -251,11 +251,8 @@ bool stem_u8_supported(int H, int W, int Cin, int K, int Kpad, int Cout, int Cy,
 hipError_t launch_stem_u8(const uint8_t* in, int B, const bf16_t* w, int Kpad, const float* bias, const float* slope,
                           int act, bf16_t* y, int Cy, int y_off, int f16, hipStream_t s) {
     // persistent blocks: 3 per CU (the VGPR limit), trip counts balanced so no block runs an extra
-    // round; FR_STEM_PERSIST=0 launches one block per tile (weights re-staged per tile)
-    static const bool persist = [] {
-        const char* e = getenv("FR_STEM_PERSIST");
-        return !(e && e[0] == '0');
-    }();
+    // round; FR_AB stem_persist=0 launches one block per tile (weights re-staged per tile)
+    static const bool persist = [] { return ab_int("stem_persist", 1) != 0; }();
     if ((size_t)B * SW * SW * 3 >= 0x80000000ull) return hipErrorInvalidValue;  // buffer offsets are 31-bit
     const int ntiles = B * (SW / SROWS);
     int nblk = ntiles;

@@ -65,6 +65,23 @@ __device__ __forceinline__ void dma16(const v4i32& rsrc, uint32_t lds_addr, uint
 }
 #pragma clang diagnostic pop
 
+// acc += w * b with the weight fragment in AGPRs (the whole weight set stays in the accumulator half of the
+// register file for the kernel; hipcc only offers MFMA operands from VGPRs and would copy every fragment
+// through v_accvgpr_read).  Not volatile: the scheduler may interleave it like the builtin.  hipcc does not pad
+// inline asm, so: a VALU-written accumulator seed needs 2 wait states before its first MFMA (the FIRST form),
+// and the MFMA result needs 8 before a VALU reads it (mfma_drain() ahead of such reads).
+template <bool F16, bool FIRST = false>
+__device__ __forceinline__ void mfma_aw(f32x4_t& acc, const typename Num<F16>::frag& w, const typename Num<F16>::frag& b) {
+    if (F16) {
+        if (FIRST) asm("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(b));
+        else asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(b));
+    } else {
+        if (FIRST) asm("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(b));
+        else asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(b));
+    }
+}
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7" ::: "memory"); }
+
 
 template <bool F16>
 __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
@@ -176,18 +193,41 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
     const float4 b2v = *(const float4*)(tab + 10 * TCH + n2);
 
     f32x4_t acc1[2][7], acc2[4], accd[4];
-    frag bx[2][7], bt[2][4];
     bf16_t* const yb = p.y + (size_t)b * OW * OW * TCH;
+    // one x-row DMA piece (u: 0..3 of row 2s + 3, 4..7 of row 2s + 4), spread over loop A's first K-steps
+    auto dma_piece = [&](int s, int u) {
+        const int row = 2 * s + 3 + (u >> 2), piece = wave + 4 * (u & 3);
+        if (row <= TW && piece < XPIECES && piece * 64 + lane < XQ) {
+            const bool rin = row < TW;
+            const uint32_t off = rin && colpart[u & 3] != OOB
+                                     ? (uint32_t)(((size_t)b * TW + row) * TW * TCH * 2) + colpart[u & 3]
+                                     : OOB;
+            dma16(xr, (uint32_t)(uintptr_t)(smem + X_OFF + ((row + 1) % XSLOTS) * XROW_B + piece * 1024), off);
+        }
+    };
+    // conv1 epilogue of tile (i, j): PReLU -> bf16 -> the t row's slot
+    auto epi1 = [&](char* tb, int i, int j) {
+        float v[8];
+        v[0] = fmaf(s1m[i].x, min0_raw(acc1[i][j][0]), acc1[i][j][0]);
+        v[1] = fmaf(s1m[i].y, min0_raw(acc1[i][j][1]), acc1[i][j][1]);
+        v[2] = fmaf(s1m[i].z, min0_raw(acc1[i][j][2]), acc1[i][j][2]);
+        v[3] = fmaf(s1m[i].w, min0_raw(acc1[i][j][3]), acc1[i][j][3]);
+        v[4] = v[5] = v[6] = v[7] = 0.f;
+        const uint4 pk = T::pack8(v);
+        *(uint2*)(tb + 1024 * j + te[i]) = make_uint2(pk.x, pk.y);
+    };
 
+    // Phase s: conv1 of t rows 2s, 2s+1 (s = 56: rows 112, 113, discarded), the downsample of output row s and
+    // conv2 of output row s - 1 (s = 0: of row 0 from the zero / not yet written t slots, discarded).  Two
+    // K loops: A = conv1 fragments 0..3 (+ the downsample's 2 K-steps, + the next rows' DMA pieces);
+    // B = conv1 fragments 4..6 + conv2, with the epilogue of fragments 0..3 interleaved; then the epilogue
+    // of fragments 4..6 and conv2's stores.  Every phase runs the same instruction stream.
 #pragma unroll 1
     for (int s = 0; s < NPH; ++s) {
-        const bool has1 = s < OW, has2 = s > 0;
-        // x rows of the next phase (rows past the bottom halo row 112 are never read)
-        if (2 * s + 3 <= TW) dma_row(2 * s + 3);
-        if (2 * s + 4 <= TW) dma_row(2 * s + 4);
-        if (has1) {
-            // ---- conv1: t row tr = 2s + r1, seeds = bias of the border class
-            const int tr = 2 * s + r1;
+        const int tr = 2 * s + r1;  // this wave's t row
+        const int o = s > 0 ? s - 1 : 0;  // conv2's output row
+        // seeds: conv1 = bias of the border class, downsample = b2 (conv2 then starts from the downsample)
+        {
             const int rc = tr == 0 ? 0 : (tr == TW - 1 ? 2 : 1);
 #pragma unroll
             for (int j = 0; j < 7; ++j) {
@@ -198,67 +238,93 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
                     acc1[i][j] = (f32x4_t){bb.x, bb.y, bb.z, bb.w};
                 }
             }
-            // x row of tap row dh: tr + dh - 1 -> slot (tr + dh) % 6
-            auto xread = [&](int ks, int buf) {
-                const int tap = ks >> 1, cg = ks & 1, dh = tap / 3, dw = tap % 3;
-                const int xb = X_OFF + ((tr + dh) % XSLOTS) * XROW_B;
-#pragma unroll
-                for (int j = 0; j < 7; ++j) bx[buf][j] = *(const frag*)(smem + xb + 2048 * j + (xo[dw] ^ (cg << 6)));
-            };
-            xread(0, 0);
-#pragma unroll
-            for (int ks = 0; ks < KS1; ++ks) {
-                if (ks + 1 < KS1) xread(ks + 1, (ks + 1) & 1);
-#pragma unroll
-                for (int j = 0; j < 7; ++j)
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) acc1[i][j] = T::mfma(w1[ks][i], bx[ks & 1][j], acc1[i][j]);
-            }
-            // ---- conv1 epilogue: PReLU -> t ring slot (tr + 1) % 5
-            char* const tb = smem + T_OFF + ((tr + 1) % TSLOTS) * TROW_B;
-#pragma unroll
-            for (int j = 0; j < 7; ++j)
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    float v[8];
-                    v[0] = fmaf(s1m[i].x, min0_raw(acc1[i][j][0]), acc1[i][j][0]);
-                    v[1] = fmaf(s1m[i].y, min0_raw(acc1[i][j][1]), acc1[i][j][1]);
-                    v[2] = fmaf(s1m[i].z, min0_raw(acc1[i][j][2]), acc1[i][j][2]);
-                    v[3] = fmaf(s1m[i].w, min0_raw(acc1[i][j][3]), acc1[i][j][3]);
-                    v[4] = v[5] = v[6] = v[7] = 0.f;
-                    const uint4 pk = T::pack8(v);
-                    *(uint2*)(tb + 1024 * j + te[i]) = make_uint2(pk.x, pk.y);
-                }
-            // ---- downsample of output row s: x row 2s (slot (2s + 1) % 6), seeded with b2
-            const int xdb = X_OFF + ((2 * s + 1) % XSLOTS) * XROW_B;
 #pragma unroll
             for (int j = 0; j < 4; ++j) accd[j] = (f32x4_t){b2v.x, b2v.y, b2v.z, b2v.w};
-#pragma unroll
-            for (int cg = 0; cg < 2; ++cg) {
-                frag bd[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) bd[j] = *(const frag*)(smem + xdb + 4096 * j + (xd ^ (cg << 6)));
-#pragma unroll
-                for (int j = 0; j < 4; ++j) accd[j] = T::mfma(w2[KS1 + cg], bd[j], accd[j]);
-            }
         }
-        if (has2) {
-            // ---- conv2 of output row o = s - 1: t row 2o + dh - 1 -> slot (2o + dh) % 5
-            const int o = s - 1;
-            auto tread = [&](int ks, int buf) {
-                const int tap = ks >> 1, cg = ks & 1, dh = tap / 3, dw = tap % 3;
-                const int tb2 = T_OFF + ((2 * o + dh) % TSLOTS) * TROW_B;
+        // x row of tap row dh for this wave's t row: tr + dh - 1 -> slot (tr + dh) % 6
+        int xb[3];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bt[buf][j] = *(const frag*)(smem + tb2 + 2048 * j + (to2[dw] ^ (cg << 6)));
+        for (int dh = 0; dh < 3; ++dh) xb[dh] = X_OFF + ((tr + dh) % XSLOTS) * XROW_B;
+        int tb2[3];  // conv2: t row 2o + dh - 1 -> slot (2o + dh) % 5
+#pragma unroll
+        for (int dh = 0; dh < 3; ++dh) tb2[dh] = T_OFF + ((2 * o + dh) % TSLOTS) * TROW_B;
+        const int xdb = X_OFF + ((2 * s + 1) % XSLOTS) * XROW_B;  // downsample: x row 2s
+
+        // ---- loop A: conv1 fragments 0..3, the downsample at K-steps 0 / 1, DMA pieces at K-steps 0..7
+        {
+            frag ba[2][4], bd[2][4];
+            auto rdA = [&](int ks, int buf) {
+                const int tap = ks >> 1, cg = ks & 1, dh = tap / 3, dw = tap % 3;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ba[buf][j] = *(const frag*)(smem + xb[dh] + 2048 * j + (xo[dw] ^ (cg << 6)));
             };
-            tread(0, 0);
+            auto rdD = [&](int cg) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bd[cg][j] = *(const frag*)(smem + xdb + 4096 * j + (xd ^ (cg << 6)));
+            };
+            rdA(0, 0);
+            rdD(0);
 #pragma unroll
             for (int ks = 0; ks < KS1; ++ks) {
-                if (ks + 1 < KS1) tread(ks + 1, (ks + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+                if (ks + 1 < KS1) rdA(ks + 1, (ks + 1) & 1);
+                if (ks == 0) rdD(1);
+                if (ks < 8) dma_piece(s, ks);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc2[j] = T::mfma(w2[ks], bt[ks & 1][j], acc2[j]);
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (ks == 0) mfma_aw<F16, true>(acc1[i][j], w1[ks][i], ba[ks & 1][j]);
+                        else mfma_aw<F16>(acc1[i][j], w1[ks][i], ba[ks & 1][j]);
+                    }
+                if (ks < 2) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (ks == 0) mfma_aw<F16, true>(accd[j], w2[KS1 + ks], bd[ks][j]);
+                        else mfma_aw<F16>(accd[j], w2[KS1 + ks], bd[ks][j]);
+                    }
+                }
             }
-            // ---- conv2 epilogue: y row o (columns >= 56 are padding)
+        }
+        // ---- loop B: conv1 fragments 4..6 + conv2 of output row o; the epilogue of fragments 0..3 rides along
+        char* const tb = smem + T_OFF + ((tr + 1) % TSLOTS) * TROW_B;  // this wave's t row slot
+        {
+            frag bb[2][3], bt[2][4];
+            auto rdB = [&](int ks, int buf) {
+                const int tap = ks >> 1, cg = ks & 1, dh = tap / 3, dw = tap % 3;
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    bb[buf][j] = *(const frag*)(smem + xb[dh] + 2048 * (4 + j) + (xo[dw] ^ (cg << 6)));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bt[buf][j] = *(const frag*)(smem + tb2[dh] + 2048 * j + (to2[dw] ^ (cg << 6)));
+            };
+            rdB(0, 0);
+#pragma unroll
+            for (int ks = 0; ks < KS1; ++ks) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (ks + 1 < KS1) rdB(ks + 1, (ks + 1) & 1);
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (ks == 0) mfma_aw<F16, true>(acc1[i][4 + j], w1[ks][i], bb[ks & 1][j]);
+                        else mfma_aw<F16>(acc1[i][4 + j], w1[ks][i], bb[ks & 1][j]);
+                    }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (ks == 0) mfma_aw<F16, true>(acc2[j], w2[ks], bt[ks & 1][j]);
+                    else mfma_aw<F16>(acc2[j], w2[ks], bt[ks & 1][j]);
+                }
+                if (ks >= 1 && ks <= 8) epi1(tb, (ks - 1) & 1, (ks - 1) >> 1);
+            }
+        }
+        // ---- tail: epilogue of fragments 4..6, conv2's output row, the downsample sums become conv2's seeds
+        mfma_drain();  // the last MFMAs' results are read by VALU below
+#pragma unroll
+        for (int j = 4; j < 7; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) epi1(tb, i, j);
+        if (s > 0) {
             bf16_t* const yr = yb + (size_t)o * OW * TCH + n2;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -271,7 +337,7 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc2[j] = accd[j];
         // the next phase's x rows landed (the y stores may stay in flight), every t write is done
-        if (has2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (s > 0) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

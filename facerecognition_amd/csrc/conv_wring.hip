@@ -373,12 +373,9 @@ hipError_t launch_kss(const ConvArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// 128-channel stages where the channel counts allow (FR_WRING_KSS=2 forces 64-channel stages)
+// 128-channel stages where the channel counts allow (FR_AB wring_kss=2 forces 64-channel stages)
 static bool use_kss4(const ConvArgs& a) {
-    static const int force = [] {
-        const char* e = getenv("FR_WRING_KSS");
-        return e ? atoi(e) : 0;
-    }();
+    static const int force = [] { return ab_int("wring_kss", 0); }();
     const bool ok = a.Cin % 128 == 0 && (!a.x2 || a.C2 % 128 == 0) && a.Kpad % 128 == 0 && a.Kpad / 128 >= 3;
     return ok && force != 2;
 }

@@ -25,6 +25,36 @@
 namespace fr {
 static thread_local std::string g_err;
 void set_error(const std::string& m) { g_err = m; }
+
+// A/B and debugging switches, all in one environment variable read once per process:
+//   FR_AB="no_trans,no_wring,stage_variant=1,head_plan=8:14"  (a bare key = 1; DESIGN.md §7 lists the keys)
+static const std::vector<std::pair<std::string, std::string>>& ab_table() {
+    static const std::vector<std::pair<std::string, std::string>> t = [] {
+        std::vector<std::pair<std::string, std::string>> r;
+        const char* e = getenv("FR_AB");
+        const std::string v = e ? e : "";
+        size_t p = 0;
+        while (p < v.size()) {
+            size_t q = v.find(',', p);
+            if (q == std::string::npos) q = v.size();
+            const std::string tok = v.substr(p, q - p);
+            const size_t eq = tok.find('=');
+            if (!tok.empty()) r.emplace_back(tok.substr(0, eq), eq == std::string::npos ? "1" : tok.substr(eq + 1));
+            p = q + 1;
+        }
+        return r;
+    }();
+    return t;
+}
+const char* ab_str(const char* key) {
+    for (const auto& kv : ab_table())
+        if (kv.first == key) return kv.second.c_str();
+    return nullptr;
+}
+int ab_int(const char* key, int dflt) {
+    const char* v = ab_str(key);
+    return v ? atoi(v) : dflt;
+}
 }  // namespace fr
 
 using namespace fr;
@@ -661,14 +691,11 @@ struct Builder {
 
     // whether a residual block's downsample folds into its last conv (igemm K-concatenation): not for
     // e4m3 convs (the fp8 kernel has no projection source) and only on the 64-channel fast-K path;
-    // FR_NO_DS_FUSE=1 keeps the separate downsample conv (A/B)
+    // FR_AB no_ds_fuse keeps the separate downsample conv (A/B)
     // whether conv `name` runs in e4m3 (FR_DTYPE_FP8 and the blob's plan gave it a .wscale)
     bool is_fp8(const std::string& name) { return h->dtype == FR_DTYPE_FP8 && find(name + ".wscale"); }
     bool fuse_ds(int cin, int c2, const std::string& pre) {
-        static const bool off = [] {
-            const char* e = getenv("FR_NO_DS_FUSE");
-            return e && e[0] == '1';
-        }();
+        static const bool off = [] { return ab_int("no_ds_fuse", 0) != 0; }();
         return !off && !is_fp8(pre + ".conv2") && !is_fp8(pre + ".downsample") && cin % 64 == 0 && c2 % 64 == 0;
     }
     // An Inception-ResNet block run as one conv_block.hip launch: begin_block() before its convs, end_block()
@@ -1262,44 +1289,29 @@ int reserve(fr_handle* h, int maxB) {
 }
 
 // layer2 band kernel (conv_img.hip): 80 us per conv vs 86 us for the implicit GEMM
-// (profiles/r01_img28.txt); FR_NO_IMG28=1 falls back to the implicit GEMM
+// (profiles/r01_img28.txt); FR_AB no_img28 falls back to the implicit GEMM
 bool img28_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_IMG28");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_img28", 0); }();
     return on;
 }
 
 bool rows_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_ROWS");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_rows", 0); }();
     return on;
 }
 
 bool img56_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_IMG56");
-        return e && e[0] == '1';
-    }();
+    static const bool on = [] { return ab_int("img56", 0) != 0; }();
     return on;
 }
 
 bool stem_fuse_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_STEM_FUSE");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_stem_fuse", 0); }();
     return on;
 }
 
 bool band_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_BAND");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_band", 0); }();
     return on;
 }
 
@@ -1360,10 +1372,7 @@ double conv_bytes(const ConvArgs& a) {
 }
 
 bool autotune_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_AUTOTUNE");
-        return !(e && e[0] == '0');
-    }();
+    static const bool on = [] { return ab_int("autotune", 1) != 0; }();
     return on;
 }
 
@@ -1391,18 +1400,12 @@ static bool find_tuned(const fr_handle* h, const ConvArgs& a, ConvChoice* c) {
 }
 
 static bool wring_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_WRING");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_wring", 0); }();
     return on;
 }
 
 static bool direct_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_DIRECT");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_direct", 0); }();
     return on;
 }
 
@@ -1424,7 +1427,7 @@ static int fit_split(const fr_handle* h, const ConvArgs& a, int split) {
     return split;
 }
 
-// The fixed policy (no measurement: FR_AUTOTUNE=0, a forced FR_CONV_TILE): the specialised kernels where they
+// The fixed policy (no measurement: FR_AB autotune=0, a forced FR_AB conv_tile): the specialised kernels where they
 // apply (each measured faster than the implicit GEMM at bs = 256), else conv_plan's cost-model tile and split.
 
 static ConvChoice default_choice(const fr_handle* h, const ConvArgs& a) {
@@ -1529,10 +1532,8 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     if (direct_enabled() && direct_supported(a)) add(TILE_DIRECT, 1);  // small-K direct conv
     // small M (a few hundred pixels: small batches): one wave per 16 px x 64 ch, no LDS, no second launch
     // (split 4 / 8: that many waves share a tile's K, summed through LDS)
-    static const bool small_nf4 = [] {  // FR_SMALL_NF4=1: only the 64-channel tiles (A/B)
-        const char* e = getenv("FR_SMALL_NF4");
-        return e && e[0] == '1';
-    }();
+    // FR_AB small_nf4: only the 64-channel tiles (A/B)
+    static const bool small_nf4 = [] { return ab_int("small_nf4", 0) != 0; }();
     if (a.M <= 8192)
         for (int sp : {1, 4, 8, 4 | 2 << 8, 8 | 2 << 8, 4 | 1 << 8, 8 | 1 << 8, 16 | 1 << 8})
             if ((!small_nf4 || sp < 256) && small_supported(a, (sp >> 8) ? (sp >> 8) : 4)) add(FR_TILE_SMALL, sp);
@@ -1648,24 +1649,18 @@ int run_conv_args(fr_handle* h, ConvArgs& a, hipStream_t s) {
 // either way, since per-conv grids of B*196 positions are a handful of tiles.  Above one round a last
 // round that is mostly empty costs a whole stage time, so auto mode then requires the rounds to be at
 // least stage_min_fill % full (B = 512: 100 %, B = 257: 50 % -> per-conv).
-// A split stage puts one image on `parts` CUs: a round is n_cu / parts images.  FR_NO_SPLIT_STAGE=1 /
+// A split stage puts one image on `parts` CUs: a round is n_cu / parts images.  FR_AB no_split_stage /
 // =28 / =56 turns the split stages off (all / layer2 / layer1) for A/B timing.
 static bool split_stage_enabled(int H) {
-    static const int off = [] {
-        const char* e = getenv("FR_NO_SPLIT_STAGE");
-        return e ? atoi(e) : 0;
-    }();
+    static const int off = [] { return ab_int("no_split_stage", 0); }();
     return !(off == 1 || off == H);
 }
 
 static int stage_choice(const fr_handle* h, int st, int B);
 
-// FR_NO_TRANS=1: IResNet100 layer1.0 always runs as its two member convs (A/B timing)
+// FR_AB no_trans: IResNet100 layer1.0 always runs as its two member convs (A/B timing)
 static bool trans_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_TRANS");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_trans", 0); }();
     return on;
 }
 
@@ -1684,12 +1679,9 @@ static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     return (int64_t)B * 100 >= (int64_t)h->stage_min_fill * rounds * cap;
 }
 
-// FR_NO_BLOCK=1: the IRV1 blocks always run per conv (A/B timing).
+// FR_AB no_block: the IRV1 blocks always run per conv (A/B timing).
 static bool block_enabled() {
-    static const bool off = [] {
-        const char* e = getenv("FR_NO_BLOCK");
-        return e && e[0] == '1';
-    }();
+    static const bool off = [] { return ab_int("no_block", 0) != 0; }();
     return !off;
 }
 
@@ -1802,12 +1794,9 @@ bool rgn_hit(const std::vector<Rgn>& a, const std::vector<Rgn>& b) {
 // 3 same-box pairs) and ResNet-50 (157.0-157.9k vs 157.8-158.5k): the branches' kernels size their grids
 // for the whole GPU (persistent conv_direct / conv_rows, full igemm tile grids), so two of them at once
 // share the CUs instead of filling idle ones.
-// FR_NO_HEAD_GEMV=1: the small-batch head runs on the implicit-GEMM tiles too (A/B timing)
+// FR_AB no_head_gemv: the small-batch head runs on the implicit-GEMM tiles too (A/B timing)
 static bool head_gemv_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_HEAD_GEMV");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_head_gemv", 0); }();
     return on;
 }
 
@@ -2181,10 +2170,7 @@ extern "C" {
 const char* fr_last_error(void) { return g_err.c_str(); }
 int fr_abi_version(void) { return FR_ABI_VERSION; }
 
-static int stage_default() {
-    const char* e = getenv("FR_NO_STAGE");
-    return (e && e[0] == '1') ? 0 : 1;
-}
+static int stage_default() { return ab_int("no_stage", 0) ? 0 : 1; }
 
 int fr_create(fr_handle** out, int device, int arch, int dtype) {
     if (!out || !valid_arch(arch) || (dtype != FR_DTYPE_BF16 && dtype != FR_DTYPE_F16 && dtype != FR_DTYPE_FP8)) {
@@ -2204,9 +2190,9 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->dtype = dtype;
     h->in_size = arch == FR_ARCH_IRV1_FACENET ? 160 : 112;
     h->stage_mode = stage_default();
-    if (const char* e = getenv("FR_SPLITK_INLAUNCH")) h->splitk_inlaunch = e[0] != '0';  // A/B timing
-    if (const char* e = getenv("FR_STAGE_VARIANT")) {  // A/B timing
-        const int v = atoi(e);
+    h->splitk_inlaunch = ab_int("splitk_inlaunch", 1) != 0;  // A/B timing
+    {
+        const int v = ab_int("stage_variant", 0);  // A/B timing
         h->stage_variant = v == 1 || v == 2 ? v : 0;
     }
     hipDeviceProp_t prop;
@@ -2307,10 +2293,7 @@ int fr_embed_dim(const fr_handle* h) { return h ? (h->proj_d ? h->proj_d : h->em
 int fr_input_size(const fr_handle* h) { return h ? h->in_size : 0; }
 
 static bool graphs_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_GRAPH");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_graph", 0); }();
     return on;
 }
 
@@ -2551,12 +2534,9 @@ static int ensure_cand(fr_handle* h, size_t need) {
     return FR_OK;
 }
 
-// FR_NO_MATCH_ROWS=1: small batches take the MFMA match kernels too (A/B timing)
+// FR_AB no_match_rows: small batches take the MFMA match kernels too (A/B timing)
 static bool match_rows_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_NO_MATCH_ROWS");
-        return !(e && e[0] == '1');
-    }();
+    static const bool on = [] { return !ab_int("no_match_rows", 0); }();
     return on;
 }
 

@@ -408,10 +408,7 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
 }  // namespace
 
 static bool p512_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FR_MATCH_P512");
-        return !(e && e[0] == '0');
-    }();
+    static const bool on = [] { return ab_int("match_p512", 1) != 0; }();
     return on;
 }
 
@@ -424,10 +421,7 @@ void match_split_plan(int B, int64_t N, int D, int k, int* n_split, int64_t* row
         const int64_t pb = (B + MP - 1) / MP, T = (N + MG - 1) / MG;
         int64_t best_r = 1;
         double best = 1e30;
-        static const int env_r = [] {
-            const char* e = getenv("FR_MATCH_TILES");  // experiments: tiles per split
-            return e ? atoi(e) : 0;
-        }();
+        static const int env_r = ab_int("match_tiles", 0);  // experiments: tiles per split
         for (int64_t r = 1; r <= T && r <= 64; ++r) {
             if (env_r > 0 && r != std::min<int64_t>(env_r, std::min<int64_t>(T, 64))) continue;
             const int64_t blocks = pb * ((T + r - 1) / r);

@@ -251,13 +251,13 @@ typedef struct fr_conv_desc {
 #define FR_TILE_128x64_S3 8  /* 3-stage DMA ring, 2 blocks/CU */
 #define FR_TILE_64x128_S3 9  /* 3-stage DMA ring, 2 blocks/CU */
 #define FR_TILE_IMG56 11     /* the same for 56x56x64->64 (layer1), 4-row bands */
-#define FR_TILE_IMG28 10     /* row-band direct 3x3/s1/p1 28x28x128->128 bf16 kernel (conv_img.hip); auto-selected (env FR_NO_IMG28=1: off) */
+#define FR_TILE_IMG28 10     /* row-band direct 3x3/s1/p1 28x28x128->128 bf16 kernel (conv_img.hip); auto-selected (FR_AB no_img28: off) */
 #define FR_TILE_ROWS 12      /* persistent weight-resident 3x3/s1/p1 kernel for Cin = 64, Cout % 64 == 0, W % 56 == 0,
-                              * H % 4 == 0, bf16 (conv_rows.hip); auto-selected (env FR_NO_ROWS=1: off) */
+                              * H % 4 == 0, bf16 (conv_rows.hip); auto-selected (FR_AB no_rows: off) */
 #define FR_TILE_WRING 13     /* implicit GEMM with a register weight ring (conv_wring.hip): Cin % 64 == 0, Cout % 256 == 0;
-                                autotuned per shape against the igemm tiles (env FR_NO_WRING=1: off) */
+                                autotuned per shape against the igemm tiles (FR_AB no_wring: off) */
 #define FR_TILE_DIRECT 14    /* persistent small-K direct conv (conv_direct.hip): Cin % 8 == 0, Kpad <= 384, Cout % 32 == 0,
-                                bias + activation epilogue; autotuned per shape (env FR_NO_DIRECT=1: off) */
+                                bias + activation epilogue; autotuned per shape (FR_AB no_direct: off) */
 /* 15: retired (round 5; a hipBLASLt candidate that never won a whole forward) */
 #define FR_TILE_SMALL 16     /* small-M implicit GEMM, one wave per 16 px x 64 ch over the whole K (conv_small.hip); bit-identical to tile 0.
                                 split_k = KS | NF << 8: KS (4 / 8 / 16) waves share a tile's K (split-K summation order), NF
@@ -284,7 +284,7 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
                  const float* bias, int normalize, float* out, int split_k, float* partial, int dtype, void* stream);
 
 /* ---- execution options (no reference counterpart: plan choices of this build) ----------------
- * FR_OPT_STAGE (default 1; env FR_NO_STAGE=1 starts at 0): run the stride-1 IResNet100 layer3 blocks
+ * FR_OPT_STAGE (default 1; FR_AB no_stage starts at 0): run the stride-1 IResNet100 layer3 blocks
  *   as one LDS-resident stage kernel per image instead of 58 separate conv launches.  Numerically the
  *   same op sequence and bf16 rounding points (f32 accumulation in a different K order).  0 = never,
  *   1 = auto: at every batch of at most one image per CU (measured faster than the per-conv launches
@@ -315,7 +315,7 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * discarded per row), 2: the 13-fragment layout at one wave per SIMD (each weight fragment loaded once per
  * CU).  All give the same bits (A/B and regression tests). */
 #define FR_OPT_STAGE_VARIANT 7
-/* FR_OPT_SPLITK_INLAUNCH (default 1; env FR_SPLITK_INLAUNCH=0 starts at 0): a split-K implicit-GEMM conv may reduce
+/* FR_OPT_SPLITK_INLAUNCH (default 1; FR_AB splitk_inlaunch=0 starts at 0): a split-K implicit-GEMM conv may reduce
  * its partials in the same launch (the last workgroup of each tile sums them in split order) where the
  * per-shape tuning measured that faster than a second launch; 0 = always the second launch.  The same bits
  * either way.  fr_debug_plan prints an in-launch split as a negative split count. */

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B per-layer profile in one process pool: tools/ab_layers.sh TAG "ENV_A" "ENV_B" (e.g. FR_CONV_DBG=128)
+# A/B per-layer profile in one process pool: tools/ab_layers.sh TAG "ENV_A" "ENV_B" (e.g. FR_AB=no_trans)
 T=$1; A=$2; B=$3
 for r in 1 2; do
   env $A tools/gpu_layer_profile.sh ${T}a$r > gpurun_out/${T}a$r.txt || exit 1

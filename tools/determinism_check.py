@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Replay determinism at full batch: embed the same bs=256 batch N times and report which calls differ
-(call 0 runs the tile-tuning pass).  Use with env toggles (FR_NO_IMG28=1, FR_NO_STAGE=1, ...) to
+(call 0 runs the tile-tuning pass).  Use with env toggles (FR_AB=no_img28, FR_AB=no_stage, ...) to
 isolate a kernel."""
 import os
 import sys
