@@ -39,6 +39,12 @@ GFLOP_PER_FACE = {"iresnet100": 24.179, "resnet50_arcface": 2.154, "irv1_facenet
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
 FP8_DENSE_PEAK_TFLOPS = 5000.0  # MI355X_MICROARCH.md: ~5 PF dense fp8 (block-scaled f8f6f4 MFMA)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec (about 6.3 TB/s achievable)
+
+
+def class_peak(name):
+    """Dense MFMA peak of a kernel class: the e4m3 classes (the per-conv fp8 kernel and the fp8 layer3 stage,
+    engine.cpp "stage8 layer3") run on the block-scaled f8f6f4 MFMA, everything else on bf16 / f16."""
+    return FP8_DENSE_PEAK_TFLOPS if name.startswith(("conv_fp8", "stage8")) else BF16_DENSE_PEAK_TFLOPS
 C4_ROWS = 1_000_000  # BASELINE config 4's gallery (the N > 1 default)
 PROF_STRIDE = 8  # roofline: sample every 8th dominant-kernel launch (event overhead ~0.5 % instead of ~4 %)
 
@@ -404,7 +410,7 @@ def main():
         ms, launches, flops, _ = kclasses[name]
         achieved = flops / (ms * 1e-3) / 1e12
         traffic = class_traffic(name, pmc)
-        peak = FP8_DENSE_PEAK_TFLOPS if name.startswith("conv_fp8") else BF16_DENSE_PEAK_TFLOPS
+        peak = class_peak(name)
         result["roofline"] = {
             "bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
@@ -424,7 +430,7 @@ def main():
         # input, weight and output byte once -- / time / 8 TB/s); "bound" is the nearer one
         def cls_entry(name, v):
             ms, launches, fl, by = v
-            peak = FP8_DENSE_PEAK_TFLOPS if name.startswith("conv_fp8") else BF16_DENSE_PEAK_TFLOPS
+            peak = class_peak(name)
             tf = fl / (ms * 1e-3) / 1e12 if fl else None
             gbs = by / (ms * 1e-3) / 1e9 if by else None
             mf = tf / peak if tf else 0.0

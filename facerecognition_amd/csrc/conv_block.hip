@@ -235,6 +235,8 @@ bool block_supported(const BlockArgs& a) {
     if (a.nconv < 1 || a.nconv > FR_BLOCK_MAX_CONVS || a.nstep < 1 || a.G < 1 || a.B < 1 || a.ld % 32 != 16 ||
         a.Cx % 4 != 0 || a.Cy % 4 != 0 || block_lds_bytes(a.G, a.H, a.W, a.ld) > 160 * 1024)
         return false;
+    // 31-bit buffer records / offsets: past 2 GiB an operand would read zeros, silently
+    if ((size_t)a.B * a.H * a.W * a.Cx * 2 > 0x7fffffffull || (size_t)a.B * a.H * a.W * a.Cy * 2 > 0x7fffffffull) return false;
     for (int i = 0; i < a.nconv; ++i) {
         const BlockConv& c = a.c[i];
         const int nfr = c.Cout / 16;

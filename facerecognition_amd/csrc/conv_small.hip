@@ -193,7 +193,11 @@ bool small_supported(const ConvArgs& a, int nf) {
            (kcat ? (a.C2 % 32 == 0 && a.Cx2 % 8 == 0 && a.x2_off % 8 == 0 && a.K1 == a.Kh * a.Kw * a.Cin &&
                     a.K1 + a.C2 <= a.Kpad && a.K == a.K1 + a.C2)
                  : a.K == a.Kh * a.Kw * a.Cin) &&
-           (!a.y_bf16 || (a.f16 && !a.res));
+           (!a.y_bf16 || (a.f16 && !a.res)) &&
+           // buffer records and offsets are 31-bit: past 2 GiB an operand would read zeros, silently
+           (size_t)a.B * a.H * a.W * a.Cx * 2 <= 0x7fffffffull && (size_t)a.Npad * a.Kpad * 2 <= 0x7fffffffull &&
+           (size_t)a.M * a.Cy * 2 <= 0x7fffffffull && (!a.res || (size_t)a.M * a.Cres * 2 <= 0x7fffffffull) &&
+           (!kcat || (size_t)a.B * a.H2 * a.W2 * a.Cx2 * 2 <= 0x7fffffffull);
 }
 
 // split = KS | NF << 8 (NF field 0: the 64-channel tile)

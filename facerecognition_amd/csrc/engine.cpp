@@ -245,6 +245,9 @@ struct fr_handle {
     int stage_min_fill = 80;  // FR_OPT_STAGE_MIN_FILL (percent)
     int n_cu = 256;
     bool keep_inter = false;
+    // FR_OPT_BATCH_INVARIANT: every kernel choice sums K in the implicit GEMM's order (no split-K, no stage /
+    // transition / block kernels, a fixed head split), so a face's embedding does not depend on its batch
+    bool invariant = false;
 };
 
 namespace {
@@ -1226,6 +1229,10 @@ size_t partial_need(fr_handle* h, int B) {
         if (op.kind == OP_HEAD) head_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
         else conv_plan(M, cw.Cout, cw.Kpad, &tile, &sp);
         if (sp > 1 || op.kind == OP_HEAD) need = std::max(need, (size_t)sp * M * cw.Npad);
+        if (op.kind == OP_HEAD) {  // FR_OPT_BATCH_INVARIANT runs bs = 256's head split at every batch
+            head_plan(256, cw.Cout, cw.Kpad, &tile, &sp);
+            need = std::max(need, (size_t)sp * M * cw.Npad);
+        }
     }
     return need;
 }
@@ -1432,6 +1439,11 @@ static int fit_split(const fr_handle* h, const ConvArgs& a, int split) {
 
 static ConvChoice default_choice(const fr_handle* h, const ConvArgs& a) {
     ConvChoice c;
+    if (h->invariant) {  // the cost model's tile, unsplit (every igemm tile sums K in the same order)
+        conv_plan(a.M, a.Cout, a.Kpad, &c.tile, &c.split);
+        c.split = 1;
+        return c;
+    }
     if (rows_ok(a)) { c.tile = FR_TILE_ROWS; return c; }
     if (img28_enabled() && img28_supported(a)) { c.tile = FR_TILE_IMG28; return c; }
     if (img56_enabled() && img56_supported(a)) { c.tile = FR_TILE_IMG56; return c; }
@@ -1516,10 +1528,11 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
         c.split = split;
         cand.push_back(c);
     };
-    if (rows_ok(a)) add(FR_TILE_ROWS, 1);
-    if (img28_enabled() && img28_supported(a)) add(FR_TILE_IMG28, 1);
-    if (img56_enabled() && img56_supported(a)) add(FR_TILE_IMG56, 1);
-    if (band_ok(a)) add(FR_TILE_BAND, 1);
+    const bool inv = h->invariant;  // only the kernels that sum K in the implicit GEMM's order (tile 0's bits)
+    if (!inv && rows_ok(a)) add(FR_TILE_ROWS, 1);
+    if (!inv && img28_enabled() && img28_supported(a)) add(FR_TILE_IMG28, 1);
+    if (!inv && img56_enabled() && img56_supported(a)) add(FR_TILE_IMG56, 1);
+    if (!inv && band_ok(a)) add(FR_TILE_BAND, 1);
     int tiles[16];
     const int nt = conv_tile_candidates(a.Cout, tiles);
     for (int i = 0; i < nt; ++i) add(tiles[i], 1);
@@ -1536,7 +1549,8 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     static const bool small_nf4 = [] { return ab_int("small_nf4", 0) != 0; }();
     if (a.M <= 8192)
         for (int sp : {1, 4, 8, 4 | 2 << 8, 8 | 2 << 8, 4 | 1 << 8, 8 | 1 << 8, 16 | 1 << 8})
-            if ((!small_nf4 || sp < 256) && small_supported(a, (sp >> 8) ? (sp >> 8) : 4)) add(FR_TILE_SMALL, sp);
+            if ((!small_nf4 || sp < 256) && (!inv || (sp & 255) == 1) && small_supported(a, (sp >> 8) ? (sp >> 8) : 4))
+                add(FR_TILE_SMALL, sp);
     // one wave per 16 px x 32 / 16 channels at any M: narrow-N convs (FaceNet Block35's N = 32 / 96) waste half of
     // every implicit-GEMM tile
     if (!small_nf4 && a.Cout <= 96)
@@ -1546,7 +1560,7 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
         int tile, split;
         conv_plan(a.M, a.Cout, a.Kpad, &tile, &split);
         split = fit_split(h, a, split);
-        if (split > 1) {
+        if (split > 1 && !inv) {
             add(tile, split);
             if (h->splitk_inlaunch) add(tile, -split);  // the same split reduced in-launch (negative split)
         }
@@ -1608,9 +1622,20 @@ static bool choice_ok(const ConvArgs& a, const ConvChoice& c) {
     }
 }
 
+static bool invariant_ok(const ConvChoice& c) {
+    switch (c.tile) {
+        case FR_TILE_ROWS: case FR_TILE_IMG28: case FR_TILE_IMG56: case FR_TILE_BAND: return false;
+        case FR_TILE_SMALL: return (c.split & 255) == 1;
+        case FR_TILE_WRING: case FR_TILE_DIRECT: return true;
+        default: return c.split == 1;
+    }
+}
+
 static ConvChoice conv_choice(const fr_handle* h, const ConvArgs& a) {
     ConvChoice c;
-    if (autotune_enabled() && !conv_tile_forced() && find_tuned(h, a, &c) && choice_ok(a, c)) return c;
+    if (autotune_enabled() && !conv_tile_forced() && find_tuned(h, a, &c) && choice_ok(a, c) &&
+        (!h->invariant || invariant_ok(c)))
+        return c;
     return default_choice(h, a);
 }
 
@@ -1665,7 +1690,7 @@ static bool trans_enabled() {
 }
 
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
-    if (h->stage_mode == 0) return false;
+    if (h->stage_mode == 0 || h->invariant) return false;
     // the fused transition keeps no t tensor and records no amax
     if (r.trans && (h->keep_inter || (h->amax && h->need_amax[r.out]) || !trans_enabled())) return false;
     if (r.parts > 1 && (h->no_split || !split_stage_enabled(r.H))) return false;
@@ -1690,7 +1715,7 @@ static bool block_enabled() {
 // intermediates (FR_OPT_KEEP_INTERMEDIATES) or in an fp8 plan.
 static bool block_runs(const fr_handle* h, int B, int bi) {
     const BlockRec& r = h->blocks[bi];
-    if (!r.ok || h->stage_mode == 0 || h->keep_inter || h->amax || !block_enabled()) return false;
+    if (!r.ok || h->stage_mode == 0 || h->invariant || h->keep_inter || h->amax || !block_enabled()) return false;
     if (h->stage_mode == 2) return true;
     const int c = stage_choice(h, (int)h->stages.size() + bi, B);
     if (c >= 0) return c == 1;
@@ -2121,11 +2146,12 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 a.w = cw.w; a.Kh = 1; a.Kw = 1; a.sh = 1; a.sw = 1; a.K = cw.K; a.Kpad = cw.Kpad;
                 a.Ho = 1; a.Wo = 1; a.M = B; a.Cout = cw.Cout; a.Npad = cw.Npad;
                 int tile, split;
-                head_plan(B, cw.Cout, cw.Kpad, &tile, &split);
+                // batch-invariant: bs = 256's plan at every batch (reserve() sizes the partials for it)
+                head_plan(h->invariant ? 256 : B, cw.Cout, cw.Kpad, &tile, &split);
                 while (split > 1 && (size_t)split * B * cw.Npad > h->partial_floats) split /= 2;
                 // B <= 4 (the online bs = 1 path): a GEMV over 8 K chunks instead of 128-row MFMA tiles
-                const bool gemv = B <= 4 && head_gemv_enabled() && head_gemv_supported(B, cw.K, cw.Kpad, cw.Npad) &&
-                                  (size_t)8 * B * cw.Npad <= h->partial_floats;
+                const bool gemv = B <= 4 && !h->invariant && head_gemv_enabled() &&
+                                  head_gemv_supported(B, cw.K, cw.Kpad, cw.Npad) && (size_t)8 * B * cw.Npad <= h->partial_floats;
                 if (gemv) split = 8;
                 a.tile = tile;
                 a.split_k = split;
@@ -2735,6 +2761,13 @@ int fr_set_option(fr_handle* h, int option, int value) {
             h->stage_variant = value;
             break;
         case FR_OPT_SPLITK_INLAUNCH: h->splitk_inlaunch = value != 0; break;
+        case FR_OPT_BATCH_INVARIANT:
+            if ((value != 0) != h->invariant) {  // the kernel choices are re-measured under the new rule
+                h->invariant = value != 0;
+                h->tuned.clear();
+                h->tuned_batches.clear();
+            }
+            break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;
     }
     drop_graphs(h);  // captured replays bake in the plan
@@ -2752,6 +2785,7 @@ int fr_get_option(const fr_handle* h, int option) {
         case FR_OPT_STAGE_SPIN_LIMIT: return h->spin_limit;
         case FR_OPT_STAGE_VARIANT: return h->stage_variant;
         case FR_OPT_SPLITK_INLAUNCH: return h->splitk_inlaunch ? 1 : 0;
+        case FR_OPT_BATCH_INVARIANT: return h->invariant ? 1 : 0;
         default: return FR_ERR_ARG;
     }
 }

@@ -66,13 +66,15 @@ class ShardedMatcher:
 
     local_search(probes [P, D], out_s [P, k] f32, out_i [P, k] int32) writes the shard's top-k (global
       indices) into out_s / out_i -- views into this rank's block of the candidate send buffer -- or
-      returns (scores, idx) tensors, which are then copied there;
+      returns (scores, idx) tensors, which are then copied there; a one-argument callable
+      local_search(probes) -> (scores, idx) (the round-3 interface) is accepted too;
     merge(xchg [world, 2, P, k] int32, k, out_s, out_i) merges the all-gathered blocks (default
       native_merge_ranks, fr_topk_merge_ranks).
 
     The candidate exchange is ONE all-gather: each rank's block is [2][P][k] 4-byte words (its scores,
     then its indices), written in place by the shard search, gathered as is and merged as is.
-    search() returns views of buffers owned by the matcher, overwritten by the next call.
+    search() returns views of buffers owned by the matcher, overwritten by the next call (clone them to keep
+    them).  At world 1 a batch shorter than the constructor's (the last, partial batch of a stream) is fine.
     """
 
     def __init__(self, batch: int, dim: int, k: int, local_search: Callable, device: torch.device,
@@ -90,10 +92,16 @@ class ShardedMatcher:
         self.out_s = torch.empty((P, k), dtype=torch.float32, device=device)
         self.out_i = torch.empty((P, k), dtype=torch.int32, device=device)
         self._send_s, self._send_i = self.send[0].view(torch.float32), self.send[1]
-        self._one_s, self._one_i = self.out_s[:batch], self.out_i[:batch]
+        import inspect
+        try:
+            n_args = len([p for p in inspect.signature(local_search).parameters.values()
+                          if p.default is inspect.Parameter.empty and p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD)])
+        except (TypeError, ValueError):
+            n_args = 3
+        self._legacy = n_args == 1
 
     def _local(self, probes, out_s, out_i):
-        r = self.local_search(probes, out_s, out_i)
+        r = self.local_search(probes) if self._legacy else self.local_search(probes, out_s, out_i)
         if r is not None:
             out_s.copy_(r[0])
             out_i.copy_(r[1])
@@ -102,8 +110,12 @@ class ShardedMatcher:
         """emb: this rank's normalized embeddings [B, D] → top-k of every rank's probes, identical on
         all ranks: (scores [world*B, k], idx [world*B, k]); row j*B + b is rank j's probe b."""
         if self.world == 1 and not self.always_exchange:
-            self._local(emb, self._one_s, self._one_i)
-            return self._one_s, self._one_i
+            B = int(emb.shape[0])
+            if B > self.B:
+                raise ValueError(f"ShardedMatcher.search: {B} probes, built for at most {self.B}")
+            s, i = self.out_s[:B], self.out_i[:B]
+            self._local(emb, s, i)
+            return s, i
         _all_gather(self.all_emb, emb, self.group)
         self._local(self.all_emb, self._send_s, self._send_i)
         _all_gather(self.xchg.view(-1), self.send.view(-1), self.group)

@@ -19,6 +19,7 @@ without facenet-pytorch (RecognitionEngine then runs on the raw image).
 from __future__ import annotations
 
 import os
+import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -121,6 +122,17 @@ def pyramid_scales(h: int, w: int, minsize: int = MIN_FACE, factor: float = FACT
 
 
 # ------------------------------------------------------------------------------ host box logic
+# Optional per-stage timing of detect_face (tools/mtcnn_bench.py): a dict here receives ms and counts
+STATS = None
+
+
+def _acc(key, t0, n=None):
+    if STATS is not None:
+        STATS[key] = STATS.get(key, 0.0) + (time.perf_counter() - t0) * 1e3
+        if n is not None:
+            STATS[key + "_n"] = STATS.get(key + "_n", 0) + int(n)
+
+
 def nms(boxes: np.ndarray, scores: np.ndarray, thresh: float, mode: str = "iou") -> np.ndarray:
     """Greedy non-maximum suppression.  mode "iou": torchvision.ops.nms (score descending, equal scores
     in index order, areas (x2 - x1)(y2 - y1), suppress IoU > thresh: a 0 / 0 IoU keeps the box); mode "min":
@@ -132,6 +144,7 @@ def nms(boxes: np.ndarray, scores: np.ndarray, thresh: float, mode: str = "iou")
     n = len(boxes)
     if n == 0:
         return np.zeros((0,), np.int64)
+    t0 = time.perf_counter()
     order = np.argsort(-scores, kind="stable") if mode == "iou" else np.argsort(scores)[::-1]
     b = np.ascontiguousarray(boxes[:, :4], dtype=np.float32)
     order = np.ascontiguousarray(order, dtype=np.int64)
@@ -139,6 +152,7 @@ def nms(boxes: np.ndarray, scores: np.ndarray, thresh: float, mode: str = "iou")
     nk = ctypes.c_int64(0)
     N.check(N.lib().fr_nms_host(b.ctypes.data, n, order.ctypes.data, float(thresh), int(mode == "min"),
                                 keep.ctypes.data, ctypes.byref(nk)), "fr_nms_host")
+    _acc("nms_ms", t0, n)
     return keep[: nk.value].copy()
 
 
@@ -196,8 +210,10 @@ def detect_face(imgs, resample, pnet, rnet, onet, minsize: int = MIN_FACE, thres
     boxes, inds, picks, offset = [], [], [], 0
     for scale in pyramid_scales(h, w, minsize, factor):
         hs, ws = int(h * scale + 1), int(w * scale + 1)
+        t0 = time.perf_counter()
         x = resample(imgs, np.array([[b, 0, 0, h, w] for b in range(B)]), hs, ws)
         out = pnet(x).cpu().numpy()  # [B, hh, ww, 6]
+        _acc("pnet_ms", t0, out.shape[0] * out.shape[1] * out.shape[2])
         prob = out[..., 1]
         bi, yy, xx = np.nonzero(prob >= f32(th[0]))
         sc = f32(scale)
@@ -228,9 +244,11 @@ def detect_face(imgs, resample, pnet, rnet, onet, minsize: int = MIN_FACE, thres
         return resample(imgs, reg, size, size), ok
 
     if len(boxes):
+        t0 = time.perf_counter()
         x, ok = crops(boxes, 24)
         boxes, inds = boxes[ok], inds[ok]
         out = rnet(x).cpu().numpy()
+        _acc("rnet_ms", t0, len(out))
         score = out[:, 1]
         ip = score > f32(th[1])
         boxes = np.concatenate([boxes[ip, :4], score[ip, None]], 1)
@@ -239,9 +257,11 @@ def detect_face(imgs, resample, pnet, rnet, onet, minsize: int = MIN_FACE, thres
         boxes, inds, mv = boxes[pk], inds[pk], mv[pk]
         boxes = _rerec(_bbreg(boxes, mv))
     if len(boxes):
+        t0 = time.perf_counter()
         x, ok = crops(boxes, 48)
         boxes, inds = boxes[ok], inds[ok]
         out = onet(x).cpu().numpy()
+        _acc("onet_ms", t0, len(out))
         score = out[:, 1]
         ip = score > f32(th[2])
         boxes = np.concatenate([boxes[ip, :4], score[ip, None]], 1)

@@ -36,6 +36,7 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
+from . import _native as N
 from . import weights as Wt
 from .extract_embeddings import (_device_index, _embed_u8, _load_u8, extract_embedding_single,
                                  get_transform, load_arcface_model, read_index, segment_means)
@@ -175,7 +176,11 @@ class RecognitionEngine:
     def __init__(self, model_path: str = "models/checkpoints/arcface/arcface_best.pth", db_path: str = None,
                  faiss_index_path: str = None, prototypes_path: str = None, label_mapping_path: str = None,
                  device: str = None, threshold: float = 0.5, use_face_detection: bool = True, model=None,
-                 face_detector=None, mtcnn_weights: str = None):
+                 face_detector=None, mtcnn_weights: str = None, batch_invariant: bool = True):
+        """batch_invariant (default True): the model runs FR_OPT_BATCH_INVARIANT, so ``recognize_batch`` returns
+        bit for bit what a loop over ``recognize`` returns, as the reference's does (recognition_engine.py:383-389);
+        False lets the model pick the fastest kernels per batch size (embeddings then differ by ~1e-4 cosine
+        between batch sizes)."""
         self.device = device or "cuda"
         self.threshold = threshold
         self.use_face_detection = use_face_detection
@@ -184,6 +189,8 @@ class RecognitionEngine:
             self.model = model
         elif model_path and os.path.exists(model_path):
             self.model, self.model_info = load_arcface_model(model_path, self.device)
+        if self.model is not None and batch_invariant:
+            self.model.set_option(N.FR_OPT_BATCH_INVARIANT, 1)
         self.transform = get_transform(Wt.INPUT_SIZE[self.model.arch] if self.model is not None else 112)
         self.face_detector = face_detector
         if self.use_face_detection and self.face_detector is None:

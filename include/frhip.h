@@ -320,6 +320,12 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * per-shape tuning measured that faster than a second launch; 0 = always the second launch.  The same bits
  * either way.  fr_debug_plan prints an in-launch split as a negative split count. */
 #define FR_OPT_SPLITK_INLAUNCH 8
+/* FR_OPT_BATCH_INVARIANT (default 0): batch-size-independent embeddings.  Every conv runs a kernel that sums K in
+ * the implicit GEMM's order (igemm tiles, register-ring, direct and small-M kernels unsplit; no split-K, no LDS-resident
+ * stage / transition / block kernels) and the head uses bs = 256's split plan at every batch, so a face's embedding
+ * is the same bits whatever batch it is in (the reference's recognize_batch is a loop over recognize,
+ * recognition_engine.py:383-389).  Slower than the default, which measures the fastest kernels per batch size. */
+#define FR_OPT_BATCH_INVARIANT 9
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);
 /* Number of probes (since the gallery was first split) whose bf16x3 candidate proof failed and were

@@ -104,3 +104,29 @@ def test_sharded_match_world2_gloo_equals_single_device():
             assert np.array_equal(r["i"], gi.astype(np.int32))
             assert np.array_equal(r["s"], gs)
         assert list(gi[3][:2]) == [17, 150] and list(gi[7][:2]) == [100, 101]
+
+
+def test_world1_short_batch_and_one_argument_search():
+    """World 1 (no process group): a batch shorter than the constructor's works, results are the matcher's views
+    of that many rows, and the round-3 one-argument local_search(probes) -> (scores, idx) is still accepted."""
+    from facerecognition_amd.distributed import ShardedMatcher
+    G, P = _data()
+
+    def three(probes, out_s, out_i):
+        s, i = topk_dot(probes.numpy(), G, K)
+        out_s.copy_(torch.from_numpy(s))
+        out_i.copy_(torch.from_numpy(i.astype(np.int32)))
+
+    def one(probes):
+        s, i = topk_dot(probes.numpy(), G, K)
+        return torch.from_numpy(s), torch.from_numpy(i.astype(np.int32))
+
+    gs, gi = topk_dot(P, G, K)
+    for fn in (three, one):
+        m = ShardedMatcher(B, D, K, fn, torch.device("cpu"))
+        s, i = m.search(torch.from_numpy(P[:B]))
+        assert np.array_equal(i.numpy(), gi[:B]) and np.array_equal(s.numpy(), gs[:B])
+        s, i = m.search(torch.from_numpy(P[:B - 2]))  # a short last batch
+        assert s.shape == (B - 2, K) and np.array_equal(i.numpy(), gi[:B - 2])
+        with pytest.raises(ValueError):
+            m.search(torch.from_numpy(P[:B + 1]))

@@ -10,6 +10,8 @@ import os
 import numpy as np
 import pytest
 
+from facerecognition_amd import _native as N
+
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "arcface_r50_golden.npz")
@@ -98,15 +100,17 @@ def test_recognize_batch_end_to_end(gold, r50, names_db):
     assert [r["identity"] for r in res[:8]] == [str(n) for n in gold["best_name"]]
     assert res[8]["status"] == "error" and res[8]["embedding"] is None
     single = eng.recognize(imgs[2])
-    # bs = 1 and bs = 9 run the kernels measured fastest at each batch size (e.g. split-K at bs = 1), whose f32
-    # summation orders differ, so the two embeddings agree to bf16 rounding, not bit for bit; both stay at the
-    # oracle bar (as the reference's own single and batched paths may differ in their last bits on a GPU)
-    assert single["identity"] == res[2]["identity"] and abs(single["confidence"] - res[2]["confidence"]) < 1e-3
+    # the engine runs FR_OPT_BATCH_INVARIANT (default): recognize_batch is bit for bit a loop over recognize, as the
+    # reference's recognize_batch is (recognition_engine.py:383-389)
+    assert r50.get_option(N.FR_OPT_BATCH_INVARIANT) == 1
+    assert np.array_equal(single["embedding"], res[2]["embedding"])
+    assert single["identity"] == res[2]["identity"] and single["confidence"] == res[2]["confidence"]
     assert _cos_dist(single["embedding"], gold["emb_single"][2]) <= COS_TOL
     assert _cos_dist(res[2]["embedding"], gold["emb_single"][2]) <= COS_TOL
     # in-place db edit is picked up by the device copy
     eng.db["zz_probe2"] = res[2]["embedding"]
     assert eng.recognize(imgs[2])["identity"] == "zz_probe2"
+    r50.set_option(N.FR_OPT_BATCH_INVARIANT, 0)  # the shared fixture goes back to the throughput default
 
 
 def test_folder_db_build_and_faiss_path(gold, r50, tmp_path):

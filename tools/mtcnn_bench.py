@@ -79,11 +79,20 @@ def main():
         t_each.append((time.perf_counter() - t) * 1e3)
         print(f"detect: {t_each[-1]:.1f} ms", flush=True)
     t_detect = float(np.median(t_each))
+    FD.STATS = {}  # one more call with the per-stage breakdown (host NMS, device nets incl. their D2H copies)
+    t = time.perf_counter()
+    fd.detect(bgr)
+    torch.cuda.synchronize()
+    total = (time.perf_counter() - t) * 1e3
+    stages = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in FD.STATS.items()}
+    stages["other_host_ms"] = round(total - sum(v for k, v in FD.STATS.items() if k.endswith("_ms")), 3)
+    FD.STATS = None
+    print("stages:", stages, flush=True)
     res = {"frame": f"{W}x{H} synthetic RGB u8", "weights": "synthetic (synth_mtcnn_state(7))",
            "pyramid_levels": len(scales), "detect_ms_median": round(t_detect, 3), "detect_iters": a.detect_iters,
            "detected": det is not None, "pnet_level0_ms": round(t_pnet0, 3), "pnet_level0_shape": [hs, ws],
            "pnet_all_levels_with_resample_ms": round(t_pyr, 3), "rnet_256_crops_ms": round(t_rnet, 3),
-           "onet_256_crops_ms": round(t_onet, 3)}
+           "onet_256_crops_ms": round(t_onet, 3), "detect_stages": stages}
     print(json.dumps(res), flush=True)
     if a.out:
         with open(a.out, "w") as f:
