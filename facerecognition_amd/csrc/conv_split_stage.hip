@@ -136,13 +136,14 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
 
     // ---- initial patch: image rows r0-1 .. r0+14 (out-of-image rows and halo columns read as zeros)
     {
+        // (the resources span this image only: 32-bit offsets at any batch size)
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)p.x, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * IW * IW * C * 2), 0x00020000);
+            (void*)(p.x + (size_t)b * IW * IW * C), 0, IW * IW * C * 2, 0x00020000);
         for (int u = 0; u < PATCH_B / 1024 / NW; ++u) {
             const int piece = wave + NW * u, q = piece * 64 + lane;
             const int plane = q / PPOS, pos = q % PPOS, ir = r0 - 1 + pos / PC, ic = pos % PC - 1;
             const uint32_t src = (unsigned)ir < (unsigned)IW && (unsigned)ic < (unsigned)IW
-                                     ? (uint32_t)((((b * IW + ir) * IW + ic) * C + plane * 8) * 2)
+                                     ? (uint32_t)(((ir * IW + ic) * C + plane * 8) * 2)
                                      : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(smem + piece * 1024), 16, src, 0, 0, 0);
         }
@@ -258,9 +259,9 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     // reaching f0 + cv + 1 means its conv cv rows are published.
     const int f0 = __hip_atomic_load(my_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const __amdgpu_buffer_rsrc_t xr_x = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)p.xchg, 0, (uint32_t)min((size_t)0x7fffffff, xchg_elems<G>(p.B) * 2), 0x00020000);
-    // element offset of row `which` of part `pt`, parity `par`
-    auto xrow_off = [&](int pt, int which, int par) { return (((b * PARTS + pt) * 2 + which) * 2 + par) * XROW; };
+        (void*)(p.xchg + (size_t)b * PARTS * 2 * 2 * XROW), 0, PARTS * 2 * 2 * XROW * 2, 0x00020000);
+    // element offset (within this image's exchange rows) of row `which` of part `pt`, parity `par`
+    auto xrow_off = [&](int pt, int which, int par) { return ((pt * 2 + which) * 2 + par) * XROW; };
 
     // Halo import of conv cv's boundary rows (published by the neighbours at the end of conv cv), issued
     // inside conv cv+1 between positions 1 and 2: wave 0 polls the neighbours' counters, the other waves

@@ -122,8 +122,9 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
     }
 
     // ---- x row DMA: row `row` into its slot (row + 1) % 6; rows outside the image read as zeros
-    const uint32_t x_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)p.B * TW * TW * TCH * 2);
-    const uint64_t xp = (uint64_t)p.x;
+    // (the resource spans this image only: 32-bit offsets at any batch size)
+    const uint32_t x_bytes = (uint32_t)(TW * TW * TCH * 2);
+    const uint64_t xp = (uint64_t)(p.x + (size_t)b * TW * TW * TCH);
     const v4i32 xr = {(int)(uint32_t)xp, (int)((xp >> 32) & 0xffff), (int)x_bytes, 0x00020000};
     // per piece u (pieces wave + 4 u): the lane's source offset within a row (or OOB for halo columns)
     uint32_t colpart[4];
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
     auto dma_row = [&](int row) {
         const int slot = (row + 1) % XSLOTS;
         const bool rin = (unsigned)row < (unsigned)TW;
-        const uint32_t rbase = (uint32_t)(((size_t)b * TW + (rin ? row : 0)) * TW * TCH * 2);
+        const uint32_t rbase = (uint32_t)((rin ? row : 0) * TW * TCH * 2);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int piece = wave + 4 * u;
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
         if (row <= TW && piece < XPIECES && piece * 64 + lane < XQ) {
             const bool rin = row < TW;
             const uint32_t off = rin && colpart[u & 3] != OOB
-                                     ? (uint32_t)(((size_t)b * TW + row) * TW * TCH * 2) + colpart[u & 3]
+                                     ? (uint32_t)(row * TW * TCH * 2) + colpart[u & 3]
                                      : OOB;
             dma16(xr, (uint32_t)(uintptr_t)(smem + X_OFF + ((row + 1) % XSLOTS) * XROW_B + piece * 1024), off);
         }
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(256) void trans_pack_kernel(const bf16_t* __restric
 
 bool trans_supported(int B, int H, int W, int Cin, int Cmid, int Cout, int K1, int K2) {
     return B > 0 && H == TW && W == TW && Cin == TCH && Cmid == TCH && Cout == TCH && K1 == 32 * KS1 &&
-           K2 == 32 * KS2 && (size_t)B * TW * TW * TCH * 2 <= 0x7fffffffu;
+           K2 == 32 * KS2;
 }
 
 size_t trans_packed_elems(int K) { return (size_t)(K / 32) * 4 * 64 * 8; }

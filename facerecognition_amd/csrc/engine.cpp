@@ -2372,8 +2372,35 @@ static int forward_graph(fr_handle* h, const void* in, int in_fmt, int B, float*
     return FR_OK;
 }
 
+static int embed_batch(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, float* out, int flags,
+                       void* stream);
+
+// Largest batch one forward runs: every activation tensor of the batch stays below 2 GiB, the range of the
+// kernels' 32-bit buffer offsets (IResNet100: 1280 faces, layer1's 112^2 x 64); bigger calls run in chunks
+// of that size, multiples of 256 (the tuned batch sizes' tiles).
+static int embed_chunk(const fr_handle* h) {
+    size_t per = 1;
+    for (const auto& t : h->tensors) per = std::max(per, (size_t)t.H * t.W * t.C * sizeof(bf16_t));
+    const size_t cap = 0x7fffffffull / per;
+    return (int)std::max<size_t>(1, cap >= 512 ? cap / 256 * 256 : cap);
+}
+
 static int embed_locked(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, float* out, int flags,
                         void* stream) {
+    const int cap = embed_chunk(h);
+    if (B <= cap || !in || !out) return embed_batch(h, in, in_fmt, B, H, W, out, flags, stream);
+    const size_t in_img = (size_t)H * W * 3 * (in_fmt == FR_IN_F32_NCHW ? sizeof(float) : 1);
+    const size_t d = (size_t)fr_embed_dim(h);
+    for (int b0 = 0; b0 < B; b0 += cap) {
+        const int rc = embed_batch(h, (const char*)in + b0 * in_img, in_fmt, std::min(cap, B - b0), H, W,
+                                   out + b0 * d, flags, stream);
+        if (rc) return rc;
+    }
+    return FR_OK;
+}
+
+static int embed_batch(fr_handle* h, const void* in, int in_fmt, int B, int H, int W, float* out, int flags,
+                       void* stream) {
     if (!h->loaded) { set_error("fr_embed: weights not loaded"); return FR_ERR_STATE; }
     if (!in || !out || B <= 0) { set_error("fr_embed: bad argument"); return FR_ERR_ARG; }
     if (H != h->in_size || W != h->in_size) {

@@ -62,3 +62,22 @@ def test_default_mode_batch_drift_measured(gpu):
     m.close()
     print("max 1-cos vs bs=256 by batch size:", {k: f"{v:.2e}" for k, v in worst.items()})
     assert all(v <= 1e-3 for v in worst.values()), worst
+
+
+def test_large_batch_runs_in_chunks(gpu):
+    """A call above the engine's chunk size (every activation tensor < 2 GiB: 1280 faces for IResNet100, whose
+    layer1 tensor is 1.6 MB per face) runs as several forwards: the faces past the first chunk get the same bits
+    as when embedded on their own (invariant mode).  Before r05 a 2000-face call read layer1 past the kernels'
+    2 GiB buffer range, and those faces got garbage."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("iresnet100", max_batch=64)
+    m.set_option(N.FR_OPT_BATCH_INVARIANT, 1)
+    x = torch.from_numpy(synthetic_crops(1300, 112, seed=35)).cuda()
+    big = m.embed(x).cpu().numpy()
+    tail = m.embed(x[1270:]).cpu().numpy()
+    head = m.embed(x[:8]).cpu().numpy()
+    m.close()
+    assert np.isfinite(big).all()
+    assert np.array_equal(big[1270:], tail)
+    assert np.array_equal(big[:8], head)
