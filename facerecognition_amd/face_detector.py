@@ -32,6 +32,11 @@ MIN_FACE = 20
 # synth_mtcnn_state: face-classification head gains and (background, face) logit offsets
 HEAD_GAIN = {"conv4_1": 40.0, "dense5_1": 40.0, "dense6_1": 150.0}
 SYNTH_LOGIT_SHIFT = {"rnet.dense5_1.bias": (-0.6, 0.6)}
+# synth_mtcnn_state(calibrated=True): extra (face - background) logit offsets measured by tools/calibrate_mtcnn.py
+# so that, on tools/mtcnn_bench.py's 1080p frame, P-net passes ~1 % of its windows, R-net ~10 % and O-net ~30 % of
+# their inputs -- the box volumes of a trained detector on a frame with a few faces (assumed; the stress weights
+# above pass 92 % of P-net windows and carry 10^5 boxes through every stage)
+CALIBRATED_LOGIT_SHIFT = {"pnet.conv4_1.bias": 2.34, "rnet.dense5_1.bias": 0.29, "onet.dense6_1.bias": 7.04}
 LANDMARK_NAMES = ("left_eye", "right_eye", "nose", "left_mouth", "right_mouth")
 
 # facenet-pytorch's P/R/O-net parameters (name -> shape), models/mtcnn.py
@@ -58,12 +63,13 @@ MTCNN_SPECS = {
 }
 
 
-def synth_mtcnn_state(seed: int = 7) -> Dict[str, np.ndarray]:
+def synth_mtcnn_state(seed: int = 7, calibrated: bool = False) -> Dict[str, np.ndarray]:
     """Seeded synthetic P/R/O-net weights (the splitmix stream of weights.synth_state_dict): layers with
     torch's default uniform init bound, PReLU 0.25, wider face-classification heads (HEAD_GAIN) with the
     logit offsets of SYNTH_LOGIT_SHIFT, and narrower regression heads (x0.3), so that on smooth synthetic
     images the face probabilities spread across every stage's threshold (each stage keeps some candidates
-    and drops others) and boxes stay near their cell."""
+    and drops others) and boxes stay near their cell.  calibrated=True also lowers the face logits by
+    CALIBRATED_LOGIT_SHIFT (trained-detector box volumes, tools/calibrate_mtcnn.py)."""
     from .weights import splitmix_uniform
     out = {}
     for net, specs in MTCNN_SPECS.items():
@@ -83,6 +89,9 @@ def synth_mtcnn_state(seed: int = 7) -> Dict[str, np.ndarray]:
                     v = v * 0.3
             if key in SYNTH_LOGIT_SHIFT:  # (background, face) logit offsets of the synthetic heads
                 v = v + np.asarray(SYNTH_LOGIT_SHIFT[key])
+            if calibrated and key in CALIBRATED_LOGIT_SHIFT:
+                d = CALIBRATED_LOGIT_SHIFT[key]
+                v = v + np.asarray([d / 2, -d / 2])
             out[key] = v.astype(np.float32)
     return out
 
@@ -131,6 +140,11 @@ def _acc(key, t0, n=None):
         STATS[key] = STATS.get(key, 0.0) + (time.perf_counter() - t0) * 1e3
         if n is not None:
             STATS[key + "_n"] = STATS.get(key + "_n", 0) + int(n)
+
+
+def _cnt(key, n):
+    if STATS is not None:
+        STATS[key] = STATS.get(key, 0) + int(n)
 
 
 def nms(boxes: np.ndarray, scores: np.ndarray, thresh: float, mode: str = "iou") -> np.ndarray:
@@ -221,6 +235,7 @@ def detect_face(imgs, resample, pnet, rnet, onet, minsize: int = MIN_FACE, thres
         q1 = np.floor((f32(2) * cell + f32(1)) / sc)
         q2 = np.floor((f32(2) * cell + f32(12)) / sc)
         bs = np.concatenate([q1, q2, prob[bi, yy, xx][:, None], out[bi, yy, xx, 2:6]], 1).astype(f32)
+        _cnt("pnet_pass_n", len(bs))
         boxes.append(bs)
         inds.append(bi)
         picks.append(batched_nms(bs, bs[:, 4], bi, 0.5) + offset)
@@ -274,6 +289,7 @@ def detect_face(imgs, resample, pnet, rnet, onet, minsize: int = MIN_FACE, thres
         boxes = _bbreg(boxes, mv)
         pk = batched_nms(boxes, boxes[:, 4], inds, 0.7, "min")
         boxes, inds, points = boxes[pk], inds[pk], points[pk]
+    _cnt("final_n", len(boxes))
     return [boxes[inds == b] for b in range(B)], [points[inds == b] for b in range(B)]
 
 

@@ -107,3 +107,30 @@ def test_face_detector_and_engine_alignment(mt, gpu):
     e1 = eng.extract_embedding(np.ascontiguousarray(rgb[..., ::-1]))
     e2 = model.embed(aligned.cpu()).cpu().numpy()[0]
     assert np.allclose(e1, e2, atol=1e-6)
+
+
+def test_calibrated_weights_1080p_matches_oracle(gpu):
+    """tools/mtcnn_bench.py's headline case: the calibrated synthetic weights (trained-detector box volumes) on
+    its smooth 1080p frame -- the same detections as the CPU restatement."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from mtcnn_bench import frame
+    state = FD.synth_mtcnn_state(7, calibrated=True)
+    dev, nets = FD.DeviceMTCNN(state, device=0), OM.build_nets(state)
+    img = frame()
+    with torch.no_grad():
+        rb, rp = OM.detect_face(img[None], *nets)
+    FD.STATS = {}
+    try:
+        gb, gp = dev.detect_face(img[None])
+        counts = dict(FD.STATS)
+    finally:
+        FD.STATS = None
+    rb, rp, gb, gp = rb[0], rp[0], gb[0], gp[0]
+    print(f"1080p calibrated: {len(gb)} device / {len(rb)} oracle detections; P-net passes {counts.get('pnet_pass_n')}, "
+          f"R-net inputs {counts.get('rnet_ms_n')}, O-net inputs {counts.get('onet_ms_n')}")
+    assert len(rb) > 0 and len(gb) == len(rb)
+    assert np.allclose(gb[:, 4], rb[:, 4], atol=1e-5)
+    assert np.allclose(gb[:, :4], rb[:, :4], atol=2e-3)
+    assert np.allclose(gp, rp, atol=2e-3)
