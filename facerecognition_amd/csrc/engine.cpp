@@ -91,7 +91,7 @@ struct TensorDesc {
     bool f16 = false;  // stored as f16 in a bf16 plan (IRV1's high-resolution stem, build_irv1)
 };
 
-enum OpKind { OP_PRE, OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_STAGE, OP_BLOCK };
+enum OpKind { OP_PRE, OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_STAGE };
 
 struct Op {
     OpKind kind;
@@ -106,8 +106,7 @@ struct Op {
     int stage = -1;  // OP_STAGE: its StageRec; OP_CONV: the stage that covers it (skipped when stages run)
     int x2 = -1, x2_off = 0, st2 = 1;  // OP_CONV with a K-concatenated downsample: its input tensor, stride
     bool fuse_stem = false;  // OP_PRE of IResNet100: u8 input runs preprocess + the next (stem) conv fused
-    int block = -1;  // OP_BLOCK: its BlockRec; OP_CONV: the block that covers it (skipped when the block runs)
-    int grp = -1;    // index into the stage/block plan (stage_plan): stages first, then blocks
+    int grp = -1;    // index into the stage plan (stage_plan)
 };
 
 // One LDS-resident stage: the stride-1 blocks of a 14x14x256 layer (conv_stage.hip: one workgroup per
@@ -133,17 +132,6 @@ struct StageRec {
     float* tep1 = nullptr;                // [9][64] conv1 bias per border class
     float* tsl1 = nullptr;                // [64] conv1 PReLU slopes
     float* tb2 = nullptr;                 // [64] conv2 + downsample bias
-};
-
-// One LDS-resident Inception-ResNet block (conv_block.hip): its member convs as a program of steps over
-// one workgroup's G images, intermediates in LDS (plan_block).
-struct BlockRec {
-    int in = -1, out = -1, H = 0, W = 0, G = 1, ld = 0, nstep = 0;
-    bool ok = false;                // the plan fits (else the members always run)
-    std::string name;
-    std::vector<int> conv_ops;      // member OP_CONV indices in program order
-    std::vector<BlockConv> conv;    // their kernel descriptors (weights resident on the device)
-    double flops_px = 0;            // MACs per pixel over the members (x 2 = FLOPs)
 };
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -218,7 +206,6 @@ struct fr_handle {
     bool tuning = false;
     // LDS-resident stage kernels (fr_set_option FR_OPT_STAGE / FR_OPT_KEEP_INTERMEDIATES)
     std::vector<StageRec> stages;
-    std::vector<BlockRec> blocks;  // LDS-resident Inception-ResNet blocks (IRV1), run by the same FR_OPT_STAGE rule
     // FaceNet projection (Linear(512, d) + F.normalize after IRV1's own L2; facenet_model.py:20-23,32-35)
     float* proj_w = nullptr;
     float* proj_b = nullptr;
@@ -246,7 +233,7 @@ struct fr_handle {
     int n_cu = 256;
     bool keep_inter = false;
     // FR_OPT_BATCH_INVARIANT: every kernel choice sums K in the implicit GEMM's order (no split-K, no stage /
-    // transition / block kernels, a fixed head split), so a face's embedding does not depend on its batch
+    // transition kernel, a fixed head split), so a face's embedding does not depend on its batch
     bool invariant = false;
 };
 
@@ -303,7 +290,6 @@ void free_weights(fr_handle* h) {
     h->weight_allocs.clear();
     h->convw.clear();
     h->stages.clear();
-    h->blocks.clear();
     h->proj_w = h->proj_b = nullptr;
     h->proj_d = 0;
 }
@@ -354,119 +340,6 @@ trunc:
 }
 
 // ------------------------------------------------------------------ plan builder
-// Unit shape of a block conv (conv_block.hip): MF pixel fragments x NF 16-channel fragments per wave unit,
-// from a cost model of one workgroup (8 waves, 2 per SIMD): MFMA cycles of the busiest SIMD, weight bytes
-// streamed from L2 (once per pixel-unit; ~32 B/clk per CU), and a pipeline fill per round of units.
-static void block_unit_shape(int n_mf, int nfr, int nks, int K, int Cout, int* mf, int* nf) {
-    double best = 1e30;
-    for (int m : {4, 2, 1})
-        for (int n : {2, 4, 1}) {
-            if (nfr % n) continue;
-            const int mus = (n_mf + m - 1) / m, units = mus * (nfr / n);
-            const double mfma = (double)((units + 3) / 4) * m * n * nks * 32.0;
-            const double wbytes = (double)mus * Cout * K * 2.0 / 32.0;
-            const double c = std::max(mfma, wbytes) + 800.0 * ((units + 7) / 8);
-            if (c < best * 0.999) { best = c; *mf = m; *nf = n; }
-        }
-}
-
-// The block whose OP_BLOCK op is ops[bo]: its members are the ops after it (all OP_CONV), x the block input and
-// y its output.  The members' other tensors become LDS columns; program steps follow the channel-range
-// dependencies.  r.ok stays false (the members always run) when anything does not fit the kernel.
-static void plan_block(fr_handle* h, int bo, int x, int y, const std::string& name) {
-    const int bi = h->ops[bo].block;
-    BlockRec& r = h->blocks[bi];
-    r.in = x; r.out = y; r.name = name;
-    r.H = h->tensors[x].H; r.W = h->tensors[x].W;
-    for (int oi = bo + 1; oi < (int)h->ops.size(); ++oi) {
-        r.conv_ops.push_back(oi);
-        h->ops[oi].block = bi;
-    }
-    if (r.conv_ops.empty() || (int)r.conv_ops.size() > FR_BLOCK_MAX_CONVS || h->tensors[x].f16 || h->tensors[y].f16 ||
-        h->tensors[y].H != r.H || h->tensors[y].W != r.W)
-        return;
-    std::unordered_map<int, int> col;  // intermediate tensor -> first LDS column
-    int cols = 0;
-    for (int oi : r.conv_ops) {
-        const Op& op = h->ops[oi];
-        if (op.kind != OP_CONV || op.wi < 0) return;
-        const DevConvW& cw = h->convw[op.wi];
-        if (op.sh != 1 || op.sw != 1 || op.x2 >= 0 || op.out2 >= 0 || cw.bias9 || cw.w8 || cw.K != op.kh * op.kw * op.cin ||
-            (op.res >= 0 && op.res != x) || op.in == y || op.out == x)
-            return;
-        for (int t : {op.in, op.out}) {
-            const auto& td = h->tensors[t];
-            if (td.H != r.H || td.W != r.W || td.f16) return;
-            if (t != x && t != y && !col.count(t)) { col[t] = cols; cols += td.C; }
-        }
-    }
-    for (int oi = 0; oi < (int)h->ops.size(); ++oi) {  // the intermediates live only inside the block
-        if (oi > bo && oi <= r.conv_ops.back()) continue;
-        const Op& op = h->ops[oi];
-        for (int t : {op.in, op.res, op.x2, op.out, op.out2})
-            if (t >= 0 && col.count(t)) return;
-    }
-    r.ld = cols;
-    while (r.ld % 32 != 16) r.ld += 8;
-    const int HW = r.H * r.W;
-    r.G = HW >= 64 ? 1 : std::max(1, 64 / HW);  // small maps: several images per workgroup (<= 4 pixel fragments)
-    while (r.G > 1 && block_lds_bytes(r.G, r.H, r.W, r.ld) > 160 * 1024) --r.G;
-    const int n_mf = (r.G * HW + 15) / 16;
-    struct Rg { int t, lo, hi; };
-    std::vector<std::vector<Rg>> rd, wr;
-    std::vector<int> step;
-    for (int oi : r.conv_ops) {
-        const Op& op = h->ops[oi];
-        const DevConvW& cw = h->convw[op.wi];
-        rd.push_back({{op.in, op.in_off, op.in_off + op.cin}});
-        wr.push_back({{op.out, op.out_off, op.out_off + cw.Cout}});
-        auto hit = [](const std::vector<Rg>& a, const std::vector<Rg>& b) {
-            for (const auto& p : a)
-                for (const auto& q : b)
-                    if (p.t == q.t && p.lo < q.hi && q.lo < p.hi) return true;
-            return false;
-        };
-        const size_t m = rd.size() - 1;
-        int st = 0;
-        for (size_t e = 0; e < m; ++e)
-            if (hit(rd[m], wr[e]) || hit(wr[m], rd[e]) || hit(wr[m], wr[e])) st = std::max(st, step[e] + 1);
-        step.push_back(st);
-        r.nstep = std::max(r.nstep, st + 1);
-        BlockConv c{};
-        c.w = cw.w; c.bias = cw.bias; c.slope = cw.slope;
-        c.Kpad = cw.Kpad; c.Npad = cw.Npad; c.Cout = cw.Cout; c.Cin = op.cin;
-        c.kh = op.kh; c.kw = op.kw; c.ph = op.ph; c.pw = op.pw; c.act = op.act;
-        c.src_lds = op.in != x;
-        c.src_off = (c.src_lds ? col[op.in] : 0) + op.in_off;
-        c.dst_lds = op.out != y;
-        c.dst_off = (c.dst_lds ? col[op.out] : 0) + op.out_off;
-        c.res = op.res == x;
-        c.res_off = op.res_off;
-        c.step = st;
-        block_unit_shape(n_mf, cw.Cout / 16, cw.K / 32, cw.K, cw.Cout, &c.mf, &c.nf);
-        {  // K-step table: the tap and channel block's byte offset from the pixel, the tap index (31 past the end)
-            const int ld = c.src_lds ? r.ld : h->tensors[x].C;
-            std::vector<int2> tab;
-            const int nks = cw.K / 32;
-            for (int s2 = 0; s2 < nks + 4; ++s2) {
-                if (s2 >= nks || op.cin % 32) { tab.push_back(make_int2(0, 31)); continue; }
-                const int k0 = 32 * s2, tap = k0 / op.cin, cc = k0 - tap * op.cin, tr = tap / op.kw, tc = tap - tr * op.kw;
-                tab.push_back(make_int2((((tr - op.ph) * r.W + (tc - op.pw)) * ld + cc) * 2, tap));
-            }
-            int2* dev = nullptr;
-            if (upload(h, &dev, tab)) return;
-            c.steps = dev;
-        }
-        r.conv.push_back(c);
-        r.flops_px += (double)cw.Cout * cw.K;
-    }
-    BlockArgs a{};
-    a.Cx = h->tensors[x].C; a.Cy = h->tensors[y].C; a.B = 1; a.H = r.H; a.W = r.W; a.G = r.G; a.ld = r.ld;
-    a.nconv = (int)r.conv.size(); a.nstep = r.nstep;
-    for (int i = 0; i < a.nconv; ++i) a.c[i] = r.conv[i];
-    r.ok = block_supported(a);
-}
-
 struct Builder {
     fr_handle* h;
     std::unordered_map<std::string, HostT>& W;
@@ -700,19 +573,6 @@ struct Builder {
     bool fuse_ds(int cin, int c2, const std::string& pre) {
         static const bool off = [] { return ab_int("no_ds_fuse", 0) != 0; }();
         return !off && !is_fp8(pre + ".conv2") && !is_fp8(pre + ".downsample") && cin % 64 == 0 && c2 % 64 == 0;
-    }
-    // An Inception-ResNet block run as one conv_block.hip launch: begin_block() before its convs, end_block()
-    // after them (plan_block); its member convs stay in the plan as the per-conv alternative.
-    int begin_block() {
-        Op op;
-        op.kind = OP_BLOCK;
-        op.block = (int)h->blocks.size();
-        h->blocks.push_back(BlockRec{});
-        h->ops.push_back(op);
-        return (int)h->ops.size() - 1;
-    }
-    void end_block(int bo, int x, int y, const std::string& name) {
-        if (!rc) plan_block(h, bo, x, y, name);
     }
     void maxpool(int in, int out, int out_off, int k, int s, int p) {
         Op op;
@@ -1148,7 +1008,6 @@ void build_irv1(Builder& b) {
     // repeat_1: Block35 x5 @17x17. cat layout [t1 | t2 | b0 | b1 | b2]; conv2d reads [64:160].
     for (int i = 0; i < 5; ++i) {
         const std::string p = m + "repeat_1." + std::to_string(i) + ".";
-        const int bo = b.begin_block();
         const int cat = b.tensor(17, 17, 160);
         b.conv({p + "branch1.0", p + "branch2.0", p + "branch0"}, x, 0, 256, cat, 0, 1, 1, 1, 1, 0, 0, 1);
         b.conv({p + "branch1.1"}, cat, 0, 32, cat, 96, 3, 3, 1, 1, 1, 1, 1);
@@ -1157,7 +1016,6 @@ void build_irv1(Builder& b) {
         b.conv({p + "branch2.2"}, t, 0, 32, cat, 128, 3, 3, 1, 1, 1, 1, 1);
         const int y = b.tensor(17, 17, 256, m + "repeat_1." + std::to_string(i));
         b.conv({p + "conv2d"}, cat, 64, 96, y, 0, 1, 1, 1, 1, 0, 0, 1, x, 0);
-        b.end_block(bo, x, y, "block35");
         x = y;
     }
     {  // mixed_6a
@@ -1174,7 +1032,6 @@ void build_irv1(Builder& b) {
     // repeat_2: Block17 x10 @8x8. cat layout [t1 | b0 | b1]; conv2d reads [128:384].
     for (int i = 0; i < 10; ++i) {
         const std::string p = m + "repeat_2." + std::to_string(i) + ".";
-        const int bo = b.begin_block();
         const int cat = b.tensor(8, 8, 384);
         b.conv({p + "branch1.0", p + "branch0"}, x, 0, 896, cat, 0, 1, 1, 1, 1, 0, 0, 1);
         const int t = b.tensor(8, 8, 128);
@@ -1182,7 +1039,6 @@ void build_irv1(Builder& b) {
         b.conv({p + "branch1.2"}, t, 0, 128, cat, 256, 7, 1, 1, 1, 3, 0, 1);
         const int y = b.tensor(8, 8, 896, m + "repeat_2." + std::to_string(i));
         b.conv({p + "conv2d"}, cat, 128, 256, y, 0, 1, 1, 1, 1, 0, 0, 1, x, 0);
-        b.end_block(bo, x, y, "block17");
         x = y;
     }
     {  // mixed_7a
@@ -1201,7 +1057,6 @@ void build_irv1(Builder& b) {
     // repeat_3: Block8 x5 + final block8 (noReLU) @3x3. cat layout [t1 | b0 | b1]; conv2d reads [192:576].
     for (int i = 0; i < 6; ++i) {
         const std::string p = i < 5 ? m + "repeat_3." + std::to_string(i) + "." : m + "block8.";
-        const int bo = b.begin_block();
         const int cat = b.tensor(3, 3, 576);
         b.conv({p + "branch1.0", p + "branch0"}, x, 0, 1792, cat, 0, 1, 1, 1, 1, 0, 0, 1);
         const int t = b.tensor(3, 3, 192);
@@ -1209,7 +1064,6 @@ void build_irv1(Builder& b) {
         b.conv({p + "branch1.2"}, t, 0, 192, cat, 384, 3, 1, 1, 1, 1, 0, 1);
         const int y = b.tensor(3, 3, 1792, i < 5 ? m + "repeat_3." + std::to_string(i) : m + "block8");
         b.conv({p + "conv2d"}, cat, 192, 384, y, 0, 1, 1, 1, 1, 0, 0, i < 5 ? 1 : 0, x, 0);
-        b.end_block(bo, x, y, "block8");
         x = y;
     }
     const int pool = b.tensor(1, 1, 1792, m + "avgpool_1a");
@@ -1704,35 +1558,15 @@ static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     return (int64_t)B * 100 >= (int64_t)h->stage_min_fill * rounds * cap;
 }
 
-// FR_AB no_block: the IRV1 blocks always run per conv (A/B timing).
-static bool block_enabled() {
-    static const bool off = [] { return ab_int("no_block", 0) != 0; }();
-    return !off;
-}
-
-// Whether an LDS-resident block runs at batch B: the FR_OPT_STAGE rule (0 off, 2 always, 1 measured per batch
-// size; before the measurement: when the workgroups fill at least half the CUs).  Never with materialised
-// intermediates (FR_OPT_KEEP_INTERMEDIATES) or in an fp8 plan.
-static bool block_runs(const fr_handle* h, int B, int bi) {
-    const BlockRec& r = h->blocks[bi];
-    if (!r.ok || h->stage_mode == 0 || h->invariant || h->keep_inter || h->amax || !block_enabled()) return false;
-    if (h->stage_mode == 2) return true;
-    const int c = stage_choice(h, (int)h->stages.size() + bi, B);
-    if (c >= 0) return c == 1;
-    return (B + r.G - 1) / r.G * 2 >= h->n_cu;
-}
-
-// Per-op skip rule: a stage / block op runs when its plan entry says so; its member convs run when it does not.
-// Entries: the stages, then the blocks (Op::grp).
+// Per-op skip rule: a stage op runs when its plan entry says so; its member convs run when it does not (Op::grp).
 static std::vector<char> stage_plan(const fr_handle* h, int B) {
-    std::vector<char> run(h->stages.size() + h->blocks.size());
+    std::vector<char> run(h->stages.size());
     for (size_t i = 0; i < h->stages.size(); ++i) run[i] = stage_runs(h, B, h->stages[i], (int)i);
-    for (size_t j = 0; j < h->blocks.size(); ++j) run[h->stages.size() + j] = block_runs(h, B, (int)j);
     return run;
 }
 
 static bool op_skipped(const Op& op, const std::vector<char>& run) {
-    if (op.kind == OP_STAGE || op.kind == OP_BLOCK) return !run[op.grp];
+    if (op.kind == OP_STAGE) return !run[op.grp];
     return op.grp >= 0 && run[op.grp];
 }
 
@@ -1935,25 +1769,6 @@ static int run_conv_op(fr_handle* h, const Op& op, int B, int f16, hipStream_t s
     return run_conv_args(h, a, s);
 }
 
-// One LDS-resident Inception-ResNet block launch (conv_block.hip).
-static int run_block(fr_handle* h, const Op& op, int B, int f16, hipStream_t s) {
-    const BlockRec& r = h->blocks[op.block];
-    BlockArgs a{};
-    a.x = h->tensors[r.in].dev; a.Cx = h->tensors[r.in].C;
-    a.y = h->tensors[r.out].dev; a.Cy = h->tensors[r.out].C;
-    a.B = B; a.H = r.H; a.W = r.W; a.G = r.G; a.ld = r.ld;
-    a.nconv = (int)r.conv.size(); a.nstep = r.nstep; a.f16 = f16;
-    for (int i = 0; i < a.nconv; ++i) a.c[i] = r.conv[i];
-    ProfScope ps(h, s);
-    const double px = (double)B * r.H * r.W;
-    ps.flops = 2.0 * px * r.flops_px;
-    ps.bytes = 2.0 * px * (a.Cx + a.Cy);
-    for (const auto& c : r.conv) ps.bytes += 2.0 * c.Cout * c.kh * c.kw * c.Cin;
-    ps.start(r.name);
-    FR_HIP_CHECK(launch_block(a, s));
-    return FR_OK;
-}
-
 // Stage or per-conv launches for a stage's blocks at batch B, measured (FR_OPT_STAGE = 1, the default): in the
 // eager tuning forward of a new batch size the member convs run (and tune their kernels), then the member
 // sequence and the stage are timed with HIP events, and the faster is kept for B (-1: not measured yet).  The
@@ -1965,10 +1780,8 @@ static int stage_choice(const fr_handle* h, int st, int B) {
 }
 
 static int measure_stage(fr_handle* h, const Op& op, int B, int f16, const std::vector<char>& stage_run, hipStream_t s) {
-    const std::vector<int>& mem = op.kind == OP_BLOCK ? h->blocks[op.block].conv_ops : h->stages[op.stage].conv_ops;
-    auto fused = [&]() {
-        return op.kind == OP_BLOCK ? run_block(h, op, B, f16, s) : run_stage(h, op, B, f16, stage_run, s);
-    };
+    const std::vector<int>& mem = h->stages[op.stage].conv_ops;
+    auto fused = [&]() { return run_stage(h, op, B, f16, stage_run, s); };
     auto members = [&]() {
         for (int oi : mem) {
             const int rc = run_conv_op(h, h->ops[oi], B, f16, s);
@@ -2074,13 +1887,10 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
         }
         const hipStream_t s = strm[target];
         switch (op.kind) {
-            case OP_STAGE:
-            case OP_BLOCK: {
+            case OP_STAGE: {
                 const bool measure = h->tuning && h->stage_mode == 1 && !h->keep_inter && !h->prof &&
                                      stage_choice(h, op.grp, B) < 0;
-                const int rc = measure                ? measure_stage(h, op, B, f16, stage_run, s)
-                               : op.kind == OP_BLOCK ? run_block(h, op, B, f16, s)
-                                                     : run_stage(h, op, B, f16, stage_run, s);
+                const int rc = measure ? measure_stage(h, op, B, f16, stage_run, s) : run_stage(h, op, B, f16, stage_run, s);
                 if (rc) return rc;
                 break;
             }
@@ -2287,8 +2097,7 @@ int fr_load_weights(fr_handle* h, const void* blob, size_t nbytes) {
     else if (h->arch == FR_ARCH_RESNET50_ARCFACE) build_resnet50(b);
     else build_irv1(b);
     if (!b.rc) b.rc = build_img_weights(h);
-    for (auto& op : h->ops)  // plan entries (stage_plan): the stages, then the blocks
-        op.grp = op.stage >= 0 ? op.stage : op.block >= 0 ? (int)h->stages.size() + op.block : -1;
+    for (auto& op : h->ops) op.grp = op.stage;  // plan entries (stage_plan)
     // the tensors whose producers record amax: inputs of e4m3 convs that run per-conv (an fp8 stage
     // scales its own input; its member convs are its fallback when the stage does not run)
     h->need_amax.assign(h->tensors.size(), 0);
@@ -2691,7 +2500,7 @@ int fr_segment_mean_normalize(const float* E, int D, const int32_t* seg_start, i
     return FR_OK;
 }
 
-// " <fused ms> <per-conv ms>" of a stage / block measured at batch B (measure_stage), else ""
+// " <fused ms> <per-conv ms>" of a stage measured at batch B (measure_stage), else ""
 static std::string meas_note(const fr_handle* h, int grp, int B) {
     for (const auto& m : h->stage_meas)
         if (m.stage == grp && m.B == B) {
@@ -2719,13 +2528,6 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
             const std::string K = std::to_string(9 * r.C);
             out += std::string(r.fp8 ? "stage8 " : "stage ") + std::to_string(B * r.H * r.H) + " " + std::to_string(r.C) + " " + K + " " + K + " " +
                    std::to_string(2 * r.nblk) + " 1 3x3 " + h->tensors[r.out].name + meas_note(h, op.grp, B) + "\n";
-            continue;
-        }
-        if (op.kind == OP_BLOCK) {  // M, 1, MACs per pixel (x 2 = FLOPs), -, 1 launch
-            const BlockRec& r = h->blocks[op.block];
-            const std::string K = std::to_string((long long)r.flops_px);
-            out += "block " + std::to_string(B * r.H * r.W) + " 1 " + K + " " + K + " 1 1 " + std::to_string(r.nstep) +
-                   "step " + (h->tensors[r.out].name.empty() ? r.name : h->tensors[r.out].name) + meas_note(h, op.grp, B) + "\n";
             continue;
         }
         if (op.kind != OP_CONV && op.kind != OP_HEAD) {
@@ -2804,7 +2606,7 @@ int fr_set_option(fr_handle* h, int option, int value) {
 int fr_get_option(const fr_handle* h, int option) {
     if (!h) return FR_ERR_ARG;
     switch (option) {
-        case FR_OPT_STAGE: return h->stages.empty() && h->blocks.empty() ? 0 : h->stage_mode;
+        case FR_OPT_STAGE: return h->stages.empty() ? 0 : h->stage_mode;
         case FR_OPT_STAGE_MIN_FILL: return h->stage_min_fill;
         case FR_OPT_KEEP_INTERMEDIATES: return h->keep_inter ? 1 : 0;
         case FR_OPT_MATCH_EXACT: return h->match_exact ? 1 : 0;

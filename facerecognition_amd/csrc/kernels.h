@@ -152,34 +152,6 @@ size_t split_stage_weight_bytes(int C, int nconv);
 void split_stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out);  // the split stages' K order
 size_t split_stage_xchg_elems(int B);  // enough for either geometry
 hipError_t launch_split_stage(const StageArgs& a, int H, int C, hipStream_t s);
-// LDS-resident Inception-ResNet block (conv_block.hip): a short program of stride-1 convs over one
-// workgroup's G images, branch intermediates in LDS, the block input / output in global memory.
-constexpr int FR_BLOCK_MAX_CONVS = 6;
-struct BlockConv {
-    const bf16_t* w;           // [Npad][Kpad] rows, K = kh * kw * Cin (channel fastest)
-    const float* bias;         // [Npad] or null
-    const float* slope;        // [Npad] PReLU slopes (act == 2)
-    int Kpad, Npad, Cout, Cin, kh, kw, ph, pw, act;
-    int src_lds, src_off;      // source: LDS columns [src_off, + Cin) or block-input channels
-    int dst_lds, dst_off;      // destination: LDS columns or block-output channels
-    int res, res_off;          // add block-input channels [res_off, + Cout) before the activation
-    int step;                  // program step (a barrier after each); convs of one step are independent
-    int mf, nf;                // unit shape: pixel fragments (1, 2, 4) x 16-channel fragments (1, 2, 4)
-    const int2* steps;         // per K-step (+ 4 past the end): {source byte offset of the tap and channel
-                               //   block relative to the pixel, tap index (31 past the end)}
-};
-struct BlockArgs {
-    const bf16_t* x; int Cx;   // block input [B][H][W][Cx]
-    bf16_t* y; int Cy;         // block output [B][H][W][Cy]
-    int B, H, W, G, ld;        // G images per workgroup; ld: LDS row stride (elements, % 32 == 16)
-    int nconv, nstep, f16;
-    BlockConv c[FR_BLOCK_MAX_CONVS];
-    void* ev0;
-    void* ev1;
-};
-size_t block_lds_bytes(int G, int H, int W, int ld);
-bool block_supported(const BlockArgs& a);
-hipError_t launch_block(const BlockArgs& a, hipStream_t s);
 // Fused IResNet100 transition block layer1.0 (conv_trans.hip): conv1 3x3/s1 + PReLU (t rows kept in LDS) ->
 // conv2 3x3/s2 + the K-concatenated 1x1/s2 downsample + bias, one workgroup per image; x [B][112][112][64] ->
 // y [B][56][56][64].  w1 / w2 = trans_pack_weights images of conv1 (K 576) and conv2 + downsample (K 640).
