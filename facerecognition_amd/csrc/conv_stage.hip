@@ -428,10 +428,11 @@ constexpr bool map13_ok() {
 }
 static_assert(map13_ok(), "13-fragment map: bank conflict or pixel not owned exactly once");
 
-// FM pixel fragments per wave starting at fragment f0, NWV waves per workgroup
-template <bool F16, int FM, int NWV>
+// FM pixel fragments per wave starting at fragment f0 x FN 16-channel fragments (channel group wn), NWV waves
+template <bool F16, int FM, int NWV, int FN = fr::FN, int RING_ = 0>
 __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, const int wave, const int lane,
                                              const int wn, const int f0) {
+    constexpr int NPW = 16 * FN;  // output channels per wave
     typedef Num<F16> T;
     typedef typename T::frag frag;
     const int b = blockIdx.x;
@@ -468,7 +469,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 #pragma unroll
         for (int j = 0; j < FM; ++j) pf[j] = *(const frag*)(pa + aoff[j]);
     };
-    constexpr int RING = FM == 13 ? RING13 : (FM == 7 ? RING7 : RING6);
+    constexpr int RING = RING_ ? RING_ : (FM == 13 ? RING13 : (FM == 7 ? RING7 : RING6));
     frag wq[RING][FN];
     auto wload = [&](frag (&w)[FN], int g) {
 #pragma unroll
@@ -575,7 +576,7 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         int ln = fresh_lane();
         const int cl = ln & 15, g = ln >> 4;
         const char* t2 = smem + TAB13 + TS13;
-        const int cb = (8 * wn + (g >> 1) - g) * PLANE13_B + (g & 1) * 8;
+        const int cb = (NPW / 8 * wn + (g >> 1) - g) * PLANE13_B + (g & 1) * 8;
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
             char* const sj = smem + aoff[j] + cb;
@@ -650,6 +651,17 @@ __global__ __launch_bounds__(64 * SNW, 1) void stage13_kernel(StageArgs p) {
 // per CU (the 8-wave kernel loads each twice, once per pixel half, ~1/3 of a conv apart: two L2 reads) and
 // the ring runs 5 K-steps ahead; no second wave shares the SIMD, so none waits at the epilogue barrier
 // for its partner's K loop either.
+// Channel-split variant (3): 8 waves, each all 13 pixel fragments x 32 output channels (26 MFMAs per K-step).
+// Every weight fragment is loaded by ONE wave per CU (the default kernel's waves w and w + 4 load the same 64
+// channels for their pixel halves: twice the L2 -> CU weight stream), at the price of twice the patch reads.
+template <bool F16>
+__global__ __launch_bounds__(64 * SNW, 1) void stage13c_kernel(StageArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    stage13_body<F16, 13, SNW, 2, 3>(p, smem, wave, lane, wave, 0);
+}
+
 template <bool F16>
 __global__ __launch_bounds__(256, 1) void stage13w_kernel(StageArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -682,13 +694,14 @@ void stage_pack_weights(const bf16_t* rows, int Kpad, int C, bf16_t* out) {
 hipError_t launch_stage(const StageArgs& a, hipStream_t s) {
     // variant 1: the legacy 14-fragment kernel; 2: the one-wave-per-SIMD 13-fragment kernel (both
     // bit-identical; FR_OPT_STAGE_VARIANT)
-    const int v = a.variant == 1 || a.variant == 2 ? a.variant : 0;
+    const int v = a.variant >= 1 && a.variant <= 3 ? a.variant : 0;
     auto k = v == 1   ? (a.f16 ? stage_kernel<true> : stage_kernel<false>)
              : v == 2 ? (a.f16 ? stage13w_kernel<true> : stage13w_kernel<false>)
+             : v == 3 ? (a.f16 ? stage13c_kernel<true> : stage13c_kernel<false>)
                       : (a.f16 ? stage13_kernel<true> : stage13_kernel<false>);
     const int lds = v == 1 ? STAGE_LDS : STAGE13_LDS;
     const int threads = v == 2 ? 256 : 64 * SNW;
-    static bool attr[6] = {false, false, false, false, false, false};
+    static bool attr[8] = {false, false, false, false, false, false, false, false};
     const int ai = 2 * v + (a.f16 ? 1 : 0);
     if (!attr[ai]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

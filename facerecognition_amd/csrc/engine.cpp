@@ -221,7 +221,8 @@ struct fr_handle {
     int* fail_host = nullptr;
     int* fail_dev = nullptr;
     int spin_limit = 0;            // FR_OPT_STAGE_SPIN_LIMIT (0: the kernel's default, < 0: every wait runs out)
-    int stage_variant = 0;         // FR_OPT_STAGE_VARIANT (1: the legacy 14-fragment layer3 stage kernel, 2: one wave per SIMD)
+    int stage_variant = 0;         // FR_OPT_STAGE_VARIANT (1: the legacy 14-fragment layer3 stage kernel, 2: one wave per SIMD,
+                                   // 3: waves split by output channel)
     bool no_split = false;         // re-run of a failed forward: split stages off
     int64_t stage_reruns = 0;      // forwards re-run on the per-conv path after a run-out wait
     hipEvent_t chk_ev = nullptr;   // completion of the last synchronous-checked forward
@@ -2029,7 +2030,7 @@ int fr_create(fr_handle** out, int device, int arch, int dtype) {
     h->splitk_inlaunch = ab_int("splitk_inlaunch", 1) != 0;  // A/B timing
     {
         const int v = ab_int("stage_variant", 0);  // A/B timing
-        h->stage_variant = v == 1 || v == 2 ? v : 0;
+        h->stage_variant = v >= 1 && v <= 3 ? v : 0;
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2586,7 +2587,7 @@ int fr_set_option(fr_handle* h, int option, int value) {
             break;
         case FR_OPT_STAGE_SPIN_LIMIT: h->spin_limit = value; break;
         case FR_OPT_STAGE_VARIANT:
-            if (value < 0 || value > 2) { set_error("fr_set_option: FR_OPT_STAGE_VARIANT is 0, 1 or 2"); return FR_ERR_ARG; }
+            if (value < 0 || value > 3) { set_error("fr_set_option: FR_OPT_STAGE_VARIANT is 0 .. 3"); return FR_ERR_ARG; }
             h->stage_variant = value;
             break;
         case FR_OPT_SPLITK_INLAUNCH: h->splitk_inlaunch = value != 0; break;

@@ -313,7 +313,8 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
 /* FR_OPT_STAGE_VARIANT (default 0): the layer3 stage kernel's pixel layout -- 0: 13 fragments of 16 pixels
  * per image (196 of 208 slots used), 1: the legacy 14 rows of 16 positions (2 halo columns computed and
  * discarded per row), 2: the 13-fragment layout at one wave per SIMD (each weight fragment loaded once per
- * CU).  All give the same bits (A/B and regression tests). */
+ * CU), 3: 8 waves split by output channel (32 each) over all 13 fragments (each weight fragment loaded once
+ * per CU, twice the patch reads).  All give the same bits (A/B and regression tests). */
 #define FR_OPT_STAGE_VARIANT 7
 /* FR_OPT_SPLITK_INLAUNCH (default 1; FR_AB splitk_inlaunch=0 starts at 0): a split-K implicit-GEMM conv may reduce
  * its partials in the same launch (the last workgroup of each tile sums them in split order) where the

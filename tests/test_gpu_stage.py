@@ -246,8 +246,9 @@ def test_two_handles_share_a_device(gpu):
 
 @pytest.mark.parametrize("dtype,B", [("bf16", 5), ("f16", 3), ("bf16", 256)])
 def test_stage_variants_bit_identical(gpu, dtype, B):
-    """The 13-fragment layer3 stage kernel (default), the legacy 14-row layout (FR_OPT_STAGE_VARIANT 1) and
-    the one-wave-per-SIMD 13-fragment kernel (2) run the same K-steps and epilogue arithmetic: every layer3 intermediate and every embedding is
+    """The 13-fragment layer3 stage kernel (default), the legacy 14-row layout (FR_OPT_STAGE_VARIANT 1), the
+    one-wave-per-SIMD 13-fragment kernel (2) and the channel-split one (3) run the same K-steps and epilogue
+    arithmetic: every layer3 intermediate and every embedding is
     bit-identical, at padded fragment counts and at the full bs = 256 grid."""
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
@@ -257,12 +258,12 @@ def test_stage_variants_bit_identical(gpu, dtype, B):
     m.set_option(N.FR_OPT_STAGE, 2)
     m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)
     out = {}
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):
         m.set_option(N.FR_OPT_STAGE_VARIANT, v)
         e = m.embed(x).cpu().numpy()
         out[v] = (e, _named(m, B, names))
     m.close()
-    for v in (1, 2):
+    for v in (1, 2, 3):
         assert np.array_equal(out[0][0], out[v][0]), v
         for n in names:
             assert torch.equal(out[0][1][n], out[v][1][n]), (v, n)
