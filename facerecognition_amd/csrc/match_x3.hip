@@ -1,9 +1,11 @@
 // Fast exact gallery match for large galleries (BASELINE config 4: 2048 probes x a 125k-row shard of a
 // 1M x 512 gallery per rank).  The exact f32 path (match.hip, v_mfma_f32_16x16x4_f32) runs at the f32
 // MFMA rate, 1/16 of bf16.  Here:
-//   1. candidates: s~ = Ph.Gh + Ph.Gl + Pl.Gh on v_mfma_f32_16x16x32_bf16 (x = xh + xl, both bf16: a
-//      3-product split), |s~ - s| <= eps = 1.25e-4 ||p|| ||g|| (split error 3 * 2^-16 plus two f32
-//      accumulations of 512 terms, worst case); per (probe, split) the top-KO by s~ of four sub-lists
+//   1. candidates: s~ = Ph.Gh + Pl.Gh on v_mfma_f32_16x16x32_bf16 (p = ph + pl split in two bf16, the gallery
+//      row rounded to ONE bf16 gh: half the gallery bytes of a hi/lo split and 2 MFMAs per product instead of
+//      3), |s~ - s| <= eps = 4.0e-3 ||p|| ||g|| (|g - gh| <= 2^-8 |g| per element, p's split residual 2^-16,
+//      two f32 accumulations of 512 terms: 2^-8 + 2^-16 + 1024 2^-24 = 3.98e-3, worst case); per (probe, split)
+//      the top-KO by s~ of four sub-lists
 //      of KP (rows 16j + 4 sub + r of each tile, kept by the lane whose accumulators hold them) and a floor: every row dropped from a sub-list, or by the
 //      filter, has s~ <= floor = the best last entry of the full sub-lists;
 //   2. rescore (one wave per probe): the global top-KC by s~ are rescored exactly with the k-ordered f32
@@ -15,8 +17,8 @@
 //      with it within 2 eps), the wave rescans the whole gallery exactly for that probe (counted).  The
 //      result is therefore always the exact top-k of the f32 scores.
 // Block = 8 waves, 128 probes; each wave keeps its 16 probes' bf16 hi/lo fragments in registers for the
-// whole kernel; gallery hi/lo chunks (64 rows x 64 dims, 16 KiB) stream through a 7-slot LDS-DMA ring
-// six chunks ahead (counted vmcnt, raw barriers; XOR-swizzled 16-B chunks): the ring depth, not HBM,
+// whole kernel; gallery chunks (64 rows x 64 dims of gh, 8 KiB) stream through a 13-slot LDS-DMA ring
+// twelve chunks ahead (counted vmcnt, raw barriers; XOR-swizzled 16-B chunks): the ring depth, not HBM,
 // sets the stream rate (in flight / L2 latency).  Blocks of one gallery split share an XCD (xcd_remap), so each XCD streams its
 // splits from HBM once and the other probe blocks hit its L2.
 #include "kernels.h"
@@ -38,7 +40,10 @@ constexpr int XD = 512;       // embedding dim (the kernel is specialised)
 constexpr int KP = 8;         // candidates per (probe, split, sub-lane): 4 sub-lanes per probe
 constexpr int KO = 16;        // candidates written per (probe, split) ...
 constexpr int KS = KO + 1;    // ... plus one floor entry (index -2)
-constexpr int KC = 16;        // candidates rescored per probe
+constexpr int KC = 32;        // candidates rescored per probe (the 2 eps band of the 2-product pass needs more
+                              // than the 3-product one's 16: with 16, random 1M-row galleries put the 5th
+                              // score within 2 eps of the 16th often enough to trigger rescans)
+constexpr float X2_EPS = 4.0e-3f;  // |s~ - s| / (||p|| ||g||), header
 
 __device__ __forceinline__ bool better(float s1, int i1, float s2, int i2) {
     return s1 > s2 || (s1 == s2 && i1 < i2);
@@ -85,13 +90,13 @@ __device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_ca
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
 
-// The candidate pass's gallery copy, in its chunk order: g = gh + gl + r (gh, gl bf16, |r| <= 2^-16 |g|),
-// chunk (tile T = 64 rows, dims 64c ..) = 16 KiB contiguous at (8T + c) x 16 KiB, [gh 64 rows x 128 B][gl
-// 64 rows x 128 B], a row's eight 16-B groups stored at slot group ^ xswz_row(row): the LDS-DMA copies a
-// chunk linearly and the fragment reads stay conflict-free.  (Row-major gh / gl arrays put a chunk's 64
+// The candidate pass's gallery copy, in its chunk order: gh = bf16(g) (|g - gh| <= 2^-8 |g|), chunk (tile
+// T = 64 rows, dims 64c ..) = 8 KiB contiguous at (8T + c) x 8 KiB, [64 rows x 128 B], a row's eight 16-B
+// groups stored at slot group ^ xswz_row(row): the LDS-DMA copies a chunk linearly and the fragment reads
+// stay conflict-free.  (Row-major gh / gl arrays put a chunk's 64
 // rows 1 KiB apart: its 128-B pieces fell on a few HBM / L2 channels, every block of a split on the same
 // ones.)  Rows past the gallery in the last tile are never candidates (the kernel masks them).
-constexpr int XCHUNK_E = 2 * 64 * 64;  // bf16 elements per chunk (16 KiB)
+constexpr int XCHUNK_E = 64 * 64;  // bf16 elements per chunk (8 KiB)
 __device__ __forceinline__ int xswz_row(int row) { return (row >> 1) & 7; }
 
 __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ G, int64_t row0, int64_t n,
@@ -103,25 +108,19 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
         const float* src = G + r * 512 + 8 * grp;
         const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
         const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        uint16_t hb[8], lb[8];
+        uint16_t hb[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            hb[e] = bf16_bits(v[e]);
-            lb[e] = bf16_bits(v[e] - __uint_as_float((uint32_t)hb[e] << 16));
-        }
+        for (int e = 0; e < 8; ++e) hb[e] = bf16_bits(v[e]);
         bf16_t* dst = T + ((r >> 6) * 8 + c) * XCHUNK_E + rr * 64 + (g ^ xswz_row(rr)) * 8;
-        uint4 hv, lv;
+        uint4 hv;
         hv.x = hb[0] | (uint32_t)hb[1] << 16; hv.y = hb[2] | (uint32_t)hb[3] << 16;
         hv.z = hb[4] | (uint32_t)hb[5] << 16; hv.w = hb[6] | (uint32_t)hb[7] << 16;
-        lv.x = lb[0] | (uint32_t)lb[1] << 16; lv.y = lb[2] | (uint32_t)lb[3] << 16;
-        lv.z = lb[4] | (uint32_t)lb[5] << 16; lv.w = lb[6] | (uint32_t)lb[7] << 16;
         *(uint4*)dst = hv;
-        *(uint4*)(dst + XCHUNK_E / 2) = lv;
     }
 }
 
-constexpr int XSLOT = 7;  // LDS ring depth (chunks): XSLOT - 1 in flight (4, 5, 9, 10 measured slower)
-constexpr int XCHUNK_B = 2 * XG * XC * 2;      // 16 KiB: [hi 64 rows x 128 B][lo 64 rows x 128 B]
+constexpr int XSLOT = 13;  // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB, as 6 of the 16-KiB hi/lo chunks)
+constexpr int XCHUNK_B = XG * XC * 2;          // 8 KiB: [64 rows x 128 B]
 static_assert(XCHUNK_B == XCHUNK_E * 2, "chunk layout");
 constexpr int XRB = XC * 2;                    // LDS row bytes
 constexpr int XPPW = XCHUNK_B / 1024 / 8;      // 1-KiB DMA pieces per wave per chunk
@@ -264,11 +263,9 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
                     const int row = 16 * j + (lane & 15);
                     const int o = row * XRB + xswz(row, kch) * 16;
                     const bf8v gh = *(const bf8v*)(ch + o);
-                    const bf8v gl = *(const bf8v*)(ch + XCHUNK_B / 2 + o);
                     // gallery rows as the A operand: D[row][probe], so each lane's accumulators belong to
                     // ONE probe (its own candidate sub-list) and the filter never leaves the registers
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, ph[t], acc[j], 0, 0, 0);
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl, ph[t], acc[j], 0, 0, 0);
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, pl[t], acc[j], 0, 0, 0);
                 }
             }
@@ -404,7 +401,7 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
     for (int d = lane; d < XD; d += 64) pp = fmaf(prow[d], prow[d], pp);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) pp += __shfl_xor(pp, o);
-    const float eps = 1.25e-4f * sqrtf(pp) * 1.001f;  // rows are unit norm within 1e-3 (or zero)
+    const float eps = X2_EPS * sqrtf(pp) * 1.001f;  // rows are unit norm within 1e-3 (or zero)
     // (c) exact top-k among the candidates
     int h1 = 0;
     float kth = INFINITY, outs = -INFINITY;

@@ -41,8 +41,10 @@ def run(rows, probes, k, iters, exact=False, x3_min_rows=None):
     flop = 2.0 * probes * rows * 512
     gbytes = rows * 512 * 4 / 1e9
     x3 = not exact and rows >= (x3_min_rows or 32768)
-    return {"rows": rows, "probes": probes, "k": k, "path": "bf16x3" if x3 else "exact-f32", "ms": round(ms, 4), "tflops_f32": round(flop / ms / 1e9, 2),
-            "gallery_GBps": round(gbytes / ms * 1e3, 1), "top1_agree_torch": agree}
+    fb = gal.fallbacks() if hasattr(gal, "fallbacks") else None
+    return {"rows": rows, "probes": probes, "k": k, "path": "bf16 candidates" if x3 else "exact-f32", "ms": round(ms, 4),
+            "tflops_f32": round(flop / ms / 1e9, 2), "gallery_GBps": round(gbytes / ms * 1e3, 1), "top1_agree_torch": agree,
+            "proof_fallbacks": fb}
 
 
 if __name__ == "__main__":
