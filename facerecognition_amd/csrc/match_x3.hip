@@ -35,7 +35,8 @@ namespace {
 constexpr int XW = 8;         // waves per block
 constexpr int XP = 16 * XW;   // probes per block
 constexpr int XG = 64;        // gallery rows per tile
-constexpr int XC = 64;        // dims per LDS chunk
+constexpr int XC = 128;       // dims per LDS chunk
+constexpr int XNC = 512 / XC; // chunks per 64-row tile
 constexpr int XD = 512;       // embedding dim (the kernel is specialised)
 constexpr int KP = 8;         // candidates per (probe, split, sub-lane): 4 sub-lanes per probe
 constexpr int KO = 16;        // candidates written per (probe, split) ...
@@ -91,27 +92,27 @@ __device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_ca
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
 
 // The candidate pass's gallery copy, in its chunk order: gh = bf16(g) (|g - gh| <= 2^-8 |g|), chunk (tile
-// T = 64 rows, dims 64c ..) = 8 KiB contiguous at (8T + c) x 8 KiB, [64 rows x 128 B], a row's eight 16-B
-// groups stored at slot group ^ xswz_row(row): the LDS-DMA copies a chunk linearly and the fragment reads
-// stay conflict-free.  (Row-major gh / gl arrays put a chunk's 64
-// rows 1 KiB apart: its 128-B pieces fell on a few HBM / L2 channels, every block of a split on the same
-// ones.)  Rows past the gallery in the last tile are never candidates (the kernel masks them).
-constexpr int XCHUNK_E = 64 * 64;  // bf16 elements per chunk (8 KiB)
-__device__ __forceinline__ int xswz_row(int row) { return (row >> 1) & 7; }
+// T = 64 rows, dims 128c ..) = 16 KiB contiguous at (4T + c) x 16 KiB, [64 rows x 256 B], a row's sixteen
+// 16-B groups stored at slot group ^ (row & 15): the LDS-DMA copies a chunk linearly and the fragment reads
+// stay conflict-free (the lanes of a ds_read_b128 group read groups kch, kch ^ 1 of 16 different rows).
+// (Row-major arrays put a chunk's 64 rows 1 KiB apart: its pieces fell on a few HBM / L2 channels, every
+// block of a split on the same ones.)  Rows past the gallery in the last tile are never candidates (the kernel masks them).
+constexpr int XCHUNK_E = 64 * XC;  // bf16 elements per chunk (16 KiB)
+__device__ __forceinline__ int xswz_row(int row) { return row & 15; }
 
 __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ G, int64_t row0, int64_t n,
                                                        bf16_t* __restrict__ T) {
     // one thread per 8 dims of one row
     for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n * 64; i += (int64_t)gridDim.x * 256) {
         const int64_t r = row0 + i / 64;
-        const int grp = (int)(i % 64), c = grp >> 3, g = grp & 7, rr = (int)(r & 63);
+        const int grp = (int)(i % 64), c = grp / (XC / 8), g = grp % (XC / 8), rr = (int)(r & 63);
         const float* src = G + r * 512 + 8 * grp;
         const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
         const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         uint16_t hb[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) hb[e] = bf16_bits(v[e]);
-        bf16_t* dst = T + ((r >> 6) * 8 + c) * XCHUNK_E + rr * 64 + (g ^ xswz_row(rr)) * 8;
+        bf16_t* dst = T + ((r >> 6) * XNC + c) * XCHUNK_E + rr * XC + (g ^ xswz_row(rr)) * 8;
         uint4 hv;
         hv.x = hb[0] | (uint32_t)hb[1] << 16; hv.y = hb[2] | (uint32_t)hb[3] << 16;
         hv.z = hb[4] | (uint32_t)hb[5] << 16; hv.w = hb[6] | (uint32_t)hb[7] << 16;
@@ -119,8 +120,8 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
     }
 }
 
-constexpr int XSLOT = 13;  // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB, as 6 of the 16-KiB hi/lo chunks)
-constexpr int XCHUNK_B = XG * XC * 2;          // 8 KiB: [64 rows x 128 B]
+constexpr int XSLOT = 7;   // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB)
+constexpr int XCHUNK_B = XG * XC * 2;          // 16 KiB: [64 rows x 256 B]
 static_assert(XCHUNK_B == XCHUNK_E * 2, "chunk layout");
 constexpr int XRB = XC * 2;                    // LDS row bytes
 constexpr int XPPW = XCHUNK_B / 1024 / 8;      // 1-KiB DMA pieces per wave per chunk
@@ -175,12 +176,12 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
     // LDS-DMA of chunk (tile t0, dims 64c..): a linear copy of its 16 KiB (split_x3_kernel's layout), 16
     // pieces of 1 KiB, wave w issues pieces 2w, 2w+1.  The resource starts at the split's first chunk
     // (32-bit offsets); look-ahead chunks past the gallery read 0, past the split are never used.
-    const size_t g_chunk0 = (size_t)(g_begin / XG) * 8;
-    const size_t g_left = ((size_t)((N + XG - 1) / XG) * 8 - g_chunk0) * XCHUNK_B;
+    const size_t g_chunk0 = (size_t)(g_begin / XG) * XNC;
+    const size_t g_left = ((size_t)((N + XG - 1) / XG) * XNC - g_chunk0) * XCHUNK_B;
     const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(GT + g_chunk0 * XCHUNK_E), 0,
                                                                         (int)min(g_left, (size_t)0x7fffffff), 0x00020000);
     auto issue_chunk = [&](int64_t t0, int c, int slot) {
-        const uint32_t cbase = (uint32_t)((((t0 - g_begin) / XG) * 8 + c) * XCHUNK_B);
+        const uint32_t cbase = (uint32_t)((((t0 - g_begin) / XG) * XNC + c) * XCHUNK_B);
 #pragma unroll
         for (int u = 0; u < XPPW; ++u) {
             const int piece = XPPW * wave + u;
@@ -314,29 +315,9 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
     }
 }
 
-// Exact score in the order of match.hip's v_mfma_f32_16x16x4_f32 sequence: per 16-dim block t16 the
-// MFMAs take components comp = 0..3 of the lanes' float4 k-groups kq = 0..3, each a k-ordered fmaf chain.
-__device__ __forceinline__ float exact_dot(const float* __restrict__ p, const float* __restrict__ g) {
-    float acc = 0.f;
-#pragma unroll 2
-    for (int t16 = 0; t16 < XD / 16; ++t16) {
-        float4 a[4], b[4];
-#pragma unroll
-        for (int kq = 0; kq < 4; ++kq) {
-            a[kq] = *(const float4*)(p + 16 * t16 + 4 * kq);
-            b[kq] = *(const float4*)(g + 16 * t16 + 4 * kq);
-        }
-#pragma unroll
-        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].x, b[kq].x, acc);
-#pragma unroll
-        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].y, b[kq].y, acc);
-#pragma unroll
-        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].z, b[kq].z, acc);
-#pragma unroll
-        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].w, b[kq].w, acc);
-    }
-    return acc;
-}
+// Exact score in the order of match.hip's v_mfma_f32_16x16x4_f32 sequence: per 16-dim block t16 the MFMAs take
+// components comp = 0..3 of the lanes' float4 k-groups kq = 0..3, each a k-ordered fmaf chain (exact_dot_lds
+// below, with the probe row in LDS).
 
 // wave-wide pop of the best (score desc, index asc) entry of per-lane sorted lists
 template <int KMAX>
@@ -357,26 +338,78 @@ __device__ __forceinline__ void wave_pop(float (&ls)[KMAX], int (&li)[KMAX], int
     if (wi == bi && bi != INT_MAX) ++head;  // indices are unique: the owner pops
 }
 
+// The exact score with the probe row in LDS (every lane reads the same address: a broadcast) and four 16-dim steps
+// of gallery loads in flight
+__device__ __forceinline__ float exact_dot_lds(const float* p, const float* __restrict__ g) {
+    float acc = 0.f;
+#pragma unroll 4
+    for (int t16 = 0; t16 < XD / 16; ++t16) {
+        float4 a[4], b[4];
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) {
+            a[kq] = *(const float4*)(p + 16 * t16 + 4 * kq);
+            b[kq] = *(const float4*)(g + 16 * t16 + 4 * kq);
+        }
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].x, b[kq].x, acc);
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].y, b[kq].y, acc);
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].z, b[kq].z, acc);
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) acc = fmaf(a[kq].w, b[kq].w, acc);
+    }
+    return acc;
+}
+
+constexpr int KL = 8;  // rescore: per-lane candidate list depth (a lane's dropped entries join the floor)
+
 __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ P, int B, const float* __restrict__ G,
                                                       int64_t N, int64_t index_base, const float* __restrict__ cs,
                                                       const int32_t* __restrict__ ci, int n_lists, int k,
                                                       float* __restrict__ out_s, int32_t* __restrict__ out_i,
                                                       int* __restrict__ n_fallback) {
-    const int lane = threadIdx.x & 63;
-    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    __shared__ __attribute__((aligned(16))) float prow_s[4][XD];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int p = blockIdx.x * 4 + wave;
     if (p >= B) return;
     const float* prow = P + (size_t)p * XD;
-    // (a) global top-KC by approximate score; T = the KC-th (or -inf with fewer candidates)
-    float ls[KC];
-    int li[KC];
+    float* const pl = prow_s[wave];
+    for (int d = 4 * lane; d < XD; d += 256) *(float4*)(pl + d) = *(const float4*)(prow + d);
+    // (a) global top-KC by approximate score; T = the KC-th (or -inf with fewer candidates).  Each lane keeps its
+    // best KL of the entries it reads (eight loads in flight per round); an entry a full list drops scores at
+    // most lane_floor, which joins the floor, so the proof below stays valid (a lane holding more than KL of
+    // the KC best can only make it fail, and then the probe is rescanned).
+    float ls[KL];
+    int li[KL];
 #pragma unroll
-    for (int q = 0; q < KC; ++q) { ls[q] = -INFINITY; li[q] = INT_MAX; }
+    for (int q = 0; q < KL; ++q) { ls[q] = -INFINITY; li[q] = INT_MAX; }
     const int n = n_lists * KS;
     float floor_s = -INFINITY;  // every row no list holds has s~ <= floor_s
-    for (int c = lane; c < n; c += 64) {
-        const int idx = ci[(size_t)p * n + c];
-        if (idx >= 0) insert<KC>(ls, li, cs[(size_t)p * n + c], idx);
-        else if (idx == -2) floor_s = fmaxf(floor_s, cs[(size_t)p * n + c]);
+    const float* csp = cs + (size_t)p * n;
+    const int32_t* cip = ci + (size_t)p * n;
+    for (int c0 = lane; c0 < n; c0 += 64 * 8) {
+        float vs[8];
+        int vi[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int c = c0 + 64 * u;
+            vi[u] = c < n ? cip[c] : -1;
+            vs[u] = c < n ? csp[c] : -INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (vi[u] >= 0) {
+                if (better(vs[u], vi[u], ls[KL - 1], li[KL - 1])) {
+                    if (li[KL - 1] != INT_MAX) floor_s = fmaxf(floor_s, ls[KL - 1]);  // pushed out of the list
+                    insert<KL>(ls, li, vs[u], vi[u]);
+                } else {
+                    floor_s = fmaxf(floor_s, vs[u]);
+                }
+            } else if (vi[u] == -2) {
+                floor_s = fmaxf(floor_s, vs[u]);
+            }
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) floor_s = fmaxf(floor_s, __shfl_xor(floor_s, o));
@@ -385,7 +418,7 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
     for (int q = 0; q < KC; ++q) {
         float ws;
         int wi;
-        wave_pop<KC>(ls, li, head, ws, wi);
+        wave_pop<KL>(ls, li, head, ws, wi);
         if (lane == q) my_idx = wi == INT_MAX ? -1 : wi;
         if (q == KC - 1) T = wi == INT_MAX ? -INFINITY : ws;
     }
@@ -394,7 +427,7 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
     float rs[1] = {-INFINITY};
     int ri[1] = {INT_MAX};
     if (lane < KC && my_idx >= 0) {
-        rs[0] = exact_dot(prow, G + (size_t)(my_idx - index_base) * XD);
+        rs[0] = exact_dot_lds(pl, G + (size_t)(my_idx - index_base) * XD);
         ri[0] = my_idx;
     }
     float pp = 0.f;
@@ -425,7 +458,7 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
         for (int q = 0; q < KC; ++q) { fs[q] = -INFINITY; fi[q] = INT_MAX; }
 #pragma unroll 1
         for (int64_t r = lane; r < N; r += 64)
-            insert<KC>(fs, fi, exact_dot(prow, G + (size_t)r * XD), (int)(r + index_base));
+            insert<KC>(fs, fi, exact_dot_lds(pl, G + (size_t)r * XD), (int)(r + index_base));
         int hh = 0;
         for (int q = 0; q < k; ++q) {
             float ws;
@@ -447,7 +480,7 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
 // recognition_engine.py:328-381).  match_p512_kernel keeps 64 probes per block in MFMA fragments, so at B = 1 a
 // block scores 63 padding probes and the split plan leaves ~80 blocks each walking 128 rows through an LDS ring
 // (32 us for 10k rows).  Here each lane scores one row at a time (R rows per lane, WPB waves per block) for every
-// probe with exact_dot's k-ordered fmaf chain (the f32 kernels' order: the scores are theirs bit for bit; 8 16-dim
+// probe with exact_dot_lds's k-ordered fmaf chain (the f32 kernels' order: the scores are theirs bit for bit; 8 16-dim
 // steps of loads in flight measured 15.7 vs 13.9 us for 1 x 10k), and keeps per-lane sorted lists; each wave's top-k per probe goes to LDS, wave 0
 // merges the block's WPB lists and writes one candidate list per block for topk_merge_kernel.  WPB = 1 while the
 // waves fit the CUs (each CU then streams one wave's 128 KiB of rows), more waves per block (fewer lists) beyond.
@@ -483,7 +516,7 @@ __global__ __launch_bounds__(64 * WPB) void match_rows_kernel(const float* __res
                 float4 pv[4];
 #pragma unroll
                 for (int kq = 0; kq < 4; ++kq) pv[kq] = *(const float4*)(P + (size_t)b * XD + 16 * t16 + 4 * kq);
-                // exact_dot's order: k = 16 t + 4 kq + c, c outer
+                // exact_dot_lds's order: k = 16 t + 4 kq + c, c outer
 #pragma unroll
                 for (int kq = 0; kq < 4; ++kq) acc[b] = fmaf(pv[kq].x, gv[kq].x, acc[b]);
 #pragma unroll
@@ -542,7 +575,7 @@ __global__ __launch_bounds__(64 * WPB) void match_rows_kernel(const float* __res
 
 }  // namespace
 
-size_t x3_gallery_elems(int64_t rows) { return (size_t)((rows + XG - 1) / XG) * 8 * XCHUNK_E; }
+size_t x3_gallery_elems(int64_t rows) { return (size_t)((rows + XG - 1) / XG) * XNC * XCHUNK_E; }
 
 hipError_t launch_split_x3(const float* G, int64_t row0, int64_t n, bf16_t* T, hipStream_t s) {
     if (n <= 0) return hipSuccess;
