@@ -35,8 +35,7 @@ namespace {
 constexpr int XW = 8;         // waves per block
 constexpr int XP = 16 * XW;   // probes per block
 constexpr int XG = 64;        // gallery rows per tile
-constexpr int XC = 128;       // dims per LDS chunk
-constexpr int XNC = 512 / XC; // chunks per 64-row tile
+constexpr int XC = 64;        // dims per LDS chunk
 constexpr int XD = 512;       // embedding dim (the kernel is specialised)
 constexpr int KP = 8;         // candidates per (probe, split, sub-lane): 4 sub-lanes per probe
 constexpr int KO = 16;        // candidates written per (probe, split) ...
@@ -92,27 +91,27 @@ __device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_ca
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
 
 // The candidate pass's gallery copy, in its chunk order: gh = bf16(g) (|g - gh| <= 2^-8 |g|), chunk (tile
-// T = 64 rows, dims 128c ..) = 16 KiB contiguous at (4T + c) x 16 KiB, [64 rows x 256 B], a row's sixteen
-// 16-B groups stored at slot group ^ (row & 15): the LDS-DMA copies a chunk linearly and the fragment reads
-// stay conflict-free (the lanes of a ds_read_b128 group read groups kch, kch ^ 1 of 16 different rows).
-// (Row-major arrays put a chunk's 64 rows 1 KiB apart: its pieces fell on a few HBM / L2 channels, every
-// block of a split on the same ones.)  Rows past the gallery in the last tile are never candidates (the kernel masks them).
-constexpr int XCHUNK_E = 64 * XC;  // bf16 elements per chunk (16 KiB)
-__device__ __forceinline__ int xswz_row(int row) { return row & 15; }
+// T = 64 rows, dims 64c ..) = 8 KiB contiguous at (8T + c) x 8 KiB, [64 rows x 128 B], a row's eight 16-B
+// groups stored at slot group ^ xswz_row(row): the LDS-DMA copies a chunk linearly and the fragment reads
+// stay conflict-free.  (Row-major gh / gl arrays put a chunk's 64
+// rows 1 KiB apart: its 128-B pieces fell on a few HBM / L2 channels, every block of a split on the same
+// ones.)  Rows past the gallery in the last tile are never candidates (the kernel masks them).
+constexpr int XCHUNK_E = 64 * 64;  // bf16 elements per chunk (8 KiB)
+__device__ __forceinline__ int xswz_row(int row) { return (row >> 1) & 7; }
 
 __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ G, int64_t row0, int64_t n,
                                                        bf16_t* __restrict__ T) {
     // one thread per 8 dims of one row
     for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n * 64; i += (int64_t)gridDim.x * 256) {
         const int64_t r = row0 + i / 64;
-        const int grp = (int)(i % 64), c = grp / (XC / 8), g = grp % (XC / 8), rr = (int)(r & 63);
+        const int grp = (int)(i % 64), c = grp >> 3, g = grp & 7, rr = (int)(r & 63);
         const float* src = G + r * 512 + 8 * grp;
         const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
         const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         uint16_t hb[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) hb[e] = bf16_bits(v[e]);
-        bf16_t* dst = T + ((r >> 6) * XNC + c) * XCHUNK_E + rr * XC + (g ^ xswz_row(rr)) * 8;
+        bf16_t* dst = T + ((r >> 6) * 8 + c) * XCHUNK_E + rr * 64 + (g ^ xswz_row(rr)) * 8;
         uint4 hv;
         hv.x = hb[0] | (uint32_t)hb[1] << 16; hv.y = hb[2] | (uint32_t)hb[3] << 16;
         hv.z = hb[4] | (uint32_t)hb[5] << 16; hv.w = hb[6] | (uint32_t)hb[7] << 16;
@@ -120,8 +119,8 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
     }
 }
 
-constexpr int XSLOT = 7;   // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB)
-constexpr int XCHUNK_B = XG * XC * 2;          // 16 KiB: [64 rows x 256 B]
+constexpr int XSLOT = 13;  // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB, as 6 of the 16-KiB hi/lo chunks)
+constexpr int XCHUNK_B = XG * XC * 2;          // 8 KiB: [64 rows x 128 B]
 static_assert(XCHUNK_B == XCHUNK_E * 2, "chunk layout");
 constexpr int XRB = XC * 2;                    // LDS row bytes
 constexpr int XPPW = XCHUNK_B / 1024 / 8;      // 1-KiB DMA pieces per wave per chunk
@@ -176,12 +175,12 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
     // LDS-DMA of chunk (tile t0, dims 64c..): a linear copy of its 16 KiB (split_x3_kernel's layout), 16
     // pieces of 1 KiB, wave w issues pieces 2w, 2w+1.  The resource starts at the split's first chunk
     // (32-bit offsets); look-ahead chunks past the gallery read 0, past the split are never used.
-    const size_t g_chunk0 = (size_t)(g_begin / XG) * XNC;
-    const size_t g_left = ((size_t)((N + XG - 1) / XG) * XNC - g_chunk0) * XCHUNK_B;
+    const size_t g_chunk0 = (size_t)(g_begin / XG) * 8;
+    const size_t g_left = ((size_t)((N + XG - 1) / XG) * 8 - g_chunk0) * XCHUNK_B;
     const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(GT + g_chunk0 * XCHUNK_E), 0,
                                                                         (int)min(g_left, (size_t)0x7fffffff), 0x00020000);
     auto issue_chunk = [&](int64_t t0, int c, int slot) {
-        const uint32_t cbase = (uint32_t)((((t0 - g_begin) / XG) * XNC + c) * XCHUNK_B);
+        const uint32_t cbase = (uint32_t)((((t0 - g_begin) / XG) * 8 + c) * XCHUNK_B);
 #pragma unroll
         for (int u = 0; u < XPPW; ++u) {
             const int piece = XPPW * wave + u;
@@ -575,7 +574,7 @@ __global__ __launch_bounds__(64 * WPB) void match_rows_kernel(const float* __res
 
 }  // namespace
 
-size_t x3_gallery_elems(int64_t rows) { return (size_t)((rows + XG - 1) / XG) * XNC * XCHUNK_E; }
+size_t x3_gallery_elems(int64_t rows) { return (size_t)((rows + XG - 1) / XG) * 8 * XCHUNK_E; }
 
 hipError_t launch_split_x3(const float* G, int64_t row0, int64_t n, bf16_t* T, hipStream_t s) {
     if (n <= 0) return hipSuccess;
