@@ -225,18 +225,24 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
         uint32_t m = 0;
 #pragma unroll
         for (int e = 0; e < 16; ++e) m |= a[e >> 2][e & 3] > thr ? 1u << e : 0u;
-        // one pass per hit of the busiest lane (usually one): pick the score by a select tree
+        // one pass per hit of the busiest lane (usually one): pick the score by a select tree of bitfield
+        // inserts on the raw bits (written as ternaries over array elements, the compiler folded the selects
+        // into a dynamically indexed array and spilled it through LDS: two LDS round trips per insert)
         while (m) {
             const int e = __builtin_ctz(m);
             m &= m - 1;
-            float v8[8], v4[4], v2[2];
+            const uint32_t m3 = 0u - (uint32_t)((e >> 3) & 1), m2 = 0u - (uint32_t)((e >> 2) & 1);
+            const uint32_t m1 = 0u - (uint32_t)((e >> 1) & 1), m0 = 0u - (uint32_t)(e & 1);
+            auto bsel = [](uint32_t msk, uint32_t x, uint32_t y) { return (msk & x) | (~msk & y); };
+            uint32_t v8[8], v4[4], v2[2];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v8[q] = (e & 8) ? a[(q + 8) >> 2][(q + 8) & 3] : a[q >> 2][q & 3];
+            for (int q = 0; q < 8; ++q)
+                v8[q] = bsel(m3, __float_as_uint(a[(q + 8) >> 2][(q + 8) & 3]), __float_as_uint(a[q >> 2][q & 3]));
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v4[q] = (e & 4) ? v8[q + 4] : v8[q];
+            for (int q = 0; q < 4; ++q) v4[q] = bsel(m2, v8[q + 4], v8[q]);
 #pragma unroll
-            for (int q = 0; q < 2; ++q) v2[q] = (e & 2) ? v4[q + 2] : v4[q];
-            const float sc = (e & 1) ? v2[1] : v2[0];
+            for (int q = 0; q < 2; ++q) v2[q] = bsel(m1, v4[q + 2], v4[q]);
+            const float sc = __uint_as_float(bsel(m0, v2[1], v2[0]));
             insert_s<KP>(ls, li, sc, (int)(tb + index_base) + 16 * (e >> 2) + 4 * my_sub + (e & 3));
         }
     };
