@@ -361,6 +361,7 @@ constexpr int L2R13[16] = {0, 8, 1, 9, 4, 12, 5, 13, 6, 14, 7, 15, 2, 10, 3, 11}
 struct Map13 {
     uint8_t pos[13][16];  // patch position of lane l's pixel in fragment f
     uint8_t cls[13][16];  // its bias-table border class 3 * rowclass + colclass (SPARE13: spare lane)
+    uint8_t pix[13][16];  // its pixel index r * 14 + c (SPARE13: spare lane)
 };
 
 __host__ __device__ constexpr int border_cls13(int r, int c) {
@@ -378,6 +379,7 @@ constexpr Map13 make_map13() {
             const int x = (c - r + 16) & 15, k = cnt[x]++, l = r2l[x];
             m.pos[k][l] = (uint8_t)pix_pos13(r, c);
             m.cls[k][l] = (uint8_t)border_cls13(r, c);
+            m.pix[k][l] = (uint8_t)(r * SW + c);
         }
     // fragment 12: residues 0 (lane 0), 1 (lane 2), 0 (lane 4), 15 (lane 11); the spare lanes read
     // residues 2,3,4,5,6,9 (lanes 1,3,12..15) and 2..7 (lanes 5..10) at interior positions 112 + x
@@ -386,10 +388,12 @@ constexpr Map13 make_map13() {
     for (int i = 0; i < 4; ++i) {
         m.pos[12][vl[i]] = (uint8_t)pix_pos13(vr[i], vc[i]);
         m.cls[12][vl[i]] = (uint8_t)border_cls13(vr[i], vc[i]);
+        m.pix[12][vl[i]] = (uint8_t)(vr[i] * SW + vc[i]);
     }
     for (int i = 0; i < 12; ++i) {
         m.pos[12][sl[i]] = (uint8_t)(112 + sx[i]);
         m.cls[12][sl[i]] = (uint8_t)SPARE13;
+        m.pix[12][sl[i]] = (uint8_t)SPARE13;
     }
     return m;
 }
@@ -419,7 +423,8 @@ constexpr bool map13_ok() {
             if (q < 16 || q > 224) return false;  // every tap stays inside the plane
             if (m.cls[f][l] == SPARE13) continue;
             const int r = q / RS13 - 1, c = q % RS13 - 1;
-            if (r < 0 || r >= SW || c < 0 || c >= SW || m.cls[f][l] != border_cls13(r, c)) return false;
+            if (r < 0 || r >= SW || c < 0 || c >= SW || m.cls[f][l] != border_cls13(r, c) || m.pix[f][l] != r * SW + c)
+                return false;
             ++owned[r * SW + c];
         }
     for (int i = 0; i < SPIX; ++i)
@@ -436,8 +441,9 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
     typedef Num<F16> T;
     typedef typename T::frag frag;
     const int b = blockIdx.x;
-    const int nconv = 2 * p.nblk;
-    const int total = nconv * KSTEPS;
+    const int nconv = 2 * p.nblk;               // the blocks' convs; then p.ntail tail halves (run_tail)
+    const int nconv_all = nconv + p.ntail;
+    const int total = nconv_all * KSTEPS;
     const uint32_t w_bytes = (uint32_t)min((size_t)0x7fffffff, (size_t)total * SLICE_B);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, w_bytes, 0x00020000);
 
@@ -503,9 +509,9 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 
     const size_t img = (size_t)b * SPIX * SC;
     const __amdgpu_buffer_rsrc_t epr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.ep, 0, (uint32_t)((size_t)nconv * TAB_ROWS_B), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.ep, 0, (uint32_t)((size_t)nconv_all * TAB_ROWS_B), 0x00020000);
     const __amdgpu_buffer_rsrc_t slr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv * SC * 4), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv_all * SC * 4), 0x00020000);
     auto issue_tab = [&](int cv, int cv_slope, int slot) {
         char* dst = smem + TAB13 + slot * TS13;
         int ln = fresh_lane();
@@ -526,9 +532,9 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
         const int k = kMap13.cls[f0 + j][ln & 15];
         return (k == SPARE13 ? 4 : k) * TROW13;
     };
-    auto seed_bias = [&]() {
+    auto seed_bias = [&](int slot) {
         int ln = fresh_lane();
-        const char* t = smem + TAB13 + (wn * NPW + 4 * (ln >> 4)) * 4;
+        const char* t = smem + TAB13 + slot * TS13 + (wn * NPW + 4 * (ln >> 4)) * 4;
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
             const int tr = tab_row(j, ln);
@@ -547,14 +553,8 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
 #pragma unroll
     for (int q = 1; q < RING - 1; ++q) wload(wq[q], q);
 
-    auto run_conv = [&](int cv, auto second_tag) {
-        constexpr bool second = decltype(second_tag)::value;
-        if (!second) {
-            seed_bias();
-            if (cv + 1 < nconv) issue_tab(cv + 1, cv, 1);
-        } else if (cv + 1 < nconv) {
-            issue_tab(cv + 1, -1, 0);
-        }
+    // the K loop of conv cv over the patch
+    auto kloop = [&](int cv) {
         pread(pA, 0, 0);
         const int g0 = cv * KSTEPS;
 #pragma unroll 1
@@ -568,6 +568,16 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
                 kstep1(g0 + cgl * 9 + tap, rs, pA, cgn, tapn);
             }
         }
+    };
+    auto run_conv = [&](int cv, auto second_tag) {
+        constexpr bool second = decltype(second_tag)::value;
+        if (!second) {
+            seed_bias(0);
+            if (cv + 1 < nconv_all) issue_tab(cv + 1, cv, 1);
+        } else if (cv + 1 < nconv_all) {
+            issue_tab(cv + 1, -1, 0);
+        }
+        kloop(cv);
         // ---- epilogue (as stage_kernel's): accumulators -> patch; spare-slot lanes write nothing
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         // Fragment-major: the lane's slot for (j, i) is its B-fragment base aoff[j] moved to the output
@@ -629,10 +639,52 @@ __device__ __forceinline__ void stage13_body(const StageArgs& p, char* smem, con
             __builtin_amdgcn_s_waitcnt(0);
         }
     };
+    // Tail (p.ntail = 2): the next conv in the network reads the stage output, which sits in the patch, as a
+    // 3x3/s1 conv 256 -> 512 with a border-class bias and PReLU (IResNet100 layer4.0.conv1): its two 256-channel
+    // halves run as convs nconv and nconv + 1 over the same patch and store to p.y2 ([B][196][512]) directly.
+    // Tables: the last conv2 DMA'd half 0's bias rows into slot 0; half 0 puts half 1's bias rows and its own
+    // slopes into slot 1; half 1 seeds from slot 1 and DMAs its slopes into slot 0.
+    auto run_tail = [&](int cv, int half) {
+        if (half == 0) {
+            seed_bias(0);
+            issue_tab(cv + 1, cv, 1);
+        } else {
+            seed_bias(1);
+            issue_tab(cv, cv, 0);
+        }
+        kloop(cv);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        int ln = fresh_lane();
+        const int cl = ln & 15, g = ln >> 4;
+        const char* tsl = smem + TAB13 + (half == 0 ? TS13 : 0) + TSL13;
+        bf16_t* const yb = p.y2 + (size_t)blockIdx.x * SPIX * (2 * SC) + half * SC;
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            const int P = kMap13.pix[f0 + j][cl];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int n = wn * NPW + 16 * i + 4 * g;
+                const float4 sl = *(const float4*)(tsl + n * 4);
+                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                v[0] = fmaf(sl.x - 1.f, min0_raw(v[0]), v[0]);
+                v[1] = fmaf(sl.y - 1.f, min0_raw(v[1]), v[1]);
+                v[2] = fmaf(sl.z - 1.f, min0_raw(v[2]), v[2]);
+                v[3] = fmaf(sl.w - 1.f, min0_raw(v[3]), v[3]);
+                float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+                const uint4 pk = T::pack8(o8);
+                if (P != SPARE13) *(uint2*)(yb + (size_t)P * (2 * SC) + n) = make_uint2(pk.x, pk.y);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
 #pragma unroll 1
     for (int blk = 0; blk < p.nblk; ++blk) {
         run_conv(2 * blk, std::false_type{});
         run_conv(2 * blk + 1, std::true_type{});
+    }
+    if (p.ntail) {
+        run_tail(nconv, 0);
+        run_tail(nconv + 1, 1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -695,6 +747,7 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t s) {
     // variant 1: the legacy 14-fragment kernel; 2: the one-wave-per-SIMD 13-fragment kernel (both
     // bit-identical; FR_OPT_STAGE_VARIANT)
     const int v = a.variant >= 1 && a.variant <= 3 ? a.variant : 0;
+    if (a.ntail && (a.ntail != 2 || v == 1 || !a.y2)) return hipErrorInvalidValue;  // the legacy kernel has no tail
     auto k = v == 1   ? (a.f16 ? stage_kernel<true> : stage_kernel<false>)
              : v == 2 ? (a.f16 ? stage13w_kernel<true> : stage13w_kernel<false>)
              : v == 3 ? (a.f16 ? stage13c_kernel<true> : stage13c_kernel<false>)

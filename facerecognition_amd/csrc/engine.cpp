@@ -132,6 +132,10 @@ struct StageRec {
     float* tep1 = nullptr;                // [9][64] conv1 bias per border class
     float* tsl1 = nullptr;                // [64] conv1 PReLU slopes
     float* tb2 = nullptr;                 // [64] conv2 + downsample bias
+    // layer3 stage tail (round 5): the conv after the stage (IResNet100 layer4.0.conv1, 3x3/s1 256 -> 512 +
+    // border-class bias + PReLU) runs on the stage's final patch (conv_stage.hip run_tail); its weights and
+    // tables follow the blocks' as two 256-channel halves; tail_op is also the last entry of conv_ops
+    int tail_op = -1;
 };
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -629,13 +633,15 @@ struct Builder {
 // Packs a stage's weights (from the member convs' [Npad][Kpad] device images) and its epilogue table.
 int build_stage(fr_handle* h, StageRec& r) {
     const int nconv = 2 * r.nblk, C = r.C;
-    const size_t wbytes = r.fp8 ? 0 : (r.parts > 1 ? split_stage_weight_bytes(C, nconv) : stage_weight_bytes(nconv));
+    const int ntail = r.tail_op >= 0 ? 2 : 0;  // the tail's two 256-channel halves follow the blocks' convs
+    const int nall = nconv + ntail;
+    const size_t wbytes = r.fp8 ? 0 : (r.parts > 1 ? split_stage_weight_bytes(C, nconv) : stage_weight_bytes(nall));
     std::vector<bf16_t> packed(wbytes / sizeof(bf16_t));
     std::vector<uint8_t> packed8(r.fp8 ? stage8_weight_bytes(nconv) : 0);
     std::vector<float> wsc(r.fp8 ? (size_t)nconv * C : 0);
     std::vector<StageConv> tab(nconv);
-    std::vector<float> ep((size_t)nconv * 9 * C, 0.f), sl((size_t)nconv * C, 0.f);
-    const size_t per = packed.size() / nconv;
+    std::vector<float> ep((size_t)nall * 9 * C, 0.f), sl((size_t)nall * C, 0.f);
+    const size_t per = packed.size() / nall;
     for (int c = 0; c < nconv; ++c) {
         const Op& op = h->ops[r.conv_ops[c]];
         const DevConvW& cw = h->convw[op.wi];
@@ -683,6 +689,28 @@ int build_stage(fr_handle* h, StageRec& r) {
             FR_HIP_CHECK(hipMemcpy(f, cw.slope, C * sizeof(float), hipMemcpyDeviceToHost));
         else
             std::fill(f, f + C, op.act == 1 ? 0.f : 1.f);
+    }
+    if (ntail) {  // rows [256 half, 256 half + 256) of the tail conv (3x3 256 -> 512): bias9 halves, PReLU slopes
+        const Op& op = h->ops[r.tail_op];
+        const DevConvW& cw = h->convw[op.wi];
+        std::vector<bf16_t> rows((size_t)cw.Npad * cw.Kpad);
+        FR_HIP_CHECK(hipMemcpy(rows.data(), cw.w, rows.size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
+        std::vector<float> b9((size_t)9 * cw.Npad, 0.f), slope(cw.Cout);
+        if (cw.bias9) {
+            FR_HIP_CHECK(hipMemcpy(b9.data(), cw.bias9, b9.size() * sizeof(float), hipMemcpyDeviceToHost));
+        } else if (cw.bias) {
+            FR_HIP_CHECK(hipMemcpy(b9.data(), cw.bias, cw.Npad * sizeof(float), hipMemcpyDeviceToHost));
+            for (int k = 1; k < 9; ++k) std::copy(b9.begin(), b9.begin() + cw.Npad, b9.begin() + (size_t)k * cw.Npad);
+        }
+        FR_HIP_CHECK(hipMemcpy(slope.data(), cw.slope, cw.Cout * sizeof(float), hipMemcpyDeviceToHost));
+        for (int hf = 0; hf < 2; ++hf) {
+            const int c = nconv + hf;
+            stage_pack_weights(rows.data() + (size_t)hf * C * cw.Kpad, cw.Kpad, C, packed.data() + c * per);
+            for (int k = 0; k < 9; ++k)
+                std::copy(b9.begin() + (size_t)k * cw.Npad + hf * C, b9.begin() + (size_t)k * cw.Npad + hf * C + C,
+                          ep.begin() + ((size_t)c * 9 + k) * C);
+            std::copy(slope.begin() + hf * C, slope.begin() + hf * C + C, sl.begin() + (size_t)c * C);
+        }
     }
     int rc = r.fp8 ? upload(h, &r.w8, packed8) : upload(h, &r.w, packed);
     if (rc) return rc;
@@ -769,6 +797,9 @@ void build_iresnet100(Builder& b) {
     h->ops[h->ops.size() - 2].fuse_stem = true;  // conv_stem.hip (u8 input)
     const int planes[4] = {64, 128, 256, 512}, nblk[4] = {3, 13, 30, 3};
     int H = 112, C = 64;
+    // the bf16 layer3 stage stays open until layer4.0.conv1 is emitted: that conv becomes its tail
+    StageRec tail_rec;
+    int tail_st_op = -1;
     for (int l = 0; l < 4; ++l) {
         const int P = planes[l], Ho = H / 2;
         // layer3 blocks 1.. (stride 1, 14x14x256) and layer2 / layer1 blocks 1..: also emitted as
@@ -776,8 +807,13 @@ void build_iresnet100(Builder& b) {
         // plan, weights.FP8_PLAN) form an e4m3 stage of their own (14x14x256 only), the rest bf16 stages.
         int st_op = -1;
         StageRec rec;
-        auto close_stage = [&]() {
-            if (st_op >= 0 && !b.rc) {
+        auto close_stage = [&](bool layer_end) {
+            if (st_op >= 0 && !b.rc && layer_end && l == 2 && rec.parts == 1 && !rec.fp8 && rec.C == 256) {  // tail candidate
+                rec.out = x;
+                rec.nblk = (int)rec.t_tensors.size();
+                tail_rec = rec;
+                tail_st_op = st_op;
+            } else if (st_op >= 0 && !b.rc) {
                 rec.out = x;
                 rec.nblk = (int)rec.t_tensors.size();
                 for (int oi : rec.conv_ops) h->ops[oi].stage = h->ops[st_op].stage;
@@ -793,7 +829,7 @@ void build_iresnet100(Builder& b) {
             const bool f8 = b.is_fp8(pre + ".conv1") && b.is_fp8(pre + ".conv2");
             const bool mixed = b.is_fp8(pre + ".conv1") != b.is_fp8(pre + ".conv2");
             const bool can = i >= 1 && P == C && !mixed && (f8 ? s14 : (s14 || parts > 0));
-            if (st_op >= 0 && (!can || f8 != rec.fp8)) close_stage();
+            if (st_op >= 0 && (!can || f8 != rec.fp8)) close_stage(false);
             if (can && st_op < 0) {
                 st_op = (int)h->ops.size();
                 rec = StageRec{};
@@ -822,6 +858,23 @@ void build_iresnet100(Builder& b) {
             }
             const int hmid = b.tensor(Hin, Hin, P, pre + ".prelu");
             b.conv({pre + ".conv1"}, x, 0, C, hmid, 0, 3, 3, 1, 1, 1, 1, 2);
+            if (tail_st_op >= 0 && !b.rc) {  // layer4.0.conv1: the layer3 stage's tail when it fits, then close it
+                const int oi = (int)h->ops.size() - 1;
+                const Op& op = h->ops[oi];
+                const DevConvW& cw = h->convw[op.wi];
+                static const bool no_tail = ab_int("no_stage_tail", 0) != 0;  // FR_AB no_stage_tail: A/B timing
+                if (!no_tail && h->dtype != FR_DTYPE_FP8 && !cw.w8 && op.act == 2 && cw.slope && cw.Cout == 512 && cw.Npad >= 512 &&
+                    cw.Cin == 256 && cw.Kh == 3 && cw.Kw == 3 && op.sh == 1 && op.sw == 1 && op.ph == 1 && op.pw == 1 &&
+                    op.in == tail_rec.out && op.in_off == 0 && op.out_off == 0 && op.res < 0 && op.x2 < 0 && op.out2 < 0 &&
+                    h->tensors[hmid].C == 512 && !h->tensors[hmid].f16)
+                    tail_rec.tail_op = oi;
+                for (int oj : tail_rec.conv_ops) h->ops[oj].stage = h->ops[tail_st_op].stage;
+                if (tail_rec.tail_op >= 0) h->ops[oi].stage = h->ops[tail_st_op].stage;
+                b.rc = build_stage(h, tail_rec);
+                if (tail_rec.tail_op >= 0) tail_rec.conv_ops.push_back(oi);
+                h->stages.push_back(tail_rec);
+                tail_st_op = -1;
+            }
             int res = x;
             if (i == 0 && !fuse) {
                 res = b.tensor(Ho, Ho, P, pre + ".downsample");
@@ -853,7 +906,7 @@ void build_iresnet100(Builder& b) {
             x = y;
             C = P;
         }
-        close_stage();
+        close_stage(true);
         H = Ho;
     }
     b.head(x);
@@ -1666,6 +1719,8 @@ static bool ms_enabled() {
 }
 
 // One LDS-resident stage launch (+ the amax pass an e4m3 reader of its output needs).
+static int run_conv_op(fr_handle* h, const Op& op, int B, int f16, hipStream_t s);
+
 static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vector<char>& stage_run, hipStream_t s) {
     const StageRec& r = h->stages[op.stage];
     if (r.trans) {
@@ -1699,10 +1754,21 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
     a.fail_host = h->fail_dev;
     a.spin_limit = h->spin_limit;
     a.variant = h->stage_variant;
+    // the tail conv runs inside the stage kernel, except under the legacy 14-fragment kernel (variant 1), which
+    // has no tail: there it runs as its own conv after the stage
+    const bool tail_in = r.tail_op >= 0 && a.variant != 1;
+    if (tail_in) {
+        a.ntail = 2;
+        a.y2 = h->tensors[h->ops[r.tail_op].out].dev;
+    }
     {
         ProfScope ps(h, s);
         ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
         ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * (r.fp8 ? 1.0 : 2.0);
+        if (tail_in) {  // + layer4.0.conv1: 3x3 256 -> 512 at 14x14, its 512-channel output and weights
+            ps.flops += 2.0 * B * r.H * r.H * 512.0 * 9.0 * r.C;
+            ps.bytes += 2.0 * B * r.H * r.H * 512.0 + 2.0 * 9.0 * r.C * 512.0;
+        }
         if (r.fp8) {
             a.w = (const bf16_t*)r.w8;
             a.wscale = r.wscale;
@@ -1712,6 +1778,10 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
             ps.start(r.H == 14 ? "stage layer3" : (r.H == 28 ? "stage layer2" : "stage layer1"));
             FR_HIP_CHECK(r.parts > 1 ? launch_split_stage(a, r.H, r.C, s) : launch_stage(a, s));
         }
+    }
+    if (r.tail_op >= 0 && !tail_in) {
+        const int rc = run_conv_op(h, h->ops[r.tail_op], B, f16, s);
+        if (rc) return rc;
     }
     // the stages have no amax epilogue: when a per-conv e4m3 conv reads the stage output (e.g.
     // layer4.0 under FR_FP8_PLAN=all), its activation scale comes from one reduction pass here

@@ -131,6 +131,11 @@ struct StageArgs {
     int* fail_host;            // host-mapped flag: set to 1 (plain vector store) by any part whose wait ran out
     int spin_limit;            // sleeps before a wait counts as run out; < 0: every wait runs out (debug)
     int variant;               // kernel variant (FR_OPT_STAGE_VARIANT): 0 default, 1 the legacy layout
+    // layer3 stage only (conv_stage.hip stage13 kernels): ntail = 2 runs the next conv (3x3/s1 256 -> 512,
+    // border-class bias + PReLU, IResNet100 layer4.0.conv1) on the final patch as two 256-channel halves,
+    // weights / tables appended as convs 2 nblk and 2 nblk + 1; its output y2 [B][14][14][512]
+    int ntail;
+    bf16_t* y2;
     int B, nblk, f16;
     void* ev0;
     void* ev1;

@@ -41,8 +41,9 @@ def test_stage_matches_per_conv_path(gpu, dtype, B):
     m = FRModel.synthetic("iresnet100", dtype=dtype)
     assert m.get_option(N.FR_OPT_STAGE) == 1
     x = torch.from_numpy(synthetic_crops(B, 112, seed=3))
-    names = {"layer3.1.prelu", "layer3.1", "layer3.15", "layer3.29", "layer2.1.prelu", "layer2.1", "layer2.6",
-             "layer2.12", "layer1.1.prelu", "layer1.1", "layer1.2"}
+    # layer4.0.prelu: the layer3 stage's tail (layer4.0.conv1 computed on the stage's final patch)
+    names = {"layer3.1.prelu", "layer3.1", "layer3.15", "layer3.29", "layer4.0.prelu", "layer2.1.prelu", "layer2.1",
+             "layer2.6", "layer2.12", "layer1.1.prelu", "layer1.1", "layer1.2"}
     m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)
     m.set_option(N.FR_OPT_STAGE, 2)  # always (auto would pick the per-conv path at these batch sizes)
     e_stage = m.embed(x).cpu().numpy()
@@ -264,6 +265,12 @@ def test_stage_variants_bit_identical(gpu, dtype, B):
         out[v] = (e, _named(m, B, names))
     m.close()
     for v in (1, 2, 3):
-        assert np.array_equal(out[0][0], out[v][0]), v
+        # (variant 1 has no layer3-stage tail: layer4.0.conv1 then runs per conv, in another f32 order, so only
+        # the layer3 tensors are bit-identical there and the embeddings agree to rounding)
+        if v == 1:
+            cos = np.sum(out[0][0] * out[v][0], axis=1)
+            assert (1 - cos).max() < 1e-4, (v, (1 - cos).max())
+        else:
+            assert np.array_equal(out[0][0], out[v][0]), v
         for n in names:
             assert torch.equal(out[0][1][n], out[v][1][n]), (v, n)
