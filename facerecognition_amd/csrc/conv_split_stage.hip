@@ -69,6 +69,7 @@ struct SplitGeo {
     static constexpr int QPR = PC / 16;              // fragments per stored row
     static constexpr int FM = HR * PC / 16 / MG;     // pixel fragments per wave
     static constexpr int XROW = IW * C;              // exchanged row (elements)
+    static constexpr bool TAIL = IW == 28;           // a tail conv can follow (layer2 -> layer3.0.conv1)
     static_assert(HR * PARTS == IW && PR == 16 && PC >= IW + 2 && PC % 16 == 0 && FM == 7, "geometry");
     static_assert(KSTEPS % 3 == 0 && (C / 32) % 2 == 0 && (SLICE_B == 8192 || SLICE_B == 4096) && LDS <= 163840,
                   "schedule");
@@ -128,8 +129,9 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     const int b = blk / (8 * PARTS) * 8 + (blk & 7), part = (blk >> 3) % PARTS;
     if (b >= p.B) return;  // grid padding (whole images)
     const int r0 = part * HR;
-    const int nconv = 2 * p.nblk;
-    const int total = nconv * KSTEPS;
+    const int nconv = 2 * p.nblk;  // the blocks' convs; then p.ntail tail halves (run_tail)
+    const int nconv_all = nconv + (G::TAIL ? p.ntail : 0);
+    const int total = nconv_all * KSTEPS;
 
     const __amdgpu_buffer_rsrc_t wr =
         __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (uint32_t)min((size_t)0x7fffffff, (size_t)total * SLICE_B), 0x00020000);
@@ -207,9 +209,9 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     // block's) at conv2's start; the K loop's per-step vmcnt waits and barriers complete them.
     const int tbase = part == 0 ? 0 : 1;
     const __amdgpu_buffer_rsrc_t epr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.ep, 0, (uint32_t)((size_t)nconv * 9 * C * 4), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.ep, 0, (uint32_t)((size_t)nconv_all * 9 * C * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t slr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv * C * 4), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.slope, 0, (uint32_t)((size_t)nconv_all * C * 4), 0x00020000);
     auto issue_tab = [&](int cv, int cv_slope, int slot) {
         char* dst = smem + G::TAB + slot * G::TS;
         int lane = opaque_tid() & 63;  // opaque: the DMA offsets are not hoisted out of the block loop
@@ -226,10 +228,10 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         const int cc = (q == 0 && cl == 0) ? 0 : ((q == QPR - 1 && cl == (IW - 1) % 16) ? 2 : 1);
         return ((rc - tbase) * 3 + cc) * C * 4;
     };
-    auto seed_bias = [&]() {
+    auto seed_bias = [&](int slot) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        const char* t = smem + G::TAB;
+        const char* t = smem + G::TAB + slot * G::TS;
         const int nl4 = (64 * wn + 4 * (ln >> 4)) * 4;  // + 64 i: the lane's channel bytes in a table row
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
@@ -310,14 +312,8 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     };
     int pending = -1;  // conv whose boundary rows are still to be imported (-1: none)
 
-    auto run_conv = [&](int cv, auto second_tag) {
-        constexpr bool second = decltype(second_tag)::value;
-        if (!second) {
-            seed_bias();  // conv2's seed (x + its bias) comes from conv1's epilogue
-            if (cv + 1 < nconv) issue_tab(cv + 1, cv, 1);
-        } else if (cv + 1 < nconv) {
-            issue_tab(cv + 1, -1, 0);  // the next block's conv1 biases
-        }
+    // the K loop of conv cv over the patch (with the previous conv's halo import and counter publish)
+    auto kloop = [&](int cv) __attribute__((always_inline)) {
         pread(pA, pos_cg(0), pos_tap(0));
 #pragma unroll
         for (int i = 0; i < FN; ++i) wread(i, 0);  // step 0 of every conv sits in slot 0 (KSTEPS % 3 == 0)
@@ -346,6 +342,16 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
             }
             halo = 0;
         }
+    };
+    auto run_conv = [&](int cv, auto second_tag) {
+        constexpr bool second = decltype(second_tag)::value;
+        if (!second) {
+            seed_bias(0);  // conv2's seed (x + its bias) comes from conv1's epilogue
+            if (cv + 1 < nconv_all) issue_tab(cv + 1, cv, 1);
+        } else if (cv + 1 < nconv_all) {
+            issue_tab(cv + 1, -1, 0);  // the next block's conv1 biases (or the tail's first half)
+        }
+        kloop(cv);
         // ---- epilogue (every wave is past its last patch read): accumulators -> patch only; the global
         // copies (boundary rows, stage output, intermediates) are read back from the patch afterwards
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         }
         // the conv's output is in the patch for every wave (the next conv's reads, the copies below)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        const bool exch = cv < nconv - 1;
+        const bool exch = cv < nconv_all - 1;  // (with a tail, the last block's rows are its halo)
         if (exch) {
             // boundary rows for the neighbours, plane-major [NPL][IW][8] per row (16-B chunks, positions
             // fastest: conflict-free LDS reads, contiguous stores), sc1 stores (the hand-off rule, header)
@@ -442,10 +448,54 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
             pending = cv;
         }
     };
+    // Tail (p.ntail = 2, layer2 -> IResNet100 layer3.0.conv1: 3x3/s1 C -> 2C, border-class bias + PReLU): the
+    // conv after the stage reads the stage output, which sits in the patch with its halo rows imported at the
+    // first half's K-step 2 (the last block published them); two C-channel halves run as convs nconv and
+    // nconv + 1 and store the part's rows to p.y2 ([B][IW][IW][2C]).  Tables as in conv_stage.hip's tail.
+    auto run_tail = [&](int cv, int half) __attribute__((always_inline)) {
+        if (half == 0) {
+            seed_bias(0);
+            issue_tab(cv + 1, cv, 1);
+        } else {
+            seed_bias(1);
+            issue_tab(cv, cv, 0);
+        }
+        kloop(cv);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int cl = ln & 15;
+        const char* tsl = smem + G::TAB + (half == 0 ? G::TS : 0) + G::TAB_ROWS_B;
+        const uint32_t nan_or = *(const volatile int*)(smem + G::FAILED) ? 0x7FC07FC0u : 0u;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+            const int n = 64 * wn + 16 * i + 4 * (ln >> 4);
+            const float4 sl = *(const float4*)(tsl + n * 4);
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                const int f = FM * wm + j, row = f / QPR, col = 16 * (f % QPR) + cl;
+                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                v[0] = fmaf(sl.x - 1.f, min0_raw(v[0]), v[0]);
+                v[1] = fmaf(sl.y - 1.f, min0_raw(v[1]), v[1]);
+                v[2] = fmaf(sl.z - 1.f, min0_raw(v[2]), v[2]);
+                v[3] = fmaf(sl.w - 1.f, min0_raw(v[3]), v[3]);
+                float o8[8] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+                const uint4 pk = T::pack8(o8);
+                if (col < IW)
+                    *(uint2*)(p.y2 + ((size_t)(b * IW + r0 + row) * IW + col) * (2 * C) + half * C + n) =
+                        make_uint2(pk.x | nan_or, pk.y | nan_or);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
 #pragma unroll 1
     for (int blkc = 0; blkc < p.nblk; ++blkc) {
         run_conv(2 * blkc, std::false_type{});
         run_conv(2 * blkc + 1, std::true_type{});
+    }
+    if (G::TAIL && p.ntail) {
+        run_tail(nconv, 0);
+        run_tail(nconv + 1, 1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs land before the LDS is released
 }

@@ -635,7 +635,7 @@ int build_stage(fr_handle* h, StageRec& r) {
     const int nconv = 2 * r.nblk, C = r.C;
     const int ntail = r.tail_op >= 0 ? 2 : 0;  // the tail's two 256-channel halves follow the blocks' convs
     const int nall = nconv + ntail;
-    const size_t wbytes = r.fp8 ? 0 : (r.parts > 1 ? split_stage_weight_bytes(C, nconv) : stage_weight_bytes(nall));
+    const size_t wbytes = r.fp8 ? 0 : (r.parts > 1 ? split_stage_weight_bytes(C, nall) : stage_weight_bytes(nall));
     std::vector<bf16_t> packed(wbytes / sizeof(bf16_t));
     std::vector<uint8_t> packed8(r.fp8 ? stage8_weight_bytes(nconv) : 0);
     std::vector<float> wsc(r.fp8 ? (size_t)nconv * C : 0);
@@ -690,7 +690,7 @@ int build_stage(fr_handle* h, StageRec& r) {
         else
             std::fill(f, f + C, op.act == 1 ? 0.f : 1.f);
     }
-    if (ntail) {  // rows [256 half, 256 half + 256) of the tail conv (3x3 256 -> 512): bias9 halves, PReLU slopes
+    if (ntail) {  // rows [C half, C half + C) of the tail conv (3x3 C -> 2C): bias9 halves, PReLU slopes
         const Op& op = h->ops[r.tail_op];
         const DevConvW& cw = h->convw[op.wi];
         std::vector<bf16_t> rows((size_t)cw.Npad * cw.Kpad);
@@ -705,7 +705,8 @@ int build_stage(fr_handle* h, StageRec& r) {
         FR_HIP_CHECK(hipMemcpy(slope.data(), cw.slope, cw.Cout * sizeof(float), hipMemcpyDeviceToHost));
         for (int hf = 0; hf < 2; ++hf) {
             const int c = nconv + hf;
-            stage_pack_weights(rows.data() + (size_t)hf * C * cw.Kpad, cw.Kpad, C, packed.data() + c * per);
+            if (r.parts > 1) split_stage_pack_weights(rows.data() + (size_t)hf * C * cw.Kpad, cw.Kpad, C, packed.data() + c * per);
+            else stage_pack_weights(rows.data() + (size_t)hf * C * cw.Kpad, cw.Kpad, C, packed.data() + c * per);
             for (int k = 0; k < 9; ++k)
                 std::copy(b9.begin() + (size_t)k * cw.Npad + hf * C, b9.begin() + (size_t)k * cw.Npad + hf * C + C,
                           ep.begin() + ((size_t)c * 9 + k) * C);
@@ -808,7 +809,9 @@ void build_iresnet100(Builder& b) {
         int st_op = -1;
         StageRec rec;
         auto close_stage = [&](bool layer_end) {
-            if (st_op >= 0 && !b.rc && layer_end && l == 2 && rec.parts == 1 && !rec.fp8 && rec.C == 256) {  // tail candidate
+            // tail candidates: the bf16 layer3 stage (-> layer4.0.conv1) and the layer2 split stage (-> layer3.0.conv1)
+            if (st_op >= 0 && !b.rc && layer_end && !rec.fp8 &&
+                ((l == 2 && rec.parts == 1 && rec.C == 256) || (l == 1 && rec.parts == 2 && rec.C == 128 && rec.H == 28))) {
                 rec.out = x;
                 rec.nblk = (int)rec.t_tensors.size();
                 tail_rec = rec;
@@ -863,10 +866,11 @@ void build_iresnet100(Builder& b) {
                 const Op& op = h->ops[oi];
                 const DevConvW& cw = h->convw[op.wi];
                 static const bool no_tail = ab_int("no_stage_tail", 0) != 0;  // FR_AB no_stage_tail: A/B timing
-                if (!no_tail && h->dtype != FR_DTYPE_FP8 && !cw.w8 && op.act == 2 && cw.slope && cw.Cout == 512 && cw.Npad >= 512 &&
-                    cw.Cin == 256 && cw.Kh == 3 && cw.Kw == 3 && op.sh == 1 && op.sw == 1 && op.ph == 1 && op.pw == 1 &&
-                    op.in == tail_rec.out && op.in_off == 0 && op.out_off == 0 && op.res < 0 && op.x2 < 0 && op.out2 < 0 &&
-                    h->tensors[hmid].C == 512 && !h->tensors[hmid].f16)
+                const int TC = tail_rec.C;
+                if (!no_tail && h->dtype != FR_DTYPE_FP8 && !cw.w8 && op.act == 2 && cw.slope && cw.Cout == 2 * TC &&
+                    cw.Npad >= 2 * TC && cw.Cin == TC && cw.Kh == 3 && cw.Kw == 3 && op.sh == 1 && op.sw == 1 && op.ph == 1 &&
+                    op.pw == 1 && op.in == tail_rec.out && op.in_off == 0 && op.out_off == 0 && op.res < 0 && op.x2 < 0 &&
+                    op.out2 < 0 && h->tensors[hmid].C == 2 * TC && !h->tensors[hmid].f16)
                     tail_rec.tail_op = oi;
                 for (int oj : tail_rec.conv_ops) h->ops[oj].stage = h->ops[tail_st_op].stage;
                 if (tail_rec.tail_op >= 0) h->ops[oi].stage = h->ops[tail_st_op].stage;
@@ -1756,7 +1760,7 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
     a.variant = h->stage_variant;
     // the tail conv runs inside the stage kernel, except under the legacy 14-fragment kernel (variant 1), which
     // has no tail: there it runs as its own conv after the stage
-    const bool tail_in = r.tail_op >= 0 && a.variant != 1;
+    const bool tail_in = r.tail_op >= 0 && (r.parts > 1 || a.variant != 1);
     if (tail_in) {
         a.ntail = 2;
         a.y2 = h->tensors[h->ops[r.tail_op].out].dev;
@@ -1765,9 +1769,9 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
         ProfScope ps(h, s);
         ps.flops = 2.0 * r.nblk * 2.0 * B * r.H * r.H * (double)r.C * 9.0 * r.C;
         ps.bytes = 2.0 * B * r.H * r.H * (double)r.C * 2.0 + 2.0 * r.nblk * 9.0 * r.C * r.C * (r.fp8 ? 1.0 : 2.0);
-        if (tail_in) {  // + layer4.0.conv1: 3x3 256 -> 512 at 14x14, its 512-channel output and weights
-            ps.flops += 2.0 * B * r.H * r.H * 512.0 * 9.0 * r.C;
-            ps.bytes += 2.0 * B * r.H * r.H * 512.0 + 2.0 * 9.0 * r.C * 512.0;
+        if (tail_in) {  // + the tail conv: 3x3 C -> 2C at H x H, its 2C-channel output and weights
+            ps.flops += 2.0 * B * r.H * r.H * 2.0 * r.C * 9.0 * r.C;
+            ps.bytes += 2.0 * B * r.H * r.H * 2.0 * r.C + 2.0 * 9.0 * r.C * 2.0 * r.C;
         }
         if (r.fp8) {
             a.w = (const bf16_t*)r.w8;

@@ -41,9 +41,10 @@ def test_stage_matches_per_conv_path(gpu, dtype, B):
     m = FRModel.synthetic("iresnet100", dtype=dtype)
     assert m.get_option(N.FR_OPT_STAGE) == 1
     x = torch.from_numpy(synthetic_crops(B, 112, seed=3))
-    # layer4.0.prelu: the layer3 stage's tail (layer4.0.conv1 computed on the stage's final patch)
+    # layer4.0.prelu / layer3.0.prelu: the layer3 / layer2 stages' tails (the next conv computed on the stage's
+    # final patch)
     names = {"layer3.1.prelu", "layer3.1", "layer3.15", "layer3.29", "layer4.0.prelu", "layer2.1.prelu", "layer2.1",
-             "layer2.6", "layer2.12", "layer1.1.prelu", "layer1.1", "layer1.2"}
+             "layer2.6", "layer2.12", "layer3.0.prelu", "layer1.1.prelu", "layer1.1", "layer1.2"}
     m.set_option(N.FR_OPT_KEEP_INTERMEDIATES, 1)
     m.set_option(N.FR_OPT_STAGE, 2)  # always (auto would pick the per-conv path at these batch sizes)
     e_stage = m.embed(x).cpu().numpy()
