@@ -1500,10 +1500,24 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
             cand_ms[c] = std::min(cand_ms[c], ms);
         }
     }
+    // the 3-stage implicit-GEMM tiles are credited FR_AB tune_s3_bias percent (default 5): the tuner's
+    // back-to-back launches run warm, where the deeper ring's latency hiding does not show, and in the
+    // forward they win (IRV1 Block17 1x7: 12.0 vs 17.4 us per launch for 11.5 vs 11.5 us tuned)
+    static const float s3_credit = 1.f - 0.01f * (float)ab_int("tune_s3_bias", 5);
+    for (size_t c = 0; c < cand.size(); ++c)
+        if (cand_ms[c] >= 0.f && (cand[c].tile == TILE_128x64_S3 || cand[c].tile == TILE_64x128_S3) && cand[c].split == 1)
+            cand_ms[c] *= s3_credit;
     size_t best = 0;
     while (best + 1 < cand.size() && cand_ms[best] < 0.f) ++best;
     for (size_t c = best + 1; c < cand.size(); ++c)
         if (cand_ms[c] >= 0.f && cand_ms[c] < cand_ms[best] * 0.99f) best = c;
+    static const bool tune_log = ab_int("tune_log", 0) != 0;  // FR_AB tune_log=1: candidate times to stderr
+    if (tune_log) {
+        fprintf(stderr, "tune M=%d N=%d K=%d %dx%d:", a.M, a.Cout, a.Kpad, a.Kh, a.Kw);
+        for (size_t c = 0; c < cand.size(); ++c)
+            fprintf(stderr, " %d/%d=%.1f%s", cand[c].tile, cand[c].split, cand_ms[c] * 1000.f / 3.f, c == best ? "*" : "");
+        fprintf(stderr, "\n");
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     fr_handle::Tuned t;
