@@ -1,10 +1,13 @@
 // Fast exact gallery match for large galleries (BASELINE config 4: 2048 probes x a 125k-row shard of a
 // 1M x 512 gallery per rank).  The exact f32 path (match.hip, v_mfma_f32_16x16x4_f32) runs at the f32
 // MFMA rate, 1/16 of bf16.  Here:
-//   1. candidates: s~ = Ph.Gh + Pl.Gh on v_mfma_f32_16x16x32_bf16 (p = ph + pl split in two bf16, the gallery
-//      row rounded to ONE bf16 gh: half the gallery bytes of a hi/lo split and 2 MFMAs per product instead of
-//      3), |s~ - s| <= eps = 4.0e-3 ||p|| ||g|| (|g - gh| <= 2^-8 |g| per element, p's split residual 2^-16,
-//      two f32 accumulations of 512 terms: 2^-8 + 2^-16 + 1024 2^-24 = 3.98e-3, worst case); per (probe, split)
+//   1. candidates: s~ = ph.gh, ONE v_mfma_f32_16x16x32_bf16 per 32 dims (probe and gallery row each rounded to
+//      bf16).  The bound is measured, not worst-case: s - ph.gh = p.(g - gh) + (p - ph).gh, so
+//      |s~ - s| <= eps(p) = ||p|| EG + ||p - ph|| GN + c (||p|| + ||p - ph||) GN, with EG = max over rows of
+//      ||g - gh|| and GN = max ||gh|| (split_x3_kernel keeps both in the buffer's header) and c = 2048 2^-24
+//      for the f32 accumulation of 512 exact products (twice the gamma_512 bound).  For unit rows this is
+//      ~3.9e-3 ||p|| -- the band of the former 2-product pass (ph.gh + pl.gh, eps 4.0e-3 worst case) at half
+//      its MFMAs and probe registers; per (probe, split)
 //      the top-KO by s~ of four sub-lists
 //      of KP (rows 16j + 4 sub + r of each tile, kept by the lane whose accumulators hold them) and a floor: every row dropped from a sub-list, or by the
 //      filter, has s~ <= floor = the best last entry of the full sub-lists;
@@ -16,7 +19,7 @@
 //      score is <= T + eps.  Unless the k-th exact score exceeds T + 2 eps (i.e. more than KC - k rows tie
 //      with it within 2 eps), the wave rescans the whole gallery exactly for that probe (counted).  The
 //      result is therefore always the exact top-k of the f32 scores.
-// Block = 8 waves, 128 probes; each wave keeps its 16 probes' bf16 hi/lo fragments in registers for the
+// Block = 8 waves, 128 probes; each wave keeps its 16 probes' bf16 fragments in registers for the
 // whole kernel; gallery chunks (64 rows x 64 dims of gh, 8 KiB) stream through a 13-slot LDS-DMA ring
 // twelve chunks ahead (counted vmcnt, raw barriers; XOR-swizzled 16-B chunks): the ring depth, not HBM,
 // sets the stream rate (in flight / L2 latency).  Blocks of one gallery split share an XCD (xcd_remap), so each XCD streams its
@@ -40,10 +43,13 @@ constexpr int XD = 512;       // embedding dim (the kernel is specialised)
 constexpr int KP = 8;         // candidates per (probe, split, sub-lane): 4 sub-lanes per probe
 constexpr int KO = 16;        // candidates written per (probe, split) ...
 constexpr int KS = KO + 1;    // ... plus one floor entry (index -2)
-constexpr int KC = 32;        // candidates rescored per probe (the 2 eps band of the 2-product pass needs more
-                              // than the 3-product one's 16: with 16, random 1M-row galleries put the 5th
-                              // score within 2 eps of the 16th often enough to trigger rescans)
-constexpr float X2_EPS = 4.0e-3f;  // |s~ - s| / (||p|| ||g||), header
+constexpr int KC = 32;        // candidates rescored per probe (a 2 eps band of ~8e-3 needs more than 16: with
+                              // 16, random 1M-row galleries put the 5th score within 2 eps of the 16th often
+                              // enough to trigger rescans)
+constexpr float X_ACC = 2048.f / 16777216.f;  // c of the header: f32 accumulation of 512 exact products
+// header of the chunk buffer (elements; 8 KiB keeps the chunks 8-KiB aligned): uint32 [0] = EG, [1] = GN as
+// f32 bits (non-negative: integer max == float max), raised by every split_x3_kernel launch
+constexpr int X3_HEAD = 4096;
 
 __device__ __forceinline__ bool better(float s1, int i1, float s2, int i2) {
     return s1 > s2 || (s1 == s2 && i1 < i2);
@@ -100,8 +106,9 @@ constexpr int XCHUNK_E = 64 * 64;  // bf16 elements per chunk (8 KiB)
 __device__ __forceinline__ int xswz_row(int row) { return (row >> 1) & 7; }
 
 __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ G, int64_t row0, int64_t n,
-                                                       bf16_t* __restrict__ T) {
-    // one thread per 8 dims of one row
+                                                       bf16_t* __restrict__ T, uint32_t* __restrict__ stats) {
+    // one thread per 8 dims of one row (a wave = one row: the grid stride is a multiple of 64)
+    float eg = 0.f, gn = 0.f;  // this lane's running max of ||g - gh|| and ||gh|| over its rows
     for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n * 64; i += (int64_t)gridDim.x * 256) {
         const int64_t r = row0 + i / 64;
         const int grp = (int)(i % 64), c = grp >> 3, g = grp & 7, rr = (int)(r & 63);
@@ -109,17 +116,36 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
         const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
         const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         uint16_t hb[8];
+        float e2 = 0.f, h2 = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) hb[e] = bf16_bits(v[e]);
+        for (int e = 0; e < 8; ++e) {
+            const __bf16 h = (__bf16)v[e];
+            hb[e] = __builtin_bit_cast(uint16_t, h);
+            const float hf = (float)h, d = v[e] - hf;
+            e2 = fmaf(d, d, e2);
+            h2 = fmaf(hf, hf, h2);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            e2 += __shfl_xor(e2, o);
+            h2 += __shfl_xor(h2, o);
+        }
+        eg = fmaxf(eg, sqrtf(e2));
+        gn = fmaxf(gn, sqrtf(h2));
         bf16_t* dst = T + ((r >> 6) * 8 + c) * XCHUNK_E + rr * 64 + (g ^ xswz_row(rr)) * 8;
         uint4 hv;
         hv.x = hb[0] | (uint32_t)hb[1] << 16; hv.y = hb[2] | (uint32_t)hb[3] << 16;
         hv.z = hb[4] | (uint32_t)hb[5] << 16; hv.w = hb[6] | (uint32_t)hb[7] << 16;
         *(uint4*)dst = hv;
     }
+    // (the norms' own f32 rounding: 1e-4 relative margin)
+    if ((threadIdx.x & 63) == 0 && gn > 0.f) {
+        atomicMax((int*)stats, __float_as_int(eg * 1.0001f));
+        atomicMax((int*)stats + 1, __float_as_int(gn * 1.0001f));
+    }
 }
 
-constexpr int XSLOT = 13;  // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB, as 6 of the 16-KiB hi/lo chunks)
+constexpr int XSLOT = 13;  // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB)
 constexpr int XCHUNK_B = XG * XC * 2;          // 8 KiB: [64 rows x 128 B]
 static_assert(XCHUNK_B == XCHUNK_E * 2, "chunk layout");
 constexpr int XRB = XC * 2;                    // LDS row bytes
@@ -145,7 +171,7 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
     // probe fragments (the MFMA's B operand): k-step t (32 dims) of probe p0 + 16*wave + (lane&15),
     // dims 32t + 8(lane>>4) .. +8
     constexpr int KT = XD / 32;
-    bf8v ph[KT], pl[KT];
+    bf8v ph[KT];
     const int my_q = 16 * wave + (lane & 15);  // this lane's probe (block-local) ...
     const int my_sub = lane >> 4;              // ... and sub-list: rows 16j + 4*my_sub + r of every tile
     {
@@ -159,11 +185,7 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
                 v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
             }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const __bf16 h = (__bf16)v[e];
-                ph[t][e] = h;
-                pl[t][e] = (__bf16)(v[e] - (float)h);
-            }
+            for (int e = 0; e < 8; ++e) ph[t][e] = (__bf16)v[e];
         }
     }
 
@@ -272,7 +294,6 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
                     // gallery rows as the A operand: D[row][probe], so each lane's accumulators belong to
                     // ONE probe (its own candidate sub-list) and the filter never leaves the registers
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, ph[t], acc[j], 0, 0, 0);
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, pl[t], acc[j], 0, 0, 0);
                 }
             }
         }
@@ -373,7 +394,7 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
                                                       int64_t N, int64_t index_base, const float* __restrict__ cs,
                                                       const int32_t* __restrict__ ci, int n_lists, int k,
                                                       float* __restrict__ out_s, int32_t* __restrict__ out_i,
-                                                      int* __restrict__ n_fallback) {
+                                                      int* __restrict__ n_fallback, const uint32_t* __restrict__ stats) {
     __shared__ __attribute__((aligned(16))) float prow_s[4][XD];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int p = blockIdx.x * 4 + wave;
@@ -435,11 +456,20 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
         rs[0] = exact_dot_lds(pl, G + (size_t)(my_idx - index_base) * XD);
         ri[0] = my_idx;
     }
-    float pp = 0.f;
-    for (int d = lane; d < XD; d += 64) pp = fmaf(prow[d], prow[d], pp);
+    float pp = 0.f, ll = 0.f;  // ||p||^2, ||p - ph||^2 (ph as the candidate pass rounds it)
+    for (int d = lane; d < XD; d += 64) {
+        const float v = prow[d], r = v - (float)(__bf16)v;
+        pp = fmaf(v, v, pp);
+        ll = fmaf(r, r, ll);
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) pp += __shfl_xor(pp, o);
-    const float eps = X2_EPS * sqrtf(pp) * 1.001f;  // rows are unit norm within 1e-3 (or zero)
+    for (int o = 32; o > 0; o >>= 1) {
+        pp += __shfl_xor(pp, o);
+        ll += __shfl_xor(ll, o);
+    }
+    const float EG = __uint_as_float(stats[0]), GN = __uint_as_float(stats[1]);
+    const float np = sqrtf(pp), nl = sqrtf(ll);
+    const float eps = (np * EG + nl * GN + X_ACC * (np + nl) * GN) * 1.001f;  // header
     // (c) exact top-k among the candidates
     int h1 = 0;
     float kth = INFINITY, outs = -INFINITY;
@@ -580,13 +610,13 @@ __global__ __launch_bounds__(64 * WPB) void match_rows_kernel(const float* __res
 
 }  // namespace
 
-size_t x3_gallery_elems(int64_t rows) { return (size_t)((rows + XG - 1) / XG) * 8 * XCHUNK_E; }
+size_t x3_gallery_elems(int64_t rows) { return X3_HEAD + (size_t)((rows + XG - 1) / XG) * 8 * XCHUNK_E; }
 
 hipError_t launch_split_x3(const float* G, int64_t row0, int64_t n, bf16_t* T, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     int64_t blocks = (n * 64 + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(split_x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, G, row0, n, T);
+    hipLaunchKernelGGL(split_x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, G, row0, n, T + X3_HEAD, (uint32_t*)T);
     return hipGetLastError();
 }
 
@@ -636,10 +666,10 @@ hipError_t launch_match_x3(const float* P, int B, const float* G, const bf16_t* 
                            int64_t rows_per_split, float* out_s, int32_t* out_i, int* n_fallback, hipStream_t s) {
     if (D != XD || k > KC || k < 1) return hipErrorInvalidValue;
     const int npb = (B + XP - 1) / XP;
-    hipLaunchKernelGGL(match_x3_kernel, dim3(npb * n_split), dim3(512), 0, s, P, B, GT, N, index_base,
+    hipLaunchKernelGGL(match_x3_kernel, dim3(npb * n_split), dim3(512), 0, s, P, B, GT + X3_HEAD, N, index_base,
                        rows_per_split, n_split, npb, cand_s, cand_i);
     hipLaunchKernelGGL(rescore_kernel, dim3((B + 3) / 4), dim3(256), 0, s, P, B, G, N, index_base, cand_s, cand_i,
-                       n_split, k, out_s, out_i, n_fallback);
+                       n_split, k, out_s, out_i, n_fallback, (const uint32_t*)GT);
     return hipGetLastError();
 }
 
