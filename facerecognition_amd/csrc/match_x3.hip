@@ -19,7 +19,7 @@
 //      score is <= T + eps.  Unless the k-th exact score exceeds T + 2 eps (i.e. more than KC - k rows tie
 //      with it within 2 eps), the wave rescans the whole gallery exactly for that probe (counted).  The
 //      result is therefore always the exact top-k of the f32 scores.
-// Block = 8 waves, 128 probes; each wave keeps its 16 probes' bf16 fragments in registers for the
+// Block = 8 waves, 16 PF probes per wave (PF = 1: 128 per block) as bf16 fragments in registers for the
 // whole kernel; gallery chunks (64 rows x 64 dims of gh, 8 KiB) stream through a 13-slot LDS-DMA ring
 // twelve chunks ahead (counted vmcnt, raw barriers; XOR-swizzled 16-B chunks): the ring depth, not HBM,
 // sets the stream rate (in flight / L2 latency).  Blocks of one gallery split share an XCD (xcd_remap), so each XCD streams its
@@ -36,7 +36,12 @@ namespace {
 
 
 constexpr int XW = 8;         // waves per block
-constexpr int XP = 16 * XW;   // probes per block
+// probe fragments (16 probes each) per wave: every gallery fragment read feeds PF MFMAs.  PF = 2 (256 probes per
+// block, 32-entry lists per lane) measured the same (2048 x 125k 0.44 vs 0.45 ms, 256 x 1M 0.48 vs 0.47): the kernel
+// is bound by the filter's VALU work (7 VALU per MFMA), not the LDS reads, and halving the probe blocks doubles
+// the splits and so the list fills
+constexpr int PF = 1;
+constexpr int XP = 16 * PF * XW;  // probes per block
 constexpr int XG = 64;        // gallery rows per tile
 constexpr int XC = 64;        // dims per LDS chunk
 constexpr int XD = 512;       // embedding dim (the kernel is specialised)
@@ -92,7 +97,6 @@ __device__ __forceinline__ void insert_s(float (&ls)[KMAX], int (&li)[KMAX], flo
     }
 }
 
-__device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
 
@@ -168,14 +172,15 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
     const int64_t g_begin = (int64_t)split * rows_per_split;
     const int64_t g_end = g_begin + rows_per_split < N ? g_begin + rows_per_split : N;
 
-    // probe fragments (the MFMA's B operand): k-step t (32 dims) of probe p0 + 16*wave + (lane&15),
-    // dims 32t + 8(lane>>4) .. +8
+    // probe fragments (the MFMA's B operand): fragment f, k-step t (32 dims) of probe
+    // p0 + 16 (PF wave + f) + (lane & 15), dims 32t + 8(lane>>4) .. +8
     constexpr int KT = XD / 32;
-    bf8v ph[KT];
-    const int my_q = 16 * wave + (lane & 15);  // this lane's probe (block-local) ...
-    const int my_sub = lane >> 4;              // ... and sub-list: rows 16j + 4*my_sub + r of every tile
-    {
-        const int p = p0 + my_q;
+    bf8v ph[PF][KT];
+    const int my_sub = lane >> 4;  // the lane's sub-list: rows 16j + 4*my_sub + r of every tile
+    auto my_q = [&](int f) { return 16 * (PF * wave + f) + (lane & 15); };  // its probe of fragment f (block-local)
+#pragma unroll
+    for (int f = 0; f < PF; ++f) {
+        const int p = p0 + my_q(f);
 #pragma unroll
         for (int t = 0; t < KT; ++t) {
             float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -185,14 +190,16 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
                 v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
             }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) ph[t][e] = (__bf16)v[e];
+            for (int e = 0; e < 8; ++e) ph[f][t][e] = (__bf16)v[e];
         }
     }
 
-    float ls[KP];
-    int li[KP];
+    float ls[PF][KP];
+    int li[PF][KP];
 #pragma unroll
-    for (int q = 0; q < KP; ++q) { ls[q] = -INFINITY; li[q] = INT_MAX; }
+    for (int f = 0; f < PF; ++f)
+#pragma unroll
+        for (int q = 0; q < KP; ++q) { ls[f][q] = -INFINITY; li[f][q] = INT_MAX; }
 
     // LDS-DMA of chunk (tile t0, dims 64c..): a linear copy of its 16 KiB (split_x3_kernel's layout), 16
     // pieces of 1 KiB, wave w issues pieces 2w, 2w+1.  The resource starts at the split's first chunk
@@ -222,8 +229,8 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
     for (int i = 0; i < XSLOT - 1; ++i) issue_next();
 
     // the tile's candidate filter and sorted inserts (a = its accumulators, tb = its first row)
-    auto filter_tile = [&](f32x4_t (&a)[4], int64_t tb) {
-        // a[j][r] = s~(probe my_q, row tb + 16*j + 4*my_sub + r).  A row not above the best KP-th score
+    auto filter_tile = [&](f32x4_t (&a)[4], float (&ls)[KP], int (&li)[KP], int64_t tb) {
+        // a[j][r] = s~(the lane's probe, row tb + 16*j + 4*my_sub + r).  A row not above the best KP-th score
         // of the probe's 4 sub-lists (lanes lane ^ 16, ^ 32) is never needed: the floor (>= that score)
         // covers it in the proof -- ties included, so the scan compares scores only.  The sorted insert
         // runs once per hit of the wave's busiest lane.
@@ -269,9 +276,11 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
         }
     };
     for (int64_t t0 = g_begin; t0 < g_end; t0 += XG) {
-        f32x4_t acc[4];
+        f32x4_t acc[PF][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        for (int f = 0; f < PF; ++f)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[f][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < XD / XC; ++c) {
             // chunk c landed (the XSLOT - 2 younger chunks' pieces may stay in flight); every wave is
@@ -293,28 +302,34 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
                     const bf8v gh = *(const bf8v*)(ch + o);
                     // gallery rows as the A operand: D[row][probe], so each lane's accumulators belong to
                     // ONE probe (its own candidate sub-list) and the filter never leaves the registers
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, ph[t], acc[j], 0, 0, 0);
+#pragma unroll
+                    for (int f = 0; f < PF; ++f)
+                        acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, ph[f][t], acc[f][j], 0, 0, 0);
                 }
             }
         }
-        filter_tile(acc, t0);
+#pragma unroll
+        for (int f = 0; f < PF; ++f) filter_tile(acc[f], ls[f], li[f], t0);
     }
     // the look-ahead DMAs (zeros past the split) land everywhere before the ring is reused as scratch
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    // merge the 4 sub-lists of each probe into its top KO: park them in the (drained) ring and let
-    // lane my_sub == 0 insert all four (a rolled loop: one inlined insert)
+    // merge the 4 sub-lists of each probe into its top KO: park them in the (drained) ring and let one
+    // lane per probe insert all four (a rolled loop: one inlined insert)
     float* ms = (float*)smem;                    // [XP][4][KP] scores (the drained DMA ring)
     int* mi = (int*)(smem + XP * 4 * KP * 4);    // [XP][4][KP] indices
     static_assert(2 * XP * 4 * KP * 4 <= XSLOT * XCHUNK_B, "merge scratch fits the ring");
     static_assert(KO == 2 * KP, "the scan's second bar assumes 4 sub-lists x KP/2 = KO");
 #pragma unroll
-    for (int q = 0; q < KP; ++q) {
-        ms[(my_q * 4 + my_sub) * KP + q] = ls[q];
-        mi[(my_q * 4 + my_sub) * KP + q] = li[q];
-    }
+    for (int f = 0; f < PF; ++f)
+#pragma unroll
+        for (int q = 0; q < KP; ++q) {
+            ms[(my_q(f) * 4 + my_sub) * KP + q] = ls[f][q];
+            mi[(my_q(f) * 4 + my_sub) * KP + q] = li[f][q];
+        }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int p = p0 + my_q;
-    if (my_sub == 0 && p < B) {
+    // lanes of sub-list 0 merge the probe of fragment 0, sub-list 1 that of fragment 1, ...
+    const int mf = my_sub % PF, mq = my_q(mf), p = p0 + mq;
+    if (my_sub < PF && p < B) {
         float os[KO];
         int oi[KO];
 #pragma unroll
@@ -322,8 +337,8 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
         float floor_s = -INFINITY;
 #pragma unroll 1
         for (int e = 0; e < 4 * KP; ++e) {
-            const float sc = ms[my_q * 4 * KP + e];
-            const int ix = mi[my_q * 4 * KP + e];
+            const float sc = ms[mq * 4 * KP + e];
+            const int ix = mi[mq * 4 * KP + e];
             if (ix == INT_MAX) continue;
             insert<KO>(os, oi, sc, ix);
             // a full sub-list may have dropped rows scoring up to its last entry
