@@ -20,8 +20,8 @@
 //      with it within 2 eps), the wave rescans the whole gallery exactly for that probe (counted).  The
 //      result is therefore always the exact top-k of the f32 scores.
 // Block = 8 waves, 16 PF probes per wave (PF = 1: 128 per block) as bf16 fragments in registers for the
-// whole kernel; gallery chunks (64 rows x 64 dims of gh, 8 KiB) stream through a 13-slot LDS-DMA ring
-// twelve chunks ahead (counted vmcnt, raw barriers; XOR-swizzled 16-B chunks): the ring depth, not HBM,
+// whole kernel; gallery chunks (64 rows x 128 dims of gh, 16 KiB) stream through a 7-slot LDS-DMA ring
+// six chunks ahead (counted vmcnt, raw barriers; XOR-swizzled 16-B chunks): the ring depth, not HBM,
 // sets the stream rate (in flight / L2 latency).  Blocks of one gallery split share an XCD (xcd_remap), so each XCD streams its
 // splits from HBM once and the other probe blocks hit its L2.
 #include "kernels.h"
@@ -43,7 +43,11 @@ constexpr int XW = 8;         // waves per block
 constexpr int PF = 1;
 constexpr int XP = 16 * PF * XW;  // probes per block
 constexpr int XG = 64;        // gallery rows per tile
-constexpr int XC = 64;        // dims per LDS chunk
+// dims per LDS chunk: 128 (16-KiB chunks, 7-slot ring) since the 1-product pass halved the MFMAs per barrier;
+// 64 (8 KiB, 13 slots) measured 2.5 % slower (2048 x 125k 0.450 vs 0.438 ms; it was 1.5-3 % faster at 2 products)
+constexpr int XC = 128;
+constexpr int XNC = 512 / XC;  // chunks per 64-row tile
+constexpr int XGR = XC / 8;    // 16-B groups per chunk row
 constexpr int XD = 512;       // embedding dim (the kernel is specialised)
 constexpr int KP = 8;         // candidates per (probe, split, sub-lane): 4 sub-lanes per probe
 constexpr int KO = 16;        // candidates written per (probe, split) ...
@@ -106,8 +110,9 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
 // stay conflict-free.  (Row-major gh / gl arrays put a chunk's 64
 // rows 1 KiB apart: its 128-B pieces fell on a few HBM / L2 channels, every block of a split on the same
 // ones.)  Rows past the gallery in the last tile are never candidates (the kernel masks them).
-constexpr int XCHUNK_E = 64 * 64;  // bf16 elements per chunk (8 KiB)
-__device__ __forceinline__ int xswz_row(int row) { return (row >> 1) & 7; }
+constexpr int XCHUNK_E = 64 * XC;  // bf16 elements per chunk
+// 128-B rows: rows r, r + 1 are 32 banks apart, so (r >> 1) & 7 separates the rest; 256-B rows start on one bank
+__device__ __forceinline__ int xswz_row(int row) { return XGR == 16 ? row & 15 : (row >> 1) & 7; }
 
 __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ G, int64_t row0, int64_t n,
                                                        bf16_t* __restrict__ T, uint32_t* __restrict__ stats) {
@@ -115,7 +120,7 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
     float eg = 0.f, gn = 0.f;  // this lane's running max of ||g - gh|| and ||gh|| over its rows
     for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n * 64; i += (int64_t)gridDim.x * 256) {
         const int64_t r = row0 + i / 64;
-        const int grp = (int)(i % 64), c = grp >> 3, g = grp & 7, rr = (int)(r & 63);
+        const int grp = (int)(i % 64), c = grp / XGR, g = grp % XGR, rr = (int)(r & 63);
         const float* src = G + r * 512 + 8 * grp;
         const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
         const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -136,7 +141,7 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
         }
         eg = fmaxf(eg, sqrtf(e2));
         gn = fmaxf(gn, sqrtf(h2));
-        bf16_t* dst = T + ((r >> 6) * 8 + c) * XCHUNK_E + rr * 64 + (g ^ xswz_row(rr)) * 8;
+        bf16_t* dst = T + ((r >> 6) * XNC + c) * XCHUNK_E + rr * XC + (g ^ xswz_row(rr)) * 8;
         uint4 hv;
         hv.x = hb[0] | (uint32_t)hb[1] << 16; hv.y = hb[2] | (uint32_t)hb[3] << 16;
         hv.z = hb[4] | (uint32_t)hb[5] << 16; hv.w = hb[6] | (uint32_t)hb[7] << 16;
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
     }
 }
 
-constexpr int XSLOT = 13;  // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB)
+constexpr int XSLOT = XC == 128 ? 7 : 13;  // LDS ring depth (chunks): XSLOT - 1 in flight (96 KiB)
 constexpr int XCHUNK_B = XG * XC * 2;          // 8 KiB: [64 rows x 128 B]
 static_assert(XCHUNK_B == XCHUNK_E * 2, "chunk layout");
 constexpr int XRB = XC * 2;                    // LDS row bytes
@@ -204,12 +209,12 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
     // LDS-DMA of chunk (tile t0, dims 64c..): a linear copy of its 16 KiB (split_x3_kernel's layout), 16
     // pieces of 1 KiB, wave w issues pieces 2w, 2w+1.  The resource starts at the split's first chunk
     // (32-bit offsets); look-ahead chunks past the gallery read 0, past the split are never used.
-    const size_t g_chunk0 = (size_t)(g_begin / XG) * 8;
-    const size_t g_left = ((size_t)((N + XG - 1) / XG) * 8 - g_chunk0) * XCHUNK_B;
+    const size_t g_chunk0 = (size_t)(g_begin / XG) * XNC;
+    const size_t g_left = ((size_t)((N + XG - 1) / XG) * XNC - g_chunk0) * XCHUNK_B;
     const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(GT + g_chunk0 * XCHUNK_E), 0,
                                                                         (int)min(g_left, (size_t)0x7fffffff), 0x00020000);
     auto issue_chunk = [&](int64_t t0, int c, int slot) {
-        const uint32_t cbase = (uint32_t)((((t0 - g_begin) / XG) * 8 + c) * XCHUNK_B);
+        const uint32_t cbase = (uint32_t)((((t0 - g_begin) / XG) * XNC + c) * XCHUNK_B);
 #pragma unroll
         for (int u = 0; u < XPPW; ++u) {
             const int piece = XPPW * wave + u;
@@ -625,7 +630,7 @@ __global__ __launch_bounds__(64 * WPB) void match_rows_kernel(const float* __res
 
 }  // namespace
 
-size_t x3_gallery_elems(int64_t rows) { return X3_HEAD + (size_t)((rows + XG - 1) / XG) * 8 * XCHUNK_E; }
+size_t x3_gallery_elems(int64_t rows) { return X3_HEAD + (size_t)((rows + XG - 1) / XG) * XNC * XCHUNK_E; }
 
 hipError_t launch_split_x3(const float* G, int64_t row0, int64_t n, bf16_t* T, hipStream_t s) {
     if (n <= 0) return hipSuccess;
