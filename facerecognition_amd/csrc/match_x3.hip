@@ -288,11 +288,11 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
             for (int j = 0; j < 4; ++j) acc[f][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < XD / XC; ++c) {
-            // chunk c landed (the XSLOT - 2 younger chunks' pieces may stay in flight); every wave is
-            // past chunk c-1, so its slot takes chunk c + XSLOT - 1
-            // (the XPPW x (XSLOT - 2) younger chunks' DMAs may stay in flight)
+            // chunk c landed (the XPPW x (XSLOT - 2) younger chunks' DMA pieces may stay in flight); every wave
+            // has its reads of chunk c - 1 back (lgkmcnt(0): the compiler may sink that chunk's MFMAs, and with
+            // them its own waits, below this barrier), so chunk c - 1's slot takes chunk c + XSLOT - 1
             static_assert(XPPW * (XSLOT - 2) < 64, "vmcnt range");
-            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(XPPW * (XSLOT - 2)) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(XPPW * (XSLOT - 2)) : "memory");
             issue_next();
             const char* ch = smem + s_read * XCHUNK_B;
             if (++s_read == XSLOT) s_read = 0;
@@ -505,6 +505,36 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
         if (q == k - 1) kth = ws;
     }
     // (d) an excluded row scores <= T + eps; ties need the index order, so require kth > T + 2 eps
+    if (!(T == -INFINITY || kth > T + 2.f * eps)) {
+        // (e) widened: candidates KC .. 2 KC - 1 on lanes KC .. 2 KC - 1 (the lists hold up to 64 x KL entries), T
+        // from the 2 KC-th; a one-wave rescan of the whole gallery (milliseconds at 1M rows) only if that fails too
+        static_assert(2 * KC == 64, "one candidate per lane");
+        float T2 = -INFINITY;
+        for (int q = KC; q < 2 * KC; ++q) {
+            float ws;
+            int wi;
+            wave_pop<KL>(ls, li, head, ws, wi);
+            if (lane == q) my_idx = wi == INT_MAX ? -1 : wi;
+            if (q == 2 * KC - 1) T2 = wi == INT_MAX ? -INFINITY : ws;
+        }
+        T2 = fmaxf(T2, floor_s);
+        if (lane >= KC && my_idx >= 0) {
+            rs[0] = exact_dot_lds(pl, G + (size_t)(my_idx - index_base) * XD);
+            ri[0] = my_idx;
+        }
+        h1 = 0;
+        for (int q = 0; q < k; ++q) {
+            float ws;
+            int wi;
+            wave_pop<1>(rs, ri, h1, ws, wi);
+            if (lane == q) {
+                outs = wi == INT_MAX ? -INFINITY : ws;
+                outi = wi == INT_MAX ? -1 : wi;
+            }
+            if (q == k - 1) kth = ws;
+        }
+        T = T2;
+    }
     if (!(T == -INFINITY || kth > T + 2.f * eps)) {
         if (lane == 0 && n_fallback) atomicAdd(n_fallback, 1);
         float fs[KC];

@@ -604,19 +604,24 @@ def test_match_x3_equals_exact(gpu, B, Ng, k):
     gal.close()
 
 
-def test_match_x3_fallback_on_ties(gpu):
-    """40 identical copies of a row: more than KC - k candidates tie within 2 eps, so the candidate
-    proof fails and the probe is rescanned exactly -- lowest indices first, like the f32 kernel."""
+@pytest.mark.parametrize("ndup,rescan", [(40, False), (70, True)])
+def test_match_x3_fallback_on_ties(gpu, ndup, rescan):
+    """ndup identical copies of a row, one per 64-row tile (at 6000 rows and 6 probes every tile is its own
+    gallery split, so no candidate sub-list overflows): more than KC - k = 27 candidates tie within 2 eps, so the
+    32-candidate proof fails.  40 copies are settled by the widened 64-candidate pass (no rescan); 70 copies
+    exceed it too and the probe is rescanned exactly.  Either way lowest indices first, like the f32 kernel."""
     from facerecognition_amd.gallery import DeviceGallery
     rng = np.random.default_rng(5)
     G = _norm(rng.standard_normal((6000, 512)))
-    G[100:140] = G[7]
+    dups = [64 * t + 5 for t in range(2, 2 + ndup)]
+    G[dups] = G[7]
     P = _norm(G[[7, 11]] + 0.01 * rng.standard_normal((2, 512)))
     P = np.concatenate([P, _norm(rng.standard_normal((4, 512)))])  # B > 4: the bf16x3 path, not match_rows
     gal = DeviceGallery(G, x3_min_rows=4096)
+    fb0 = gal.fallbacks()
     s3, i3 = gal.search(P, 5)
-    assert gal.fallbacks() >= 1
-    assert list(i3[0]) == [7, 100, 101, 102, 103]
+    assert (gal.fallbacks() - fb0 >= 1) == rescan
+    assert list(i3[0]) == [7] + dups[:4]
     gal.set_exact(True)
     se, ie = gal.search(P, 5)
     assert np.array_equal(i3, ie) and np.array_equal(s3, se)
