@@ -126,6 +126,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip the per-kernel event timing (roofline)")
+    ap.add_argument("--eager-prof", action="store_true",
+                    help="time every 8th launch of the dominant class in eager steps instead of graph slots")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 --pmc traffic passes (roofline.traffic = null)")
     ap.add_argument("--share-device", action="store_true",
@@ -323,10 +325,11 @@ def main():
         torch.cuda.synchronize(dev)
         kclasses_all = N.prof_read(model.handle)
         dominant = max(kclasses_all.items(), key=lambda kv: kv[1][0])[0]
-        if kclasses_all[dominant][1] == 2:
-            # one launch per forward (IResNet100: the layer3 stage): the timed steps replay hipGraphs, as
-            # the product path does, each step its own captured graph with an event pair around the
-            # dominant launch (fr_prof_slots); two untimed forwards per slot: first sighting, capture
+        if kclasses_all[dominant][1] % 2 == 0 and not args.eager_prof:
+            # the timed steps replay hipGraphs, as the product path does, each step its own captured graph
+            # with an event pair around ONE launch of the dominant class (fr_prof_slots): step i times the
+            # class's launch i mod L (L launches per forward; IResNet100: the layer3 stage, L = 1); two
+            # untimed forwards per slot: first sighting, capture
             N.check(L.fr_prof_enable(model.handle, 0), "fr_prof_enable")
             N.check(L.fr_prof_slots(model.handle, dominant.encode(), args.steps), "fr_prof_slots")
             for i in range(args.steps):
@@ -356,15 +359,19 @@ def main():
     kclasses = {}
     if slot_mode:
         L = N.lib()
-        ms_slots = []
+        ms_slots, fl_slots, by_slots = [], [], []
         for i in range(args.steps):
             v = ctypes.c_float(0.0)
+            fl, by = ctypes.c_double(0.0), ctypes.c_double(0.0)
             N.check(L.fr_prof_slot_ms(model.handle, i, ctypes.byref(v)), "fr_prof_slot_ms")
+            N.check(L.fr_prof_slot_work(model.handle, i, ctypes.byref(fl), ctypes.byref(by)), "fr_prof_slot_work")
             ms_slots.append(v.value)
+            fl_slots.append(fl.value)
+            by_slots.append(by.value)
         N.check(L.fr_prof_slot_select(model.handle, -1), "fr_prof_slot_select")
         N.check(L.fr_prof_slots(model.handle, None, 0), "fr_prof_slots")
-        tot_ms, n_all, fl_all, by_all = kclasses_all[dominant]
-        kclasses = {dominant: (float(np.sum(ms_slots)), args.steps, fl_all / n_all * args.steps, by_all / n_all * args.steps)}
+        # the sampled launches (one per timed step) with their own algorithmic work
+        kclasses = {dominant: (float(np.sum(ms_slots)), args.steps, float(np.sum(fl_slots)), float(np.sum(by_slots)))}
     elif not args.no_prof:
         kclasses = N.prof_read(model.handle)
         N.check(N.lib().fr_prof_enable(model.handle, 0), "fr_prof_enable")
@@ -420,7 +427,8 @@ def main():
                                "2*FETCH_SIZE + WRITE_SIZE (KiB, gfx950 FETCH half-count correction)")
                               if traffic is not None else (pmc_why if pmc is None else f"no rocprof kernel mapping for {name!r}"),
             "sampled_launches": launches, "sample_stride": 1 if slot_mode else PROF_STRIDE,
-            "timing": ("HIP event pair around the launch in every timed step, captured into that step's hipGraph "
+            "timing": ("HIP event pair around one launch of the class in every timed step (step i: launch i mod "
+                       f"{kclasses_all[name][1] // 2} of the forward), captured into that step's hipGraph "
                        "(the timed steps replay graphs, as the product path does)") if slot_mode else
                       ("HIP events stamped by every sample_stride-th dispatch (hipExtLaunchKernel), eager launches"),
             "us_per_launch": round(ms / launches * 1e3, 2), "gflop_per_launch": round(flops / launches / 1e9, 3),

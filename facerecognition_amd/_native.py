@@ -99,6 +99,7 @@ _SIGS = {
     "fr_prof_slots": (c_int, [c_void_p, ctypes.c_char_p, c_int]),
     "fr_prof_slot_select": (c_int, [c_void_p, c_int]),
     "fr_prof_slot_ms": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_float)]),
+    "fr_prof_slot_work": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "fr_prof_get": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t, ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "fr_prof_get_bytes": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_double)]),

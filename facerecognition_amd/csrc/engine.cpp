@@ -187,12 +187,16 @@ struct fr_handle {
     // forward replays as hipGraphs, keyed by the call's pointers / shape (captured on the second call
     // with a key; the first call runs eagerly and warms per-kernel attributes)
     struct GraphEnt { const void* in; float* out; int fmt, B, flags, slot; hipGraphExec_t exec; bool no_graph; uint64_t used; };
-    // graph-slot timing (fr_prof_slots): an event pair per slot around the first launch of one kernel
-    // class, captured into the graph of that slot, so timed steps replay graphs and still time the class
+    // graph-slot timing (fr_prof_slots): an event pair per slot around one launch of one kernel class --
+    // slot i times launch i mod (the class's launches per forward) -- captured into the graph of that slot,
+    // so timed steps replay graphs and still time the class
     std::string slot_class;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> slot_events;
+    std::vector<std::pair<double, double>> slot_work;  // the timed launch's algorithmic FLOPs and bytes
     int slot = -1;         // the slot the next forward captures / replays (-1: none)
     bool slot_done = false;  // the slot's pair is placed in the current forward
+    int slot_seen = 0;     // launches of slot_class so far in the current forward
+    int slot_nl = 0;       // launches of slot_class per forward (learned by the first slot forward)
     std::vector<GraphEnt> graphs;
     hipStream_t cap_stream = nullptr;
     // branch-parallel capture (forward_graph): a second capturing stream and one event per op
@@ -1253,10 +1257,14 @@ struct ProfScope {
     bool slot_pair = false;
     void start(const std::string& c, ConvArgs* ka = nullptr) {
         cls = c;
-        if (!h->prof && h->slot >= 0 && !h->slot_done && cls == h->slot_class) {  // graph-slot timing
-            (void)hipEventRecord(h->slot_events[h->slot].first, s);
-            h->slot_done = true;
-            slot_pair = true;
+        if (!h->prof && h->slot >= 0 && cls == h->slot_class) {  // graph-slot timing
+            const int ord = h->slot_seen++;
+            if (h->slot_seen > h->slot_nl) h->slot_nl = h->slot_seen;
+            if (!h->slot_done && ord == h->slot % h->slot_nl) {
+                (void)hipEventRecord(h->slot_events[h->slot].first, s);
+                h->slot_done = true;
+                slot_pair = true;
+            }
             return;
         }
         if (!h->prof || (!h->prof_only.empty() && h->prof_only != cls)) return;
@@ -1268,7 +1276,10 @@ struct ProfScope {
         else (void)hipEventRecord(a, s);
     }
     ~ProfScope() {
-        if (slot_pair) (void)hipEventRecord(h->slot_events[h->slot].second, s);
+        if (slot_pair) {
+            (void)hipEventRecord(h->slot_events[h->slot].second, s);
+            h->slot_work[h->slot] = {flops, bytes};
+        }
         if (!a) return;
         if (!stamped) (void)hipEventRecord(b, s);
         h->prof_pending.push_back({cls, a, b, flops, bytes});
@@ -1913,6 +1924,7 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
     // cannot leave a count behind.  The memset node is ~6 us of a 1 ms bs = 1 forward that may have no such split.
     if (h->splitk_cnt && h->inlaunch_used) FR_HIP_CHECK(hipMemsetAsync(h->splitk_cnt, 0, FR_SPLITK_TILES * sizeof(int), s_main));
     h->slot_done = false;
+    h->slot_seen = 0;
     const bool ms = h->ms_on;
     const size_t nops = h->ops.size();
     std::vector<std::vector<Rgn>> rd, wr;
@@ -2796,6 +2808,8 @@ int fr_prof_slots(fr_handle* h, const char* kernel_class, int n) {
     }
     h->slot_events.clear();
     h->slot = -1;
+    h->slot_nl = 0;
+    h->slot_work.assign(n > 0 ? n : 0, {0.0, 0.0});
     h->slot_class = n > 0 ? kernel_class : "";
     for (int i = 0; i < n; ++i) {
         hipEvent_t a, b;
@@ -2819,6 +2833,17 @@ int fr_prof_slot_ms(fr_handle* h, int slot, float* ms) {
     FR_HIP_CHECK(hipSetDevice(h->device));
     FR_HIP_CHECK(hipEventSynchronize(h->slot_events[slot].second));
     FR_HIP_CHECK(hipEventElapsedTime(ms, h->slot_events[slot].first, h->slot_events[slot].second));
+    return FR_OK;
+}
+
+int fr_prof_slot_work(fr_handle* h, int slot, double* flops, double* bytes) {
+    if (!h || !flops || !bytes || slot < 0 || slot >= (int)h->slot_work.size()) {
+        set_error("fr_prof_slot_work: bad argument");
+        return FR_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    *flops = h->slot_work[slot].first;
+    *bytes = h->slot_work[slot].second;
     return FR_OK;
 }
 

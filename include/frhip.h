@@ -358,12 +358,14 @@ int fr_prof_only(fr_handle* h, const char* kernel_class);
 int fr_prof_collect(fr_handle* h);
 /* Graph-slot timing (bench.py's timed steps, which replay hipGraphs like the product path):
  * fr_prof_slots(h, class, n) makes n event pairs (n = 0 frees them); with slot i selected
- * (fr_prof_slot_select, -1 = none) a forward records pair i around the first launch of `class` --
- * captured into slot i's own graph, so every replay of that graph re-stamps the pair on the launching
- * stream; fr_prof_slot_ms reads pair i (milliseconds between the two events). */
+ * (fr_prof_slot_select, -1 = none) a forward records pair i around launch i mod L of `class` (L = the
+ * class's launches per forward, counted by the first slot forward) -- captured into slot i's own graph, so
+ * every replay of that graph re-stamps the pair on the launching stream; fr_prof_slot_ms reads pair i
+ * (milliseconds between the two events), fr_prof_slot_work the timed launch's algorithmic FLOPs and bytes. */
 int fr_prof_slots(fr_handle* h, const char* kernel_class, int n);
 int fr_prof_slot_select(fr_handle* h, int slot);
 int fr_prof_slot_ms(fr_handle* h, int slot, float* ms);
+int fr_prof_slot_work(fr_handle* h, int slot, double* flops, double* bytes);
 int fr_prof_get(const fr_handle* h, int i, char* name, size_t n, double* total_ms, int64_t* launches,
                 double* flops);
 /* Algorithmic HBM bytes of class i over its timed launches (each input / weight / output byte once;

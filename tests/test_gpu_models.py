@@ -275,6 +275,53 @@ def test_prof_slot_graph_timing(gpu):
     assert torch.equal(out, ref)
 
 
+def test_prof_slot_rotates_over_launches(gpu):
+    """A class with L launches per forward: slot i times launch i mod L (fr_prof_slot_work reports that launch's
+    algorithmic FLOPs), so L consecutive slots cover every launch once -- their FLOPs sum to the class's total."""
+    import ctypes
+    import math
+    import torch
+    from facerecognition_amd import _native as N
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    L = N.lib()
+    m = FRModel.synthetic("iresnet100", max_batch=8)
+    x = torch.from_numpy(synthetic_crops(8, 112, seed=7)).cuda()
+    out = torch.empty((8, 512), device="cuda")
+    m.embed(x, out=out)
+    torch.cuda.synchronize()
+    ref = out.clone()
+    N.check(L.fr_prof_enable(m.handle, 1), "fr_prof_enable")
+    m.embed(x, out=out)
+    torch.cuda.synchronize()
+    classes = N.prof_read(m.handle)
+    N.check(L.fr_prof_enable(m.handle, 0), "fr_prof_enable")
+    cls = max(classes, key=lambda c: classes[c][1])
+    nl, flops = classes[cls][1], classes[cls][2]
+    assert nl >= 2, classes
+    n = nl + 1
+    N.check(L.fr_prof_slots(m.handle, cls.encode(), n), "fr_prof_slots")
+    try:
+        for i in range(n):
+            N.check(L.fr_prof_slot_select(m.handle, i), "fr_prof_slot_select")
+            for _ in range(2):  # first sighting (eager), capture
+                m.embed(x, out=out)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref)
+        work = []
+        for i in range(n):
+            v, fl, by = ctypes.c_float(0.0), ctypes.c_double(0.0), ctypes.c_double(0.0)
+            N.check(L.fr_prof_slot_ms(m.handle, i, ctypes.byref(v)), "fr_prof_slot_ms")
+            N.check(L.fr_prof_slot_work(m.handle, i, ctypes.byref(fl), ctypes.byref(by)), "fr_prof_slot_work")
+            assert math.isfinite(v.value) and 0.0 < v.value < 1000.0 and fl.value > 0 and by.value > 0
+            work.append(fl.value)
+        assert math.isclose(sum(work[:nl]), flops, rel_tol=1e-9), (sum(work[:nl]), flops)
+        assert work[nl] == work[0]  # slot L wraps to launch 0
+    finally:
+        N.check(L.fr_prof_slot_select(m.handle, -1), "fr_prof_slot_select")
+        N.check(L.fr_prof_slots(m.handle, None, 0), "fr_prof_slots")
+
+
 def test_facenet_projection_head(gpu):
     """FaceNetModel with embedding_size=128 (projection Linear(512,128) + F.normalize after IRV1's own
     L2, facenet_model.py:20-23,32-35) vs the oracle, and the raw (pre-normalize) projection output."""

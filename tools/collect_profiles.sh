@@ -5,7 +5,7 @@ T=${1:?tag}; R=${2:?round prefix}; O=gpurun_out/$T
 set -e
 cp $O/bench.json profiles/${R}_bench.json
 : > profiles/${R}_bench_runs.jsonl
-for b in bench bench_noprof bench_host bench_irv1 bench_irv1_f16 bench_r50 bench_fp8 bench_1m bench_bs1 bench_r50_bs1 bench_2share; do
+for b in bench bench_noprof bench_host bench_irv1 bench_irv1_f16 bench_irv1_graph bench_r50 bench_r50_graph bench_fp8 bench_1m bench_bs1 bench_r50_bs1 bench_2share; do
   [ -f $O/$b.log ] && python3 -c "import json,sys; print(json.dumps({'run': sys.argv[1], 'line': json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])}))" $b $O/$b.log >> profiles/${R}_bench_runs.jsonl
 done
 cp "$(find $O/prof -name '*kernel_stats.csv' | head -1)" profiles/${R}_bench_kernel_stats.csv
