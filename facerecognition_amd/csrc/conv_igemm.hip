@@ -583,11 +583,8 @@ int conv_tile_candidates(int Cout, int* out) {
     // forward (cold operands) the 3-stage tile is the faster one (IRV1 Block17 1x7 / 7x1: 12.0 vs 17.4 us)
     static const int tiles[] = {TILE_128x64_S3, TILE_64x128_S3, TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128,
                                 TILE_256x128, TILE_128x256};
-    static const int old_order[] = {TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128, TILE_256x128, TILE_128x256,
-                                    TILE_128x64_S3, TILE_64x128_S3};
-    static const bool s3_last = ab_int("tune_s3_last", 0) != 0;  // FR_AB tune_s3_last=1: the round-4 order (A/B)
     int n = 0;
-    for (int t : s3_last ? old_order : tiles) {
+    for (int t : tiles) {
         const int BN = conv_tile_bn(t);
         if (BN >= 128 && Cout <= 64) continue;
         if (BN == 256 && Cout <= 128) continue;
