@@ -74,6 +74,45 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const bf16_t* __restrict__
     }
 }
 
+// k = 3 (IRV1's and ResNet-50's pools): the nine 16-B loads of a window issued together (clamped addresses,
+// out-of-image taps masked to -inf afterwards) instead of one dependent load per loop trip; same values
+template <bool F16>
+__global__ __launch_bounds__(256) void maxpool3_kernel(const bf16_t* __restrict__ x, int B, int H, int W, int Cx,
+                                                       int x_off, int C, int stride, int pad,
+                                                       bf16_t* __restrict__ y, int Cy, int y_off, int Ho, int Wo) {
+    const int G = C / 8;
+    const size_t total = (size_t)B * Ho * Wo * G;
+    for (size_t it = blockIdx.x * 256ull + threadIdx.x; it < total; it += (size_t)gridDim.x * 256) {
+        const int g = (int)(it % G);
+        const size_t pix = it / G;
+        const int ow = (int)(pix % Wo);
+        const int oh = (int)((pix / Wo) % Ho);
+        const int b = (int)(pix / ((size_t)Wo * Ho));
+        uint4 v[9];
+        unsigned ok = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int ih = oh * stride - pad + t / 3, iw = ow * stride - pad + t % 3;
+            const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+            ok |= in ? 1u << t : 0u;
+            const int ch = in ? ih : 0, cw = in ? iw : 0;
+            v[t] = *(const uint4*)(x + ((size_t)(b * H + ch) * W + cw) * Cx + x_off + g * 8);
+        }
+        float m[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            if (!(ok >> t & 1u)) continue;
+            float f[8];
+            Num<F16>::unpack8(v[t], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+        }
+        *(uint4*)(y + pix * Cy + y_off + g * 8) = Num<F16>::pack8(m);
+    }
+}
+
 template <bool F16>
 __global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t* __restrict__ x, int B, int HW, int C,
                                                       bf16_t* __restrict__ y) {
@@ -307,6 +346,15 @@ hipError_t launch_maxpool(const bf16_t* x, int B, int H, int W, int Cx, int x_of
     const size_t total = (size_t)B * Ho * Wo * (C / 8);
     int blocks = (int)((total + 255) / 256);
     if (blocks > 8192) blocks = 8192;
+    if (k == 3) {
+        if (f16)
+            hipLaunchKernelGGL(maxpool3_kernel<true>, dim3(blocks), dim3(256), 0, s, x, B, H, W, Cx, x_off, C, stride, pad,
+                               y, Cy, y_off, Ho, Wo);
+        else
+            hipLaunchKernelGGL(maxpool3_kernel<false>, dim3(blocks), dim3(256), 0, s, x, B, H, W, Cx, x_off, C, stride, pad,
+                               y, Cy, y_off, Ho, Wo);
+        return hipGetLastError();
+    }
     if (f16)
         hipLaunchKernelGGL(maxpool_kernel<true>, dim3(blocks), dim3(256), 0, s, x, B, H, W, Cx, x_off, C, k, stride,
                            pad, y, Cy, y_off, Ho, Wo);
