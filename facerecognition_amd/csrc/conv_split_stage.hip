@@ -58,7 +58,10 @@ struct SplitGeo {
     static constexpr int PATCH_B = NPL * PLANE_B;
     static constexpr int SLICE_B = 4 * C * 16;       // one K-step: [4 groups of 8 ch][C rows][16 B]
     static constexpr int NSLOT = 3;
-    static constexpr int TAB_ROWS_B = 6 * C * 4;     // the 6 border classes a part can meet, [6][C] f32
+    static constexpr int TROW = C * 4 + 16;          // table row bytes, one 16-B bank slot of padding: the rows
+                                                     // of different border classes a fragment's lanes read at
+                                                     // once fall on different banks (C * 4 is 0 mod 256 B)
+    static constexpr int TAB_ROWS_B = 6 * TROW;      // the 6 border classes a part can meet, [6][C] f32 (padded)
     static constexpr int TS = TAB_ROWS_B + C * 4;      // + one row: the PReLU slope of the conv before
     static constexpr int TAB = PATCH_B + NSLOT * SLICE_B;
     static constexpr int FAILED = TAB + 2 * TS;      // int: this part's bounded wait ran out
@@ -215,8 +218,8 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
     auto issue_tab = [&](int cv, int cv_slope, int slot) {
         char* dst = smem + G::TAB + slot * G::TS;
         int lane = opaque_tid() & 63;  // opaque: the DMA offsets are not hoisted out of the block loop
-        if (wave * 1024 < G::TAB_ROWS_B && wave * 1024 + lane * 16 < G::TAB_ROWS_B)
-            dma16s(epr, dst + wave * 1024, (uint32_t)(wave * 1024 + lane * 16), (uint32_t)((cv * 9 + 3 * tbase) * C * 4));
+        if (wave < 6 && lane * 16 < C * 4)  // wave r: table row r (padded rows: one DMA per row)
+            dma16s(epr, dst + wave * G::TROW, (uint32_t)(wave * C * 4 + lane * 16), (uint32_t)((cv * 9 + 3 * tbase) * C * 4));
         if (cv_slope >= 0 && wave == NW - 1 && lane * 16 < C * 4)
             dma16s(slr, dst + G::TAB_ROWS_B, (uint32_t)(lane * 16), (uint32_t)(cv_slope * C * 4));
     };
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         const int f = FM * wm + j, q = f % QPR, cl = ln & 15;
         const int rc = (part == 0 && f < QPR) ? 0 : ((part == PARTS - 1 && f >= (HR - 1) * QPR) ? 2 : 1);
         const int cc = (q == 0 && cl == 0) ? 0 : ((q == QPR - 1 && cl == (IW - 1) % 16) ? 2 : 1);
-        return ((rc - tbase) * 3 + cc) * C * 4;
+        return ((rc - tbase) * 3 + cc) * G::TROW;
     };
     auto seed_bias = [&](int slot) {
         int ln = lane;
