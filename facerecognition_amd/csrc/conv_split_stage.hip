@@ -58,9 +58,10 @@ struct SplitGeo {
     static constexpr int PATCH_B = NPL * PLANE_B;
     static constexpr int SLICE_B = 4 * C * 16;       // one K-step: [4 groups of 8 ch][C rows][16 B]
     static constexpr int NSLOT = 3;
-    static constexpr int TROW = C * 4 + 16;          // table row bytes, one 16-B bank slot of padding: the rows
+    static constexpr int TROW = C * 4 + 32;          // table row bytes, two 16-B bank slots of padding: the rows
                                                      // of different border classes a fragment's lanes read at
-                                                     // once fall on different banks (C * 4 is 0 mod 256 B)
+                                                     // once fall on different banks (C * 4 is 0 mod 256 B; one
+                                                     // slot would meet the lanes reading 4 channels further on)
     static constexpr int TAB_ROWS_B = 6 * TROW;      // the 6 border classes a part can meet, [6][C] f32 (padded)
     static constexpr int TS = TAB_ROWS_B + C * 4;      // + one row: the PReLU slope of the conv before
     static constexpr int TAB = PATCH_B + NSLOT * SLICE_B;
@@ -431,8 +432,13 @@ __global__ __launch_bounds__(64 * NW, 1) void split_stage_kernel(StageArgs p) {
         if (yo) {  // the part's rows, NHWC (once per stage; every conv for intermediates)
             // a part whose halo wait ran out writes NaN (16-bit quiet NaN in both dtypes' high half)
             const uint32_t nan_or = *(const volatile int*)(smem + G::FAILED) ? 0x7FC07FC0u : 0u;
-            for (int c = opaque_tid(); c < HR * IW * NPL; c += 64 * NW) {
-                const int pix = c / NPL, pl = c - pix * NPL, row = pix / IW, pos = pix - row * IW;
+            // 16 pixels x 4 planes per wave instruction (16 lanes of one plane read 16 positions: distinct
+            // banks; plane-fastest put every lane of a 16-lane group on one bank slot)
+            constexpr int NPIX = HR * IW, NIT = (NPIX + 15) / 16 * 16 * NPL;
+            for (int c = opaque_tid(); c < NIT; c += 64 * NW) {
+                const int r = c >> 6, pix = (r / (NPL / 4)) * 16 + (c & 15), pl = (r % (NPL / 4)) * 4 + ((c >> 4) & 3);
+                if (pix >= NPIX) continue;
+                const int row = pix / IW, pos = pix - row * IW;
                 uint4 v = *(const uint4*)(smem + pl * PLANE_B + ((row + 1) * PC + pos + 1) * 16);
                 v.x |= nan_or; v.y |= nan_or; v.z |= nan_or; v.w |= nan_or;
                 *(uint4*)(yo + ((size_t)(b * IW + r0 + row) * IW + pos) * C + pl * 8) = v;
