@@ -42,8 +42,10 @@ constexpr int TROW_B = TPOS * 128;        // 14464
 constexpr int TSLOTS = 5;
 constexpr int T_OFF = 0;
 constexpr int X_OFF = TSLOTS * TROW_B;    // 72320
-constexpr int TAB = X_OFF + XSLOTS * XROW_B;  // 159872: ep1 [9][64], slope1 [64], b2 [64] (f32)
-constexpr int TAB_B = (9 + 2) * TCH * 4;
+constexpr int TAB = X_OFF + XSLOTS * XROW_B;  // 159872: ep1 [9][64] (rows TROWF apart), slope1 [64], b2 [64] (f32)
+constexpr int TROWF = TCH + 8;             // ep1 row stride in floats: 2 bank slots of padding (the rows of a
+                                           // fragment's border classes fall on different banks)
+constexpr int TAB_B = (9 * TROWF + 2 * TCH) * 4;
 constexpr int TRANS_LDS = 163840;         // the whole LDS (padding-lane fragment reads stay inside it)
 static_assert(TAB + TAB_B <= TRANS_LDS, "lds");
 constexpr int NPH = OW + 1;               // phases
@@ -109,10 +111,10 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
     // ---- epilogue tables into LDS; t ring: the zero row -1 (slot 0) and the zero column -1 of every slot
     {
         float* tab = (float*)(smem + TAB);
-        for (int i = threadIdx.x; i < 9 * TCH; i += 256) tab[i] = p.ep1[i];
+        for (int i = threadIdx.x; i < 9 * TCH; i += 256) tab[(i / TCH) * TROWF + i % TCH] = p.ep1[i];
         for (int i = threadIdx.x; i < TCH; i += 256) {
-            tab[9 * TCH + i] = p.slope1[i];
-            tab[10 * TCH + i] = p.b2[i];
+            tab[9 * TROWF + i] = p.slope1[i];
+            tab[9 * TROWF + TCH + i] = p.b2[i];
         }
         for (int i = threadIdx.x; i < TROW_B / 16; i += 256) *(uint4*)(smem + T_OFF + i * 16) = make_uint4(0, 0, 0, 0);
         if (threadIdx.x < (TSLOTS - 1) * 8) {
@@ -187,11 +189,11 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
     float4 s1m[2];  // conv1 PReLU: slope - 1
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        const float4 sl = *(const float4*)(tab + 9 * TCH + 16 * (2 * np + i) + 4 * lg);
+        const float4 sl = *(const float4*)(tab + 9 * TROWF + 16 * (2 * np + i) + 4 * lg);
         s1m[i] = make_float4(sl.x - 1.f, sl.y - 1.f, sl.z - 1.f, sl.w - 1.f);
     }
     const int n2 = 16 * wave + 4 * lg;  // conv2: the lane's 4 output channels
-    const float4 b2v = *(const float4*)(tab + 10 * TCH + n2);
+    const float4 b2v = *(const float4*)(tab + 9 * TROWF + TCH + n2);
 
     f32x4_t acc1[2][7], acc2[4], accd[4];
     bf16_t* const yb = p.y + (size_t)b * OW * OW * TCH;
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256, 1) void trans_kernel(TransArgs p) {
                 const int cc = (j == 0 && l15 == 0) ? 0 : ((j == 6 && l15 == 15) ? 2 : 1);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const float4 bb = *(const float4*)(tab + (3 * rc + cc) * TCH + 16 * (2 * np + i) + 4 * lg);
+                    const float4 bb = *(const float4*)(tab + (3 * rc + cc) * TROWF + 16 * (2 * np + i) + 4 * lg);
                     acc1[i][j] = (f32x4_t){bb.x, bb.y, bb.z, bb.w};
                 }
             }
