@@ -292,7 +292,8 @@ def main():
     emb = torch.empty((B, 512), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    matcher = ShardedMatcher(B, 512, K, lambda p, s, i: gallery.search_device(p, K, s, i), dev)
+    matcher = ShardedMatcher(B, 512, K, lambda p, s, i: gallery.search_device(p, K, s, i), dev,
+                             pad_short=False)  # full batches every step
 
     u8_host = u8.cpu().pin_memory() if args.host_input else None
 
@@ -460,7 +461,7 @@ def main():
         # has a same-workload N = 1 point (the headline `value` stays config 2's 10k gallery)
         g1m = DeviceGallery(device=local, index_base=0)
         g1m.set_device_rows(synthetic_gallery_rows(0, C4_ROWS, dev))
-        m1m = ShardedMatcher(B, 512, K, lambda p, s, i: g1m.search_device(p, K, s, i), dev)
+        m1m = ShardedMatcher(B, 512, K, lambda p, s, i: g1m.search_device(p, K, s, i), dev, pad_short=False)
 
         def step1m():
             model.embed(u8, out=emb, sync=False)

@@ -2692,6 +2692,13 @@ int fr_set_option(fr_handle* h, int option, int value) {
             break;
         case FR_OPT_SPLITK_INLAUNCH: h->splitk_inlaunch = value != 0; break;
         case FR_OPT_BATCH_INVARIANT:
+            // an e4m3 conv scales its activations by the amax of the whole batch (kernels.h need_amax), so an fp8
+            // handle cannot promise batch-independent bits: refused rather than silently broken
+            if (value != 0 && h->dtype == FR_DTYPE_FP8) {
+                set_error("fr_set_option: FR_OPT_BATCH_INVARIANT is not available on FR_DTYPE_FP8 handles (their e4m3 "
+                          "convs scale activations by a per-batch amax)");
+                return FR_ERR_ARG;
+            }
             if ((value != 0) != h->invariant) {  // the kernel choices are re-measured under the new rule
                 h->invariant = value != 0;
                 h->tuned.clear();

@@ -14,6 +14,7 @@
 // is the numpy code's, in float32 and in the same operation order (this file is built with -ffp-contract=off), so
 // the kept set is the same: degenerate boxes (non-positive extent or area, non-finite coordinates: 'Min' mode's
 // 0 / 0 = NaN suppresses regardless of distance) are compared with every kept box instead.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <unordered_map>
@@ -48,6 +49,10 @@ inline bool suppressed(const Box& k, const Box& c, float t, bool min_mode) {
 constexpr int NCLASS = 40;
 constexpr double MARGIN = 2.0;           // 'Min' mode counts one more pixel per side; one more for rounding
 constexpr int64_t DENSE_MAX = 1 << 24;   // cells of a dense class grid; larger extents hash their cells
+// ... and only while the grid is not mostly empty: batched_nms offsets image i by i x (frame + 1), so a batch of B
+// frames spreads its boxes along a diagonal and a dense grid would grow as B^2; a class grid stays dense
+// while it has at most DENSE_FILL cells per box of the class (or DENSE_MIN cells in all)
+constexpr int64_t DENSE_MIN = 1 << 16, DENSE_FILL = 16;
 
 // The kept boxes of one grid cell, contiguous (a cell holds a handful: one or two cache lines per lookup).
 typedef std::vector<Box> Cell;
@@ -63,6 +68,7 @@ bool cell_hits(const Cell& k, const Box& c, float t) {
 // Cell of kept boxes keyed by the cell of the box's (x1, y1) corner
 struct ClassGrid {
     bool used = false, dense = true;
+    int64_t count = 0;                               // boxes of the class
     double cs = 1.0, ext = 0.0;
     float amin = INFINITY, amax = 0.f;               // area range of the class
     float wmax = 0.f, hmax = 0.f;                    // largest width / height (IoU mode: x2 - x1, y2 - y1)
@@ -115,6 +121,7 @@ int nms_run(const float* boxes, int64_t n, const int64_t* order, float thresh, i
         while (g < NCLASS - 1 && std::ldexp(1.0, g) < e) ++g;
         cls[(size_t)i] = (signed char)g;
         grid[(size_t)g].used = true;
+        grid[(size_t)g].count++;
         grid[(size_t)g].ext = std::fmax(grid[(size_t)g].ext, e);
         grid[(size_t)g].amin = std::fmin(grid[(size_t)g].amin, q.area);
         grid[(size_t)g].amax = std::fmax(grid[(size_t)g].amax, q.area);
@@ -134,7 +141,8 @@ int nms_run(const float* boxes, int64_t n, const int64_t* order, float thresh, i
         G.cs = MIN_MODE ? G.ext : std::fmax(G.ext * (1.0 - 2.0 * (double)thresh / (1.0 + (double)thresh)), 2.0);
         G.nx = (int64_t)std::floor((Mx + 2 * MARGIN - ox) / G.cs) + 1;
         G.ny = (int64_t)std::floor((My + 2 * MARGIN - oy) / G.cs) + 1;
-        G.dense = G.nx > 0 && G.ny > 0 && G.nx <= DENSE_MAX / G.ny;
+        G.dense = G.nx > 0 && G.ny > 0 && G.nx <= DENSE_MAX / G.ny &&
+                  G.nx * G.ny <= std::max(DENSE_MIN, DENSE_FILL * G.count);
         if (G.dense) G.slot.assign((size_t)(G.nx * G.ny), -1);
     }
     std::vector<int64_t> kept_degen, kept_all;

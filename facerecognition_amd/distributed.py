@@ -74,15 +74,25 @@ class ShardedMatcher:
     The candidate exchange is ONE all-gather: each rank's block is [2][P][k] 4-byte words (its scores,
     then its indices), written in place by the shard search, gathered as is and merged as is.
     search() returns views of buffers owned by the matcher, overwritten by the next call (clone them to keep
-    them).  At world 1 a batch shorter than the constructor's (the last, partial batch of a stream) is fine.
+    them).
+
+    Short batches (the last, partial batch of a stream; ranks may differ): a rank with B' < batch probes pads its
+    block with masked rows (every element PAD_MARK = 2.0, which no L2-normalized embedding holds; a non-degenerate
+    probe, so the shard search costs what a real one does), and after the merge every masked row reads (-inf, -1),
+    FAISS's "no result".  Rows j*batch + b, b < rank j's count, are rank j's probes; ``valid`` marks them.  The
+    masking adds three small device ops per call; ``pad_short=False`` (callers whose batches are always full, such
+    as bench.py) skips it.  At world 1 a short batch returns just its B' rows.
     """
 
+    PAD_MARK = 2.0
+
     def __init__(self, batch: int, dim: int, k: int, local_search: Callable, device: torch.device,
-                 merge: Optional[Callable] = None, group=None, always_exchange: bool = False):
+                 merge: Optional[Callable] = None, group=None, always_exchange: bool = False, pad_short: bool = True):
         import torch.distributed as dist
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.always_exchange = always_exchange  # run steps 1-4 even at world 1 (tests of the collectives)
         self.group, self.k, self.B = group, k, batch
+        self.pad_short = pad_short
         self.local_search = local_search
         self.merge = merge or native_merge_ranks
         W, P = self.world, self.world * batch
@@ -92,13 +102,18 @@ class ShardedMatcher:
         self.out_s = torch.empty((P, k), dtype=torch.float32, device=device)
         self.out_i = torch.empty((P, k), dtype=torch.int32, device=device)
         self._send_s, self._send_i = self.send[0].view(torch.float32), self.send[1]
+        self._pad = torch.empty((batch, dim), dtype=torch.float32, device=device) if pad_short else None
+        self.valid = torch.ones(P, dtype=torch.bool, device=device)
         import inspect
+        # the round-3 interface local_search(probes) -> (scores, idx): ONE positional parameter in all (a defaulted
+        # out_s / out_i still makes the three-argument form)
         try:
-            n_args = len([p for p in inspect.signature(local_search).parameters.values()
-                          if p.default is inspect.Parameter.empty and p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD)])
+            params = inspect.signature(local_search).parameters.values()
+            n_pos = len([p for p in params if p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD)])
+            var = any(p.kind == p.VAR_POSITIONAL for p in params)
         except (TypeError, ValueError):
-            n_args = 3
-        self._legacy = n_args == 1
+            n_pos, var = 3, False
+        self._legacy = n_pos <= 1 and not var
 
     def _local(self, probes, out_s, out_i):
         r = self.local_search(probes) if self._legacy else self.local_search(probes, out_s, out_i)
@@ -116,8 +131,21 @@ class ShardedMatcher:
             s, i = self.out_s[:B], self.out_i[:B]
             self._local(emb, s, i)
             return s, i
+        B = int(emb.shape[0])
+        if B != self.B:
+            if B > self.B or not self.pad_short:
+                raise ValueError(f"ShardedMatcher.search: {B} probes on a matcher built for {self.B} per rank"
+                                 + ("" if B > self.B else " with pad_short=False"))
+            self._pad[:B].copy_(emb)
+            self._pad[B:].fill_(self.PAD_MARK)
+            emb = self._pad
         _all_gather(self.all_emb, emb, self.group)
         self._local(self.all_emb, self._send_s, self._send_i)
         _all_gather(self.xchg.view(-1), self.send.view(-1), self.group)
         self.merge(self.xchg, self.k, self.out_s, self.out_i)
+        if self.pad_short:  # masked rows of every rank -> (-inf, -1)
+            torch.ne(self.all_emb[:, 0], self.PAD_MARK, out=self.valid)
+            inv = ~self.valid[:, None]
+            self.out_s.masked_fill_(inv, float("-inf"))
+            self.out_i.masked_fill_(inv, -1)
         return self.out_s, self.out_i

@@ -176,21 +176,31 @@ class RecognitionEngine:
     def __init__(self, model_path: str = "models/checkpoints/arcface/arcface_best.pth", db_path: str = None,
                  faiss_index_path: str = None, prototypes_path: str = None, label_mapping_path: str = None,
                  device: str = None, threshold: float = 0.5, use_face_detection: bool = True, model=None,
-                 face_detector=None, mtcnn_weights: str = None, batch_invariant: bool = True):
-        """batch_invariant (default True): the model runs FR_OPT_BATCH_INVARIANT, so ``recognize_batch`` returns
-        bit for bit what a loop over ``recognize`` returns, as the reference's does (recognition_engine.py:383-389);
-        False lets the model pick the fastest kernels per batch size (embeddings then differ by ~1e-4 cosine
-        between batch sizes)."""
+                 face_detector=None, mtcnn_weights: str = None, batch_invariant: Optional[bool] = None):
+        """batch_invariant: True runs the model with FR_OPT_BATCH_INVARIANT, so ``recognize_batch`` returns bit for
+        bit what a loop over ``recognize`` returns, as the reference's does (recognition_engine.py:383-389); False
+        lets the model pick the fastest kernels per batch size (embeddings then differ by ~1e-4 cosine between
+        batch sizes).  None (default): True for a model the engine loads itself; a caller-supplied ``model=`` keeps
+        its own setting (the option re-tunes the handle, which other users of a shared model would feel).  An
+        explicit True/False is applied to a supplied model too.  fp8 models cannot be batch-invariant (their e4m3
+        convs scale by a per-batch amax): they stay in the default mode, with a warning when True was asked."""
         self.device = device or "cuda"
         self.threshold = threshold
         self.use_face_detection = use_face_detection
         self.model, self.model_info = None, None
+        owned = False
         if model is not None:  # an already-built FRModel (tests, services sharing one model)
             self.model = model
         elif model_path and os.path.exists(model_path):
             self.model, self.model_info = load_arcface_model(model_path, self.device)
-        if self.model is not None and batch_invariant:
-            self.model.set_option(N.FR_OPT_BATCH_INVARIANT, 1)
+            owned = True
+        inv = owned if batch_invariant is None else bool(batch_invariant)
+        if self.model is not None and (inv or batch_invariant is not None):
+            if inv and getattr(self.model, "dtype", None) == "fp8":
+                if batch_invariant:
+                    print("batch_invariant: not available for fp8 models; the model keeps per-batch kernels")
+            else:
+                self.model.set_option(N.FR_OPT_BATCH_INVARIANT, 1 if inv else 0)
         self.transform = get_transform(Wt.INPUT_SIZE[self.model.arch] if self.model is not None else 112)
         self.face_detector = face_detector
         if self.use_face_detection and self.face_detector is None:

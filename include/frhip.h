@@ -325,7 +325,8 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * the implicit GEMM's order (igemm tiles, register-ring, direct and small-M kernels unsplit; no split-K, no LDS-resident
  * stage / transition / block kernels) and the head uses bs = 256's split plan at every batch, so a face's embedding
  * is the same bits whatever batch it is in (the reference's recognize_batch is a loop over recognize,
- * recognition_engine.py:383-389).  Slower than the default, which measures the fastest kernels per batch size. */
+ * recognition_engine.py:383-389).  Slower than the default, which measures the fastest kernels per batch size.
+ * FR_DTYPE_FP8 handles refuse value 1 (FR_ERR_ARG): their e4m3 convs scale activations by a per-batch amax. */
 #define FR_OPT_BATCH_INVARIANT 9
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);

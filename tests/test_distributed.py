@@ -62,7 +62,12 @@ def _worker(rank, world, port, out_dir):
         s2, i2 = m.search(torch.from_numpy(P[rank * B:(rank + 1) * B]))  # buffers reused, same answer
         assert (m.send.data_ptr(), m.xchg.data_ptr(), m.out_s.data_ptr()) == bufs
         assert torch.equal(s, s2) and torch.equal(i, i2)
-        np.savez(os.path.join(out_dir, f"r{rank}.npz"), s=s.numpy(), i=i.numpy())
+        s, i = s.clone(), i.clone()
+        # short last batches, a different count per rank: masked rows ride along
+        n = B - 2 + rank
+        ss, si = m.search(torch.from_numpy(P[rank * B:rank * B + n]))
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), s=s.numpy(), i=i.numpy(), ss=ss.numpy(), si=si.numpy(),
+                 valid=m.valid.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -104,6 +109,16 @@ def test_sharded_match_world2_gloo_equals_single_device():
             assert np.array_equal(r["i"], gi.astype(np.int32))
             assert np.array_equal(r["s"], gs)
         assert list(gi[3][:2]) == [17, 150] and list(gi[7][:2]) == [100, 101]
+        # short batches: rank j sent B - 2 + j probes; its valid rows are the single-device answer, the rest
+        # (-inf, -1)
+        valid = np.zeros(2 * B, bool)
+        for j in (0, 1):
+            valid[j * B:j * B + B - 2 + j] = True
+        for r in (r0, r1):
+            assert np.array_equal(r["valid"], valid)
+            assert np.array_equal(r["si"][valid], gi[valid].astype(np.int32))
+            assert np.array_equal(r["ss"][valid], gs[valid])
+            assert (r["si"][~valid] == -1).all() and np.isneginf(r["ss"][~valid]).all()
 
 
 def test_world1_short_batch_and_one_argument_search():
@@ -121,8 +136,12 @@ def test_world1_short_batch_and_one_argument_search():
         s, i = topk_dot(probes.numpy(), G, K)
         return torch.from_numpy(s), torch.from_numpy(i.astype(np.int32))
 
+    def defaulted(probes, out_s=None, out_i=None):  # three positional parameters: the three-argument form
+        assert out_s is not None and out_i is not None
+        three(probes, out_s, out_i)
+
     gs, gi = topk_dot(P, G, K)
-    for fn in (three, one):
+    for fn in (three, one, defaulted):
         m = ShardedMatcher(B, D, K, fn, torch.device("cpu"))
         s, i = m.search(torch.from_numpy(P[:B]))
         assert np.array_equal(i.numpy(), gi[:B]) and np.array_equal(s.numpy(), gs[:B])

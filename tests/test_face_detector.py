@@ -119,6 +119,26 @@ def test_nms_grid_windows_against_oracle():
         assert np.array_equal(FD.nms(boxes, scores, t, "min"), OM.nms_numpy(boxes, scores, t, "Min"))
 
 
+def test_batched_nms_many_frames_against_oracle():
+    """batched_nms over B = 16 frames (the coordinate-offset trick spreads them along a diagonal, so a dense class
+    grid would grow as B^2 cells: ADVICE r05): the same kept set as the oracle's per-image pass, in bounded time."""
+    import time
+    rng = np.random.default_rng(9)
+    B, per = 16, 2000
+    xy = rng.uniform(0, 1900, (B * per, 2)).astype(np.float32)
+    wh = rng.choice([12.0, 24.0, 48.0, 300.0], (B * per, 1)).astype(np.float32)
+    boxes = np.concatenate([xy, xy + wh], 1)
+    scores = np.round(rng.uniform(0.6, 1.0, B * per), 3).astype(np.float32)
+    inds = np.repeat(np.arange(B), per)
+    t0 = time.perf_counter()
+    got = FD.batched_nms(boxes, scores, inds, 0.5, "iou")
+    dt = time.perf_counter() - t0
+    off = inds.astype(np.float32) * (boxes.max() + np.float32(1))
+    ref = OM.nms_iou((boxes + off[:, None]).astype(np.float32), scores, 0.5)
+    assert np.array_equal(got, ref)
+    assert dt < 2.0, f"batched_nms over {B} frames took {dt:.2f} s"
+
+
 def test_pyramid_and_pool_shapes():
     assert FD.pyramid_scales(150, 190) == OM.pyramid_scales(150, 190)
     for n in range(2, 60):

@@ -28,21 +28,41 @@ def _embed_in_chunks(m, x, bs):
     return np.concatenate([m.embed(x[i:i + bs]).cpu().numpy() for i in range(0, len(x), bs)])
 
 
-@pytest.mark.parametrize("arch", ["iresnet100", "irv1_facenet"])
+@pytest.mark.parametrize("arch", ["iresnet100", "irv1_facenet", "resnet50_arcface"])
 def test_invariant_mode_is_bitwise_batch_independent(gpu, arch):
+    """bs = 256 (the bench batch, where the tuner sees the largest M and may pick the 3-stage, 256x128, 128x256,
+    register-ring or direct kernels) against bs = 64, 9 and 1 (small-M kernels): the same bits in invariant mode."""
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
-    m = FRModel.synthetic(arch, max_batch=64)
+    m = FRModel.synthetic(arch, max_batch=256)
     m.set_option(N.FR_OPT_BATCH_INVARIANT, 1)
-    x = torch.from_numpy(synthetic_crops(64, m.input_size, seed=31)).cuda()
-    e64 = m.embed(x).cpu().numpy()
-    plan = _plan(m, 64)
-    assert not any(l.split()[0] in ("stage", "stage8", "trans", "block") for l in plan.splitlines() if l.strip())
+    x = torch.from_numpy(synthetic_crops(256, m.input_size, seed=31)).cuda()
+    e256 = m.embed(x).cpu().numpy()
+    for B in (256, 64):
+        plan = _plan(m, B)
+        assert not any(l.split()[0] in ("stage", "stage8", "trans", "block", "chain")
+                       for l in plan.splitlines() if l.strip()), plan
+    e64 = m.embed(x[:64]).cpu().numpy()
     e9 = _embed_in_chunks(m, x[:18], 9)
     e1 = _embed_in_chunks(m, x[:4], 1)
     m.close()
-    assert np.array_equal(e9, e64[:18]), "bs = 9 vs bs = 64 differ in invariant mode"
-    assert np.array_equal(e1, e64[:4]), "bs = 1 vs bs = 64 differ in invariant mode"
+    assert np.array_equal(e64, e256[:64]), "bs = 64 vs bs = 256 differ in invariant mode"
+    assert np.array_equal(e9, e256[:18]), "bs = 9 vs bs = 256 differ in invariant mode"
+    assert np.array_equal(e1, e256[:4]), "bs = 1 vs bs = 256 differ in invariant mode"
+
+
+def test_invariant_mode_refused_on_fp8(gpu):
+    """fp8 handles scale their e4m3 convs' activations by a per-batch amax: the option is refused, and
+    the engine leaves such a model in its default mode."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.recognition_engine import RecognitionEngine
+    m = FRModel.synthetic("iresnet100", dtype="fp8", max_batch=8)
+    with pytest.raises(RuntimeError, match="FP8"):
+        m.set_option(N.FR_OPT_BATCH_INVARIANT, 1)
+    assert m.get_option(N.FR_OPT_BATCH_INVARIANT) == 0
+    RecognitionEngine(model_path=None, use_face_detection=False, model=m, batch_invariant=True)
+    assert m.get_option(N.FR_OPT_BATCH_INVARIANT) == 0
+    m.close()
 
 
 def test_default_mode_batch_drift_measured(gpu):

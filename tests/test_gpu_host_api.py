@@ -93,15 +93,19 @@ def test_recognize_batch_end_to_end(gold, r50, names_db):
     from PIL import Image
     from facerecognition_amd.recognition_engine import RecognitionEngine
     _, db = names_db
-    eng = RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.5, model=r50)
+    # a caller-supplied model keeps its own setting unless batch_invariant is given (no silent re-tune of
+    # a shared handle)
+    RecognitionEngine(model_path=None, use_face_detection=False, model=r50)
+    assert r50.get_option(N.FR_OPT_BATCH_INVARIANT) == 0
+    eng = RecognitionEngine(model_path=None, use_face_detection=False, threshold=0.5, model=r50, batch_invariant=True)
     eng.db = db
     imgs = [Image.fromarray(p) for p in gold["probes"]] + ["/nonexistent.jpg"]
     res = eng.recognize_batch(imgs)
     assert [r["identity"] for r in res[:8]] == [str(n) for n in gold["best_name"]]
     assert res[8]["status"] == "error" and res[8]["embedding"] is None
     single = eng.recognize(imgs[2])
-    # the engine runs FR_OPT_BATCH_INVARIANT (default): recognize_batch is bit for bit a loop over recognize, as the
-    # reference's recognize_batch is (recognition_engine.py:383-389)
+    # batch_invariant=True: recognize_batch is bit for bit a loop over recognize, as the reference's recognize_batch
+    # is (recognition_engine.py:383-389)
     assert r50.get_option(N.FR_OPT_BATCH_INVARIANT) == 1
     assert np.array_equal(single["embedding"], res[2]["embedding"])
     assert single["identity"] == res[2]["identity"] and single["confidence"] == res[2]["confidence"]
