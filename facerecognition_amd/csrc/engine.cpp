@@ -136,6 +136,10 @@ struct StageRec {
     // border-class bias + PReLU) runs on the stage's final patch (conv_stage.hip run_tail); its weights and
     // tables follow the blocks' as two 256-channel halves; tail_op is also the last entry of conv_ops
     int tail_op = -1;
+    // IRV1 repeat_2 as one launch (conv_chain.hip): conv_ops = per block {branch1.0 + branch0, 1x7, 7x1, conv2d}
+    bool chain = false;
+    bf16_t* cw = nullptr;                 // chain17_pack_block streams of all blocks
+    float* cbias = nullptr;               // [nblk][1408] the member convs' biases
 };
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -740,7 +744,7 @@ int build_stage(fr_handle* h, StageRec& r) {
 // Device pointer table of a stage's intermediate tensors (filled after every activation reserve).
 int fill_stage_dbg(fr_handle* h) {
     for (auto& r : h->stages) {
-        if (r.trans) continue;  // no intermediates: the member convs run when they are kept
+        if (r.trans || r.chain) continue;  // no intermediates: the member convs run when they are kept
         std::vector<bf16_t*> p(2 * r.nblk);
         for (int i = 0; i < r.nblk; ++i) {
             p[i] = h->tensors[r.x_tensors[i]].dev;
@@ -784,6 +788,59 @@ int build_trans(fr_handle* h, StageRec& r) {
     if ((rc = upload(h, &r.tep1, ep))) return rc;
     if ((rc = upload(h, &r.tsl1, sl))) return rc;
     return upload(h, &r.tb2, b2);
+}
+
+// Packs IRV1 repeat_2's member convs (per block: branch1.0 + branch0 as one 1x1 896 -> 256, the 1x7 and 7x1
+// 128 -> 128, conv2d 256 -> 896 with the residual) into conv_chain.hip's per-wave streams and bias table.
+int build_chain17(fr_handle* h, StageRec& r) {
+    const int nblk = r.nblk;
+    if ((int)r.conv_ops.size() != 4 * nblk) {
+        set_error("plan: chain member count");
+        return FR_ERR_ARG;
+    }
+    std::vector<bf16_t> packed(chain17_weight_elems(nblk));
+    std::vector<float> bias(chain17_bias_floats(nblk), 0.f);
+    for (int blk = 0; blk < nblk; ++blk) {
+        const Op* op[4];
+        const DevConvW* cw[4];
+        std::vector<bf16_t> rows[4];
+        for (int k = 0; k < 4; ++k) {
+            op[k] = &h->ops[r.conv_ops[4 * blk + k]];
+            cw[k] = &h->convw[op[k]->wi];
+            if (cw[k]->w8 || !cw[k]->bias || op[k]->act != 1) {
+                set_error("plan: chain member conv is not bf16 / f16 + bias + ReLU");
+                return FR_ERR_ARG;
+            }
+            rows[k].resize((size_t)cw[k]->Npad * cw[k]->Kpad);
+            FR_HIP_CHECK(hipMemcpy(rows[k].data(), cw[k]->w, rows[k].size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
+        }
+        const bool shapes = cw[0]->Cout == 256 && cw[0]->K == 896 && cw[0]->Kh == 1 && cw[0]->Kw == 1 &&
+                            cw[1]->Cout == 128 && cw[1]->K == 896 && cw[1]->Kh == 1 && cw[1]->Kw == 7 &&
+                            cw[2]->Cout == 128 && cw[2]->K == 896 && cw[2]->Kh == 7 && cw[2]->Kw == 1 &&
+                            cw[3]->Cout == 896 && cw[3]->K == 256 && cw[3]->Kh == 1 && cw[3]->Kw == 1 &&
+                            op[3]->res >= 0 && op[3]->res_off == 0 && op[0]->res < 0 && op[1]->res < 0 && op[2]->res < 0;
+        if (!shapes) {
+            set_error("plan: chain member convs do not have Block17's shapes");
+            return FR_ERR_ARG;
+        }
+        chain17_pack_block(rows[0].data(), cw[0]->Kpad, rows[1].data(), cw[1]->Kpad, rows[2].data(), cw[2]->Kpad,
+                           rows[3].data(), cw[3]->Kpad, blk, nblk, packed.data());
+        // [A = branch1.0 | B = 1x7 | C = 7x1 | D = branch0 | E = conv2d]
+        float* t = bias.data() + (size_t)blk * 1408;
+        std::vector<float> b0(256), b3(896), b1(128), b2(128);
+        FR_HIP_CHECK(hipMemcpy(b0.data(), cw[0]->bias, 256 * sizeof(float), hipMemcpyDeviceToHost));
+        FR_HIP_CHECK(hipMemcpy(b1.data(), cw[1]->bias, 128 * sizeof(float), hipMemcpyDeviceToHost));
+        FR_HIP_CHECK(hipMemcpy(b2.data(), cw[2]->bias, 128 * sizeof(float), hipMemcpyDeviceToHost));
+        FR_HIP_CHECK(hipMemcpy(b3.data(), cw[3]->bias, 896 * sizeof(float), hipMemcpyDeviceToHost));
+        std::copy(b0.begin(), b0.begin() + 128, t);
+        std::copy(b1.begin(), b1.end(), t + 128);
+        std::copy(b2.begin(), b2.end(), t + 256);
+        std::copy(b0.begin() + 128, b0.end(), t + 384);
+        std::copy(b3.begin(), b3.end(), t + 512);
+    }
+    int rc = upload(h, &r.cw, packed);
+    if (rc) return rc;
+    return upload(h, &r.cbias, bias);
 }
 
 std::string L(int l, int i) { return "layer" + std::to_string(l) + "." + std::to_string(i); }
@@ -1091,7 +1148,19 @@ void build_irv1(Builder& b) {
         b.maxpool(x, cat, 640, 3, 2, 0);
         x = cat;
     }
-    // repeat_2: Block17 x10 @8x8. cat layout [t1 | b0 | b1]; conv2d reads [128:384].
+    // repeat_2: Block17 x10 @8x8. cat layout [t1 | b0 | b1]; conv2d reads [128:384].  Also emitted as one
+    // chain launch (conv_chain.hip) beside its member convs; the faster is measured per batch size.
+    int ch_op = -1;
+    StageRec ch;
+    if (h->dtype != FR_DTYPE_FP8 && chain17_supported(8, 8, 896, 10)) {
+        ch_op = (int)h->ops.size();
+        Op op;
+        op.kind = OP_STAGE;
+        op.stage = (int)h->stages.size();
+        h->ops.push_back(op);
+        ch.chain = true;
+        ch.in = x; ch.H = 8; ch.C = 896; ch.nblk = 10;
+    }
     for (int i = 0; i < 10; ++i) {
         const std::string p = m + "repeat_2." + std::to_string(i) + ".";
         const int cat = b.tensor(8, 8, 384);
@@ -1101,7 +1170,15 @@ void build_irv1(Builder& b) {
         b.conv({p + "branch1.2"}, t, 0, 128, cat, 256, 7, 1, 1, 1, 3, 0, 1);
         const int y = b.tensor(8, 8, 896, m + "repeat_2." + std::to_string(i));
         b.conv({p + "conv2d"}, cat, 128, 256, y, 0, 1, 1, 1, 1, 0, 0, 1, x, 0);
+        if (ch_op >= 0)
+            for (int k = 4; k >= 1; --k) ch.conv_ops.push_back((int)h->ops.size() - k);
         x = y;
+    }
+    if (ch_op >= 0 && !b.rc) {
+        ch.out = x;
+        for (int oi : ch.conv_ops) h->ops[oi].stage = h->ops[ch_op].stage;
+        b.rc = build_chain17(h, ch);
+        h->stages.push_back(ch);
     }
     {  // mixed_7a
         const std::string p = m + "mixed_7a.";
@@ -1626,11 +1703,18 @@ static bool trans_enabled() {
     return on;
 }
 
+// FR_AB no_chain: IRV1 repeat_2 always runs as its member convs (A/B timing)
+static bool chain_enabled() {
+    static const bool on = [] { return !ab_int("no_chain", 0); }();
+    return on;
+}
+
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     if (h->stage_mode == 0 || h->invariant) return false;
     // the fused transition keeps no t tensor and records no amax
     if (r.trans && (h->keep_inter || (h->amax && h->need_amax[r.out]) || !trans_enabled())) return false;
     if (r.parts > 1 && (h->no_split || !split_stage_enabled(r.H))) return false;
+    if (r.chain && (h->keep_inter || !chain_enabled())) return false;  // no intermediates; FR_AB no_chain
     if (h->stage_mode == 1) {  // measured at this batch size (measure_stage)
         const int c = stage_choice(h, st, B);
         if (c >= 0) return c == 1;
@@ -1752,6 +1836,19 @@ static int run_conv_op(fr_handle* h, const Op& op, int B, int f16, hipStream_t s
 
 static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vector<char>& stage_run, hipStream_t s) {
     const StageRec& r = h->stages[op.stage];
+    if (r.chain) {
+        Chain17Args c{};
+        c.x = h->tensors[r.in].dev;
+        c.y = h->tensors[r.out].dev;
+        c.w = r.cw; c.bias = r.cbias; c.B = B; c.nblk = r.nblk; c.f16 = f16;
+        ProfScope ps(h, s);
+        // per block and pixel: 896 x 256 (branch1.0 + branch0) + 2 x 896 x 128 (1x7, 7x1) + 256 x 896 MACs
+        ps.flops = 2.0 * B * 64.0 * 688128.0 * r.nblk;
+        ps.bytes = 2.0 * 2.0 * B * 64.0 * 896.0 + 2.0 * 688128.0 * r.nblk;
+        ps.start("chain block17");
+        FR_HIP_CHECK(launch_chain17(c, s));
+        return FR_OK;
+    }
     if (r.trans) {
         TransArgs t{};
         t.x = h->tensors[r.in].dev;
@@ -2622,6 +2719,12 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
             const StageRec& r = h->stages[op.stage];
             out += "trans " + std::to_string(B * 3136) + " 64 2944 2944 1 1 3x3 " + h->tensors[r.out].name +
                    meas_note(h, op.grp, B) + "\n";
+            continue;
+        }
+        if (op.kind == OP_STAGE && h->stages[op.stage].chain) {  // M x 896 x (688128 / 896) MACs per block
+            const StageRec& r = h->stages[op.stage];
+            out += "chain " + std::to_string(B * 64) + " 896 768 768 " + std::to_string(4 * r.nblk) + " 1 1x1 " +
+                   h->tensors[r.out].name + meas_note(h, op.grp, B) + "\n";
             continue;
         }
         if (op.kind == OP_STAGE) {

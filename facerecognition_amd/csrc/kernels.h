@@ -176,6 +176,24 @@ bool trans_supported(int B, int H, int W, int Cin, int Cmid, int Cout, int K1, i
 size_t trans_packed_elems(int K);
 hipError_t trans_pack_weights(const bf16_t* w, int Kpad, int K, bf16_t* out, hipStream_t s);
 hipError_t launch_trans(const TransArgs& a, hipStream_t s);
+// FaceNet IRV1 repeat_2 (Block17 x nblk at 8x8x896) as one launch (conv_chain.hip): one workgroup per image, the
+// block input resident in LDS across all blocks; w = chain17_pack_block streams, bias = [nblk][A B C D (128 each)
+// | E (896)] f32 (the member convs' folded biases: branch1.0, 1x7, 7x1, branch0, conv2d).
+struct Chain17Args {
+    const bf16_t* x;      // [B][8][8][896] (mixed_6a)
+    bf16_t* y;            // [B][8][8][896] (the last block's output)
+    const bf16_t* w;
+    const float* bias;
+    int B, nblk, f16;
+    void* ev0;
+    void* ev1;
+};
+bool chain17_supported(int H, int W, int C, int nblk);
+size_t chain17_weight_elems(int nblk);
+size_t chain17_bias_floats(int nblk);
+void chain17_pack_block(const bf16_t* rA, int kpA, const bf16_t* r17, int kp17, const bf16_t* r71, int kp71,
+                        const bf16_t* rE, int kpE, int blk, int nblk, bf16_t* out);
+hipError_t launch_chain17(const Chain17Args& a, hipStream_t s);
 // Split-K reduction + the same fused epilogue as the conv kernel.
 hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
 // Number of K-tiles of 64 (for split-k planning).

@@ -1,0 +1,99 @@
+"""FaceNet IRV1 repeat_2 as one launch (conv_chain.hip: the ten Block17 with the block input resident in LDS, one
+workgroup per image) vs the plan's 40 member convs, and vs the fp32 oracle (reference: facenet_model.py:12-16 ->
+facenet_pytorch InceptionResnetV1.repeat_2).
+
+Both paths apply the same folded weights and round t1, t, b1, b0 and every block output to the storage format at
+the same points; only the f32 summation order differs (the chain accumulates conv2d onto bias + x), so the
+repeat_2 output agrees to rounding noise and the embeddings to the stage tests' bar."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from facerecognition_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+
+def _tensor(m, B, name):
+    L = N.lib()
+    for t in range(L.fr_debug_tensor_count(m.handle)):
+        if L.fr_debug_tensor_name(m.handle, t).decode() != name:
+            continue
+        dt = torch.float16 if L.fr_debug_tensor_dtype(m.handle, t) == N.FR_DTYPE_F16 else torch.bfloat16
+        H, W, C = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        N.check(L.fr_debug_tensor_shape(m.handle, t, ctypes.byref(H), ctypes.byref(W), ctypes.byref(C)))
+        buf = torch.empty((B, H.value, W.value, C.value), dtype=dt, device="cuda")
+        N.check(L.fr_debug_copy_tensor(m.handle, t, B, buf.data_ptr(), N.stream_ptr()))
+        torch.cuda.synchronize()
+        return buf.float().cpu()
+    raise KeyError(name)
+
+
+def _plan(m, B):
+    buf = ctypes.create_string_buffer(1 << 20)
+    N.check(N.lib().fr_debug_plan(m.handle, B, buf, len(buf)), "fr_debug_plan")
+    return buf.value.decode()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("B", [1, 3, 9])
+def test_chain_matches_member_convs(gpu, dtype, B):
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("irv1_facenet", dtype=dtype)
+    x = torch.from_numpy(synthetic_crops(B, 160, seed=13))
+    m.set_option(N.FR_OPT_STAGE, 2)  # the chain runs (auto would measure per batch size)
+    assert "chain " in _plan(m, B)
+    e_f = m.embed(x).cpu().numpy()
+    mid_f = _tensor(m, B, "model.mixed_6a")
+    y_f = _tensor(m, B, "model.repeat_2.9")
+    m.set_option(N.FR_OPT_STAGE, 0)
+    assert "chain " not in _plan(m, B)
+    e_c = m.embed(x).cpu().numpy()
+    mid_c = _tensor(m, B, "model.mixed_6a")
+    y_c = _tensor(m, B, "model.repeat_2.9")
+    m.close()
+    assert torch.equal(mid_f, mid_c), "the chain's input differs: the runs are not comparable"
+    rel = ((y_f - y_c).norm() / y_c.norm()).item()
+    # 50 roundings to 16 bits per element in both paths; a different f32 summation order flips a few of them
+    assert rel < (6e-3 if dtype == "bf16" else 8e-4), f"repeat_2: chain vs member convs rel err {rel:.3e}"
+    cos = np.sum(e_f * e_c, axis=1)
+    tol = 3e-4 if dtype == "bf16" else 5e-5
+    assert np.all(1 - cos <= tol), f"chain vs member-conv embeddings: 1-cos = {1 - cos}"
+    print(f"{dtype} B={B}: repeat_2 rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
+
+
+def test_chain_full_batch_against_oracle(gpu):
+    """bs = 256 (one image per CU), chain forced on: every sampled face within the 1e-3 cosine bar of the fp32
+    oracle, and the same planted top-1 as the oracle embedding."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    from facerecognition_amd.weights import synth_state_dict
+    from oracle import models as M
+    B = 256
+    m = FRModel.synthetic("irv1_facenet", max_batch=B)
+    m.set_option(N.FR_OPT_STAGE, 2)
+    u8 = synthetic_crops(B, 160, seed=23)
+    e = m.embed(torch.from_numpy(u8)).cpu().numpy()
+    assert "chain " in _plan(m, B)
+    m.close()
+    assert np.all(np.isfinite(e))
+    idx = np.arange(0, B, 32)  # an oracle sample (fp32 CPU forward)
+    ref = M.embed(M.build_model("irv1_facenet", synth_state_dict("irv1_facenet")), "irv1_facenet", u8[idx])
+    cos = np.sum(e[idx] * ref, axis=1) / (np.linalg.norm(e[idx], axis=1) * np.linalg.norm(ref, axis=1))
+    print(f"chain bs=256 vs oracle: max 1-cos {float((1 - cos).max()):.2e}")
+    assert np.all(1 - cos <= 1e-3), f"1-cos vs oracle {1 - cos}"
+
+
+def test_chain_graph_replay_repeatable(gpu):
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("irv1_facenet")
+    m.set_option(N.FR_OPT_STAGE, 2)
+    x = torch.from_numpy(synthetic_crops(6, 160, seed=7)).cuda()
+    outs = [m.embed(x).cpu().numpy() for _ in range(4)]
+    m.close()
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
