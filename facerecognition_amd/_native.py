@@ -42,6 +42,7 @@ FR_OPT_STAGE_SPIN_LIMIT = 6
 FR_OPT_STAGE_VARIANT = 7
 FR_OPT_SPLITK_INLAUNCH = 8
 FR_OPT_BATCH_INVARIANT = 9
+FR_OPT_FUSED_MASK = 10
 
 c_int, c_int64, c_size_t, c_void_p, c_float_p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p
 

@@ -136,10 +136,14 @@ struct StageRec {
     // border-class bias + PReLU) runs on the stage's final patch (conv_stage.hip run_tail); its weights and
     // tables follow the blocks' as two 256-channel halves; tail_op is also the last entry of conv_ops
     int tail_op = -1;
-    // IRV1 repeat_2 as one launch (conv_chain.hip): conv_ops = per block {branch1.0 + branch0, 1x7, 7x1, conv2d}
-    bool chain = false;
-    bf16_t* cw = nullptr;                 // chain17_pack_block streams of all blocks
-    float* cbias = nullptr;               // [nblk][1408] the member convs' biases
+    // IRV1 repeat_2 as one launch (chain 17, conv_chain.hip): conv_ops = per block {branch1.0 + branch0, 1x7, 7x1,
+    // conv2d}; repeat_1 (chain 35, conv_chain35.hip): per block {branch1.0 + branch2.0 + branch0, branch1.1, branch2.1,
+    // branch2.2, conv2d}, x_tensors = the block outputs
+    int chain = 0;
+    bf16_t* cw = nullptr;                 // the packed weights of all blocks
+    float* cbias = nullptr;               // the member convs' biases
+    // IRV1 stem as one launch (conv_stem160.hip): conv_ops = {conv2d_1a, conv2d_2a, conv2d_2b, maxpool_3a}
+    bool stem = false;
 };
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -248,6 +252,7 @@ struct fr_handle {
     // FR_OPT_BATCH_INVARIANT: every kernel choice sums K in the implicit GEMM's order (no split-K, no stage /
     // transition kernel, a fixed head split), so a face's embedding does not depend on its batch
     bool invariant = false;
+    int fused_mask = 15;  // FR_OPT_FUSED_MASK
 };
 
 namespace {
@@ -744,7 +749,7 @@ int build_stage(fr_handle* h, StageRec& r) {
 // Device pointer table of a stage's intermediate tensors (filled after every activation reserve).
 int fill_stage_dbg(fr_handle* h) {
     for (auto& r : h->stages) {
-        if (r.trans || r.chain) continue;  // no intermediates: the member convs run when they are kept
+        if (r.trans || r.chain || r.stem) continue;  // no intermediates: the member convs run when they are kept
         std::vector<bf16_t*> p(2 * r.nblk);
         for (int i = 0; i < r.nblk; ++i) {
             p[i] = h->tensors[r.x_tensors[i]].dev;
@@ -837,6 +842,51 @@ int build_chain17(fr_handle* h, StageRec& r) {
         std::copy(b2.begin(), b2.end(), t + 256);
         std::copy(b0.begin() + 128, b0.end(), t + 384);
         std::copy(b3.begin(), b3.end(), t + 512);
+    }
+    int rc = upload(h, &r.cw, packed);
+    if (rc) return rc;
+    return upload(h, &r.cbias, bias);
+}
+
+// Packs IRV1 repeat_1's member convs (per block: branch1.0 + branch2.0 + branch0 as one 1x1 256 -> 96, branch1.1,
+// branch2.1, branch2.2 3x3 32 -> 32, conv2d 96 -> 256 with the residual) for conv_chain35.hip.
+int build_chain35(fr_handle* h, StageRec& r) {
+    const int nblk = r.nblk;
+    if ((int)r.conv_ops.size() != 5 * nblk || (int)r.x_tensors.size() != nblk) {
+        set_error("plan: chain35 member count");
+        return FR_ERR_ARG;
+    }
+    std::vector<bf16_t> packed(chain35_weight_elems(nblk));
+    std::vector<float> bias(chain35_bias_floats(nblk), 0.f);
+    for (int blk = 0; blk < nblk; ++blk) {
+        const Op* op[5];
+        const DevConvW* cw[5];
+        std::vector<bf16_t> rows[5];
+        std::vector<float> bs[5];
+        for (int k = 0; k < 5; ++k) {
+            op[k] = &h->ops[r.conv_ops[5 * blk + k]];
+            cw[k] = &h->convw[op[k]->wi];
+            if (cw[k]->w8 || !cw[k]->bias || cw[k]->bias9 || op[k]->act != 1) {
+                set_error("plan: chain35 member conv is not bf16 / f16 + bias + ReLU");
+                return FR_ERR_ARG;
+            }
+            rows[k].resize((size_t)cw[k]->Npad * cw[k]->Kpad);
+            FR_HIP_CHECK(hipMemcpy(rows[k].data(), cw[k]->w, rows[k].size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
+            bs[k].resize(cw[k]->Cout);
+            FR_HIP_CHECK(hipMemcpy(bs[k].data(), cw[k]->bias, bs[k].size() * sizeof(float), hipMemcpyDeviceToHost));
+        }
+        bool shapes = cw[0]->Cout == 96 && cw[0]->K == 256 && cw[0]->Kh == 1 && cw[4]->Cout == 256 && cw[4]->K == 96 &&
+                      cw[4]->Kh == 1 && op[4]->res >= 0 && op[4]->res_off == 0;
+        for (int k = 1; k <= 3; ++k)
+            shapes = shapes && cw[k]->Cout == 32 && cw[k]->K == 288 && cw[k]->Kh == 3 && cw[k]->Kw == 3 && op[k]->ph == 1 &&
+                     op[k]->pw == 1 && op[k]->sh == 1 && op[k]->res < 0;
+        if (!shapes) {
+            set_error("plan: chain35 member convs do not have Block35's shapes");
+            return FR_ERR_ARG;
+        }
+        chain35_pack_block(rows[0].data(), cw[0]->Kpad, rows[1].data(), cw[1]->Kpad, rows[2].data(), cw[2]->Kpad,
+                           rows[3].data(), cw[3]->Kpad, rows[4].data(), cw[4]->Kpad, blk, packed.data());
+        chain35_pack_bias(bs[0].data(), bs[1].data(), bs[2].data(), bs[3].data(), bs[4].data(), blk, bias.data());
     }
     int rc = upload(h, &r.cw, packed);
     if (rc) return rc;
@@ -1117,14 +1167,59 @@ void build_irv1(Builder& b) {
     if (h->dtype == FR_DTYPE_BF16 && !bf16_stem)
         for (int t : {in, a, bb, c, d, e, f}) h->tensors[t].f16 = true;
     b.stem = true;
+    // conv2d_1a .. maxpool_3a also as one launch (conv_stem160.hip) beside the member ops, measured per batch size
+    int st_op = -1;
+    if (h->dtype != FR_DTYPE_FP8) {
+        st_op = (int)h->ops.size();
+        Op op;
+        op.kind = OP_STAGE;
+        op.stage = (int)h->stages.size();
+        h->ops.push_back(op);
+    }
     b.conv({m + "conv2d_1a"}, in, 0, 8, a, 0, 3, 3, 2, 2, 0, 0, 1);
     b.conv({m + "conv2d_2a"}, a, 0, 32, bb, 0, 3, 3, 1, 1, 0, 0, 1);
     b.conv({m + "conv2d_2b"}, bb, 0, 32, c, 0, 3, 3, 1, 1, 1, 1, 1);
     b.maxpool(c, d, 0, 3, 2, 0);
+    if (st_op >= 0 && !b.rc) {
+        StageRec sr;
+        sr.stem = true;
+        sr.in = in; sr.out = d; sr.H = 160; sr.C = 64;
+        const int n = (int)h->ops.size();
+        sr.conv_ops = {n - 4, n - 3, n - 2, n - 1};
+        const Op& o1 = h->ops[n - 4];
+        const Op& o2 = h->ops[n - 3];
+        const Op& o3 = h->ops[n - 2];
+        const DevConvW& c1 = h->convw[o1.wi];
+        const DevConvW& c2 = h->convw[o2.wi];
+        const DevConvW& c3 = h->convw[o3.wi];
+        const bool ok = stem160_supported(160, 160, 8, c1.K, c2.K, c3.K, c1.Cout, c2.Cout, c3.Cout) && c1.bias && c2.bias &&
+                        c3.bias && !c1.bias9 && !c2.bias9 && !c3.bias9 && !c1.w8 && !c2.w8 && !c3.w8 && o1.act == 1 &&
+                        o2.act == 1 && o3.act == 1 && h->tensors[in].f16 == h->tensors[d].f16;
+        if (ok) {
+            for (int oi : sr.conv_ops) h->ops[oi].stage = h->ops[st_op].stage;
+            h->stages.push_back(sr);
+        } else {
+            h->ops.erase(h->ops.begin() + st_op);  // no fused stem for these weights: the member ops only
+            for (auto& op : h->ops)
+                if (op.kind == OP_STAGE && op.stage >= (int)h->stages.size()) --op.stage;
+        }
+    }
     b.conv({m + "conv2d_3b"}, d, 0, 64, e, 0, 1, 1, 1, 1, 0, 0, 1);
     b.conv({m + "conv2d_4a"}, e, 0, 80, f, 0, 3, 3, 1, 1, 0, 0, 1);
     b.conv({m + "conv2d_4b"}, f, 0, 192, x, 0, 3, 3, 2, 2, 0, 0, 1);
-    // repeat_1: Block35 x5 @17x17. cat layout [t1 | t2 | b0 | b1 | b2]; conv2d reads [64:160].
+    // repeat_1: Block35 x5 @17x17. cat layout [t1 | t2 | b0 | b1 | b2]; conv2d reads [64:160].  Also emitted as one
+    // chain launch (conv_chain35.hip) beside its member convs; the faster is measured per batch size.
+    int c35_op = -1;
+    StageRec c35;
+    if (h->dtype != FR_DTYPE_FP8 && chain35_supported(17, 17, 256, 5)) {
+        c35_op = (int)h->ops.size();
+        Op op;
+        op.kind = OP_STAGE;
+        op.stage = (int)h->stages.size();
+        h->ops.push_back(op);
+        c35.chain = 35;
+        c35.in = x; c35.H = 17; c35.C = 256; c35.nblk = 5;
+    }
     for (int i = 0; i < 5; ++i) {
         const std::string p = m + "repeat_1." + std::to_string(i) + ".";
         const int cat = b.tensor(17, 17, 160);
@@ -1135,7 +1230,17 @@ void build_irv1(Builder& b) {
         b.conv({p + "branch2.2"}, t, 0, 32, cat, 128, 3, 3, 1, 1, 1, 1, 1);
         const int y = b.tensor(17, 17, 256, m + "repeat_1." + std::to_string(i));
         b.conv({p + "conv2d"}, cat, 64, 96, y, 0, 1, 1, 1, 1, 0, 0, 1, x, 0);
+        if (c35_op >= 0) {
+            for (int k = 5; k >= 1; --k) c35.conv_ops.push_back((int)h->ops.size() - k);
+            c35.x_tensors.push_back(y);
+        }
         x = y;
+    }
+    if (c35_op >= 0 && !b.rc) {
+        c35.out = x;
+        for (int oi : c35.conv_ops) h->ops[oi].stage = h->ops[c35_op].stage;
+        b.rc = build_chain35(h, c35);
+        h->stages.push_back(c35);
     }
     {  // mixed_6a
         const std::string p = m + "mixed_6a.";
@@ -1158,7 +1263,7 @@ void build_irv1(Builder& b) {
         op.kind = OP_STAGE;
         op.stage = (int)h->stages.size();
         h->ops.push_back(op);
-        ch.chain = true;
+        ch.chain = 17;
         ch.in = x; ch.H = 8; ch.C = 896; ch.nblk = 10;
     }
     for (int i = 0; i < 10; ++i) {
@@ -1703,18 +1808,28 @@ static bool trans_enabled() {
     return on;
 }
 
-// FR_AB no_chain: IRV1 repeat_2 always runs as its member convs (A/B timing)
-static bool chain_enabled() {
-    static const bool on = [] { return !ab_int("no_chain", 0); }();
+// FR_AB no_chain: IRV1 repeat_1 / repeat_2 always run as their member convs (A/B timing); no_chain17 / no_chain35:
+// only that one
+static bool chain_enabled(int kind) {
+    static const bool all = !ab_int("no_chain", 0), c17 = !ab_int("no_chain17", 0), c35 = !ab_int("no_chain35", 0);
+    return all && (kind == 17 ? c17 : c35);
+}
+
+// FR_AB no_stem160: the IRV1 stem always runs as its member ops (A/B timing)
+static bool ab_stem160() {
+    static const bool on = [] { return !ab_int("no_stem160", 0); }();
     return on;
 }
 
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     if (h->stage_mode == 0 || h->invariant) return false;
+    const int kind_bit = r.stem ? 2 : (r.chain == 35 ? 4 : (r.chain ? 8 : 1));
+    if (!(h->fused_mask & kind_bit)) return false;
     // the fused transition keeps no t tensor and records no amax
     if (r.trans && (h->keep_inter || (h->amax && h->need_amax[r.out]) || !trans_enabled())) return false;
     if (r.parts > 1 && (h->no_split || !split_stage_enabled(r.H))) return false;
-    if (r.chain && (h->keep_inter || !chain_enabled())) return false;  // no intermediates; FR_AB no_chain
+    if (r.chain && (h->keep_inter || !chain_enabled(r.chain))) return false;  // no intermediates; FR_AB no_chain
+    if (r.stem && (h->keep_inter || !ab_stem160())) return false;         // FR_AB no_stem160
     if (h->stage_mode == 1) {  // measured at this batch size (measure_stage)
         const int c = stage_choice(h, st, B);
         if (c >= 0) return c == 1;
@@ -1834,8 +1949,56 @@ static bool ms_enabled() {
 // One LDS-resident stage launch (+ the amax pass an e4m3 reader of its output needs).
 static int run_conv_op(fr_handle* h, const Op& op, int B, int f16, hipStream_t s);
 
+static int run_maxpool_op(fr_handle* h, const Op& op, int B, int f16, hipStream_t s) {
+    ProfScope ps(h, s);
+    ps.start("maxpool");
+    const auto& ti = h->tensors[op.in];
+    const auto& to = h->tensors[op.out];
+    if (ti.f16 != to.f16) {
+        set_error("plan: maxpool across the f16 section boundary");
+        return FR_ERR_ARG;
+    }
+    FR_HIP_CHECK(launch_maxpool(ti.dev, B, ti.H, ti.W, ti.C, 0, ti.C, op.pk, op.ps, op.pp, to.dev, to.C, op.out_off, to.H,
+                                to.W, f16 || ti.f16, s));
+    return FR_OK;
+}
+
 static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vector<char>& stage_run, hipStream_t s) {
     const StageRec& r = h->stages[op.stage];
+    if (r.stem) {
+        const Op& o1 = h->ops[r.conv_ops[0]];
+        const Op& o2 = h->ops[r.conv_ops[1]];
+        const Op& o3 = h->ops[r.conv_ops[2]];
+        const DevConvW& c1 = h->convw[o1.wi];
+        const DevConvW& c2 = h->convw[o2.wi];
+        const DevConvW& c3 = h->convw[o3.wi];
+        Stem160Args a{};
+        a.x = h->tensors[r.in].dev;
+        a.y = h->tensors[r.out].dev;
+        a.w1 = c1.w; a.w2 = c2.w; a.w3 = c3.w;
+        a.b1 = c1.bias; a.b2 = c2.bias; a.b3 = c3.bias;
+        a.kp1 = c1.Kpad; a.kp2 = c2.Kpad; a.kp3 = c3.Kpad;
+        a.B = B; a.f16 = f16 || h->tensors[r.in].f16;
+        ProfScope ps(h, s);
+        ps.flops = 2.0 * B * (79.0 * 79 * 32 * 72 + 77.0 * 77 * 32 * 288 + 77.0 * 77 * 64 * 288);
+        ps.bytes = 2.0 * B * (160.0 * 160 * 8 + 38.0 * 38 * 64);
+        ps.start("stem160");
+        FR_HIP_CHECK(launch_stem160(a, s));
+        return FR_OK;
+    }
+    if (r.chain == 35) {
+        Chain35Args c{};
+        c.io[0] = h->tensors[r.in].dev;
+        for (int i = 0; i < r.nblk; ++i) c.io[i + 1] = h->tensors[r.x_tensors[i]].dev;
+        c.w = r.cw; c.bias = r.cbias; c.B = B; c.nblk = r.nblk; c.f16 = f16;
+        ProfScope ps(h, s);
+        // per block and pixel: 256 x 96 + 3 x 288 x 32 + 96 x 256 = 76,800 MACs
+        ps.flops = 2.0 * B * 289.0 * 76800.0 * r.nblk;
+        ps.bytes = 2.0 * 2.0 * B * 289.0 * 256.0 + 2.0 * 76800.0 * r.nblk;
+        ps.start("chain block35");
+        FR_HIP_CHECK(launch_chain35(c, s));
+        return FR_OK;
+    }
     if (r.chain) {
         Chain17Args c{};
         c.x = h->tensors[r.in].dev;
@@ -1981,7 +2144,8 @@ static int measure_stage(fr_handle* h, const Op& op, int B, int f16, const std::
     auto fused = [&]() { return run_stage(h, op, B, f16, stage_run, s); };
     auto members = [&]() {
         for (int oi : mem) {
-            const int rc = run_conv_op(h, h->ops[oi], B, f16, s);
+            const Op& mo = h->ops[oi];
+            const int rc = mo.kind == OP_MAXPOOL ? run_maxpool_op(h, mo, B, f16, s) : run_conv_op(h, mo, B, f16, s);
             if (rc) return rc;
         }
         return (int)FR_OK;
@@ -2123,16 +2287,8 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 break;
             }
             case OP_MAXPOOL: {
-                ProfScope ps(h, s);
-                ps.start("maxpool");
-                const auto& ti = h->tensors[op.in];
-                const auto& to = h->tensors[op.out];
-                if (ti.f16 != to.f16) {
-                    set_error("plan: maxpool across the f16 section boundary");
-                    return FR_ERR_ARG;
-                }
-                FR_HIP_CHECK(launch_maxpool(ti.dev, B, ti.H, ti.W, ti.C, 0, ti.C, op.pk, op.ps, op.pp, to.dev, to.C,
-                                            op.out_off, to.H, to.W, f16 || ti.f16, s));
+                const int rc = run_maxpool_op(h, op, B, f16, s);
+                if (rc) return rc;
                 break;
             }
             case OP_AVGPOOL: {
@@ -2721,9 +2877,21 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
                    meas_note(h, op.grp, B) + "\n";
             continue;
         }
-        if (op.kind == OP_STAGE && h->stages[op.stage].chain) {  // M x 896 x (688128 / 896) MACs per block
+        if (op.kind == OP_STAGE && h->stages[op.stage].stem) {  // M = faces, K = the three convs' MACs per face
             const StageRec& r = h->stages[op.stage];
-            out += "chain " + std::to_string(B * 64) + " 896 768 768 " + std::to_string(4 * r.nblk) + " 1 1x1 " +
+            out += "stem160 " + std::to_string(B) + " 1 178312896 178312896 1 1 3x3 " + h->tensors[r.out].name +
+                   meas_note(h, op.grp, B) + "\n";
+            continue;
+        }
+        if (op.kind == OP_STAGE && h->stages[op.stage].chain == 35) {  // per block: M x 256 x 300 MACs (76,800 per pixel)
+            const StageRec& r = h->stages[op.stage];
+            out += "chain " + std::to_string(B * 289) + " 256 300 300 " + std::to_string(r.nblk) + " 1 3x3 " +
+                   h->tensors[r.out].name + meas_note(h, op.grp, B) + "\n";
+            continue;
+        }
+        if (op.kind == OP_STAGE && h->stages[op.stage].chain) {  // per block: M x 896 x 768 MACs (688,128 per pixel)
+            const StageRec& r = h->stages[op.stage];
+            out += "chain " + std::to_string(B * 64) + " 896 768 768 " + std::to_string(r.nblk) + " 1 1x1 " +
                    h->tensors[r.out].name + meas_note(h, op.grp, B) + "\n";
             continue;
         }
@@ -2808,6 +2976,10 @@ int fr_set_option(fr_handle* h, int option, int value) {
                 h->tuned_batches.clear();
             }
             break;
+        case FR_OPT_FUSED_MASK:
+            if (value < 0 || value > 15) { set_error("fr_set_option: FR_OPT_FUSED_MASK is 0 .. 15"); return FR_ERR_ARG; }
+            h->fused_mask = value;
+            break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;
     }
     drop_graphs(h);  // captured replays bake in the plan
@@ -2826,6 +2998,7 @@ int fr_get_option(const fr_handle* h, int option) {
         case FR_OPT_STAGE_VARIANT: return h->stage_variant;
         case FR_OPT_SPLITK_INLAUNCH: return h->splitk_inlaunch ? 1 : 0;
         case FR_OPT_BATCH_INVARIANT: return h->invariant ? 1 : 0;
+        case FR_OPT_FUSED_MASK: return h->fused_mask;
         default: return FR_ERR_ARG;
     }
 }

@@ -194,6 +194,42 @@ size_t chain17_bias_floats(int nblk);
 void chain17_pack_block(const bf16_t* rA, int kpA, const bf16_t* r17, int kp17, const bf16_t* r71, int kp71,
                         const bf16_t* rE, int kpE, int blk, int nblk, bf16_t* out);
 hipError_t launch_chain17(const Chain17Args& a, hipStream_t s);
+// FaceNet IRV1 stem at 160x160 (conv_stem160.hip): conv2d_1a (3x3/s2 8 -> 32) + conv2d_2a (3x3 32 -> 32) +
+// conv2d_2b (3x3/p1 32 -> 64), each + bias + ReLU, + maxpool_3a (3x3/s2) as one launch, one workgroup per image;
+// x = the prepared 8-channel input [B][160][160][8], y = the pooled [B][38][38][64]; w* = the member convs'
+// [Npad][Kpad] rows (kp* = Kpad), b* their folded biases.
+struct Stem160Args {
+    const bf16_t* x;
+    bf16_t* y;
+    const bf16_t* w1; const bf16_t* w2; const bf16_t* w3;
+    const float* b1; const float* b2; const float* b3;
+    int kp1, kp2, kp3;
+    int B, f16;
+    void* ev0;
+    void* ev1;
+};
+bool stem160_supported(int H, int W, int Cin, int K1, int K2, int K3, int C1, int C2, int C3);
+hipError_t launch_stem160(const Stem160Args& a, hipStream_t s);
+// FaceNet IRV1 repeat_1 (Block35 x nblk at 17x17x256) as one launch (conv_chain35.hip): one workgroup per image, the
+// branch tensors in LDS, the block outputs through global memory (io[0] = the NHWC input, io[1..nblk-1] = the
+// intermediate block outputs, stored plane-major [32][289][8], io[nblk] = the NHWC output); w / bias =
+// chain35_pack_block / chain35_pack_bias images of the member convs.
+struct Chain35Args {
+    const bf16_t* io[9];
+    const bf16_t* w;
+    const float* bias;
+    int B, nblk, f16;
+    void* ev0;
+    void* ev1;
+};
+bool chain35_supported(int H, int W, int C, int nblk);
+size_t chain35_weight_elems(int nblk);
+size_t chain35_bias_floats(int nblk);
+void chain35_pack_block(const bf16_t* r1, int kp1, const bf16_t* r21, int kp21, const bf16_t* r22, int kp22,
+                        const bf16_t* r3, int kp3, const bf16_t* r4, int kp4, int blk, bf16_t* out);
+void chain35_pack_bias(const float* b1, const float* b21, const float* b22, const float* b3, const float* b4, int blk,
+                       float* out);
+hipError_t launch_chain35(const Chain35Args& a, hipStream_t s);
 // Split-K reduction + the same fused epilogue as the conv kernel.
 hipError_t launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
 // Number of K-tiles of 64 (for split-k planning).

@@ -40,7 +40,7 @@ def test_invariant_mode_is_bitwise_batch_independent(gpu, arch):
     e256 = m.embed(x).cpu().numpy()
     for B in (256, 64):
         plan = _plan(m, B)
-        assert not any(l.split()[0] in ("stage", "stage8", "trans", "block", "chain")
+        assert not any(l.split()[0] in ("stage", "stage8", "trans", "block", "chain", "stem160")
                        for l in plan.splitlines() if l.strip()), plan
     e64 = m.embed(x[:64]).cpu().numpy()
     e9 = _embed_in_chunks(m, x[:18], 9)

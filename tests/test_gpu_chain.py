@@ -45,6 +45,7 @@ def test_chain_matches_member_convs(gpu, dtype, B):
     m = FRModel.synthetic("irv1_facenet", dtype=dtype)
     x = torch.from_numpy(synthetic_crops(B, 160, seed=13))
     m.set_option(N.FR_OPT_STAGE, 2)  # the chain runs (auto would measure per batch size)
+    m.set_option(N.FR_OPT_FUSED_MASK, 8)  # ... and no other fused kernel before it
     assert "chain " in _plan(m, B)
     e_f = m.embed(x).cpu().numpy()
     mid_f = _tensor(m, B, "model.mixed_6a")
@@ -56,13 +57,14 @@ def test_chain_matches_member_convs(gpu, dtype, B):
     y_c = _tensor(m, B, "model.repeat_2.9")
     m.close()
     assert torch.equal(mid_f, mid_c), "the chain's input differs: the runs are not comparable"
+    rel_in = 0.0
     rel = ((y_f - y_c).norm() / y_c.norm()).item()
     # 50 roundings to 16 bits per element in both paths; a different f32 summation order flips a few of them
     assert rel < (6e-3 if dtype == "bf16" else 8e-4), f"repeat_2: chain vs member convs rel err {rel:.3e}"
     cos = np.sum(e_f * e_c, axis=1)
     tol = 3e-4 if dtype == "bf16" else 5e-5
     assert np.all(1 - cos <= tol), f"chain vs member-conv embeddings: 1-cos = {1 - cos}"
-    print(f"{dtype} B={B}: repeat_2 rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
+    print(f"{dtype} B={B}: mixed_6a rel {rel_in:.2e}, repeat_2 rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
 
 
 def test_chain_full_batch_against_oracle(gpu):
@@ -97,3 +99,62 @@ def test_chain_graph_replay_repeatable(gpu):
     m.close()
     for o in outs[1:]:
         assert np.array_equal(o, outs[0])
+
+
+# ---- the IRV1 stem as one launch (conv_stem160.hip: conv2d_1a .. maxpool_3a, row rings in LDS)
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("B", [1, 3, 9])
+def test_stem160_matches_member_ops(gpu, dtype, B):
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("irv1_facenet", dtype=dtype)
+    x = torch.from_numpy(synthetic_crops(B, 160, seed=17))
+    m.set_option(N.FR_OPT_STAGE, 2)
+    m.set_option(N.FR_OPT_FUSED_MASK, 2)
+    assert "stem160 " in _plan(m, B)
+    e_f = m.embed(x).cpu().numpy()
+    y_f = _tensor(m, B, "model.maxpool_3a")
+    m.set_option(N.FR_OPT_STAGE, 0)
+    assert "stem160 " not in _plan(m, B)
+    e_c = m.embed(x).cpu().numpy()
+    y_c = _tensor(m, B, "model.maxpool_3a")
+    m.close()
+    rel = ((y_f - y_c).norm() / y_c.norm()).item()
+    # the stem is f16 in both plans (engine.cpp build_irv1): 3 roundings per element, f32 order differences only
+    cos = np.sum(e_f * e_c, axis=1)
+    print(f"{dtype} B={B}: maxpool_3a rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
+    # measured 4-5e-5: a few f16 rounding flips from the different f32 summation order
+    assert rel < 2e-4, f"maxpool_3a: fused vs member ops rel err {rel:.3e}"
+    # the bf16 body amplifies a 5e-5 perturbation at the stem ~15x by the embedding (the f16 plan does not: 1e-5), the
+    # fragility DESIGN.md §5 measures against the oracle; the bf16 bound here is the north star's 1e-3
+    tol = 1e-3 if dtype == "bf16" else 5e-5
+    assert np.all(1 - cos <= tol), f"fused stem vs member-op embeddings: 1-cos = {1 - cos}"
+
+
+# ---- repeat_1 as one launch (conv_chain35.hip: five Block35, branch tensors in LDS, block outputs through global)
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("B", [1, 3, 9])
+def test_chain35_matches_member_convs(gpu, dtype, B):
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("irv1_facenet", dtype=dtype)
+    x = torch.from_numpy(synthetic_crops(B, 160, seed=19))
+    m.set_option(N.FR_OPT_STAGE, 2)
+    m.set_option(N.FR_OPT_FUSED_MASK, 4)
+    assert " 256 300 300 5 " in _plan(m, B)
+    e_f = m.embed(x).cpu().numpy()
+    in_f = _tensor(m, B, "model.conv2d_4b")
+    y_f = _tensor(m, B, "model.repeat_1.4")
+    m.set_option(N.FR_OPT_STAGE, 0)
+    e_c = m.embed(x).cpu().numpy()
+    in_c = _tensor(m, B, "model.conv2d_4b")
+    y_c = _tensor(m, B, "model.repeat_1.4")
+    m.close()
+    assert torch.equal(in_f, in_c), "the chain's input differs: the runs are not comparable"
+    rel = ((y_f - y_c).norm() / y_c.norm()).item()
+    cos = np.sum(e_f * e_c, axis=1)
+    print(f"{dtype} B={B}: repeat_1 rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
+    assert rel < (6e-3 if dtype == "bf16" else 1.5e-3), f"repeat_1: chain vs member convs rel err {rel:.3e}"
+    # rounding-level differences at repeat_1 are amplified by the bf16 body after it (see the stem test)
+    tol = 1e-3 if dtype == "bf16" else 5e-5
+    assert np.all(1 - cos <= tol), f"chain35 vs member-conv embeddings: 1-cos = {1 - cos}"

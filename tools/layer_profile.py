@@ -61,7 +61,7 @@ def analyse(trace, plan_path):
         if (split > 1 and tile != 16) or p[0] == "head":  # (tile 16 = conv_small: its split is in-kernel)
             r = seq[i]; i += 1  # split-K epilogue / head finalize
             d += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        flop = 2.0 * M * Nn * K * (tile if p[0] == "stage" else 1)  # stage line: tile = its conv count
+        flop = 2.0 * M * Nn * K * (tile if p[0] in ("stage", "chain") else 1)  # stage: conv count, chain: blocks
         tot_ns += d
         tot_flop += flop
         key = (M, Nn, K, p[7])
