@@ -5,8 +5,8 @@
 // could use (0.38 ms at bs = 256 for 57 GFLOP, profiles/r05_irv1_layer_profile.txt).  Here one workgroup owns one
 // image for all five blocks; the 32-channel branch tensors live in LDS, the 256-channel block input / output goes
 // through global memory (148 KB per image does not fit beside them):
-//   P1  [t1 | t2 | b0] = relu(W [b1.0 | b2.0 | b0] x + b)   K 256 (8 K-steps, x staged per K-step into LDS by
-//       LDS-DMA, double-buffered), N 96
+//   P1  [t1 | t2 | b0] = relu(W [b1.0 | b2.0 | b0] x + b)   K 256 (8 K-steps, x fragments from global memory two
+//       K-steps ahead in registers), N 96
 //   P2  b1 = relu(3x3(t1) + b), t = relu(3x3(t2) + b)         K 9 taps x 32, two convs side by side
 //   P3  b2 = relu(3x3(t) + b)                                  K 9 x 32
 //   P4  y = relu(W' [b0 | b1 | b2] + b' + x)                   K 96, N 256 in two halves (W', b' carry the 0.17)
@@ -15,7 +15,7 @@
 //   so every tap is a uniform shift of the lane's position; b2 reuses t1's buffer;
 // * 8 waves: px-group (w & 3) = five 16-pixel fragments (20 fragments: 289 pixels + 31 discarded), and the upper
 //   bit picks the n-fragments: P1 3 of 6, P2 the conv, P3 one of 2, P4 4 of 8 per half; weight fragments come
-//   straight from global memory (L1 / L2: 150 KB per block), one K-step ahead;
+//   straight from global memory (L1 / L2: 150 KB per block), ahead of their pass;
 // * the block outputs between blocks are stored plane-major in global memory ([32 planes][289 pixels][16 B]:
 //   coalesced 16-B staging / stores); the chain input (conv2d_4b) and output (repeat_1.4, read by mixed_6a) are NHWC;
 // * the same rounding points as the per-conv path (t1, t2, b0, b1, t, b2 and every block output in the storage
@@ -40,12 +40,10 @@ constexpr int T2_OFF = T1_OFF + TP_B;
 constexpr int T_OFF = T2_OFF + TP_B;
 constexpr int B0_OFF = T_OFF + TP_B;       // 76800
 constexpr int B1_OFF = B0_OFF + TU_B;
-constexpr int XS_OFF = B1_OFF + TU_B;      // 117760: x staging, 2 slots
-constexpr int C35_LDS = XS_OFF + 2 * TU_B; // 158720
+constexpr int C35_LDS = B1_OFF + TU_B;     // 117760
 static_assert(C35_LDS <= 163840, "lds");
 static_assert(PW * PW <= PPL / 16 && PPL % 256 == 0, "padded plane");
 constexpr int NWV = 8;
-constexpr uint32_t OOB = 0x80000000u;
 
 // per-block packed weights: W1 [96][256] | W21 [32][288] | W22 [32][288] | W3 [32][288] | W4 [256][96]
 constexpr int W1_E = 96 * 256, W2_E = 32 * 288, W4_E = 256 * 96;
@@ -53,17 +51,6 @@ constexpr int W21_O = W1_E, W22_O = W21_O + W2_E, W3_O = W22_O + W2_E, W4_O = W3
 constexpr int WBLK = W4_O + W4_E;          // 76,800 elements per block
 // per-block biases: 96 | 32 | 32 | 32 | 256
 constexpr int BB2A = 96, BB2B = 128, BB3 = 160, BB4 = 192, BBLK = 448;
-
-typedef int v4i32 __attribute__((ext_vector_type(4)));
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void dma16(const v4i32& rsrc, uint32_t lds_addr, uint32_t voff) {
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
-                 :
-                 : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
-                 : "memory", "m0");
-}
-#pragma clang diagnostic pop
 
 __device__ __forceinline__ int fresh_lane() {
     int l;
@@ -99,7 +86,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
 
     f32x4_t acc[5][5];
     const size_t img = (size_t)b * NPX * 256;
-    const uint32_t img_b = (uint32_t)(NPX * 256 * 2);
 
 #pragma unroll 1
     for (int blk = 0; blk < p.nblk; ++blk) {
@@ -108,55 +94,121 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
         const bool in_planar = blk > 0, out_planar = blk + 1 < p.nblk;
         const bf16_t* W = p.w + (size_t)blk * WBLK;
         const float* BI = p.bias + (size_t)blk * BBLK;
-        const uint64_t xp = (uint64_t)(xin + img);
-        const v4i32 xr = {(int)(uint32_t)xp, (int)((xp >> 32) & 0xffff), (int)img_b, 0x00020000};
-        // x staging of K-step s (channels 32 s .. 32 s + 31 = x planes 4 s .. 4 s + 3) into slot s & 1: 20 pieces
-        // of 64 pixel slots (slots >= 289 read zeros)
-        auto stage = [&](int s) {
-            const int ln = fresh_lane();
-            for (int u = wave; u < 20; u += NWV) {
-                const int pl = u / 5, q = 64 * (u % 5) + ln, cg = 4 * s + pl;
-                const uint32_t off = q >= NPX ? OOB
-                                              : (in_planar ? (uint32_t)((cg * NPX + q) * 16) : (uint32_t)((q * 256 + cg * 8) * 2));
-                dma16(xr, (uint32_t)(uintptr_t)(smem + XS_OFF + (s & 1) * TU_B + pl * UPL + (u % 5) * 1024), off);
+        // 3x3 over a padded 32-channel tensor: NF n-fragments (weights wt, loaded a pass ahead), the wave's five pixel
+        // fragments
+        auto conv3 = [&](auto nf_tag, int src_off, const frag (&wt)[9][2]) {
+            constexpr int NF = decltype(nf_tag)::value;
+            const int ln = fresh_lane(), l15 = ln & 15, lg = ln >> 4;
+            int pos[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) pos[j] = src_off + lg * PPL + ppos(16 * (5 * pg + j) + l15) * 16;
+            frag bq[2][5];
+            auto rd = [&](int t, frag (&q)[5]) {
+                const int sh = ((t / 3 - 1) * PW + (t % 3 - 1)) * 16;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) q[j] = *(const frag*)(smem + pos[j] + sh);
+            };
+            rd(0, bq[0]);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (t + 1 < 9) rd(t + 1, bq[(t + 1) & 1]);
+#pragma unroll
+                for (int i = 0; i < NF; ++i)
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) acc[i][j] = T::mfma(wt[t][i], bq[t & 1][j], acc[i][j]);
             }
         };
-        stage(0);
+        auto relu_store = [&](int NF, int dst_off, bool padded, int n0) {
+            const int ln = fresh_lane(), l15 = ln & 15, lg = ln >> 4;
+            for (int i = 0; i < NF; ++i) {
+                const int pl = 2 * (n0 + i) + (lg >> 1);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int px = 16 * (5 * pg + j) + l15;
+                    if (px < NPX) {
+                        const int a = dst_off + (padded ? pl * PPL + ppos(px) * 16 : pl * UPL + px * 16) + (lg & 1) * 8;
+                        *(uint2*)(smem + a) = pack4<F16>(fmaxf(acc[i][j][0], 0.f), fmaxf(acc[i][j][1], 0.f),
+                                                         fmaxf(acc[i][j][2], 0.f), fmaxf(acc[i][j][3], 0.f));
+                    }
+                }
+            }
+        };
+        // 3x3 weights of NF n-fragments (n0 ..) of a [32][288] image: lane (lg, l15) of (tap t, i) = row 16 (n0 + i) + l15,
+        // K 32 t + 8 lg
+        auto load3 = [&](frag (&wt)[9][2], const bf16_t* wc, int n0, int NF) {
+            const int ln = fresh_lane(), l15 = ln & 15, lg = ln >> 4;
+            const bf16_t* wl = wc + (size_t)(16 * n0 + l15) * 288 + 8 * lg;
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+                for (int i = 0; i < NF; ++i) wt[t][i] = *(const frag*)(wl + (size_t)16 * 288 * i + 32 * t);
+        };
+        // P4 half h: the weights of its 4 n-fragments and the residual x at the lane's channels / pixels
+        frag w4[3][4];
+        uint2 rx[4][5];
+        auto load4 = [&](int h) {
+            const int ln = fresh_lane(), l15 = ln & 15, lg = ln >> 4;
+            const int n0 = 8 * h + 4 * hi;
+            const bf16_t* wl = W + W4_O + (size_t)(16 * n0 + l15) * 96 + 8 * lg;
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w4[s][i] = *(const frag*)(wl + (size_t)16 * 96 * i + 32 * s);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int n = 16 * (n0 + i) + 4 * lg;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int px = min(16 * (5 * pg + j) + l15, NPX - 1);
+                    const size_t o = in_planar ? (size_t)((n >> 3) * NPX + px) * 8 + (n & 7) : (size_t)px * 256 + n;
+                    rx[i][j] = *(const uint2*)(xin + img + o);
+                }
+            }
+        };
 
-        // ---------------- P1: [t1 | t2 | b0] = relu(W1 x + b), n-fragments 3 hi .. 3 hi + 2
+        frag wt[9][2];
+
+        // ---------------- P1: [t1 | t2 | b0] = relu(W1 x + b), n-fragments 3 hi .. 3 hi + 2.  The x fragments come
+        // straight from global memory (16 pixels of one 8-channel plane: 256 contiguous bytes in the plane-major
+        // layout) two K-steps ahead in registers, like the weights; no LDS staging and no barrier in the K loop
         {
             const int ln = fresh_lane(), l15 = ln & 15, lg = ln >> 4;
             float4 bs[3];
 #pragma unroll
             for (int i = 0; i < 3; ++i) bs[i] = *(const float4*)(BI + 16 * (3 * hi + i) + 4 * lg);
+            const bf16_t* wl = W + (size_t)(16 * 3 * hi + l15) * 256 + 8 * lg;  // row 16 nf + l15, K 32 s + 8 lg
+            // element offset of the lane's x fragment j at K-step 0 (plane lg); + 4 planes per K-step
+            int xo[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int px = min(16 * (5 * pg + j) + l15, NPX - 1);  // discarded pixels re-read pixel 288
+                xo[j] = in_planar ? (lg * NPX + px) * 8 : px * 256 + lg * 8;
+            }
+            const int xstep = in_planar ? 4 * NPX * 8 : 32;
+            const bf16_t* xi = xin + img;
+            frag wq[3][3], xq[3][5];
+            auto ld = [&](int s, int slot) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) wq[slot][i] = *(const frag*)(wl + (size_t)16 * 256 * i + 32 * s);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) xq[slot][j] = *(const frag*)(xi + xo[j] + s * xstep);
+            };
+            ld(0, 0);
+            ld(1, 1);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t){bs[i].x, bs[i].y, bs[i].z, bs[i].w};
-            const bf16_t* wl = W + (size_t)(16 * 3 * hi + l15) * 256 + 8 * lg;  // row 16 nf + l15, K 32 s + 8 lg
-            frag wf[2][3];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) wf[0][i] = *(const frag*)(wl + (size_t)16 * 256 * i);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // K-step 0's x slot landed (every wave's pieces)
-            const int xb = XS_OFF + lg * UPL + (16 * 5 * pg + l15) * 16;
-#pragma unroll 1
             for (int s = 0; s < 8; ++s) {
-                if (s + 1 < 8) stage(s + 1);
-                frag wn[3];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) wn[i] = *(const frag*)(wl + (size_t)16 * 256 * i + 32 * (s + 1 < 8 ? s + 1 : s));
-                frag bq[5];
-#pragma unroll
-                for (int j = 0; j < 5; ++j) bq[j] = *(const frag*)(smem + xb + (s & 1) * TU_B + j * 256);
+                __builtin_amdgcn_sched_barrier(0);
+                if (s + 2 < 8) ld(s + 2, (s + 2) % 3);
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
 #pragma unroll
-                    for (int j = 0; j < 5; ++j) acc[i][j] = T::mfma(wf[0][i], bq[j], acc[i][j]);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) wf[0][i] = wn[i];
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                    for (int j = 0; j < 5; ++j) acc[i][j] = T::mfma(wq[s % 3][i], xq[s % 3][j], acc[i][j]);
             }
+            load3(wt, W + (hi ? W22_O : W21_O), 0, 2);  // P2's weights, in flight during this epilogue and barrier
             // epilogue: n-fragment 3 hi + i -> t1 (0, 1: padded), t2 (2, 3: padded), b0 (4, 5)
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
@@ -175,54 +227,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
 
-        // 3x3 over a padded 32-channel tensor: NF n-fragments (n0 ..), the wave's five pixel fragments
-        auto conv3 = [&](auto nf_tag, int src_off, const bf16_t* wc, int n0) {
-            constexpr int NF = decltype(nf_tag)::value;
-            const int ln = fresh_lane(), l15 = ln & 15, lg = ln >> 4;
-            int pos[5];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) pos[j] = src_off + lg * PPL + ppos(16 * (5 * pg + j) + l15) * 16;
-            const bf16_t* wl = wc + (size_t)(16 * n0 + l15) * 288 + 8 * lg;
-            frag wf[2][NF];
-#pragma unroll
-            for (int i = 0; i < NF; ++i) wf[0][i] = *(const frag*)(wl + (size_t)16 * 288 * i);
-            frag bq[2][5];
-            auto rd = [&](int t, frag (&q)[5]) {
-                const int sh = ((t / 3 - 1) * PW + (t % 3 - 1)) * 16;
-#pragma unroll
-                for (int j = 0; j < 5; ++j) q[j] = *(const frag*)(smem + pos[j] + sh);
-            };
-            rd(0, bq[0]);
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                __builtin_amdgcn_sched_barrier(0);
-                if (t + 1 < 9) {
-                    rd(t + 1, bq[(t + 1) & 1]);
-#pragma unroll
-                    for (int i = 0; i < NF; ++i) wf[(t + 1) & 1][i] = *(const frag*)(wl + (size_t)16 * 288 * i + 32 * (t + 1));
-                }
-#pragma unroll
-                for (int i = 0; i < NF; ++i)
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) acc[i][j] = T::mfma(wf[t & 1][i], bq[t & 1][j], acc[i][j]);
-            }
-        };
-        auto relu_store = [&](int NF, int dst_off, bool padded, int n0) {
-            const int ln = fresh_lane(), l15 = ln & 15, lg = ln >> 4;
-            for (int i = 0; i < NF; ++i) {
-                const int pl = 2 * (n0 + i) + (lg >> 1);
-#pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    const int px = 16 * (5 * pg + j) + l15;
-                    if (px < NPX) {
-                        const int a = dst_off + (padded ? pl * PPL + ppos(px) * 16 : pl * UPL + px * 16) + (lg & 1) * 8;
-                        *(uint2*)(smem + a) = pack4<F16>(fmaxf(acc[i][j][0], 0.f), fmaxf(acc[i][j][1], 0.f),
-                                                         fmaxf(acc[i][j][2], 0.f), fmaxf(acc[i][j][3], 0.f));
-                    }
-                }
-            }
-        };
-
         // ---------------- P2: b1 = relu(3x3 t1), t = relu(3x3 t2) -- waves 0-3 the first, 4-7 the second
         {
             const int ln = fresh_lane(), lg = ln >> 4;
@@ -233,7 +237,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
 #pragma unroll
                 for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t){v.x, v.y, v.z, v.w};
             }
-            conv3(std::integral_constant<int, 2>{}, hi ? T2_OFF : T1_OFF, W + (hi ? W22_O : W21_O), 0);
+            conv3(std::integral_constant<int, 2>{}, hi ? T2_OFF : T1_OFF, wt);
+            load3(wt, W + W3_O, hi, 1);  // P3's weights, in flight during this epilogue and barrier
             if (hi) relu_store(2, T_OFF, true, 0);
             else relu_store(2, B1_OFF, false, 0);
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -244,36 +249,30 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
             const float4 v = *(const float4*)(BI + BB3 + 16 * hi + 4 * lg);
 #pragma unroll
             for (int j = 0; j < 5; ++j) acc[0][j] = (f32x4_t){v.x, v.y, v.z, v.w};
-            conv3(std::integral_constant<int, 1>{}, T_OFF, W + W3_O, hi);
+            conv3(std::integral_constant<int, 1>{}, T_OFF, wt);
+            load4(0);
             relu_store(1, T1_OFF, true, hi);
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
         // ---------------- P4: y = relu(W4 [b0 | b1 | b2] + b + x), two halves of 128 channels, 4 n-fragments per wave
-#pragma unroll 1
+#pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int ln = fresh_lane(), l15 = ln & 15, lg = ln >> 4;
             const int n0 = 8 * h + 4 * hi;
             // seeds: bias + the residual x at the lane's 4 channels of each of its pixels
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int n = 16 * (n0 + i) + 4 * lg;
-                const float4 v = *(const float4*)(BI + BB4 + n);
+                const float4 v = *(const float4*)(BI + BB4 + 16 * (n0 + i) + 4 * lg);
 #pragma unroll
                 for (int j = 0; j < 5; ++j) {
-                    const int px = min(16 * (5 * pg + j) + l15, NPX - 1);
-                    const size_t o = in_planar ? (size_t)((n >> 3) * NPX + px) * 8 + (n & 7) : (size_t)px * 256 + n;
-                    const uint2 xv = *(const uint2*)(xin + img + o);
                     float f[8];
-                    T::unpack8(make_uint4(xv.x, xv.y, 0, 0), f);
+                    T::unpack8(make_uint4(rx[i][j].x, rx[i][j].y, 0, 0), f);
                     acc[i][j] = (f32x4_t){v.x + f[0], v.y + f[1], v.z + f[2], v.w + f[3]};
                 }
             }
-            const bf16_t* wl = W + W4_O + (size_t)(16 * n0 + l15) * 96 + 8 * lg;
 #pragma unroll
             for (int s = 0; s < 3; ++s) {
-                frag wf[4], bq[5];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) wf[i] = *(const frag*)(wl + (size_t)16 * 96 * i + 32 * s);
+                frag bq[5];
 #pragma unroll
                 for (int j = 0; j < 5; ++j) {
                     const int px = 16 * (5 * pg + j) + l15;
@@ -284,8 +283,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 5; ++j) acc[i][j] = T::mfma(wf[i], bq[j], acc[i][j]);
+                    for (int j = 0; j < 5; ++j) acc[i][j] = T::mfma(w4[s][i], bq[j], acc[i][j]);
             }
+            if (h == 0) load4(1);  // the second half's weights and residual, in flight during these stores
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int n = 16 * (n0 + i) + 4 * lg;

@@ -229,7 +229,9 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
             const int r = s - 5;
             if (r >= 0) {
                 for (int it = threadIdx.x; it < WP * 8; it += 256) {
-                    const int oc = it >> 3, pl = it & 7;
+                    // lanes walk the output columns of one plane: their 16-B reads are 32 B apart (2-way bank sharing);
+                    // walking the planes of one column put 8 lanes on the same banks
+                    const int pl = it / WP, oc = it - pl * WP;
                     float m[8];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
