@@ -243,8 +243,9 @@ hipError_t launch_preprocess(const void* in, int in_fmt, int B, int H, int W, bf
 bool stem_u8_supported(int H, int W, int Cin, int K, int Kpad, int Cout, int Cy, int y_off);
 hipError_t launch_stem_u8(const uint8_t* in, int B, const bf16_t* w, int Kpad, const float* bias, const float* slope,
                           int act, bf16_t* y, int Cy, int y_off, int f16, hipStream_t s);
+// y_bf16: f16 input, bf16 output (3x3 only: the end of an f16 plan section)
 hipError_t launch_maxpool(const bf16_t* x, int B, int H, int W, int Cx, int x_off, int C, int k, int stride,
-                          int pad, bf16_t* y, int Cy, int y_off, int Ho, int Wo, int f16, hipStream_t s);
+                          int pad, bf16_t* y, int Cy, int y_off, int Ho, int Wo, int f16, hipStream_t s, int y_bf16 = 0);
 hipError_t launch_avgpool(const bf16_t* x, int B, int H, int W, int C, bf16_t* y, int f16, hipStream_t s);
 // Sum split-K partials [split][B][Npad] + bias, optional L2 normalize → out [B][N] f32.
 bool head_gemv_supported(int B, int K, int Kpad, int Npad);

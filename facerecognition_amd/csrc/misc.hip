@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const bf16_t* __restrict__
 
 // k = 3 (IRV1's and ResNet-50's pools): the nine 16-B loads of a window issued together (clamped addresses,
 // out-of-image taps masked to -inf afterwards) instead of one dependent load per loop trip; same values
-template <bool F16>
+template <bool F16, bool YB = false>  // YB: f16 input, bf16 output (the end of an f16 plan section)
 __global__ __launch_bounds__(256) void maxpool3_kernel(const bf16_t* __restrict__ x, int B, int H, int W, int Cx,
                                                        int x_off, int C, int stride, int pad,
                                                        bf16_t* __restrict__ y, int Cy, int y_off, int Ho, int Wo) {
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void maxpool3_kernel(const bf16_t* __restrict_
 #pragma unroll
             for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
         }
-        *(uint4*)(y + pix * Cy + y_off + g * 8) = Num<F16>::pack8(m);
+        *(uint4*)(y + pix * Cy + y_off + g * 8) = YB ? Num<false>::pack8(m) : Num<F16>::pack8(m);
     }
 }
 
@@ -342,10 +342,16 @@ hipError_t launch_preprocess(const void* in, int in_fmt, int B, int H, int W, bf
 }
 
 hipError_t launch_maxpool(const bf16_t* x, int B, int H, int W, int Cx, int x_off, int C, int k, int stride,
-                          int pad, bf16_t* y, int Cy, int y_off, int Ho, int Wo, int f16, hipStream_t s) {
+                          int pad, bf16_t* y, int Cy, int y_off, int Ho, int Wo, int f16, hipStream_t s, int y_bf16) {
     const size_t total = (size_t)B * Ho * Wo * (C / 8);
     int blocks = (int)((total + 255) / 256);
     if (blocks > 8192) blocks = 8192;
+    if (y_bf16) {  // f16 -> bf16: 3x3 only
+        if (!f16 || k != 3) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((maxpool3_kernel<true, true>), dim3(blocks), dim3(256), 0, s, x, B, H, W, Cx, x_off, C, stride,
+                           pad, y, Cy, y_off, Ho, Wo);
+        return hipGetLastError();
+    }
     if (k == 3) {
         if (f16)
             hipLaunchKernelGGL(maxpool3_kernel<true>, dim3(blocks), dim3(256), 0, s, x, B, H, W, Cx, x_off, C, stride, pad,
