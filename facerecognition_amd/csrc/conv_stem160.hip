@@ -5,7 +5,10 @@
 //   2a  3x3/s1 valid 32 -> 32    79 -> 77
 //   2b  3x3/s1 pad 1 32 -> 64    77 -> 77
 //   maxpool 3x3/s2   64          77 -> 38
-// each conv + folded BN + ReLU.  As four launches the 1a / 2a / 2b tensors (0.4 / 0.38 / 0.76 MB per face) went
+//   3b  1x1          64 -> 80    38 -> 38  (round 6)
+// each conv + folded BN + ReLU.  With u8 crops (the product input) the kernel also does the input preparation
+// (misc.hip preprocess_u8: q = 2u - 255, exact in f16) on the rows it loads, so nothing but the crops (76.8 KB per
+// face) is read.  As four launches the 1a / 2a / 2b tensors (0.4 / 0.38 / 0.76 MB per face) went
 // to HBM and back and every conv paid its few-K-step prologue: 0.35 ms at bs = 256 for 87 GFLOP
 // (profiles/r05_irv1_layer_profile.txt).  Here one workgroup (4 waves, one per SIMD) owns one image and walks
 // down it in 43 phases; only row rings live in LDS:
@@ -14,15 +17,17 @@
 //   * A1  6 rows of 1a, A2 6 rows of 2a (+ one zero row: 2b's padding rows), B2 5 rows of 2b; each row is
 //         plane-major ([C/8 planes][80 positions][16 B]: a fragment's 16 lanes read 256 contiguous bytes) and
 //         A2 keeps zero halo positions 0 and 78 (2b's padding columns);
-//   * phase s: 1a rows 2s, 2s+1; 2a rows 2s-4, 2s-3; 2b rows 2s-7, 2s-6; maxpool row s-5 -- each reads only rows
-//     finished in earlier phases, so one barrier per phase; wave w takes row (w >> 1) of each pair: 1a / 2a
+//   * PL  2 pooled rows (maxpool output, [8 planes][48 positions][16 B]), the 1x1 conv2d_3b's B operand;
+//   * phase s: 1a rows 2s, 2s+1; 2a rows 2s-4, 2s-3; 2b rows 2s-7, 2s-6; maxpool row s-5; 3b row s-6 -- each reads
+//     only rows finished in earlier phases, so one barrier per phase; wave w takes row (w >> 1) of each pair: 1a / 2a
 //     n-fragment (w & 1) (16 of 32 channels), 2b n-fragments 2 (w & 1) .. +1 (32 of 64), five 16-column
 //     fragments (80 columns: 1-3 discarded);
 //   * all weights (1a 3 + 2a 9 + 2b 18 fragments per wave) stay in registers; bias + ReLU seeds / epilogues;
 //     outputs rounded to the storage format exactly where the per-conv path rounds them (1a, 2a, 2b; the max
 //     of rounded values is exact), so only the f32 summation order differs.
-// Bounds: per face 2 x (79^2 x 32 x 72 + 77^2 x 32 x 288 + 77^2 x 64 x 288) = 0.338 GFLOP (K of 1a as stored,
-// 72); HBM: the prepared input once (409.6 KB) + the pooled output once (184.8 KB).
+// Bounds: per face 2 x (79^2 x 32 x 72 + 77^2 x 32 x 288 + 77^2 x 64 x 288 + 38^2 x 80 x 64) = 0.371 GFLOP (K of
+// 1a as stored, 72); HBM: the u8 crop once (76.8 KB; the prepared input, 409.6 KB, for f32 input) + the conv2d_3b
+// output once (231 KB).
 #include "kernels.h"
 
 #include <hip/hip_ext.h>
@@ -41,9 +46,12 @@ constexpr int A2_OFF = A1_OFF + A1_SLOTS * A1_ROW;    // 53760
 constexpr int A2_ROW = 4 * PL, A2_SLOTS = 6;          // + the zero row (slot 6)
 constexpr int B2_OFF = A2_OFF + (A2_SLOTS + 1) * A2_ROW;  // 89600
 constexpr int B2_ROW = 8 * PL, B2_SLOTS = 5;          // 10240
-constexpr int STEM_END = B2_OFF + B2_SLOTS * B2_ROW;  // 140800
+constexpr int PO_OFF = B2_OFF + B2_SLOTS * B2_ROW;   // 140800: pooled rows
+constexpr int PO_PL = 48 * 16, PO_ROW = 8 * PO_PL;    // 768 B per plane (38 + 10 discarded positions)
+constexpr int STEM_END = PO_OFF + 2 * PO_ROW;         // 153088
 constexpr int STEM_LDS = STEM_END + 2048;             // discarded columns' taps read up to 2 positions past a row
-constexpr int NPH = 43;                               // phases: maxpool row s - 5 for s = 5 .. 42
+constexpr int NPH = 44;                               // phases: maxpool row s - 5, 3b row s - 6 (s = 6 .. 43)
+constexpr int C3B = 80;                               // conv2d_3b output channels
 constexpr uint32_t OOB = 0x80000000u;
 static_assert(STEM_LDS <= 163840, "lds");
 
@@ -72,7 +80,7 @@ __device__ __forceinline__ int fresh_lane() {
     return l;
 }
 
-template <bool F16>
+template <bool F16, bool U8>
 __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
@@ -99,6 +107,17 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
     float4 bb3[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) bb3[i] = *(const float4*)(p.b3 + 16 * (2 * nh + i) + 4 * lg);
+    // conv2d_3b: n-fragments wave and (wave 0) 4; K 64 = 2 steps
+    const int n4[2] = {wave, wave == 0 ? 4 : -1};
+    frag w4[2][2];
+    float4 bb4[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int nf = n4[i] < 0 ? 0 : n4[i];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) w4[i][ks] = *(const frag*)(p.w4 + (size_t)(16 * nf + l15) * p.kp4 + 32 * ks + 8 * lg);
+        bb4[i] = *(const float4*)(p.b4 + 16 * nf + 4 * lg);
+    }
 
     // ---- input rows: DMA of row `row` (3 pieces: slots 0-63, 64-127, 128-159) into its ring slot; out of the
     // image: zeros (OOB offsets)
@@ -114,23 +133,64 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
             dma16(xr, (uint32_t)(uintptr_t)(smem + IN_OFF + (row % IN_SLOTS) * IN_ROW + piece * 1024), off);
         }
     };
-    // prologue: rows 0..4 (15 pieces), zero A2 (halo positions and the zero row)
-    for (int u = wave; u < 15; u += 4) dma_piece(u / 3, u % 3);
+    // u8 crops: thread t < 40 k converts positions 4 (t % 40) .. + 3 of row (first + t / 40) into the prepared
+    // 8-channel form [q0 q1 q2 q0 q1 q2 0 0], q = 2u - 255 (exact in f16 / bf16), and stores them de-interleaved
+    const uint8_t* ub = p.u8 + (size_t)b * IW * IW * 3;
+    auto u8_load = [&](int row, uint32_t (&v)[3]) {
+        const int t = threadIdx.x % 40;
+        v[0] = v[1] = v[2] = 0;
+        if ((unsigned)row < (unsigned)IW) {
+            const uint32_t* src = (const uint32_t*)(ub + (size_t)row * IW * 3 + 12 * t);
+            v[0] = src[0]; v[1] = src[1]; v[2] = src[2];
+        }
+    };
+    auto u8_store = [&](int row, const uint32_t (&v)[3]) {
+        const int t = threadIdx.x % 40;
+        char* dst = smem + IN_OFF + (row % IN_SLOTS) * IN_ROW;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float q[8];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int byte = 3 * e + c;
+                const uint32_t u = (v[byte >> 2] >> (8 * (byte & 3))) & 0xffu;
+                q[c] = q[c + 3] = 2.0f * (float)u - 255.0f;
+            }
+            q[6] = q[7] = 0.f;
+            const int pos = 4 * t + e, slot = (pos & 1) ? 80 + (pos >> 1) : (pos >> 1);
+            *(uint4*)(dst + slot * 16) = T::pack8(q);
+        }
+    };
+    // prologue: rows 0..4, zero A2 (halo positions and the zero row)
+    if (U8) {
+        if (threadIdx.x < 200) {
+            uint32_t v[3];
+            u8_load(threadIdx.x / 40, v);
+            u8_store(threadIdx.x / 40, v);
+        }
+    } else {
+        for (int u = wave; u < 15; u += 4) dma_piece(u / 3, u % 3);
+    }
     for (int i = threadIdx.x; i < (A2_SLOTS + 1) * A2_ROW / 16; i += 256)
         *(uint4*)(smem + A2_OFF + i * 16) = make_uint4(0, 0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    bf16_t* const yb = p.y + (size_t)b * WP * WP * 64;
+    bf16_t* const yb = p.y + (size_t)b * WP * WP * C3B;
     f32x4_t acc[2][5];
 
 #pragma unroll 1
     for (int s = 0; s < NPH; ++s) {
-        // next phase's input rows 4s+5 .. 4s+8: 12 pieces, 3 per wave
+        // next phase's input rows 4s+5 .. 4s+8: 12 DMA pieces, 3 per wave; u8: loaded now, stored at the phase end
+        uint32_t uv[3];
+        if (U8) {
+            if (threadIdx.x < 160) u8_load(4 * s + 5 + threadIdx.x / 40, uv);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int u = wave + 4 * k;
-            dma_piece(4 * s + 5 + u / 3, u % 3);
+            for (int k = 0; k < 3; ++k) {
+                const int u = wave + 4 * k;
+                dma_piece(4 * s + 5 + u / 3, u % 3);
+            }
         }
         const int ln = fresh_lane(), c15 = ln & 15, g = ln >> 4;
         // ---- 1a: row i1 = 2s + hr, K = 3 steps of 4 taps x 8 channels (tap 8 repeated for the zero-weight pad)
@@ -224,10 +284,44 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
                                            fmaxf(acc[i][f][3], 0.f));
             }
         }
-        // ---- maxpool row r = s - 5 from 2b rows 2r .. 2r + 2 (written in earlier phases): 38 x 8 planes
+        // ---- 3b: row r3 = s - 6 of the pooled rows (1x1 64 -> 80), straight to global memory
+        {
+            const int r3 = s - 6;
+            if (r3 >= 0) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int f = 0; f < 3; ++f) acc[i][f] = (f32x4_t){bb4[i].x, bb4[i].y, bb4[i].z, bb4[i].w};
+                const char* src = smem + PO_OFF + (r3 & 1) * PO_ROW + g * PO_PL + c15 * 16;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    frag bq[3];
+#pragma unroll
+                    for (int f = 0; f < 3; ++f) bq[f] = *(const frag*)(src + 4 * ks * PO_PL + f * 256);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        if (n4[i] >= 0)
+#pragma unroll
+                            for (int f = 0; f < 3; ++f) acc[i][f] = T::mfma(w4[i][ks], bq[f], acc[i][f]);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    if (n4[i] >= 0)
+#pragma unroll
+                        for (int f = 0; f < 3; ++f) {
+                            const int px = 16 * f + c15;
+                            if (px < WP)
+                                *(uint2*)(yb + ((size_t)r3 * WP + px) * C3B + 16 * n4[i] + 4 * g) =
+                                    pack4<F16>(fmaxf(acc[i][f][0], 0.f), fmaxf(acc[i][f][1], 0.f), fmaxf(acc[i][f][2], 0.f),
+                                               fmaxf(acc[i][f][3], 0.f));
+                        }
+            }
+        }
+        // ---- maxpool row r = s - 5 from 2b rows 2r .. 2r + 2 (written in earlier phases): 38 x 8 planes, into the
+        // pooled ring (3b reads it next phase)
         {
             const int r = s - 5;
-            if (r >= 0) {
+            if (r >= 0 && r < WP) {
                 for (int it = threadIdx.x; it < WP * 8; it += 256) {
                     // lanes walk the output columns of one plane: their 16-B reads are 32 B apart (2-way bank sharing);
                     // walking the planes of one column put 8 lanes on the same banks
@@ -246,10 +340,11 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
                             for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
                         }
                     }
-                    *(uint4*)(yb + ((size_t)r * WP + oc) * 64 + pl * 8) = T::pack8(m);
+                    *(uint4*)(smem + PO_OFF + (r & 1) * PO_ROW + pl * PO_PL + oc * 16) = T::pack8(m);
                 }
             }
         }
+        if (U8 && threadIdx.x < 160) u8_store(4 * s + 5 + threadIdx.x / 40, uv);
         // the next phase's input rows landed, every ring write of this phase is visible
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
@@ -257,19 +352,23 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
 
 }  // namespace
 
-bool stem160_supported(int H, int W, int Cin, int K1, int K2, int K3, int C1, int C2, int C3) {
-    return H == IW && W == IW && Cin == 8 && K1 == 72 && K2 == 288 && K3 == 288 && C1 == 32 && C2 == 32 && C3 == 64;
+bool stem160_supported(int H, int W, int Cin, int K1, int K2, int K3, int K4, int C1, int C2, int C3, int C4) {
+    return H == IW && W == IW && Cin == 8 && K1 == 72 && K2 == 288 && K3 == 288 && K4 == 64 && C1 == 32 && C2 == 32 &&
+           C3 == 64 && C4 == C3B;
 }
 
 hipError_t launch_stem160(const Stem160Args& a, hipStream_t s) {
-    if (a.B <= 0 || !a.x || !a.y || !a.w1 || !a.w2 || !a.w3 || !a.b1 || !a.b2 || !a.b3 || a.kp1 < 96 || a.kp2 < 288 ||
-        a.kp3 < 288)
+    if (a.B <= 0 || (!a.x && !a.u8) || !a.y || !a.w1 || !a.w2 || !a.w3 || !a.w4 || !a.b1 || !a.b2 || !a.b3 || !a.b4 ||
+        a.kp1 < 96 || a.kp2 < 288 || a.kp3 < 288 || a.kp4 < 64)
         return hipErrorInvalidValue;
-    auto k = a.f16 ? stem160_kernel<true> : stem160_kernel<false>;
-    static bool attr[2] = {false, false};
-    if (!attr[a.f16 ? 1 : 0]) {
+    const bool u8 = a.u8 != nullptr;
+    auto k = a.f16 ? (u8 ? stem160_kernel<true, true> : stem160_kernel<true, false>)
+                   : (u8 ? stem160_kernel<false, true> : stem160_kernel<false, false>);
+    static bool attr[4] = {false, false, false, false};
+    const int ai = (a.f16 ? 2 : 0) + (u8 ? 1 : 0);
+    if (!attr[ai]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, STEM_LDS);
-        attr[a.f16 ? 1 : 0] = true;
+        attr[ai] = true;
     }
     if (a.ev0)
         hipExtLaunchKernelGGL(k, dim3(a.B), dim3(256), STEM_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);

@@ -253,6 +253,7 @@ struct fr_handle {
     // transition kernel, a fixed head split), so a face's embedding does not depend on its batch
     bool invariant = false;
     int fused_mask = 15;  // FR_OPT_FUSED_MASK
+    const uint8_t* fwd_u8 = nullptr;  // the current forward's u8 crops when the IRV1 fused stem prepares them itself
 };
 
 namespace {
@@ -1180,7 +1181,7 @@ void build_irv1(Builder& b) {
     const bool mid16b = mid16 && f16_mid >= 2;
     if (mid16) h->tensors[x].f16 = true;
     b.stem = true;
-    // conv2d_1a .. maxpool_3a also as one launch (conv_stem160.hip) beside the member ops, measured per batch size
+    // conv2d_1a .. conv2d_3b also as one launch (conv_stem160.hip) beside the member ops, measured per batch size
     int st_op = -1;
     if (h->dtype != FR_DTYPE_FP8) {
         st_op = (int)h->ops.size();
@@ -1193,21 +1194,24 @@ void build_irv1(Builder& b) {
     b.conv({m + "conv2d_2a"}, a, 0, 32, bb, 0, 3, 3, 1, 1, 0, 0, 1);
     b.conv({m + "conv2d_2b"}, bb, 0, 32, c, 0, 3, 3, 1, 1, 1, 1, 1);
     b.maxpool(c, d, 0, 3, 2, 0);
+    b.conv({m + "conv2d_3b"}, d, 0, 64, e, 0, 1, 1, 1, 1, 0, 0, 1);
     if (st_op >= 0 && !b.rc) {
         StageRec sr;
         sr.stem = true;
-        sr.in = in; sr.out = d; sr.H = 160; sr.C = 64;
+        sr.in = in; sr.out = e; sr.H = 160; sr.C = 80;
         const int n = (int)h->ops.size();
-        sr.conv_ops = {n - 4, n - 3, n - 2, n - 1};
-        const Op& o1 = h->ops[n - 4];
-        const Op& o2 = h->ops[n - 3];
-        const Op& o3 = h->ops[n - 2];
+        sr.conv_ops = {n - 5, n - 4, n - 3, n - 2, n - 1};
+        const Op& o1 = h->ops[n - 5];
+        const Op& o2 = h->ops[n - 4];
+        const Op& o3 = h->ops[n - 3];
+        const Op& o4 = h->ops[n - 1];
         const DevConvW& c1 = h->convw[o1.wi];
         const DevConvW& c2 = h->convw[o2.wi];
         const DevConvW& c3 = h->convw[o3.wi];
-        const bool ok = stem160_supported(160, 160, 8, c1.K, c2.K, c3.K, c1.Cout, c2.Cout, c3.Cout) && c1.bias && c2.bias &&
-                        c3.bias && !c1.bias9 && !c2.bias9 && !c3.bias9 && !c1.w8 && !c2.w8 && !c3.w8 && o1.act == 1 &&
-                        o2.act == 1 && o3.act == 1 && h->tensors[in].f16 == h->tensors[d].f16;
+        const DevConvW& c4 = h->convw[o4.wi];
+        bool ok = stem160_supported(160, 160, 8, c1.K, c2.K, c3.K, c4.K, c1.Cout, c2.Cout, c3.Cout, c4.Cout) &&
+                  h->tensors[in].f16 == h->tensors[e].f16 && o1.act == 1 && o2.act == 1 && o3.act == 1 && o4.act == 1;
+        for (const DevConvW* cw : {&c1, &c2, &c3, &c4}) ok = ok && cw->bias && !cw->bias9 && !cw->w8;
         if (ok) {
             for (int oi : sr.conv_ops) h->ops[oi].stage = h->ops[st_op].stage;
             h->stages.push_back(sr);
@@ -1217,7 +1221,6 @@ void build_irv1(Builder& b) {
                 if (op.kind == OP_STAGE && op.stage >= (int)h->stages.size()) --op.stage;
         }
     }
-    b.conv({m + "conv2d_3b"}, d, 0, 64, e, 0, 1, 1, 1, 1, 0, 0, 1);
     b.conv({m + "conv2d_4a"}, e, 0, 80, f, 0, 3, 3, 1, 1, 0, 0, 1);
     b.conv({m + "conv2d_4b"}, f, 0, 192, x, 0, 3, 3, 2, 2, 0, 0, 1);
     // repeat_1: Block35 x5 @17x17. cat layout [t1 | t2 | b0 | b1 | b2]; conv2d reads [64:160].  Also emitted as one
@@ -1987,22 +1990,20 @@ static int run_maxpool_op(fr_handle* h, const Op& op, int B, int f16, hipStream_
 static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vector<char>& stage_run, hipStream_t s) {
     const StageRec& r = h->stages[op.stage];
     if (r.stem) {
-        const Op& o1 = h->ops[r.conv_ops[0]];
-        const Op& o2 = h->ops[r.conv_ops[1]];
-        const Op& o3 = h->ops[r.conv_ops[2]];
-        const DevConvW& c1 = h->convw[o1.wi];
-        const DevConvW& c2 = h->convw[o2.wi];
-        const DevConvW& c3 = h->convw[o3.wi];
+        const DevConvW* cw[4];
+        for (int k = 0, j = 0; k < 5; ++k)
+            if (h->ops[r.conv_ops[k]].kind == OP_CONV) cw[j++] = &h->convw[h->ops[r.conv_ops[k]].wi];
         Stem160Args a{};
         a.x = h->tensors[r.in].dev;
+        a.u8 = h->fwd_u8;  // the crops when the forward skipped the preparation op (forward, OP_PRE)
         a.y = h->tensors[r.out].dev;
-        a.w1 = c1.w; a.w2 = c2.w; a.w3 = c3.w;
-        a.b1 = c1.bias; a.b2 = c2.bias; a.b3 = c3.bias;
-        a.kp1 = c1.Kpad; a.kp2 = c2.Kpad; a.kp3 = c3.Kpad;
+        a.w1 = cw[0]->w; a.w2 = cw[1]->w; a.w3 = cw[2]->w; a.w4 = cw[3]->w;
+        a.b1 = cw[0]->bias; a.b2 = cw[1]->bias; a.b3 = cw[2]->bias; a.b4 = cw[3]->bias;
+        a.kp1 = cw[0]->Kpad; a.kp2 = cw[1]->Kpad; a.kp3 = cw[2]->Kpad; a.kp4 = cw[3]->Kpad;
         a.B = B; a.f16 = f16 || h->tensors[r.in].f16;
         ProfScope ps(h, s);
-        ps.flops = 2.0 * B * (79.0 * 79 * 32 * 72 + 77.0 * 77 * 32 * 288 + 77.0 * 77 * 64 * 288);
-        ps.bytes = 2.0 * B * (160.0 * 160 * 8 + 38.0 * 38 * 64);
+        ps.flops = 2.0 * B * (79.0 * 79 * 32 * 72 + 77.0 * 77 * 32 * 288 + 77.0 * 77 * 64 * 288 + 38.0 * 38 * 80 * 64);
+        ps.bytes = (double)B * ((a.u8 ? 3.0 : 16.0) * 160 * 160 + 2.0 * 38 * 38 * 80);
         ps.start("stem160");
         FR_HIP_CHECK(launch_stem160(a, s));
         return FR_OK;
@@ -2278,6 +2279,14 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
                 break;
             }
             case OP_PRE: {
+                h->fwd_u8 = nullptr;
+                if (in_fmt == FR_IN_U8_NHWC && oi + 1 < h->ops.size() && h->ops[oi + 1].kind == OP_STAGE &&
+                    h->stages[h->ops[oi + 1].stage].stem && !op_skipped(h->ops[oi + 1], stage_run) &&
+                    !(h->tuning && h->stage_mode == 1 && !h->keep_inter && !h->prof &&
+                      stage_choice(h, h->ops[oi + 1].grp, B) < 0)) {
+                    h->fwd_u8 = (const uint8_t*)in;  // conv_stem160.hip prepares the crops itself (no prepared tensor)
+                    break;
+                }
                 ProfScope ps(h, s);
                 // u8 crops: preprocess + stem conv in one launch (conv_stem.hip).  Not when an e4m3 conv
                 // reads the stem output (it needs the amax from the conv epilogue).
@@ -2900,7 +2909,7 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
         }
         if (op.kind == OP_STAGE && h->stages[op.stage].stem) {  // M = faces, K = the three convs' MACs per face
             const StageRec& r = h->stages[op.stage];
-            out += "stem160 " + std::to_string(B) + " 1 178312896 178312896 1 1 3x3 " + h->tensors[r.out].name +
+            out += "stem160 " + std::to_string(B) + " 1 185697536 185697536 1 1 3x3 " + h->tensors[r.out].name +
                    meas_note(h, op.grp, B) + "\n";
             continue;
         }

@@ -195,20 +195,22 @@ void chain17_pack_block(const bf16_t* rA, int kpA, const bf16_t* r17, int kp17, 
                         const bf16_t* rE, int kpE, int blk, int nblk, bf16_t* out);
 hipError_t launch_chain17(const Chain17Args& a, hipStream_t s);
 // FaceNet IRV1 stem at 160x160 (conv_stem160.hip): conv2d_1a (3x3/s2 8 -> 32) + conv2d_2a (3x3 32 -> 32) +
-// conv2d_2b (3x3/p1 32 -> 64), each + bias + ReLU, + maxpool_3a (3x3/s2) as one launch, one workgroup per image;
-// x = the prepared 8-channel input [B][160][160][8], y = the pooled [B][38][38][64]; w* = the member convs'
+// conv2d_2b (3x3/p1 32 -> 64) + maxpool_3a (3x3/s2) + conv2d_3b (1x1 64 -> 80), each conv + bias + ReLU, as one
+// launch, one workgroup per image; input: u8 crops [B][160][160][3] (u8 != null: the preparation is done in-kernel)
+// or the prepared 8-channel input x [B][160][160][8]; y = conv2d_3b's [B][38][38][80]; w* = the member convs'
 // [Npad][Kpad] rows (kp* = Kpad), b* their folded biases.
 struct Stem160Args {
     const bf16_t* x;
+    const uint8_t* u8;
     bf16_t* y;
-    const bf16_t* w1; const bf16_t* w2; const bf16_t* w3;
-    const float* b1; const float* b2; const float* b3;
-    int kp1, kp2, kp3;
+    const bf16_t* w1; const bf16_t* w2; const bf16_t* w3; const bf16_t* w4;
+    const float* b1; const float* b2; const float* b3; const float* b4;
+    int kp1, kp2, kp3, kp4;
     int B, f16;
     void* ev0;
     void* ev1;
 };
-bool stem160_supported(int H, int W, int Cin, int K1, int K2, int K3, int C1, int C2, int C3);
+bool stem160_supported(int H, int W, int Cin, int K1, int K2, int K3, int K4, int C1, int C2, int C3, int C4);
 hipError_t launch_stem160(const Stem160Args& a, hipStream_t s);
 // FaceNet IRV1 repeat_1 (Block35 x nblk at 17x17x256) as one launch (conv_chain35.hip): one workgroup per image, the
 // branch tensors in LDS, the block outputs through global memory (io[0] = the NHWC input, io[1..nblk-1] = the

@@ -32,10 +32,13 @@ def analyse(trace, plan_path):
     plan = [l.split() for l in open(plan_path).read().splitlines() if l.strip()]
     rows = list(csv.DictReader(open(trace)))
     ours = [r for r in rows if "fr::" in r["Kernel_Name"]]
-    starts = [i for i, r in enumerate(ours) if "preprocess" in r["Kernel_Name"] or "stem_u8" in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(ours)
+              if any(k in r["Kernel_Name"] for k in ("preprocess", "stem_u8", "stem160"))]
     seq = ours[starts[-1]:]
     i = 0
     fused_stem = "stem_u8" in seq[0]["Kernel_Name"]
+    if "stem160" in seq[0]["Kernel_Name"]:  # the IRV1 fused stem prepares u8 crops itself: no preprocess dispatch
+        plan = [p for p in plan if p[0] != "pre"]
     skip_next_conv = False
     tot_ns = tot_flop = 0
     agg = {}
