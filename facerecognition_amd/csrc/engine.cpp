@@ -1720,9 +1720,10 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     // the 3-stage implicit-GEMM tiles are credited FR_AB tune_s3_bias percent (default 5): the tuner's
     // back-to-back launches run warm, where the deeper ring's latency hiding does not show, and in the
     // forward they win (IRV1 Block17 1x7: 12.0 vs 17.4 us per launch for 11.5 vs 11.5 us tuned)
-    static const float s3_credit = 1.f - 0.01f * (float)ab_int("tune_s3_bias", 5);
+    static const float s3_credit = 1.f - 0.01f * (float)ab_int("tune_s3_bias", 5);  // (the 64x64 3-stage tile too)
     for (size_t c = 0; c < cand.size(); ++c)
-        if (cand_ms[c] >= 0.f && (cand[c].tile == TILE_128x64_S3 || cand[c].tile == TILE_64x128_S3) && cand[c].split == 1)
+        if (cand_ms[c] >= 0.f && (cand[c].tile == TILE_128x64_S3 || cand[c].tile == TILE_64x128_S3 || cand[c].tile == TILE_64x64_S3) &&
+            cand[c].split == 1)
             cand_ms[c] *= s3_credit;
     size_t best = 0;
     while (best + 1 < cand.size() && cand_ms[best] < 0.f) ++best;
@@ -3364,7 +3365,10 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         return FR_OK;
     }
     if (d->tile > 0) {
-        if (d->tile > NUM_TILE_IDS) { set_error("fr_op_conv2d: bad tile"); return FR_ERR_ARG; }
+        if (d->tile > NUM_TILE_IDS && d->tile - 1 != TILE_64x64_S3 && d->tile - 1 != TILE_64x64) {
+            set_error("fr_op_conv2d: bad tile");
+            return FR_ERR_ARG;
+        }
         a.tile = d->tile - 1;
     } else {
         int tile, sp;

@@ -189,6 +189,29 @@ def test_conv_wring(gpu, case):
         conv_op(x, torch.randn(64, Cin, 3, 3, generator=g), pad=(1, 1), tile=N.FR_TILE_WRING)
 
 
+TILE64_CASES = [  # (B, H, W, Cin, Cout, kh, kw, pad): IRV1 Block8 / mixed_7a shapes (M = 9 B), a ragged M, Cin % 64 != 0
+    (4, 3, 3, 1792, 384, 1, 1, (0, 0)), (4, 3, 3, 192, 192, 1, 3, (0, 1)), (4, 3, 3, 384, 1792, 1, 1, (0, 0)),
+    (3, 8, 8, 256, 256, 3, 3, (1, 1)), (2, 5, 7, 96, 64, 3, 3, (1, 1))]
+
+
+@pytest.mark.parametrize("tile", ["FR_TILE_64x64_S3", "FR_TILE_64x64"])
+@pytest.mark.parametrize("case", TILE64_CASES)
+def test_conv_tile64(gpu, case, tile):
+    """The 64 x 64 implicit-GEMM tiles (round 6, autotuner candidates for small-M convs): they sum K in tile 0's
+    order, so they must equal it bit for bit (bias + residual, bias + ReLU)."""
+    B, H, W, Cin, Cout, kh, kw, pd = case
+    g = torch.Generator().manual_seed(B + H + Cin + Cout + kh)
+    x = torch.randn(B, H, W, Cin, generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn(Cout, Cin, kh, kw, generator=g) / np.sqrt(Cin * kh * kw)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    res = torch.randn(B, H, W, Cout, generator=g).to(torch.bfloat16).to(gpu)
+    t = getattr(N, tile)
+    y = conv_op(x, w, pad=pd, bias=bias, res=res, tile=t)
+    _close(y, conv_ref(x, w, pad=pd, bias=bias, res=res))
+    assert torch.equal(y, conv_op(x, w, pad=pd, bias=bias, res=res, tile=0))
+    assert torch.equal(conv_op(x, w, pad=pd, bias=bias, act=1, tile=t), conv_op(x, w, pad=pd, bias=bias, act=1, tile=0))
+
+
 DIRECT_CASES = [
     # B, H, W, Cin, Cout, kh, kw, stride, pad, act   (FaceNet IRV1 shapes, smaller images)
     (2, 41, 41, 8, 32, 3, 3, (2, 2), (0, 0), 1),      # conv2d_1a (Cin padded to 8, K = 72)
