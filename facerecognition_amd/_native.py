@@ -35,6 +35,7 @@ FR_TILE_DIRECT = 14
 FR_TILE_SMALL = 16
 FR_TILE_64x64_S3 = 17
 FR_TILE_64x64 = 18
+FR_TILE_32x64_S3 = 19
 FR_OPT_STAGE = 1
 FR_OPT_KEEP_INTERMEDIATES = 2
 FR_OPT_MATCH_EXACT = 3

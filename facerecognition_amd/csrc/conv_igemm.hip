@@ -541,6 +541,7 @@ hipError_t launch_dtype(const ConvArgs& a, hipStream_t s) {
         case TILE_64x128_S3: return launch_variant<F16, 64, 128, 2, 2, 3>(a, s);
         case TILE_64x64_S3: return launch_variant<F16, 64, 64, 2, 2, 3>(a, s);
         case TILE_64x64: return launch_variant<F16, 64, 64, 2, 2, 2>(a, s);
+        case TILE_32x64_S3: return launch_variant<F16, 32, 64, 2, 2, 3>(a, s);
         default: return launch_variant<F16, 128, 128, 2, 2, 2>(a, s);
     }
 }
@@ -551,12 +552,14 @@ int conv_tile_bm(int tile) {
     switch (tile) {
         case TILE_256x64: case TILE_256x128: return 256;
         case TILE_64x128: case TILE_64x128_S3: case TILE_64x64_S3: case TILE_64x64: return 64;
+        case TILE_32x64_S3: return 32;
         default: return 128;
     }
 }
 int conv_tile_bn(int tile) {
     switch (tile) {
-        case TILE_256x64: case TILE_128x64: case TILE_128x64_S3: case TILE_64x64_S3: case TILE_64x64: return 64;
+        case TILE_256x64: case TILE_128x64: case TILE_128x64_S3: case TILE_64x64_S3: case TILE_64x64: case TILE_32x64_S3:
+            return 64;
         case TILE_128x256: return 256;
         default: return 128;
     }
@@ -584,7 +587,7 @@ int conv_tile_candidates(int Cout, int* out) {
     // its repeated launches run with warm caches, where the deeper ring's latency hiding does not show; in the
     // forward (cold operands) the 3-stage tile is the faster one (IRV1 Block17 1x7 / 7x1: 12.0 vs 17.4 us)
     static const int tiles[] = {TILE_128x64_S3, TILE_64x128_S3, TILE_128x128, TILE_256x64, TILE_128x64, TILE_64x128,
-                                TILE_256x128, TILE_128x256, TILE_64x64_S3, TILE_64x64};
+                                TILE_256x128, TILE_128x256, TILE_64x64_S3, TILE_64x64, TILE_32x64_S3};
     int n = 0;
     for (int t : tiles) {
         const int BN = conv_tile_bn(t);

@@ -1722,7 +1722,8 @@ int tune_conv(fr_handle* h, ConvArgs a, hipStream_t s) {
     // forward they win (IRV1 Block17 1x7: 12.0 vs 17.4 us per launch for 11.5 vs 11.5 us tuned)
     static const float s3_credit = 1.f - 0.01f * (float)ab_int("tune_s3_bias", 5);  // (the 64x64 3-stage tile too)
     for (size_t c = 0; c < cand.size(); ++c)
-        if (cand_ms[c] >= 0.f && (cand[c].tile == TILE_128x64_S3 || cand[c].tile == TILE_64x128_S3 || cand[c].tile == TILE_64x64_S3) &&
+        if (cand_ms[c] >= 0.f && (cand[c].tile == TILE_128x64_S3 || cand[c].tile == TILE_64x128_S3 || cand[c].tile == TILE_64x64_S3 ||
+                                  cand[c].tile == TILE_32x64_S3) &&
             cand[c].split == 1)
             cand_ms[c] *= s3_credit;
     size_t best = 0;
@@ -3365,7 +3366,7 @@ int fr_op_conv2d(const fr_conv_desc* d, void* stream) {
         return FR_OK;
     }
     if (d->tile > 0) {
-        if (d->tile > NUM_TILE_IDS && d->tile - 1 != TILE_64x64_S3 && d->tile - 1 != TILE_64x64) {
+        if (d->tile > NUM_TILE_IDS && d->tile - 1 != TILE_64x64_S3 && d->tile - 1 != TILE_64x64 && d->tile - 1 != TILE_32x64_S3) {
             set_error("fr_op_conv2d: bad tile");
             return FR_ERR_ARG;
         }

@@ -11,7 +11,7 @@ enum { TILE_128x128 = 0, TILE_256x64 = 1, TILE_128x64 = 2, TILE_64x128 = 3,
        TILE_128x64_S3 = 8, TILE_64x128_S3 = 9, NUM_TILE_IDS = 10,     // (7 = the band kernel's id in the ABI)
        TILE_WRING = 13,    // conv_wring.hip (= FR_TILE_WRING), an autotuner candidate beside the igemm tiles
        TILE_DIRECT = 14,   // conv_direct.hip (= FR_TILE_DIRECT), the same
-       TILE_64x64_S3 = 17, TILE_64x64 = 18 };  // round 6: small-M GEMMs (IRV1 Block8: M = 2304) over more CUs
+       TILE_64x64_S3 = 17, TILE_64x64 = 18, TILE_32x64_S3 = 19 };  // round 6: small-M GEMMs (IRV1 Block8: M = 2304) over more CUs
 
 // Implicit-GEMM convolution, NHWC bf16 in/out, f32 accumulate, fused epilogue.
 // GEMM view: M = B*Ho*Wo output pixels, N = Cout, K = Kh*Kw*Cin (c fastest).

@@ -261,6 +261,7 @@ typedef struct fr_conv_desc {
 /* 15: retired (round 5; a hipBLASLt candidate that never won a whole forward) */
 #define FR_TILE_64x64_S3 17  /* 3-stage DMA ring, 64 x 64 tiles (round 6: small-M GEMMs over more CUs) */
 #define FR_TILE_64x64 18
+#define FR_TILE_32x64_S3 19
 #define FR_TILE_SMALL 16     /* small-M implicit GEMM, one wave per 16 px x 64 ch over the whole K (conv_small.hip); bit-identical to tile 0.
                                 split_k = KS | NF << 8: KS (4 / 8 / 16) waves share a tile's K (split-K summation order), NF
                                 (2 / 1; 0 = 4) 16-channel fragments per tile: 1, 4, 8, 1|2<<8, 4|2<<8, 8|2<<8, 1|1<<8, 4|1<<8,

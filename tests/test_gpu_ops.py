@@ -194,7 +194,7 @@ TILE64_CASES = [  # (B, H, W, Cin, Cout, kh, kw, pad): IRV1 Block8 / mixed_7a sh
     (3, 8, 8, 256, 256, 3, 3, (1, 1)), (2, 5, 7, 96, 64, 3, 3, (1, 1))]
 
 
-@pytest.mark.parametrize("tile", ["FR_TILE_64x64_S3", "FR_TILE_64x64"])
+@pytest.mark.parametrize("tile", ["FR_TILE_64x64_S3", "FR_TILE_64x64", "FR_TILE_32x64_S3"])
 @pytest.mark.parametrize("case", TILE64_CASES)
 def test_conv_tile64(gpu, case, tile):
     """The 64 x 64 implicit-GEMM tiles (round 6, autotuner candidates for small-M convs): they sum K in tile 0's
