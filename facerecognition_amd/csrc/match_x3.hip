@@ -9,8 +9,10 @@
 //      ~3.9e-3 ||p|| -- the band of the former 2-product pass (ph.gh + pl.gh, eps 4.0e-3 worst case) at half
 //      its MFMAs and probe registers; per (probe, split)
 //      the top-KO by s~ of four sub-lists
-//      of KP (rows 16j + 4 sub + r of each tile, kept by the lane whose accumulators hold them) and a floor: every row dropped from a sub-list, or by the
-//      filter, has s~ <= floor = the best last entry of the full sub-lists;
+//      of KP (rows 16j + 4 sub + r of each tile, kept by the lane whose accumulators hold them) and a floor: every row
+//      dropped from a sub-list, or by the filter, has s~ <= floor = the larger of the best last entry of the full
+//      sub-lists and the least (KP/2)-th entry (the filter's second bar; round 6: before, rows that bar dropped were
+//      not covered, a gap only a 16-row near-tie within 2 eps in one split could have exposed);
 //   2. rescore (one wave per probe): the global top-KC by s~ are rescored exactly with the k-ordered f32
 //      fmaf chain of the exact kernel (same order, so the scores are bit-identical to match.hip) and
 //      the top-k is taken by (score desc, index asc);
@@ -87,17 +89,15 @@ __device__ __forceinline__ void insert(float (&ls)[KMAX], int (&li)[KMAX], float
 template <int KMAX>
 __device__ __forceinline__ void insert_s(float (&ls)[KMAX], int (&li)[KMAX], float s, int idx) {
     if (!(s > ls[KMAX - 1])) return;
-    float cs = s;
-    int ci = idx;
+    bool b[KMAX];
 #pragma unroll
-    for (int q = 0; q < KMAX; ++q) {
-        const bool b = cs > ls[q];
-        const float ts = ls[q];
-        const int ti = li[q];
-        ls[q] = b ? cs : ts;
-        li[q] = b ? ci : ti;
-        cs = b ? ts : cs;
-        ci = b ? ti : ci;
+    for (int q = 0; q < KMAX; ++q) b[q] = s > ls[q];
+#pragma unroll
+    for (int q = KMAX - 1; q >= 0; --q) {
+        const float sh = q > 0 && b[q - 1] ? ls[q - 1] : s;
+        const int ih = q > 0 && b[q - 1] ? li[q - 1] : idx;
+        ls[q] = b[q] ? sh : ls[q];
+        li[q] = b[q] ? ih : li[q];
     }
 }
 
@@ -233,6 +233,15 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < XSLOT - 1; ++i) issue_next();
 
+    // Lane reductions over a probe's 4 sub-list lanes (lane ^ 16, ^ 32, ^ 48): two v_permlane{32,16}_swap (max and
+    // min are symmetric, so the swapped halves pair up as xor 32 / 16), no LDS round trip on the tile's critical path.
+    auto red4 = [](float x, bool mx) {
+        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        const float y = mx ? fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]))
+                           : fminf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+        auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+        return mx ? fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1])) : fminf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+    };
     // the tile's candidate filter and sorted inserts (a = its accumulators, tb = its first row)
     auto filter_tile = [&](f32x4_t (&a)[4], float (&ls)[KP], int (&li)[KP], int64_t tb) {
         // a[j][r] = s~(the lane's probe, row tb + 16*j + 4*my_sub + r).  A row not above the best KP-th score
@@ -250,12 +259,7 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
         // also: when every sub-list holds >= KP/2 entries above x, the probe's top KO = 2 KP (the merge
         // keeps exactly those) are all above x, so min over the sub-lists of the (KP/2)-th score is a
         // valid (usually higher) bar too
-        float thr = ls[KP - 1], thr2 = ls[KP / 2 - 1];
-        thr = fmaxf(thr, __shfl_xor(thr, 16));
-        thr2 = fminf(thr2, __shfl_xor(thr2, 16));
-        thr = fmaxf(thr, __shfl_xor(thr, 32));
-        thr2 = fminf(thr2, __shfl_xor(thr2, 32));
-        thr = fmaxf(thr, thr2);
+        const float thr = fmaxf(red4(ls[KP - 1], true), red4(ls[KP / 2 - 1], false));
         uint32_t m = 0;
 #pragma unroll
         for (int e = 0; e < 16; ++e) m |= a[e >> 2][e & 3] > thr ? 1u << e : 0u;
@@ -339,16 +343,19 @@ __global__ __launch_bounds__(512) void match_x3_kernel(const float* __restrict__
         int oi[KO];
 #pragma unroll
         for (int q = 0; q < KO; ++q) { os[q] = -INFINITY; oi[q] = INT_MAX; }
-        float floor_s = -INFINITY;
+        // every row the scan dropped scores at most the final bar: a full sub-list dropped rows up to its last
+        // entry, and the filter's second bar (the least (KP/2)-th entry) dropped rows up to at most its final value
+        float floor_s = -INFINITY, half = INFINITY;
 #pragma unroll 1
         for (int e = 0; e < 4 * KP; ++e) {
             const float sc = ms[mq * 4 * KP + e];
             const int ix = mi[mq * 4 * KP + e];
+            if (e % KP == KP / 2 - 1) half = fminf(half, ix == INT_MAX ? -INFINITY : sc);
             if (ix == INT_MAX) continue;
             insert<KO>(os, oi, sc, ix);
-            // a full sub-list may have dropped rows scoring up to its last entry
             if (e % KP == KP - 1) floor_s = fmaxf(floor_s, sc);
         }
+        floor_s = fmaxf(floor_s, half);
         const size_t o = ((size_t)p * n_split + split) * KS;
 #pragma unroll
         for (int q = 0; q < KO; ++q) {
