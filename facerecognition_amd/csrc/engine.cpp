@@ -138,7 +138,8 @@ struct StageRec {
     int tail_op = -1;
     // IRV1 repeat_2 as one launch (chain 17, conv_chain.hip): conv_ops = per block {branch1.0 + branch0, 1x7, 7x1,
     // conv2d}; repeat_1 (chain 35, conv_chain35.hip): per block {branch1.0 + branch2.0 + branch0, branch1.1, branch2.1,
-    // branch2.2, conv2d}, x_tensors = the block outputs
+    // branch2.2, conv2d}, x_tensors = the block outputs; ResNet-50 layer3.1 .. 3.5 (chain 50, conv_chain_r50.hip):
+    // per block {conv1, conv2, conv3}
     int chain = 0;
     bf16_t* cw = nullptr;                 // the packed weights of all blocks
     float* cbias = nullptr;               // the member convs' biases
@@ -252,7 +253,7 @@ struct fr_handle {
     // FR_OPT_BATCH_INVARIANT: every kernel choice sums K in the implicit GEMM's order (no split-K, no stage /
     // transition kernel, a fixed head split), so a face's embedding does not depend on its batch
     bool invariant = false;
-    int fused_mask = 15;  // FR_OPT_FUSED_MASK
+    int fused_mask = 31;  // FR_OPT_FUSED_MASK
     const uint8_t* fwd_u8 = nullptr;  // the current forward's u8 crops when the IRV1 fused stem prepares them itself
 };
 
@@ -852,6 +853,51 @@ int build_chain17(fr_handle* h, StageRec& r) {
     return upload(h, &r.cbias, bias);
 }
 
+// Packs ResNet-50 layer3.1 .. layer3.5's member convs (per block: conv1 1x1 1024 -> 256, conv2 3x3 256 -> 256,
+// conv3 1x1 256 -> 1024 with the residual; BN folded, each + bias + ReLU) into conv_chain_r50.hip's per-wave streams.
+int build_chain_r50(fr_handle* h, StageRec& r) {
+    const int nblk = r.nblk;
+    if ((int)r.conv_ops.size() != 3 * nblk) {
+        set_error("plan: chain_r50 member count");
+        return FR_ERR_ARG;
+    }
+    std::vector<bf16_t> packed(chain_r50_weight_elems(nblk));
+    std::vector<float> bias(chain_r50_bias_floats(nblk), 0.f);
+    for (int blk = 0; blk < nblk; ++blk) {
+        const Op* op[3];
+        const DevConvW* cw[3];
+        std::vector<bf16_t> rows[3];
+        for (int k = 0; k < 3; ++k) {
+            op[k] = &h->ops[r.conv_ops[3 * blk + k]];
+            cw[k] = &h->convw[op[k]->wi];
+            if (cw[k]->w8 || !cw[k]->bias || op[k]->act != 1) {
+                set_error("plan: chain_r50 member conv is not bf16 / f16 + bias + ReLU");
+                return FR_ERR_ARG;
+            }
+            rows[k].resize((size_t)cw[k]->Npad * cw[k]->Kpad);
+            FR_HIP_CHECK(hipMemcpy(rows[k].data(), cw[k]->w, rows[k].size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
+        }
+        const bool shapes = cw[0]->Cout == 256 && cw[0]->K == 1024 && cw[0]->Kh == 1 && cw[0]->Kw == 1 &&
+                            cw[1]->Cout == 256 && cw[1]->K == 2304 && cw[1]->Kh == 3 && cw[1]->Kw == 3 &&
+                            op[1]->sh == 1 && op[1]->ph == 1 && op[1]->pw == 1 &&
+                            cw[2]->Cout == 1024 && cw[2]->K == 256 && cw[2]->Kh == 1 && cw[2]->Kw == 1 &&
+                            op[2]->res >= 0 && op[2]->res_off == 0 && op[0]->res < 0 && op[1]->res < 0;
+        if (!shapes) {
+            set_error("plan: chain_r50 member convs do not have layer3's Bottleneck shapes");
+            return FR_ERR_ARG;
+        }
+        chain_r50_pack_block(rows[0].data(), cw[0]->Kpad, rows[1].data(), cw[1]->Kpad, rows[2].data(), cw[2]->Kpad, blk,
+                             nblk, packed.data());
+        float* t = bias.data() + chain_r50_bias_floats(1) * blk;
+        FR_HIP_CHECK(hipMemcpy(t, cw[0]->bias, 256 * sizeof(float), hipMemcpyDeviceToHost));
+        FR_HIP_CHECK(hipMemcpy(t + 256, cw[1]->bias, 256 * sizeof(float), hipMemcpyDeviceToHost));
+        FR_HIP_CHECK(hipMemcpy(t + 512, cw[2]->bias, 1024 * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    int rc = upload(h, &r.cw, packed);
+    if (rc) return rc;
+    return upload(h, &r.cbias, bias);
+}
+
 // Packs IRV1 repeat_1's member convs (per block: branch1.0 + branch2.0 + branch0 as one 1x1 256 -> 96, branch1.1,
 // branch2.1, branch2.2 3x3 32 -> 32, conv2d 96 -> 256 with the residual) for conv_chain35.hip.
 int build_chain35(fr_handle* h, StageRec& r) {
@@ -1116,10 +1162,24 @@ void build_resnet50(Builder& b) {
     b.maxpool(c1, x, 0, 3, 2, 1);
     const int planes[4] = {64, 128, 256, 512}, nblk[4] = {3, 4, 6, 3}, strd[4] = {1, 2, 2, 2};
     int H = 28, C = 64;
+    // layer3.1 .. layer3.5 (7x7x1024) are also emitted as one chain launch (conv_chain_r50.hip) beside their member
+    // convs; the faster is measured per batch size
+    int ch_op = -1;
+    StageRec ch;
     for (int l = 0; l < 4; ++l) {
         const int P = planes[l];
         for (int i = 0; i < nblk[l]; ++i) {
             const std::string pre = "backbone." + L(l + 1, i);
+            if (l == 2 && i == 1 && h->dtype != FR_DTYPE_FP8 && H == 7 && chain_r50_supported(H, H, C, nblk[l] - 1)) {
+                ch_op = (int)h->ops.size();
+                Op op;
+                op.kind = OP_STAGE;
+                op.stage = (int)h->stages.size();
+                h->ops.push_back(op);
+                ch.chain = 50;
+                ch.in = x; ch.H = H; ch.C = C; ch.nblk = nblk[l] - 1;
+            }
+            const size_t op0 = h->ops.size();
             const int s = i == 0 ? strd[l] : 1;
             const int Ho = (H + 2 - 3) / s + 1;
             const int h1 = b.tensor(H, H, P);
@@ -1137,9 +1197,17 @@ void build_resnet50(Builder& b) {
                 b.conv_ds({pre + ".conv3"}, h2, 0, P, y, 0, 1, 1, 1, 1, 0, 0, 1, -1, 0, -1, "", pre + ".downsample", x, C, s);
             else
                 b.conv({pre + ".conv3"}, h2, 0, P, y, 0, 1, 1, 1, 1, 0, 0, 1, id, 0);
+            if (ch_op >= 0 && l == 2 && i >= 1)
+                for (size_t k = op0; k < h->ops.size(); ++k) ch.conv_ops.push_back((int)k);
             x = y;
             C = 4 * P;
             H = Ho;
+        }
+        if (ch_op >= 0 && l == 2 && !b.rc) {
+            ch.out = x;
+            for (int oi : ch.conv_ops) h->ops[oi].stage = h->ops[ch_op].stage;
+            b.rc = build_chain_r50(h, ch);
+            h->stages.push_back(ch);
         }
     }
     const int pool = b.tensor(1, 1, C, "backbone.avgpool");
@@ -1834,11 +1902,12 @@ static bool trans_enabled() {
     return on;
 }
 
-// FR_AB no_chain: IRV1 repeat_1 / repeat_2 always run as their member convs (A/B timing); no_chain17 / no_chain35:
-// only that one
+// FR_AB no_chain: IRV1 repeat_1 / repeat_2 and ResNet-50 layer3 always run as their member convs (A/B timing);
+// no_chain17 / no_chain35 / no_chain50: only that one
 static bool chain_enabled(int kind) {
-    static const bool all = !ab_int("no_chain", 0), c17 = !ab_int("no_chain17", 0), c35 = !ab_int("no_chain35", 0);
-    return all && (kind == 17 ? c17 : c35);
+    static const bool all = !ab_int("no_chain", 0), c17 = !ab_int("no_chain17", 0), c35 = !ab_int("no_chain35", 0),
+                      c50 = !ab_int("no_chain50", 0);
+    return all && (kind == 17 ? c17 : kind == 35 ? c35 : c50);
 }
 
 // FR_AB no_stem160: the IRV1 stem always runs as its member ops (A/B timing)
@@ -1849,7 +1918,7 @@ static bool ab_stem160() {
 
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     if (h->stage_mode == 0 || h->invariant) return false;
-    const int kind_bit = r.stem ? 2 : (r.chain == 35 ? 4 : (r.chain ? 8 : 1));
+    const int kind_bit = r.stem ? 2 : r.chain == 35 ? 4 : r.chain == 50 ? 16 : r.chain ? 8 : 1;
     if (!(h->fused_mask & kind_bit)) return false;
     // the fused transition keeps no t tensor and records no amax
     if (r.trans && (h->keep_inter || (h->amax && h->need_amax[r.out]) || !trans_enabled())) return false;
@@ -2021,6 +2090,19 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
         ps.bytes = 2.0 * 2.0 * B * 289.0 * 256.0 + 2.0 * 76800.0 * r.nblk;
         ps.start("chain block35");
         FR_HIP_CHECK(launch_chain35(c, s));
+        return FR_OK;
+    }
+    if (r.chain == 50) {
+        Chain17Args c{};
+        c.x = h->tensors[r.in].dev;
+        c.y = h->tensors[r.out].dev;
+        c.w = r.cw; c.bias = r.cbias; c.B = B; c.nblk = r.nblk; c.f16 = f16;
+        ProfScope ps(h, s);
+        // per block and pixel: 1024 x 256 + 2304 x 256 + 256 x 1024 = 1,114,112 MACs
+        ps.flops = 2.0 * B * 49.0 * 1114112.0 * r.nblk;
+        ps.bytes = 2.0 * 2.0 * B * 49.0 * 1024.0 + 2.0 * 1114112.0 * r.nblk;
+        ps.start("chain r50 layer3");
+        FR_HIP_CHECK(launch_chain_r50(c, s));
         return FR_OK;
     }
     if (r.chain) {
@@ -2915,6 +2997,12 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
                    meas_note(h, op.grp, B) + "\n";
             continue;
         }
+        if (op.kind == OP_STAGE && h->stages[op.stage].chain == 50) {  // per block: M x 1024 x 1088 MACs (1,114,112 per pixel)
+            const StageRec& r = h->stages[op.stage];
+            out += "chain " + std::to_string(B * 49) + " 1024 1088 1088 " + std::to_string(r.nblk) + " 1 3x3 " +
+                   h->tensors[r.out].name + meas_note(h, op.grp, B) + "\n";
+            continue;
+        }
         if (op.kind == OP_STAGE && h->stages[op.stage].chain == 35) {  // per block: M x 256 x 300 MACs (76,800 per pixel)
             const StageRec& r = h->stages[op.stage];
             out += "chain " + std::to_string(B * 289) + " 256 300 300 " + std::to_string(r.nblk) + " 1 3x3 " +
@@ -3009,7 +3097,7 @@ int fr_set_option(fr_handle* h, int option, int value) {
             }
             break;
         case FR_OPT_FUSED_MASK:
-            if (value < 0 || value > 15) { set_error("fr_set_option: FR_OPT_FUSED_MASK is 0 .. 15"); return FR_ERR_ARG; }
+            if (value < 0 || value > 31) { set_error("fr_set_option: FR_OPT_FUSED_MASK is 0 .. 31"); return FR_ERR_ARG; }
             h->fused_mask = value;
             break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;

@@ -195,6 +195,15 @@ size_t chain17_bias_floats(int nblk);
 void chain17_pack_block(const bf16_t* rA, int kpA, const bf16_t* r17, int kp17, const bf16_t* r71, int kp71,
                         const bf16_t* rE, int kpE, int blk, int nblk, bf16_t* out);
 hipError_t launch_chain17(const Chain17Args& a, hipStream_t s);
+// ResNet-50 layer3.1 .. layer3.5 (five Bottlenecks at 7x7x1024) as one launch, one workgroup per image
+// (conv_chain_r50.hip); the args are Chain17Args' (x = layer3.0's output, y = the last block's, w =
+// chain_r50_pack_block streams, bias = [nblk][conv1 256 | conv2 256 | conv3 1024] f32)
+bool chain_r50_supported(int H, int W, int C, int nblk);
+size_t chain_r50_weight_elems(int nblk);
+size_t chain_r50_bias_floats(int nblk);
+void chain_r50_pack_block(const bf16_t* r1, int kp1, const bf16_t* r2, int kp2, const bf16_t* r3, int kp3, int blk,
+                          int nblk, bf16_t* out);
+hipError_t launch_chain_r50(const Chain17Args& a, hipStream_t s);
 // FaceNet IRV1 stem at 160x160 (conv_stem160.hip): conv2d_1a (3x3/s2 8 -> 32) + conv2d_2a (3x3 32 -> 32) +
 // conv2d_2b (3x3/p1 32 -> 64) + maxpool_3a (3x3/s2) + conv2d_3b (1x1 64 -> 80), each conv + bias + ReLU, as one
 // launch, one workgroup per image; input: u8 crops [B][160][160][3] (u8 != null: the preparation is done in-kernel)

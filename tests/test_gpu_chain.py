@@ -163,3 +163,58 @@ def test_chain35_matches_member_convs(gpu, dtype, B):
     # rounding-level differences at repeat_1 are amplified by the bf16 body after it (see the stem test)
     tol = 1e-3 if dtype == "bf16" else 5e-5
     assert np.all(1 - cos <= tol), f"chain35 vs member-conv embeddings: 1-cos = {1 - cos}"
+
+
+# ---- ResNet-50 layer3.1 .. layer3.5 as one launch (conv_chain_r50.hip: five Bottlenecks at 7x7x1024, the block input
+# resident in LDS; reference: arcface_model.py:118-132, the torchvision resnet50 backbone)
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("B", [1, 3, 9])
+def test_chain_r50_matches_member_convs(gpu, dtype, B):
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("resnet50_arcface", dtype=dtype)
+    x = torch.from_numpy(synthetic_crops(B, 112, seed=29))
+    m.set_option(N.FR_OPT_STAGE, 2)
+    m.set_option(N.FR_OPT_FUSED_MASK, 16)
+    assert " 1024 1088 1088 5 " in _plan(m, B)
+    e_f = m.embed(x).cpu().numpy()
+    e_f2 = m.embed(x).cpu().numpy()  # graph replay
+    in_f = _tensor(m, B, "backbone.layer3.0")
+    y_f = _tensor(m, B, "backbone.layer3.5")
+    m.set_option(N.FR_OPT_STAGE, 0)
+    assert " 1024 1088 1088 5 " not in _plan(m, B)
+    e_c = m.embed(x).cpu().numpy()
+    in_c = _tensor(m, B, "backbone.layer3.0")
+    y_c = _tensor(m, B, "backbone.layer3.5")
+    m.close()
+    assert np.array_equal(e_f, e_f2)
+    assert torch.equal(in_f, in_c), "the chain's input differs: the runs are not comparable"
+    rel = ((y_f - y_c).norm() / y_c.norm()).item()
+    cos = np.sum(e_f * e_c, axis=1)
+    print(f"{dtype} B={B}: layer3.5 rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
+    # 15 roundings to 16 bits per element in both paths; a different f32 summation order flips a few of them
+    assert rel < (6e-3 if dtype == "bf16" else 1.5e-3), f"layer3.5: chain vs member convs rel err {rel:.3e}"
+    tol = 2e-4 if dtype == "bf16" else 2e-5
+    assert np.all(1 - cos <= tol), f"chain_r50 vs member-conv embeddings: 1-cos = {1 - cos}"
+
+
+def test_chain_r50_full_batch_against_oracle(gpu):
+    """bs = 256 (one image per CU), the chain forced on: sampled faces within the 1e-3 cosine bar of the fp32 oracle
+    (the reference's own ResNet-50 ArcFace, golden-pinned in test_golden.py)."""
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    from facerecognition_amd.weights import synth_state_dict
+    from oracle import models as M
+    B = 256
+    m = FRModel.synthetic("resnet50_arcface", max_batch=B)
+    m.set_option(N.FR_OPT_STAGE, 2)
+    u8 = synthetic_crops(B, 112, seed=31)
+    e = m.embed(torch.from_numpy(u8)).cpu().numpy()
+    assert " 1024 1088 1088 5 " in _plan(m, B)
+    m.close()
+    assert np.all(np.isfinite(e))
+    idx = np.arange(0, B, 32)
+    ref = M.embed(M.build_model("resnet50_arcface", synth_state_dict("resnet50_arcface")), "resnet50_arcface", u8[idx])
+    cos = np.sum(e[idx] * ref, axis=1) / (np.linalg.norm(e[idx], axis=1) * np.linalg.norm(ref, axis=1))
+    print(f"chain_r50 bs=256 vs oracle: max 1-cos {float((1 - cos).max()):.2e}")
+    assert np.all(1 - cos <= 1e-3), f"1-cos vs oracle {1 - cos}"

@@ -119,10 +119,19 @@ def test_stage_auto_rule_by_batch(gpu):
 
 
 def test_stage_absent_for_other_archs(gpu):
+    """ResNet-50 gets none of IResNet100's LDS-resident stages or fused transition; its one fused launch is the
+    layer3.1-3.5 chain (round 6, conv_chain_r50.hip), which the stage option governs like the others."""
+    import ctypes
     from facerecognition_amd.model import FRModel
     m = FRModel.synthetic("resnet50_arcface")
-    assert m.get_option(N.FR_OPT_STAGE) == 0
+    assert m.get_option(N.FR_OPT_STAGE) == 1
+    m.set_option(N.FR_OPT_STAGE, 2)
+    buf = ctypes.create_string_buffer(1 << 20)
+    N.check(N.lib().fr_debug_plan(m.handle, 256, buf, len(buf)), "fr_debug_plan")
+    lines = buf.value.decode().splitlines()
     m.close()
+    assert not [ln for ln in lines if ln.split()[0] in ("stage", "stage8", "trans", "stem160")]
+    assert [ln for ln in lines if ln.startswith("chain ") and " 1024 1088 1088 5 " in ln]
 
 
 SPLIT_CASES = [("layer2.12", "layer2.1.prelu", 2, B) for B in (1, 3, 17, 130)] + \
