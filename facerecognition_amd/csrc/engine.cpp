@@ -139,7 +139,8 @@ struct StageRec {
     // IRV1 repeat_2 as one launch (chain 17, conv_chain.hip): conv_ops = per block {branch1.0 + branch0, 1x7, 7x1,
     // conv2d}; repeat_1 (chain 35, conv_chain35.hip): per block {branch1.0 + branch2.0 + branch0, branch1.1, branch2.1,
     // branch2.2, conv2d}, x_tensors = the block outputs; ResNet-50 layer3.1 .. 3.5 (chain 50, conv_chain_r50.hip):
-    // per block {conv1, conv2, conv3}
+    // per block {conv1, conv2, conv3}; ResNet-50 layer1.1 / 1.2 (chain 28, conv_bneck28.hip, one launch per block):
+    // per block {conv1, conv2, conv3}, x_tensors = the block outputs
     int chain = 0;
     bf16_t* cw = nullptr;                 // the packed weights of all blocks
     float* cbias = nullptr;               // the member convs' biases
@@ -253,7 +254,7 @@ struct fr_handle {
     // FR_OPT_BATCH_INVARIANT: every kernel choice sums K in the implicit GEMM's order (no split-K, no stage /
     // transition kernel, a fixed head split), so a face's embedding does not depend on its batch
     bool invariant = false;
-    int fused_mask = 31;  // FR_OPT_FUSED_MASK
+    int fused_mask = 63;  // FR_OPT_FUSED_MASK
     const uint8_t* fwd_u8 = nullptr;  // the current forward's u8 crops when the IRV1 fused stem prepares them itself
 };
 
@@ -898,6 +899,51 @@ int build_chain_r50(fr_handle* h, StageRec& r) {
     return upload(h, &r.cbias, bias);
 }
 
+// Packs ResNet-50 layer1.1 / layer1.2's member convs (conv1 1x1 256 -> 64, conv2 3x3 64 -> 64, conv3 1x1 64 -> 256
+// with the residual; BN folded, each + bias + ReLU) into conv_bneck28.hip's per-quarter register images.
+int build_bneck28(fr_handle* h, StageRec& r) {
+    const int nblk = r.nblk;
+    if ((int)r.conv_ops.size() != 3 * nblk || (int)r.x_tensors.size() != nblk) {
+        set_error("plan: bneck28 member count");
+        return FR_ERR_ARG;
+    }
+    std::vector<bf16_t> packed(bneck28_weight_elems(nblk));
+    std::vector<float> bias((size_t)nblk * 384, 0.f);
+    for (int blk = 0; blk < nblk; ++blk) {
+        const Op* op[3];
+        const DevConvW* cw[3];
+        std::vector<bf16_t> rows[3];
+        for (int k = 0; k < 3; ++k) {
+            op[k] = &h->ops[r.conv_ops[3 * blk + k]];
+            cw[k] = &h->convw[op[k]->wi];
+            if (op[k]->kind != OP_CONV || cw[k]->w8 || !cw[k]->bias || op[k]->act != 1) {
+                set_error("plan: bneck28 member conv is not bf16 / f16 + bias + ReLU");
+                return FR_ERR_ARG;
+            }
+            rows[k].resize((size_t)cw[k]->Npad * cw[k]->Kpad);
+            FR_HIP_CHECK(hipMemcpy(rows[k].data(), cw[k]->w, rows[k].size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
+        }
+        const bool shapes = cw[0]->Cout == 64 && cw[0]->K == 256 && cw[0]->Kh == 1 && cw[0]->Kw == 1 &&
+                            cw[1]->Cout == 64 && cw[1]->K == 576 && cw[1]->Kh == 3 && cw[1]->Kw == 3 &&
+                            op[1]->sh == 1 && op[1]->ph == 1 && op[1]->pw == 1 &&
+                            cw[2]->Cout == 256 && cw[2]->K == 64 && cw[2]->Kh == 1 && cw[2]->Kw == 1 &&
+                            op[2]->res >= 0 && op[2]->res_off == 0 && op[0]->res < 0 && op[1]->res < 0;
+        if (!shapes) {
+            set_error("plan: bneck28 member convs do not have layer1's Bottleneck shapes");
+            return FR_ERR_ARG;
+        }
+        bneck28_pack_block(rows[0].data(), cw[0]->Kpad, rows[1].data(), cw[1]->Kpad, rows[2].data(), cw[2]->Kpad, blk,
+                           packed.data());
+        float* t = bias.data() + 384 * blk;
+        FR_HIP_CHECK(hipMemcpy(t, cw[0]->bias, 64 * sizeof(float), hipMemcpyDeviceToHost));
+        FR_HIP_CHECK(hipMemcpy(t + 64, cw[1]->bias, 64 * sizeof(float), hipMemcpyDeviceToHost));
+        FR_HIP_CHECK(hipMemcpy(t + 128, cw[2]->bias, 256 * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    int rc = upload(h, &r.cw, packed);
+    if (rc) return rc;
+    return upload(h, &r.cbias, bias);
+}
+
 // Packs IRV1 repeat_1's member convs (per block: branch1.0 + branch2.0 + branch0 as one 1x1 256 -> 96, branch1.1,
 // branch2.1, branch2.2 3x3 32 -> 32, conv2d 96 -> 256 with the residual) for conv_chain35.hip.
 int build_chain35(fr_handle* h, StageRec& r) {
@@ -1164,12 +1210,22 @@ void build_resnet50(Builder& b) {
     int H = 28, C = 64;
     // layer3.1 .. layer3.5 (7x7x1024) are also emitted as one chain launch (conv_chain_r50.hip) beside their member
     // convs; the faster is measured per batch size
-    int ch_op = -1;
-    StageRec ch;
+    int ch_op = -1, bn_op = -1;
+    StageRec ch, bn;
     for (int l = 0; l < 4; ++l) {
         const int P = planes[l];
         for (int i = 0; i < nblk[l]; ++i) {
             const std::string pre = "backbone." + L(l + 1, i);
+            // layer1.1 / layer1.2 (28x28x256) likewise, one launch per block (conv_bneck28.hip)
+            if (l == 0 && i == 1 && h->dtype != FR_DTYPE_FP8 && bneck28_supported(H, H, C, P)) {
+                bn_op = (int)h->ops.size();
+                Op op;
+                op.kind = OP_STAGE;
+                op.stage = (int)h->stages.size();
+                h->ops.push_back(op);
+                bn.chain = 28;
+                bn.in = x; bn.H = H; bn.C = C; bn.nblk = nblk[l] - 1;
+            }
             if (l == 2 && i == 1 && h->dtype != FR_DTYPE_FP8 && H == 7 && chain_r50_supported(H, H, C, nblk[l] - 1)) {
                 ch_op = (int)h->ops.size();
                 Op op;
@@ -1199,9 +1255,19 @@ void build_resnet50(Builder& b) {
                 b.conv({pre + ".conv3"}, h2, 0, P, y, 0, 1, 1, 1, 1, 0, 0, 1, id, 0);
             if (ch_op >= 0 && l == 2 && i >= 1)
                 for (size_t k = op0; k < h->ops.size(); ++k) ch.conv_ops.push_back((int)k);
+            if (bn_op >= 0 && l == 0 && i >= 1) {
+                for (size_t k = op0; k < h->ops.size(); ++k) bn.conv_ops.push_back((int)k);
+                bn.x_tensors.push_back(y);
+            }
             x = y;
             C = 4 * P;
             H = Ho;
+        }
+        if (bn_op >= 0 && l == 0 && !b.rc) {
+            bn.out = x;
+            for (int oi : bn.conv_ops) h->ops[oi].stage = h->ops[bn_op].stage;
+            b.rc = build_bneck28(h, bn);
+            h->stages.push_back(bn);
         }
         if (ch_op >= 0 && l == 2 && !b.rc) {
             ch.out = x;
@@ -1902,12 +1968,12 @@ static bool trans_enabled() {
     return on;
 }
 
-// FR_AB no_chain: IRV1 repeat_1 / repeat_2 and ResNet-50 layer3 always run as their member convs (A/B timing);
-// no_chain17 / no_chain35 / no_chain50: only that one
+// FR_AB no_chain: IRV1 repeat_1 / repeat_2 and ResNet-50 layer1 / layer3 always run as their member convs (A/B
+// timing); no_chain17 / no_chain35 / no_chain50 / no_bneck28: only that one
 static bool chain_enabled(int kind) {
     static const bool all = !ab_int("no_chain", 0), c17 = !ab_int("no_chain17", 0), c35 = !ab_int("no_chain35", 0),
-                      c50 = !ab_int("no_chain50", 0);
-    return all && (kind == 17 ? c17 : kind == 35 ? c35 : c50);
+                      c50 = !ab_int("no_chain50", 0), c28 = !ab_int("no_bneck28", 0);
+    return all && (kind == 17 ? c17 : kind == 35 ? c35 : kind == 28 ? c28 : c50);
 }
 
 // FR_AB no_stem160: the IRV1 stem always runs as its member ops (A/B timing)
@@ -1918,7 +1984,7 @@ static bool ab_stem160() {
 
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     if (h->stage_mode == 0 || h->invariant) return false;
-    const int kind_bit = r.stem ? 2 : r.chain == 35 ? 4 : r.chain == 50 ? 16 : r.chain ? 8 : 1;
+    const int kind_bit = r.stem ? 2 : r.chain == 35 ? 4 : r.chain == 50 ? 16 : r.chain == 28 ? 32 : r.chain ? 8 : 1;
     if (!(h->fused_mask & kind_bit)) return false;
     // the fused transition keeps no t tensor and records no amax
     if (r.trans && (h->keep_inter || (h->amax && h->need_amax[r.out]) || !trans_enabled())) return false;
@@ -2090,6 +2156,21 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
         ps.bytes = 2.0 * 2.0 * B * 289.0 * 256.0 + 2.0 * 76800.0 * r.nblk;
         ps.start("chain block35");
         FR_HIP_CHECK(launch_chain35(c, s));
+        return FR_OK;
+    }
+    if (r.chain == 28) {
+        Chain17Args c{};
+        c.w = r.cw; c.bias = r.cbias; c.B = B; c.nblk = r.nblk; c.f16 = f16;
+        for (int i = 0; i < r.nblk; ++i) {
+            c.x = h->tensors[i ? r.x_tensors[i - 1] : r.in].dev;
+            c.y = h->tensors[r.x_tensors[i]].dev;
+            ProfScope ps(h, s);
+            // per pixel: 256 x 64 + 576 x 64 + 64 x 256 = 69,632 MACs
+            ps.flops = 2.0 * B * 784.0 * 69632.0;
+            ps.bytes = 2.0 * 2.0 * B * 784.0 * 256.0 + 2.0 * 69632.0;
+            ps.start("bneck28 layer1");
+            FR_HIP_CHECK(launch_bneck28(c, i, s));
+        }
         return FR_OK;
     }
     if (r.chain == 50) {
@@ -2997,6 +3078,12 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
                    meas_note(h, op.grp, B) + "\n";
             continue;
         }
+        if (op.kind == OP_STAGE && h->stages[op.stage].chain == 28) {  // per block: M x 256 x 272 MACs (69,632 per pixel)
+            const StageRec& r = h->stages[op.stage];
+            out += "chain " + std::to_string(B * 784) + " 256 272 272 " + std::to_string(r.nblk) + " 1 3x3 " +
+                   h->tensors[r.out].name + meas_note(h, op.grp, B) + "\n";
+            continue;
+        }
         if (op.kind == OP_STAGE && h->stages[op.stage].chain == 50) {  // per block: M x 1024 x 1088 MACs (1,114,112 per pixel)
             const StageRec& r = h->stages[op.stage];
             out += "chain " + std::to_string(B * 49) + " 1024 1088 1088 " + std::to_string(r.nblk) + " 1 3x3 " +
@@ -3097,7 +3184,7 @@ int fr_set_option(fr_handle* h, int option, int value) {
             }
             break;
         case FR_OPT_FUSED_MASK:
-            if (value < 0 || value > 31) { set_error("fr_set_option: FR_OPT_FUSED_MASK is 0 .. 31"); return FR_ERR_ARG; }
+            if (value < 0 || value > 63) { set_error("fr_set_option: FR_OPT_FUSED_MASK is 0 .. 63"); return FR_ERR_ARG; }
             h->fused_mask = value;
             break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;
