@@ -5,11 +5,13 @@
 // conv3 reads the residual again, and the 64-channel intermediates make two more HBM round trips.  Here one workgroup
 // owns one image and walks down it row by row, so only the block input (read once) and output (written once) touch
 // HBM:
-//   * phase r: conv1 of x row r + 1 into a 3-row ring of t1 rows (zero halo columns; a zero row stands in for the
-//     rows outside the image), conv2 of output row r from t1 rows r - 1 .. r + 1, conv3 of row r onto bias + the
-//     residual x row r into an LDS staging row, then the row's coalesced 16-B stores; four barriers per phase;
-//   * x rows arrive by LDS-DMA into a 4-row ring three phases ahead (inline asm, hidden from the compiler's waitcnt
-//     pass; counted vmcnt waits per phase: every phase issues the same VMEM ops, past the image a dummy row);
+//   * software-pipelined rows, ONE barrier per phase: phase r runs conv1 of x row r + 2 (into a 4-row ring of t1 rows
+//     with zero halo columns; a zero row stands in for the rows outside the image), conv2 of row r (t1 rows r - 1 ..
+//     r + 1, into a 2-row t2 ring) and conv3 of row r - 1 onto bias + the residual x row r - 1 (into a 2-row NHWC
+//     staging ring) -- three independent accumulator chains per wave, interleaved K-step by K-step -- after the
+//     coalesced 16-B stores of row r - 2 from the staging ring;
+//   * x rows arrive by LDS-DMA into a 6-row ring two phases ahead (inline asm, hidden from the compiler's waitcnt
+//     pass; counted vmcnt waits per phase; past the image a dummy row keeps the count fixed);
 //   * ALL weights live in registers for the whole kernel (34 fragments = 136 VGPRs per wave: wave w computes pixel
 //     fragment w >> 2 of the row -- 28 pixels in two 16-pixel fragments -- and output channels 16 (w & 3) .. of
 //     conv1 / conv2, 64 (w & 3) .. of conv3);
@@ -24,6 +26,8 @@
 
 #include <hip/hip_ext.h>
 
+#include <type_traits>
+
 namespace fr {
 namespace {
 
@@ -33,16 +37,18 @@ constexpr int XPL = IW * 16;               // 448: x plane bytes (one row)
 constexpr int XROW = (CX / 8) * XPL;       // 14336: one x row
 constexpr int TPL = 32 * 16;               // 512: t1 / t2 plane bytes (32 positions)
 constexpr int TROW = (CP / 8) * TPL;       // 4096
-constexpr int X_OFF = 0;                   // 4 x rows
-constexpr int T1_OFF = X_OFF + 4 * XROW;   // 57344: t1 rows (slots 0-2) + the zero row (slot 3)
-constexpr int T2_OFF = T1_OFF + 4 * TROW;  // 73728
-constexpr int Y_OFF = T2_OFF + TROW;       // 77824: the output row, NHWC, 16-B chunks XOR-swizzled by the pixel
-constexpr int BN28_LDS = Y_OFF + XROW;     // 92160
+constexpr int XR = 6;                      // x ring rows (7, three phases ahead, measured slower)
+constexpr int X_OFF = 0;
+constexpr int T1_OFF = X_OFF + XR * XROW;  // 86016: t1 rows (slots 0-3) + the zero row (slot 4)
+constexpr int T2_OFF = T1_OFF + 5 * TROW;  // 106496: 2 t2 rows
+constexpr int Y_OFF = T2_OFF + 2 * TROW;   // 114688: 2 output rows, NHWC, 16-B chunks XOR-swizzled by the pixel
+constexpr int BN28_LDS = Y_OFF + 2 * XROW; // 143360
 constexpr int NWV = 8;
 constexpr int NFR = 8 + 18 + 8;            // weight fragments per wave: conv1 8 K-steps, conv2 18, conv3 2 x 4
 constexpr int XPIECES = XROW / 16;         // 896 16-B pieces per row = 14 DMA instructions
 static_assert((8 * XPL) % 256 == 0 && TPL % 256 == 0, "conflict-free planes");
 static_assert(XPIECES == 14 * 64, "DMA split");
+static_assert(BN28_LDS <= 160 * 1024, "LDS");
 
 typedef int v4i32 __attribute__((ext_vector_type(4)));
 #pragma clang diagnostic push
@@ -66,19 +72,16 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
     return make_uint2(pack2_bf16(a, b), pack2_bf16(c, d));
 }
 
-// VMEM ops a wave issues per phase: D DMA instructions (waves 0-5: two of the 14, 6-7: one) and S row stores
-// (waves 0-5: two 16-B pieces per thread, 6-7: one)
+// Phase r waits for x row r + 2 (issued in phase r - 2, rows 0 / 1 before the loop).  VMEM ops per phase, in issue
+// order: D DMA instructions (the row r + 4; waves 0-5: two of the 14, 6-7: one), then S stores of row r - 2 when
+// r >= 2 (waves 0-5: two 16-B pieces per thread, 6-7: one).  Younger than row r + 2's DMA: phases -2 .. 2 -> the
+// next DMA only; 3 -> + phase 2's stores; >= 4 -> + phases r - 2 and r - 1's stores.
 template <int D, int S>
-struct Waits {
-    static constexpr int OPS = D + S;
-    __device__ static void before_row0() { wait_vm<3 * D>(); }                   // rows 1-3 may stay in flight
-    __device__ static void before(int r) {                                      // phase r needs x row r + 1
-        if (r >= 3) wait_vm<S + 2 * OPS>();
-        else if (r == 2) wait_vm<2 * OPS>();
-        else if (r == 1) wait_vm<D + OPS>();
-        else wait_vm<2 * D>();
-    }
-};
+__device__ __forceinline__ void wait_row(int r) {
+    if (r >= 4) wait_vm<D + 2 * S>();
+    else if (r == 3) wait_vm<D + S>();
+    else wait_vm<D>();
+}
 
 template <bool F16>
 __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
@@ -94,10 +97,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
     const bool pv = px < IW;
 
     // t1 (all slots: halos, the zero row) starts zero; epilogues write interior positions only
-    for (int i = threadIdx.x; i < 4 * TROW / 16; i += 64 * NWV) *(uint4*)(smem + T1_OFF + i * 16) = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < 5 * TROW / 16; i += 64 * NWV) *(uint4*)(smem + T1_OFF + i * 16) = make_uint4(0, 0, 0, 0);
 
-    // ---- weights (this wave's 34 fragments) and biases, into registers once
-    const frag* wp = (const frag*)p.w + (size_t)(blockIdx.y * 4 + q) * NFR * 64 + lane;
+    // ---- weights (this wave's 34 fragments) and biases, into registers once (issued before the first x rows: the
+    // first row wait covers them)
+    const frag* wp = (const frag*)p.w + (size_t)q * NFR * 64 + lane;
     frag w1[8], w2[18], w3[2][4];
 #pragma unroll
     for (int s = 0; s < 8; ++s) w1[s] = wp[64 * s];
@@ -107,13 +111,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
     for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i) w3[s][i] = wp[64 * (26 + 4 * s + i)];
-    const float* bb = p.bias + (size_t)blockIdx.y * 384;
-    const float4 b1 = *(const float4*)(bb + 16 * q + 4 * lg), b2 = *(const float4*)(bb + 64 + 16 * q + 4 * lg);
+    const float4 b1 = *(const float4*)(p.bias + 16 * q + 4 * lg), b2 = *(const float4*)(p.bias + 64 + 16 * q + 4 * lg);
     float4 b3[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) b3[i] = *(const float4*)(bb + 128 + 16 * (4 * q + i) + 4 * lg);
-    // (issued before the first x rows: the row-0 wait below covers them)
-
+    for (int i = 0; i < 4; ++i) b3[i] = *(const float4*)(p.bias + 128 + 16 * (4 * q + i) + 4 * lg);
 
     // ---- x row DMA: instruction k (0..13) = pieces 64 k .. 64 k + 63 (piece = plane * 28 + pixel); wave w issues k = w
     // and k = w + 8 (< 14)
@@ -128,97 +129,111 @@ __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
     auto dma_row = [&](int row) {  // rows past the image re-read the last one (a dummy keeping the VMEM count fixed)
         const int rr = row < IW ? row : IW - 1;
         const uint32_t so = (uint32_t)(((size_t)b * IW + rr) * IW * CX * 2);
-        char* const dst = smem + X_OFF + (row & 3) * XROW;
+        char* const dst = smem + X_OFF + (row % XR) * XROW;
         dma16(xr, (uint32_t)(uintptr_t)(dst + 1024 * wave), src0, so);
         if (wave + 8 < 14) dma16(xr, (uint32_t)(uintptr_t)(dst + 1024 * (wave + 8)), src1, so);
     };
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dma_row(r);
+    dma_row(0);
+    dma_row(1);
 
-
-    // conv1 of x row `row` (< 28) into t1 slot row % 3
-    auto conv1 = [&](int row) {
-        f32x4_t acc = (f32x4_t){b1.x, b1.y, b1.z, b1.w};
-        const char* xs = smem + X_OFF + (row & 3) * XROW + px * 16;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) acc = T::mfma(w1[s], *(const frag*)(xs + (s + 8 * lg) * XPL), acc);
-        if (pv)
-            *(uint2*)(smem + T1_OFF + (row % 3) * TROW + (2 * q + (lg >> 1)) * TPL + (px + 1) * 16 + (lg & 1) * 8) =
-                pack4<F16>(fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f), fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
-    };
-    const uint32_t ysw = (uint32_t)(px & 31);  // the staging row's chunk swizzle of the lane's pixel
-
-    Waits<2, 2> wa;
-    Waits<1, 1> wb;
-    if (wave < 6) wa.before_row0(); else wb.before_row0();
-    lds_barrier();  // row 0 landed everywhere; t1 zeroed
-    conv1(0);
-
-#pragma unroll 1
-    for (int r = 0; r < IW; ++r) {
-        if (wave < 6) wa.before(r); else wb.before(r);
-        lds_barrier();  // x row r + 1 landed everywhere; t1 row r (and r - 1) complete
-        if (r + 1 < IW) conv1(r + 1);
-        lds_barrier();  // t1 row r + 1 complete
-        // conv2 of row r: tap (kh, kw), channel half c: K-step 2 (3 kh + kw) + c; rows outside the image read the zero row
-        {
-            f32x4_t acc = (f32x4_t){b2.x, b2.y, b2.z, b2.w};
-#pragma unroll
-            for (int kh = 0; kh < 3; ++kh) {
-                const int row = r + kh - 1;
-                const int slot = (unsigned)row < (unsigned)IW ? row % 3 : 3;
-                const char* ts = smem + T1_OFF + slot * TROW + lg * TPL + px * 16;
-#pragma unroll
-                for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c)
-                        acc = T::mfma(w2[2 * (3 * kh + kw) + c], *(const frag*)(ts + 4 * c * TPL + kw * 16), acc);
-            }
-            if (pv)
-                *(uint2*)(smem + T2_OFF + (2 * q + (lg >> 1)) * TPL + px * 16 + (lg & 1) * 8) =
-                    pack4<F16>(fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f), fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
-        }
-        lds_barrier();  // t2 row r complete
-        // conv3 of row r onto bias + the residual x row r, into the staging row
-        {
-            f32x4_t acc[4];
-            const char* xs = smem + X_OFF + (r & 3) * XROW + px * 16 + (lg & 1) * 8;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint2 xv = *(const uint2*)(xs + (2 * (4 * q + i) + (lg >> 1)) * XPL);  // (px >= 28: never stored)
-                float f[8];
-                T::unpack8(make_uint4(xv.x, xv.y, 0, 0), f);
-                acc[i] = (f32x4_t){b3[i].x + f[0], b3[i].y + f[1], b3[i].z + f[2], b3[i].w + f[3]};
-            }
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const frag bq = *(const frag*)(smem + T2_OFF + (4 * s + lg) * TPL + px * 16);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc[i] = T::mfma(w3[s][i], bq, acc[i]);
-            }
-            if (pv) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t ch = 16 * (4 * q + i) + 4 * lg;  // 4 channels: chunk ch / 8, half (ch & 4)
-                    *(uint2*)(smem + Y_OFF + px * 512 + (((ch >> 3) ^ ysw) << 4) + (ch & 4) * 2) =
-                        pack4<F16>(fmaxf(acc[i][0], 0.f), fmaxf(acc[i][1], 0.f), fmaxf(acc[i][2], 0.f), fmaxf(acc[i][3], 0.f));
-                }
-            }
-        }
-        lds_barrier();  // staging row r complete; x row r consumed (its slot takes row r + 4)
-        dma_row(r + 4);
-        // row r -> y: 896 16-B pieces, contiguous in global; thread t stores pieces t and t + 512
-        bf16_t* yr = p.y + ((size_t)b * IW + r) * IW * CX;
+    const uint32_t ysw = (uint32_t)(px & 31);  // the staging rows' chunk swizzle of the lane's pixel
+    auto store_row = [&](int row) {  // staging slot row % 2 -> y row: 896 16-B pieces; thread t stores t and t + 512
+        bf16_t* yr = p.y + ((size_t)b * IW + row) * IW * CX;
+        const char* st = smem + Y_OFF + (row & 1) * XROW;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int k = threadIdx.x + 512 * u;
             if (k < XPIECES) {
                 const int x = k >> 5, c = k & 31;
-                *(uint4*)(yr + (size_t)k * 8) = *(const uint4*)(smem + Y_OFF + x * 512 + ((c ^ (x & 31)) << 4));
+                *(uint4*)(yr + (size_t)k * 8) = *(const uint4*)(st + x * 512 + ((c ^ (x & 31)) << 4));
             }
         }
-    }
-    wait_vm<0>();
+    };
+    auto t1_slot = [](int row) { return (unsigned)row < (unsigned)IW ? row & 3 : 4; };
+
+    // one phase: conv1 of row r + 2 (C1), conv2 of row r (C2), conv3 of row r - 1 (C3)
+    auto phase = [&](auto c1_tag, auto c2_tag, auto c3_tag, int r) {
+        constexpr bool C1 = decltype(c1_tag)::value, C2 = decltype(c2_tag)::value, C3 = decltype(c3_tag)::value;
+        if (wave < 6) wait_row<2, 2>(r); else wait_row<1, 1>(r);
+        lds_barrier();  // x row r + 2 landed; t1 row r + 1, t2 row r - 1 and staging row r - 2 complete; the slots
+                        // written below were last read in phase r - 1
+        dma_row(r + 4);  // into the slot of row r - 2 (last read by phase r - 1's conv3)
+        if (r >= 2) store_row(r - 2);
+
+        const int a = r + 2, c = r - 1;
+        const char* xs1 = smem + X_OFF + (C1 ? a % XR : 0) * XROW + px * 16;
+        const char* ts[3];
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) ts[kh] = smem + T1_OFF + t1_slot(r + kh - 1) * TROW + lg * TPL + px * 16;
+        const char* t2s = smem + T2_OFF + (C3 ? c & 1 : 0) * TROW + lg * TPL + px * 16;
+
+        f32x4_t a1 = (f32x4_t){b1.x, b1.y, b1.z, b1.w}, a2 = (f32x4_t){b2.x, b2.y, b2.z, b2.w}, a3[4];
+        if (C3) {
+            const char* xs = smem + X_OFF + (c % XR) * XROW + px * 16 + (lg & 1) * 8;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint2 xv = *(const uint2*)(xs + (2 * (4 * q + i) + (lg >> 1)) * XPL);  // (px >= 28: never stored)
+                float f[8];
+                T::unpack8(make_uint4(xv.x, xv.y, 0, 0), f);
+                a3[i] = (f32x4_t){b3[i].x + f[0], b3[i].y + f[1], b3[i].z + f[2], b3[i].w + f[3]};
+            }
+        }
+        // K-step k: conv2 step k (tap k / 2, channel half k % 2), conv1 step k (< 8), conv3 step k (< 2)
+        auto rd = [&](int k, frag& f1, frag& f2, frag& f3) {
+            if (C2) {
+                const int t = k >> 1, kh = t / 3, kw = t - 3 * kh;
+                f2 = *(const frag*)(ts[kh] + 4 * (k & 1) * TPL + kw * 16);
+            }
+            if (C1 && k < 8) f1 = *(const frag*)(xs1 + (k + 8 * lg) * XPL);
+            if (C3 && k < 2) f3 = *(const frag*)(t2s + 4 * k * TPL);
+        };
+        frag f1[2], f2[2], f3[2];
+        constexpr int KS = C2 ? 18 : C1 ? 8 : 2;
+        rd(0, f1[0], f2[0], f3[0]);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            __builtin_amdgcn_sched_barrier(0);  // keep each step's loads in that step
+            if (k + 1 < KS) rd(k + 1, f1[(k + 1) & 1], f2[(k + 1) & 1], f3[(k + 1) & 1]);
+            if (C3 && k < 2) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a3[i] = T::mfma(w3[k][i], f3[k & 1], a3[i]);
+            }
+            if (C1 && k < 8) a1 = T::mfma(w1[k], f1[k & 1], a1);
+            if (C2) a2 = T::mfma(w2[k], f2[k & 1], a2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // epilogues (pixels < 28): t1 row a (position px + 1), t2 row r, staging row c
+        if (pv) {
+            if (C1)
+                *(uint2*)(smem + T1_OFF + (a & 3) * TROW + (2 * q + (lg >> 1)) * TPL + (px + 1) * 16 + (lg & 1) * 8) =
+                    pack4<F16>(fmaxf(a1[0], 0.f), fmaxf(a1[1], 0.f), fmaxf(a1[2], 0.f), fmaxf(a1[3], 0.f));
+            if (C2)
+                *(uint2*)(smem + T2_OFF + (r & 1) * TROW + (2 * q + (lg >> 1)) * TPL + px * 16 + (lg & 1) * 8) =
+                    pack4<F16>(fmaxf(a2[0], 0.f), fmaxf(a2[1], 0.f), fmaxf(a2[2], 0.f), fmaxf(a2[3], 0.f));
+            if (C3) {
+                char* const st = smem + Y_OFF + (c & 1) * XROW + px * 512;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t ch = 16 * (4 * q + i) + 4 * lg;  // 4 channels: chunk ch / 8, half (ch & 4)
+                    *(uint2*)(st + (((ch >> 3) ^ ysw) << 4) + (ch & 4) * 2) =
+                        pack4<F16>(fmaxf(a3[i][0], 0.f), fmaxf(a3[i][1], 0.f), fmaxf(a3[i][2], 0.f), fmaxf(a3[i][3], 0.f));
+                }
+            }
+        }
+    };
+    typedef std::true_type Y;
+    typedef std::false_type N;
+    phase(Y{}, N{}, N{}, -2);
+    phase(Y{}, N{}, N{}, -1);
+    phase(Y{}, Y{}, N{}, 0);
+#pragma unroll 1
+    for (int r = 1; r <= IW - 3; ++r) phase(Y{}, Y{}, Y{}, r);
+    phase(N{}, Y{}, Y{}, IW - 2);
+    phase(N{}, Y{}, Y{}, IW - 1);
+    phase(N{}, N{}, Y{}, IW);
+    lds_barrier();  // staging row 27 complete
+    store_row(IW - 1);
+    wait_vm<0>();  // (the dummy DMA rows too) -- nothing in flight when the workgroup ends
 }
 
 }  // namespace
@@ -255,7 +270,7 @@ hipError_t launch_bneck28(const Chain17Args& a, int blk, hipStream_t s) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, BN28_LDS);
         attr[a.f16 ? 1 : 0] = true;
     }
-    // blockIdx.y selects the block's weights and biases (grid.y = 1, offset through the pointers)
+    // the block's weights and biases: offset through the pointers
     Chain17Args b = a;
     b.w = a.w + (size_t)blk * 4 * NFR * 512;
     b.bias = a.bias + (size_t)blk * 384;
