@@ -139,9 +139,11 @@ struct StageRec {
     // IRV1 repeat_2 as one launch (chain 17, conv_chain.hip): conv_ops = per block {branch1.0 + branch0, 1x7, 7x1,
     // conv2d}; repeat_1 (chain 35, conv_chain35.hip): per block {branch1.0 + branch2.0 + branch0, branch1.1, branch2.1,
     // branch2.2, conv2d}, x_tensors = the block outputs; ResNet-50 layer3.1 .. 3.5 (chain 50, conv_chain_r50.hip):
-    // per block {conv1, conv2, conv3}; ResNet-50 layer1.1 / 1.2 (chain 28, conv_bneck28.hip, one launch per block):
-    // per block {conv1, conv2, conv3}, x_tensors = the block outputs
+    // per block {conv1, conv2, conv3}; ResNet-50 layer1 (chain 28, conv_bneck28.hip, one launch per block): per block
+    // {conv1, conv2, conv3}, x_tensors = the block outputs; bn_ds: the first is layer1.0 (conv3 + K-concatenated
+    // downsample)
     int chain = 0;
+    bool bn_ds = false;
     bf16_t* cw = nullptr;                 // the packed weights of all blocks
     float* cbias = nullptr;               // the member convs' biases
     // IRV1 stem as one launch (conv_stem160.hip): conv_ops = {conv2d_1a, conv2d_2a, conv2d_2b, maxpool_3a}
@@ -907,9 +909,11 @@ int build_bneck28(fr_handle* h, StageRec& r) {
         set_error("plan: bneck28 member count");
         return FR_ERR_ARG;
     }
-    std::vector<bf16_t> packed(bneck28_weight_elems(nblk));
+    std::vector<bf16_t> packed(bneck28_block_elems(false) * nblk + (r.bn_ds ? bneck28_block_elems(true) - bneck28_block_elems(false) : 0));
     std::vector<float> bias((size_t)nblk * 384, 0.f);
+    size_t w_off = 0;
     for (int blk = 0; blk < nblk; ++blk) {
+        const bool ds = r.bn_ds && blk == 0;
         const Op* op[3];
         const DevConvW* cw[3];
         std::vector<bf16_t> rows[3];
@@ -923,17 +927,21 @@ int build_bneck28(fr_handle* h, StageRec& r) {
             rows[k].resize((size_t)cw[k]->Npad * cw[k]->Kpad);
             FR_HIP_CHECK(hipMemcpy(rows[k].data(), cw[k]->w, rows[k].size() * sizeof(bf16_t), hipMemcpyDeviceToHost));
         }
-        const bool shapes = cw[0]->Cout == 64 && cw[0]->K == 256 && cw[0]->Kh == 1 && cw[0]->Kw == 1 &&
+        const bool common = cw[0]->Cout == 64 && cw[0]->K == (ds ? 64 : 256) && cw[0]->Kh == 1 && cw[0]->Kw == 1 &&
                             cw[1]->Cout == 64 && cw[1]->K == 576 && cw[1]->Kh == 3 && cw[1]->Kw == 3 &&
-                            op[1]->sh == 1 && op[1]->ph == 1 && op[1]->pw == 1 &&
-                            cw[2]->Cout == 256 && cw[2]->K == 64 && cw[2]->Kh == 1 && cw[2]->Kw == 1 &&
-                            op[2]->res >= 0 && op[2]->res_off == 0 && op[0]->res < 0 && op[1]->res < 0;
+                            op[1]->sh == 1 && op[1]->ph == 1 && op[1]->pw == 1 && cw[2]->Cout == 256 &&
+                            cw[2]->Kh == 1 && cw[2]->Kw == 1 && op[0]->res < 0 && op[1]->res < 0 && op[0]->in_off == 0;
+        // layer1.0: conv3's K = [t2 64 | maxpool output 64] at stride 1, no residual; 1.1 / 1.2: K 64 + the residual x
+        const bool shapes = common && (ds ? cw[2]->K == 128 && cw[2]->K1 == 64 && cw[2]->C2 == 64 && op[2]->x2 == op[0]->in &&
+                                                op[2]->x2_off == 0 && op[2]->st2 == 1 && op[2]->res < 0
+                                          : cw[2]->K == 64 && op[2]->x2 < 0 && op[2]->res == op[0]->in && op[2]->res_off == 0);
         if (!shapes) {
             set_error("plan: bneck28 member convs do not have layer1's Bottleneck shapes");
             return FR_ERR_ARG;
         }
-        bneck28_pack_block(rows[0].data(), cw[0]->Kpad, rows[1].data(), cw[1]->Kpad, rows[2].data(), cw[2]->Kpad, blk,
-                           packed.data());
+        bneck28_pack_block(rows[0].data(), cw[0]->Kpad, rows[1].data(), cw[1]->Kpad, rows[2].data(), cw[2]->Kpad, ds,
+                           packed.data() + w_off);
+        w_off += bneck28_block_elems(ds);
         float* t = bias.data() + 384 * blk;
         FR_HIP_CHECK(hipMemcpy(t, cw[0]->bias, 64 * sizeof(float), hipMemcpyDeviceToHost));
         FR_HIP_CHECK(hipMemcpy(t + 64, cw[1]->bias, 64 * sizeof(float), hipMemcpyDeviceToHost));
@@ -1216,15 +1224,18 @@ void build_resnet50(Builder& b) {
         const int P = planes[l];
         for (int i = 0; i < nblk[l]; ++i) {
             const std::string pre = "backbone." + L(l + 1, i);
-            // layer1.1 / layer1.2 (28x28x256) likewise, one launch per block (conv_bneck28.hip)
-            if (l == 0 && i == 1 && h->dtype != FR_DTYPE_FP8 && bneck28_supported(H, H, C, P)) {
+            // layer1 (28x28) likewise, one launch per block (conv_bneck28.hip): from layer1.0 when its downsample folds
+            // into conv3 (fuse_ds), else from layer1.1
+            const bool bn_ds = i == 0 && C == P && b.fuse_ds(P, C, pre);
+            if (l == 0 && bn_op < 0 && (bn_ds || i == 1) && h->dtype != FR_DTYPE_FP8 && bneck28_supported(H, H, 4 * P, P)) {
                 bn_op = (int)h->ops.size();
                 Op op;
                 op.kind = OP_STAGE;
                 op.stage = (int)h->stages.size();
                 h->ops.push_back(op);
                 bn.chain = 28;
-                bn.in = x; bn.H = H; bn.C = C; bn.nblk = nblk[l] - 1;
+                bn.bn_ds = bn_ds;
+                bn.in = x; bn.H = H; bn.C = C; bn.nblk = nblk[l] - i;
             }
             if (l == 2 && i == 1 && h->dtype != FR_DTYPE_FP8 && H == 7 && chain_r50_supported(H, H, C, nblk[l] - 1)) {
                 ch_op = (int)h->ops.size();
@@ -1255,7 +1266,7 @@ void build_resnet50(Builder& b) {
                 b.conv({pre + ".conv3"}, h2, 0, P, y, 0, 1, 1, 1, 1, 0, 0, 1, id, 0);
             if (ch_op >= 0 && l == 2 && i >= 1)
                 for (size_t k = op0; k < h->ops.size(); ++k) ch.conv_ops.push_back((int)k);
-            if (bn_op >= 0 && l == 0 && i >= 1) {
+            if (bn_op >= 0 && l == 0) {
                 for (size_t k = op0; k < h->ops.size(); ++k) bn.conv_ops.push_back((int)k);
                 bn.x_tensors.push_back(y);
             }
@@ -2160,16 +2171,22 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
     }
     if (r.chain == 28) {
         Chain17Args c{};
-        c.w = r.cw; c.bias = r.cbias; c.B = B; c.nblk = r.nblk; c.f16 = f16;
+        c.B = B; c.nblk = 1; c.f16 = f16;
+        size_t w_off = 0;
         for (int i = 0; i < r.nblk; ++i) {
+            const bool ds = r.bn_ds && i == 0;
             c.x = h->tensors[i ? r.x_tensors[i - 1] : r.in].dev;
             c.y = h->tensors[r.x_tensors[i]].dev;
+            c.w = r.cw + w_off;
+            c.bias = r.cbias + 384 * i;
+            w_off += bneck28_block_elems(ds);
             ProfScope ps(h, s);
-            // per pixel: 256 x 64 + 576 x 64 + 64 x 256 = 69,632 MACs
-            ps.flops = 2.0 * B * 784.0 * 69632.0;
-            ps.bytes = 2.0 * 2.0 * B * 784.0 * 256.0 + 2.0 * 69632.0;
-            ps.start("bneck28 layer1");
-            FR_HIP_CHECK(launch_bneck28(c, i, s));
+            // per pixel: 256 x 64 + 576 x 64 + 64 x 256 = 69,632 MACs (layer1.0: 64 x 64 + 576 x 64 + 128 x 256 = 73,728)
+            const double macs = ds ? 73728.0 : 69632.0;
+            ps.flops = 2.0 * B * 784.0 * macs;
+            ps.bytes = 2.0 * B * 784.0 * ((ds ? 64.0 : 256.0) + 256.0) + 2.0 * macs;
+            ps.start(ds ? "bneck28 layer1.0" : "bneck28 layer1");
+            FR_HIP_CHECK(launch_bneck28(c, ds, s));
         }
         return FR_OK;
     }
@@ -3078,7 +3095,8 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
                    meas_note(h, op.grp, B) + "\n";
             continue;
         }
-        if (op.kind == OP_STAGE && h->stages[op.stage].chain == 28) {  // per block: M x 256 x 272 MACs (69,632 per pixel)
+        if (op.kind == OP_STAGE && h->stages[op.stage].chain == 28) {  // per block: M x 256 x 272 MACs (69,632 per pixel;
+                                                                        // layer1.0 288)
             const StageRec& r = h->stages[op.stage];
             out += "chain " + std::to_string(B * 784) + " 256 272 272 " + std::to_string(r.nblk) + " 1 3x3 " +
                    h->tensors[r.out].name + meas_note(h, op.grp, B) + "\n";

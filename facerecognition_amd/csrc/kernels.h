@@ -204,14 +204,15 @@ size_t chain_r50_bias_floats(int nblk);
 void chain_r50_pack_block(const bf16_t* r1, int kp1, const bf16_t* r2, int kp2, const bf16_t* r3, int kp3, int blk,
                           int nblk, bf16_t* out);
 hipError_t launch_chain_r50(const Chain17Args& a, hipStream_t s);
-// ResNet-50 layer1.1 / layer1.2 (Bottleneck 256 -> 64 -> 64 -> 256 at 28x28) as one launch per block, one
-// workgroup per image walking its rows (conv_bneck28.hip); Chain17Args' x / y are the block's input / output, w =
-// bneck28_pack_block images, bias = [nblk][conv1 64 | conv2 64 | conv3 256] f32; blk selects the block
+// ResNet-50 layer1 Bottlenecks (28x28: 1.1 / 1.2 256 -> 64 -> 64 -> 256 + x; ds: 1.0, 64 -> 64 -> 64 -> 256 with the
+// downsample K-concatenated into conv3) as one launch per block, one workgroup per image walking its rows
+// (conv_bneck28.hip); Chain17Args' x / y are the block's input / output, w = its bneck28_pack_block images
+// (bneck28_block_elems), bias = its [conv1 64 | conv2 64 | conv3 256] f32
 bool bneck28_supported(int H, int W, int C, int P);
-size_t bneck28_weight_elems(int nblk);
-void bneck28_pack_block(const bf16_t* r1, int kp1, const bf16_t* r2, int kp2, const bf16_t* r3, int kp3, int blk,
+size_t bneck28_block_elems(bool ds);
+void bneck28_pack_block(const bf16_t* r1, int kp1, const bf16_t* r2, int kp2, const bf16_t* r3, int kp3, bool ds,
                         bf16_t* out);
-hipError_t launch_bneck28(const Chain17Args& a, int blk, hipStream_t s);
+hipError_t launch_bneck28(const Chain17Args& a, bool ds, hipStream_t s);
 // FaceNet IRV1 stem at 160x160 (conv_stem160.hip): conv2d_1a (3x3/s2 8 -> 32) + conv2d_2a (3x3 32 -> 32) +
 // conv2d_2b (3x3/p1 32 -> 64) + maxpool_3a (3x3/s2) + conv2d_3b (1x1 64 -> 80), each conv + bias + ReLU, as one
 // launch, one workgroup per image; input: u8 crops [B][160][160][3] (u8 != null: the preparation is done in-kernel)

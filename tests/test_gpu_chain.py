@@ -211,7 +211,7 @@ def test_chain_r50_full_batch_against_oracle(gpu):
     u8 = synthetic_crops(B, 112, seed=31)
     e = m.embed(torch.from_numpy(u8)).cpu().numpy()
     plan = _plan(m, B)
-    assert " 1024 1088 1088 5 " in plan and " 256 272 272 2 " in plan
+    assert " 1024 1088 1088 5 " in plan and " 256 272 272 3 " in plan
     m.close()
     assert np.all(np.isfinite(e))
     idx = np.arange(0, B, 32)
@@ -221,8 +221,8 @@ def test_chain_r50_full_batch_against_oracle(gpu):
     assert np.all(1 - cos <= 1e-3), f"1-cos vs oracle {1 - cos}"
 
 
-# ---- ResNet-50 layer1.1 / layer1.2 (conv_bneck28.hip: one launch per Bottleneck at 28x28x256, one workgroup per image
-# walking its rows; reference: arcface_model.py:118-132)
+# ---- ResNet-50 layer1 (conv_bneck28.hip: one launch per Bottleneck at 28x28, one workgroup per image walking its rows;
+# layer1.0 with its downsample K-concatenated into conv3; reference: arcface_model.py:118-132)
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 @pytest.mark.parametrize("B", [1, 3, 9])
 def test_bneck28_matches_member_convs(gpu, dtype, B):
@@ -232,27 +232,33 @@ def test_bneck28_matches_member_convs(gpu, dtype, B):
     x = torch.from_numpy(synthetic_crops(B, 112, seed=37))
     m.set_option(N.FR_OPT_STAGE, 2)
     m.set_option(N.FR_OPT_FUSED_MASK, 32)
-    assert " 256 272 272 2 " in _plan(m, B)
+    assert " 256 272 272 3 " in _plan(m, B)
     e_f = m.embed(x).cpu().numpy()
     e_f2 = m.embed(x).cpu().numpy()  # graph replay
-    in_f = _tensor(m, B, "backbone.layer1.0")
+    in_f = _tensor(m, B, "backbone.maxpool")
+    y0_f = _tensor(m, B, "backbone.layer1.0")
     y1_f = _tensor(m, B, "backbone.layer1.1")
     y_f = _tensor(m, B, "backbone.layer1.2")
     m.set_option(N.FR_OPT_STAGE, 0)
-    assert " 256 272 272 2 " not in _plan(m, B)
+    assert " 256 272 272 3 " not in _plan(m, B)
     e_c = m.embed(x).cpu().numpy()
-    in_c = _tensor(m, B, "backbone.layer1.0")
+    in_c = _tensor(m, B, "backbone.maxpool")
+    y0_c = _tensor(m, B, "backbone.layer1.0")
     y1_c = _tensor(m, B, "backbone.layer1.1")
     y_c = _tensor(m, B, "backbone.layer1.2")
     m.close()
     assert np.array_equal(e_f, e_f2)
-    assert torch.equal(in_f, in_c), "the kernel's input differs: the runs are not comparable"
+    assert torch.equal(in_f, in_c), "the kernels' input differs: the runs are not comparable"
+    rel0 = ((y0_f - y0_c).norm() / y0_c.norm()).item()
     rel1 = ((y1_f - y1_c).norm() / y1_c.norm()).item()
     rel = ((y_f - y_c).norm() / y_c.norm()).item()
     cos = np.sum(e_f * e_c, axis=1)
-    print(f"{dtype} B={B}: layer1.1 rel {rel1:.2e}, layer1.2 rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
+    print(f"{dtype} B={B}: layer1.0 rel {rel0:.2e}, layer1.1 rel {rel1:.2e}, layer1.2 rel {rel:.2e}, "
+          f"max 1-cos {float((1 - cos).max()):.2e}")
     # 3 roundings to 16 bits per block in both paths; only the f32 summation order differs
+    assert rel0 < (3e-3 if dtype == "bf16" else 7e-4), f"layer1.0: kernel vs member convs rel err {rel0:.3e}"
     assert rel1 < (4e-3 if dtype == "bf16" else 1e-3), f"layer1.1: kernel vs member convs rel err {rel1:.3e}"
     assert rel < (6e-3 if dtype == "bf16" else 1.5e-3), f"layer1.2: kernel vs member convs rel err {rel:.3e}"
-    tol = 2e-4 if dtype == "bf16" else 2e-5
+    # three blocks of flipped bf16 roundings carried through the 13 blocks after them (the oracle bar is 1e-3)
+    tol = 4e-4 if dtype == "bf16" else 2e-5
     assert np.all(1 - cos <= tol), f"bneck28 vs member-conv embeddings: 1-cos = {1 - cos}"
