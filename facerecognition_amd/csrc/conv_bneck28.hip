@@ -191,7 +191,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
         lds_barrier();  // x row r + 2 landed; t1 row r + 1, t2 row r - 1 and staging row r - 2 complete; the slots
                         // written below were last read in phase r - 1
         dma_row(r + 4);  // into the slot of row r - 2 (last read by phase r - 1's conv3)
-        if (r >= 2) store_row(r - 2);
 
         const int a = r + 2, c = r - 1;
         const char* xs1 = smem + X_OFF + (C1 ? a % XR : 0) * XROW + px * 16;  // (+ plane * XPL)
@@ -224,19 +223,23 @@ __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
             if (C1 && k < KS1) f1 = *(const frag*)(xs1 + G::plane1(k, lg) * XPL);
             if (C3 && k < KS3) f3 = *(const frag*)(k < 2 ? t2s + 4 * k * TPL : xs3 + 4 * (k - 2) * XPL);
         };
-        frag f1[2], f2[2], f3[2];
+        // fragments read PD steps ahead; row r - 2's stores issue once the MFMAs run (step 1)
+        constexpr int PD = 2, NB = PD + 1;
+        frag f1[NB], f2[NB], f3[NB];
         constexpr int KS = C2 ? 18 : (C1 && KS1 > KS3) || !C3 ? KS1 : KS3;
-        rd(0, f1[0], f2[0], f3[0]);
+#pragma unroll
+        for (int k = 0; k < PD; ++k) rd(k, f1[k], f2[k], f3[k]);
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
             __builtin_amdgcn_sched_barrier(0);  // keep each step's loads in that step
-            if (k + 1 < KS) rd(k + 1, f1[(k + 1) & 1], f2[(k + 1) & 1], f3[(k + 1) & 1]);
+            if (k + PD < KS) rd(k + PD, f1[(k + PD) % NB], f2[(k + PD) % NB], f3[(k + PD) % NB]);
+            if (k == 1 && r >= 2) store_row(r - 2);
             if (C3 && k < KS3) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) a3[i] = T::mfma(w3[k][i], f3[k & 1], a3[i]);
+                for (int i = 0; i < 4; ++i) a3[i] = T::mfma(w3[k][i], f3[k % NB], a3[i]);
             }
-            if (C1 && k < KS1) a1 = T::mfma(w1[k], f1[k & 1], a1);
-            if (C2) a2 = T::mfma(w2[k], f2[k & 1], a2);
+            if (C1 && k < KS1) a1 = T::mfma(w1[k], f1[k % NB], a1);
+            if (C2) a2 = T::mfma(w2[k], f2[k % NB], a2);
         }
         __builtin_amdgcn_sched_barrier(0);
         // epilogues (pixels < 28): t1 row a (position px + 1), t2 row r, staging row c
