@@ -141,7 +141,7 @@ struct StageRec {
     // branch2.2, conv2d}, x_tensors = the block outputs; ResNet-50 layer3.1 .. 3.5 (chain 50, conv_chain_r50.hip):
     // per block {conv1, conv2, conv3}; ResNet-50 layer1 (chain 28, conv_bneck28.hip, one launch per block): per block
     // {conv1, conv2, conv3}, x_tensors = the block outputs; bn_ds: the first is layer1.0 (conv3 + K-concatenated
-    // downsample)
+    // downsample); ResNet-50 stem (chain 56, conv_stem_r50.hip): {conv1, maxpool}
     int chain = 0;
     bool bn_ds = false;
     bf16_t* cw = nullptr;                 // the packed weights of all blocks
@@ -256,7 +256,7 @@ struct fr_handle {
     // FR_OPT_BATCH_INVARIANT: every kernel choice sums K in the implicit GEMM's order (no split-K, no stage /
     // transition kernel, a fixed head split), so a face's embedding does not depend on its batch
     bool invariant = false;
-    int fused_mask = 63;  // FR_OPT_FUSED_MASK
+    int fused_mask = 127;  // FR_OPT_FUSED_MASK
     const uint8_t* fwd_u8 = nullptr;  // the current forward's u8 crops when the IRV1 fused stem prepares them itself
 };
 
@@ -1210,10 +1210,35 @@ void build_resnet50(Builder& b) {
     const int in = b.tensor(112, 112, 8);
     h->ops.push_back(Op{OP_PRE, -1, 0, 0, in});
     const int c1 = b.tensor(56, 56, 64, "backbone.relu");
+    // conv1 + maxpool are also emitted as one launch (conv_stem_r50.hip) beside the member ops
+    const bool st = h->dtype != FR_DTYPE_FP8;
+    const int st_op = (int)h->ops.size();
+    if (st) {
+        Op op;
+        op.kind = OP_STAGE;
+        op.stage = (int)h->stages.size();
+        h->ops.push_back(op);
+    }
     b.stem = true;
     b.conv({"backbone.conv1"}, in, 0, 8, c1, 0, 7, 7, 2, 2, 3, 3, 1);
     int x = b.tensor(28, 28, 64, "backbone.maxpool");
     b.maxpool(c1, x, 0, 3, 2, 1);
+    if (st && !b.rc) {
+        StageRec sr;
+        sr.chain = 56;
+        sr.in = in; sr.out = x; sr.H = 112; sr.C = 8; sr.nblk = 1;
+        sr.conv_ops = {st_op + 1, st_op + 2};
+        const Op& cv = h->ops[st_op + 1];
+        const DevConvW& cw = h->convw[cv.wi];
+        if (!stem_r50_supported(112, 112, cv.cin, cw.K, cw.Kpad, cw.Cout) || cw.w8 || !cw.bias || cv.act != 1 ||
+            cv.sh != 2 || cv.ph != 3 || cv.res >= 0 || h->ops[st_op + 2].kind != OP_MAXPOOL) {
+            set_error("plan: ResNet-50 stem does not have the fused kernel's shape");
+            b.rc = FR_ERR_ARG;
+        } else {
+            for (int oi : sr.conv_ops) h->ops[oi].stage = h->ops[st_op].stage;
+            h->stages.push_back(sr);
+        }
+    }
     const int planes[4] = {64, 128, 256, 512}, nblk[4] = {3, 4, 6, 3}, strd[4] = {1, 2, 2, 2};
     int H = 28, C = 64;
     // layer3.1 .. layer3.5 (7x7x1024) are also emitted as one chain launch (conv_chain_r50.hip) beside their member
@@ -1979,12 +2004,12 @@ static bool trans_enabled() {
     return on;
 }
 
-// FR_AB no_chain: IRV1 repeat_1 / repeat_2 and ResNet-50 layer1 / layer3 always run as their member convs (A/B
-// timing); no_chain17 / no_chain35 / no_chain50 / no_bneck28: only that one
+// FR_AB no_chain: IRV1 repeat_1 / repeat_2 and ResNet-50's stem / layer1 / layer3 always run as their member ops
+// (A/B timing); no_chain17 / no_chain35 / no_chain50 / no_bneck28 / no_stem_r50: only that one
 static bool chain_enabled(int kind) {
     static const bool all = !ab_int("no_chain", 0), c17 = !ab_int("no_chain17", 0), c35 = !ab_int("no_chain35", 0),
-                      c50 = !ab_int("no_chain50", 0), c28 = !ab_int("no_bneck28", 0);
-    return all && (kind == 17 ? c17 : kind == 35 ? c35 : kind == 28 ? c28 : c50);
+                      c50 = !ab_int("no_chain50", 0), c28 = !ab_int("no_bneck28", 0), c56 = !ab_int("no_stem_r50", 0);
+    return all && (kind == 17 ? c17 : kind == 35 ? c35 : kind == 28 ? c28 : kind == 56 ? c56 : c50);
 }
 
 // FR_AB no_stem160: the IRV1 stem always runs as its member ops (A/B timing)
@@ -1995,7 +2020,8 @@ static bool ab_stem160() {
 
 static bool stage_runs(const fr_handle* h, int B, const StageRec& r, int st) {
     if (h->stage_mode == 0 || h->invariant) return false;
-    const int kind_bit = r.stem ? 2 : r.chain == 35 ? 4 : r.chain == 50 ? 16 : r.chain == 28 ? 32 : r.chain ? 8 : 1;
+    const int kind_bit = r.stem ? 2 : r.chain == 35 ? 4 : r.chain == 50 ? 16 : r.chain == 28 ? 32 : r.chain == 56 ? 64
+                       : r.chain ? 8 : 1;
     if (!(h->fused_mask & kind_bit)) return false;
     // the fused transition keeps no t tensor and records no amax
     if (r.trans && (h->keep_inter || (h->amax && h->need_amax[r.out]) || !trans_enabled())) return false;
@@ -2167,6 +2193,20 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
         ps.bytes = 2.0 * 2.0 * B * 289.0 * 256.0 + 2.0 * 76800.0 * r.nblk;
         ps.start("chain block35");
         FR_HIP_CHECK(launch_chain35(c, s));
+        return FR_OK;
+    }
+    if (r.chain == 56) {
+        const Op& cv = h->ops[r.conv_ops[0]];
+        const DevConvW& cw = h->convw[cv.wi];
+        StemR50Args a{};
+        a.x = h->tensors[r.in].dev;
+        a.y = h->tensors[r.out].dev;
+        a.w = cw.w; a.bias = cw.bias; a.Kpad = cw.Kpad; a.B = B; a.f16 = f16 || h->tensors[r.in].f16;
+        ProfScope ps(h, s);
+        ps.flops = 2.0 * B * 3136.0 * 64.0 * 392.0;
+        ps.bytes = (double)B * (112.0 * 112 * 16 + 28.0 * 28 * 64 * 2);
+        ps.start("stem r50");
+        FR_HIP_CHECK(launch_stem_r50(a, s));
         return FR_OK;
     }
     if (r.chain == 28) {
@@ -3095,6 +3135,12 @@ int fr_debug_plan(fr_handle* h, int B, char* buf, size_t n) {
                    meas_note(h, op.grp, B) + "\n";
             continue;
         }
+        if (op.kind == OP_STAGE && h->stages[op.stage].chain == 56) {  // the conv: M x 64 x 392 MACs
+            const StageRec& r = h->stages[op.stage];
+            out += "chain " + std::to_string(B * 3136) + " 64 392 392 1 1 7x7 " + h->tensors[r.out].name +
+                   meas_note(h, op.grp, B) + "\n";
+            continue;
+        }
         if (op.kind == OP_STAGE && h->stages[op.stage].chain == 28) {  // per block: M x 256 x 272 MACs (69,632 per pixel;
                                                                         // layer1.0 288)
             const StageRec& r = h->stages[op.stage];
@@ -3202,7 +3248,7 @@ int fr_set_option(fr_handle* h, int option, int value) {
             }
             break;
         case FR_OPT_FUSED_MASK:
-            if (value < 0 || value > 63) { set_error("fr_set_option: FR_OPT_FUSED_MASK is 0 .. 63"); return FR_ERR_ARG; }
+            if (value < 0 || value > 127) { set_error("fr_set_option: FR_OPT_FUSED_MASK is 0 .. 127"); return FR_ERR_ARG; }
             h->fused_mask = value;
             break;
         default: set_error("fr_set_option: unknown option " + std::to_string(option)); return FR_ERR_ARG;

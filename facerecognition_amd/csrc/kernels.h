@@ -213,6 +213,20 @@ size_t bneck28_block_elems(bool ds);
 void bneck28_pack_block(const bf16_t* r1, int kp1, const bf16_t* r2, int kp2, const bf16_t* r3, int kp3, bool ds,
                         bf16_t* out);
 hipError_t launch_bneck28(const Chain17Args& a, bool ds, hipStream_t s);
+// ResNet-50 stem (conv1 7x7/s2 3 -> 64 + ReLU + maxpool 3x3/s2) in one launch, one workgroup per image
+// (conv_stem_r50.hip): x = the prepared [B][112][112][8] input (launch_preprocess's stem format), y = the pooled
+// [B][28][28][64], w / Kpad / bias = the conv's [Npad][Kpad] rows (stem hi/lo split) and folded bias
+struct StemR50Args {
+    const bf16_t* x;
+    bf16_t* y;
+    const bf16_t* w;
+    const float* bias;
+    int Kpad, B, f16;
+    void* ev0;
+    void* ev1;
+};
+bool stem_r50_supported(int H, int W, int Cin, int K, int Kpad, int Cout);
+hipError_t launch_stem_r50(const StemR50Args& a, hipStream_t s);
 // FaceNet IRV1 stem at 160x160 (conv_stem160.hip): conv2d_1a (3x3/s2 8 -> 32) + conv2d_2a (3x3 32 -> 32) +
 // conv2d_2b (3x3/p1 32 -> 64) + maxpool_3a (3x3/s2) + conv2d_3b (1x1 64 -> 80), each conv + bias + ReLU, as one
 // launch, one workgroup per image; input: u8 crops [B][160][160][3] (u8 != null: the preparation is done in-kernel)

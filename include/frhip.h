@@ -331,11 +331,12 @@ int fr_op_linear(const void* x, int B, int K, const void* w, int N, int Npad, in
  * recognition_engine.py:383-389).  Slower than the default, which measures the fastest kernels per batch size.
  * FR_DTYPE_FP8 handles refuse value 1 (FR_ERR_ARG): their e4m3 convs scale activations by a per-batch amax. */
 #define FR_OPT_BATCH_INVARIANT 9
-/* FR_OPT_FUSED_MASK (default 63): which kinds of fused multi-conv kernels a forward may run (each still measured
+/* FR_OPT_FUSED_MASK (default 127): which kinds of fused multi-conv kernels a forward may run (each still measured
  * against its member convs per batch size under FR_OPT_STAGE 1): bit 0 the IResNet100 LDS-resident stages and the
  * fused layer1.0 transition, bit 1 the IRV1 stem (conv_stem160.hip), bit 2 IRV1 repeat_1 (conv_chain35.hip), bit 3
- * IRV1 repeat_2 (conv_chain.hip), bit 4 ResNet-50 layer3.1-3.5 (conv_chain_r50.hip), bit 5 ResNet-50 layer1.1-1.2
- * (conv_bneck28.hip).  For A/B timing and for tests that check one fused kernel against its members. */
+ * IRV1 repeat_2 (conv_chain.hip), bit 4 ResNet-50 layer3.1-3.5 (conv_chain_r50.hip), bit 5 ResNet-50 layer1.0-1.2
+ * (conv_bneck28.hip), bit 6 the ResNet-50 stem conv + max-pool (conv_stem_r50.hip).  For A/B timing and for tests
+ * that check one fused kernel against its members. */
 #define FR_OPT_FUSED_MASK 10
 int fr_set_option(fr_handle* h, int option, int value);
 int fr_get_option(const fr_handle* h, int option);

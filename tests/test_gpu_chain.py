@@ -199,7 +199,7 @@ def test_chain_r50_matches_member_convs(gpu, dtype, B):
 
 
 def test_chain_r50_full_batch_against_oracle(gpu):
-    """bs = 256 (one image per CU), the layer3 chain and the layer1 Bottleneck kernels forced on: sampled faces within the 1e-3 cosine bar of the fp32 oracle
+    """bs = 256 (one image per CU), the stem, layer1 Bottleneck and layer3 chain kernels forced on: sampled faces within the 1e-3 cosine bar of the fp32 oracle
     (the reference's own ResNet-50 ArcFace, golden-pinned in test_golden.py)."""
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
@@ -211,7 +211,7 @@ def test_chain_r50_full_batch_against_oracle(gpu):
     u8 = synthetic_crops(B, 112, seed=31)
     e = m.embed(torch.from_numpy(u8)).cpu().numpy()
     plan = _plan(m, B)
-    assert " 1024 1088 1088 5 " in plan and " 256 272 272 3 " in plan
+    assert " 1024 1088 1088 5 " in plan and " 256 272 272 3 " in plan and " 64 392 392 1 " in plan
     m.close()
     assert np.all(np.isfinite(e))
     idx = np.arange(0, B, 32)
@@ -262,3 +262,33 @@ def test_bneck28_matches_member_convs(gpu, dtype, B):
     # three blocks of flipped bf16 roundings carried through the 13 blocks after them (the oracle bar is 1e-3)
     tol = 4e-4 if dtype == "bf16" else 2e-5
     assert np.all(1 - cos <= tol), f"bneck28 vs member-conv embeddings: 1-cos = {1 - cos}"
+
+
+# ---- ResNet-50 stem (conv_stem_r50.hip: conv1 7x7/s2 + ReLU + maxpool 3x3/s2 in one launch, one workgroup per image;
+# reference: arcface_model.py:118-132, the torchvision resnet50 stem)
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("B", [1, 3, 9])
+def test_stem_r50_matches_member_ops(gpu, dtype, B):
+    from facerecognition_amd.model import FRModel
+    from facerecognition_amd.synthetic import synthetic_crops
+    m = FRModel.synthetic("resnet50_arcface", dtype=dtype)
+    x = torch.from_numpy(synthetic_crops(B, 112, seed=41))
+    m.set_option(N.FR_OPT_STAGE, 2)
+    m.set_option(N.FR_OPT_FUSED_MASK, 64)
+    assert " 64 392 392 1 " in _plan(m, B)
+    e_f = m.embed(x).cpu().numpy()
+    e_f2 = m.embed(x).cpu().numpy()  # graph replay
+    y_f = _tensor(m, B, "backbone.maxpool")
+    m.set_option(N.FR_OPT_STAGE, 0)
+    assert " 64 392 392 1 " not in _plan(m, B)
+    e_c = m.embed(x).cpu().numpy()
+    y_c = _tensor(m, B, "backbone.maxpool")
+    m.close()
+    assert np.array_equal(e_f, e_f2)
+    rel = ((y_f - y_c).norm() / y_c.norm()).item()
+    cos = np.sum(e_f * e_c, axis=1)
+    print(f"{dtype} B={B}: maxpool rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
+    # one rounding to 16 bits (the conv output) in both paths; only the conv's f32 summation order differs
+    assert rel < (2e-3 if dtype == "bf16" else 3e-4), f"stem: kernel vs member ops rel err {rel:.3e}"
+    tol = 3e-4 if dtype == "bf16" else 2e-5
+    assert np.all(1 - cos <= tol), f"stem_r50 vs member-op embeddings: 1-cos = {1 - cos}"
