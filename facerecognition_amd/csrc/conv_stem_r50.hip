@@ -2,14 +2,14 @@
 // (arcface_model.py:118-132, the torchvision resnet50 stem) -- in one launch.  As member ops at bs = 256 the conv is
 // ~100 us (profiles/r06_r50_layer_profile.txt: K = 392 per pixel, its 51 MB output written and re-read) and the
 // max-pool ~31 us.  Here one 512-thread workgroup per image walks the pooled rows:
-//   * phase m: conv rows 2m and 2m + 1 (waves 0-3 / 4-7, one 16-channel fragment per wave and all four 16-pixel
-//     fragments of the 56-pixel row) into a 6-row ring, then pooled row m - 1 from conv rows 2m - 3 .. 2m - 1 with
+//   * phase m: conv rows 2m and 2m + 1 (waves 0-3 / 4-7; per wave two 16-channel fragments x two of the four
+//     16-pixel fragments of the 56-pixel row, so each B fragment read feeds two MFMAs) into a 6-row ring, then pooled row m - 1 from conv rows 2m - 3 .. 2m - 1 with
 //     one 16-B store per (pixel, 8 channels); one barrier per phase;
 //   * the prepared input rows (launch_preprocess's 8-channel [v v v v v v 0 0] pixels, the stem's hi/lo weight
 //     split) arrive by LDS-DMA into a 20-row ring two phases ahead, columns de-interleaved by parity with the 3-pixel
 //     zero pad written by the DMA itself (out-of-range offsets read 0), so a stride-2 tap reads 16 consecutive
 //     pixels' 16-B chunks: B fragment = one conflict-free ds_read_b128;
-//   * the conv's weight rows ([Npad][Kpad], K = (tap, 8 channels), taps 49 .. 51 zero) stay in registers (13
+//   * the conv's weight rows ([Npad][Kpad], K = (tap, 8 channels), taps 49 .. 51 zero) stay in registers (2 x 13
 //     fragments per wave);
 //   * the max-pool compares the stored 16-bit values as unsigned integers: after ReLU (written as +0 for v <= 0)
 //     bf16 / f16 bit patterns order like the values, and the padding never wins a window that holds a value >= 0.
@@ -73,18 +73,28 @@ __global__ __launch_bounds__(64 * NWV, 1) void stem_r50_kernel(StemR50Args p) {
     const int lane = threadIdx.x & 63, l15 = lane & 15, lg = lane >> 4;
     const int b = blockIdx.x;
     if (b >= p.B) return;
-    const int sel = wave >> 2, q = wave & 3;  // conv row 2m + sel, channels 16 q ..
+    // conv row 2m + sel, channel fragments 2 np and 2 np + 1, pixel fragments 2 ph and 2 ph + 1 (each B fragment read
+    // feeds two MFMAs)
+    const int sel = wave >> 2, np = (wave >> 1) & 1, ph = wave & 1;
 
-    // ---- weights (13 fragments) and bias, into registers once, before the first DMA
-    frag wa[KS];
+    // ---- weights (2 x 13 fragments) and biases, into registers once, before the first DMA
+    frag wa[2][KS];
+    float4 bias[2];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) wa[ks] = *(const frag*)(p.w + (size_t)(16 * q + l15) * p.Kpad + 32 * ks + 8 * lg);
-    float4 bias = *(const float4*)(p.bias + 16 * q + 4 * lg);
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            wa[i][ks] = *(const frag*)(p.w + (size_t)(16 * (2 * np + i) + l15) * p.Kpad + 32 * ks + 8 * lg);
+        bias[i] = *(const float4*)(p.bias + 16 * (2 * np + i) + 4 * lg);
+    }
     // consumed here, so the compiler's wait for these loads sits before the loop (its waitcnt pass does not see the
     // DMAs: a wait at a first use inside the loop would be a vmcnt(0) in every phase)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(wa[ks]));
-    asm volatile("" : "+v"(bias.x), "+v"(bias.y), "+v"(bias.z), "+v"(bias.w));
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(wa[i][ks]));
+        asm volatile("" : "+v"(bias[i].x), "+v"(bias[i].y), "+v"(bias[i].z), "+v"(bias[i].w));
+    }
 
     // ---- input DMA: group G(k) = rows 4k + 2 .. 4k + 5; wave w moves row 4k + 2 + (w >> 1), parity plane w & 1: lane
     // i = padded column 2i + (w & 1), pixel 2i + (w & 1) - 3 (outside the row or the image: offset out of range, 0)
@@ -118,17 +128,19 @@ __global__ __launch_bounds__(64 * NWV, 1) void stem_r50_kernel(StemR50Args p) {
         if (m < PWD) {
             const int y = 2 * m + sel;
             const int s0 = (2 * y + 5) % XR;  // slot of input row 2y - 3 (kh = 0)
-            f32x4_t acc[4];
+            f32x4_t acc[2][2];
 #pragma unroll
-            for (int f = 0; f < 4; ++f) acc[f] = (f32x4_t){bias.x, bias.y, bias.z, bias.w};
-            frag bq[3][4];
-            auto rd = [&](int ks, frag (&d)[4]) {
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4_t){bias[i].x, bias[i].y, bias[i].z, bias[i].w};
+            frag bq[3][2];
+            auto rd = [&](int ks, frag (&d)[2]) {
                 int kh;
                 const int o = tap_off(ks, kh);
                 const int sl = s0 + kh >= XR ? s0 + kh - XR : s0 + kh;
-                const char* src = smem + X_OFF + sl * XROWB + o;
+                const char* src = smem + X_OFF + sl * XROWB + o + 512 * ph;
 #pragma unroll
-                for (int f = 0; f < 4; ++f) d[f] = *(const frag*)(src + 256 * f);  // pixel fragment f: + 16 chunks
+                for (int j = 0; j < 2; ++j) d[j] = *(const frag*)(src + 256 * j);  // pixel fragment 2 ph + j: + 16 chunks
             };
             rd(0, bq[0]);
             rd(1, bq[1]);
@@ -137,21 +149,27 @@ __global__ __launch_bounds__(64 * NWV, 1) void stem_r50_kernel(StemR50Args p) {
                 __builtin_amdgcn_sched_barrier(0);  // keep each step's reads in that step
                 if (ks + 2 < KS) rd(ks + 2, bq[(ks + 2) % 3]);
 #pragma unroll
-                for (int f = 0; f < 4; ++f) acc[f] = T::mfma(wa[ks], bq[ks % 3][f], acc[f]);
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j] = T::mfma(wa[i][ks], bq[ks % 3][j], acc[i][j]);
             }
             __builtin_amdgcn_sched_barrier(0);
-            // epilogue: ReLU (v <= 0 -> +0) into conv ring row y; lane = channels 16 q + 4 lg .. + 3 of pixel 16 f + l15
+            // epilogue: ReLU (v <= 0 -> +0) into conv ring row y; lane = channels 16 (2 np + i) + 4 lg .. + 3 of pixel
+            // 16 (2 ph + j) + l15
             char* const cr = smem + C_OFF + (y % CR) * CROWB;
-            const int n = 16 * q + 4 * lg;
 #pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                const int px = 16 * f + l15;
-                if (px < CWD) {
-                    float v[8];
+            for (int i = 0; i < 2; ++i) {
+                const int n = 16 * (2 * np + i) + 4 * lg;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = acc[f][e] > 0.f ? acc[f][e] : 0.f;
-                    const uint4 pk = T::pack8(v);
-                    *(uint2*)(cr + px * 128 + (((n >> 3) ^ (px & 7)) << 4) + (n & 4) * 2) = make_uint2(pk.x, pk.y);
+                for (int j = 0; j < 2; ++j) {
+                    const int px = 16 * (2 * ph + j) + l15;
+                    if (px < CWD) {
+                        float v[8];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] > 0.f ? acc[i][j][e] : 0.f;
+                        const uint4 pk = T::pack8(v);
+                        *(uint2*)(cr + px * 128 + (((n >> 3) ^ (px & 7)) << 4) + (n & 4) * 2) = make_uint2(pk.x, pk.y);
+                    }
                 }
             }
         }
