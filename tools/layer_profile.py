@@ -61,7 +61,11 @@ def analyse(trace, plan_path):
         d = 0
         r = seq[i]; i += 1
         d += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        if (split > 1 and tile != 16) or p[0] == "head":  # (tile 16 = conv_small: its split is in-kernel)
+        if p[0] == "chain" and "bneck28" in r["Kernel_Name"]:  # one launch per block
+            for _ in range(tile - 1):
+                r = seq[i]; i += 1
+                d += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        elif (split > 1 and tile != 16) or p[0] == "head":  # (tile 16 = conv_small: its split is in-kernel)
             r = seq[i]; i += 1  # split-K epilogue / head finalize
             d += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         flop = 2.0 * M * Nn * K * (tile if p[0] in ("stage", "chain") else 1)  # stage: conv count, chain: blocks
