@@ -6,7 +6,8 @@
 //     16-pixel fragments of the 56-pixel row, so each B fragment read feeds two MFMAs) into a 6-row ring, then pooled row m - 1 from conv rows 2m - 3 .. 2m - 1 with
 //     one 16-B store per (pixel, 8 channels); one barrier per phase;
 //   * the prepared input rows (launch_preprocess's 8-channel [v v v v v v 0 0] pixels, the stem's hi/lo weight
-//     split) arrive by LDS-DMA into a 20-row ring two phases ahead, columns de-interleaved by parity with the 3-pixel
+//     split; from u8 crops the kernel prepares them itself, one phase behind the raw rows' DMA, and the preprocess
+//     launch is skipped) arrive by LDS-DMA into a 20-row ring two phases ahead, columns de-interleaved by parity with the 3-pixel
 //     zero pad written by the DMA itself (out-of-range offsets read 0), so a stride-2 tap reads 16 consecutive
 //     pixels' 16-B chunks: B fragment = one conflict-free ds_read_b128;
 //   * the conv's weight rows ([Npad][Kpad], K = (tap, 8 channels), taps 49 .. 51 zero) stay in registers (2 x 13
@@ -34,7 +35,9 @@ constexpr int CROWB = CWD * CO * 2;          // 7168: one conv row, [56 px][64 c
 constexpr int CR = 6;                        // conv ring rows
 constexpr int X_OFF = 0;
 constexpr int C_OFF = X_OFF + XR * XROWB;    // 40960
-constexpr int SR50_LDS = C_OFF + CR * CROWB; // 83968
+constexpr int RAW_OFF = C_OFF + CR * CROWB;  // 83968: u8 input, 2 slots of one DMA group (4 rows, 1344 B)
+constexpr int RAWB = 2048;                   // (two waves' DMA spans)
+constexpr int SR50_LDS = RAW_OFF + 2 * RAWB; // 88064
 constexpr int KS = 13;                       // K-steps: 52 tap slots of 8 channels (49 used)
 constexpr int NWV = 8;
 
@@ -64,7 +67,14 @@ __device__ __forceinline__ void wait_group(int m) {
     else wait_vm<1>();
 }
 
-template <bool F16>
+// u8 input: phase m waits for the raw group G(m + 1) (issued in phase m - 1; G(1) after the prologue's conversions);
+// younger: phase m - 1's pooled-row store (waves 0-1 issue the raw DMA and store in every phase m >= 1)
+__device__ __forceinline__ void wait_raw(int m) {
+    if (m >= 2) wait_vm<1>();
+    else wait_vm<0>();
+}
+
+template <bool F16, bool U8>
 __global__ __launch_bounds__(64 * NWV, 1) void stem_r50_kernel(StemR50Args p) {
     typedef Num<F16> T;
     typedef typename T::frag frag;
@@ -107,8 +117,44 @@ __global__ __launch_bounds__(64 * NWV, 1) void stem_r50_kernel(StemR50Args p) {
         const uint32_t off = ok ? (uint32_t)((((size_t)b * IH + row) * IH + dpx) * 16) : 0x80000000u;
         dma16(xr, (uint32_t)(uintptr_t)(smem + X_OFF + ((row + 8) % XR) * XROWB + (wave & 1) * XPAR), off);
     };
+    // ---- u8 crops (U8): group G(k) = 1344 contiguous bytes (21 16-B chunks per row) into raw slot k & 1 by waves 0-1,
+    // then converted in LDS to the prepared pixels [v v v v v v 0 0], v = 2q - 255 (launch_preprocess's values)
+    const uint64_t up = (uint64_t)p.u8;
+    const v4i32 ur = {(int)(uint32_t)up, (int)((up >> 32) & 0xffff), (int)((size_t)p.B * IH * IH * 3), 0x00020000};
+    auto dma_raw = [&](int k) {
+        if (wave < 2) {
+            const int e = 64 * wave + lane, row = 4 * k + 2 + e / 21;
+            const bool ok = e < 84 && (unsigned)row < (unsigned)IH;
+            const uint32_t off = ok ? (uint32_t)(((size_t)b * IH + 4 * k + 2) * IH * 3 + 16 * e) : 0x80000000u;
+            dma16(ur, (uint32_t)(uintptr_t)(smem + RAW_OFF + (k & 1) * RAWB + 1024 * wave), off);
+        }
+    };
+    auto convert = [&](int k) {  // thread t: row 4k + 2 + (t >> 7), parity plane (t >> 6) & 1, column index t & 63
+        const int t = threadIdx.x, rr = t >> 7, par = (t >> 6) & 1, i = t & 63;
+        const int row = 4 * k + 2 + rr, px = 2 * i + par - 3;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if ((unsigned)row < (unsigned)IH && (unsigned)px < (unsigned)IH) {
+            const uint8_t* qb = (const uint8_t*)(smem + RAW_OFF + (k & 1) * RAWB + rr * (IH * 3) + 3 * px);
+            const uint32_t a = T::cvt(2.0f * (float)qb[0] - 255.0f), c1 = T::cvt(2.0f * (float)qb[1] - 255.0f),
+                           c2 = T::cvt(2.0f * (float)qb[2] - 255.0f);
+            v = make_uint4(a | (c1 << 16), c2 | (a << 16), c1 | (c2 << 16), 0u);
+        }
+        *(uint4*)(smem + X_OFF + ((row + 8) % XR) * XROWB + par * XPAR + i * 16) = v;
+    };
+    if (U8) {
+        dma_raw(-1);
+        dma_raw(0);
+        wait_vm<0>();
+        lds_barrier();
+        convert(-2);  // (all rows outside the image: zeros)
+        convert(-1);
+        convert(0);
+        lds_barrier();  // raw slot 1 read before G(1) overwrites it
+        dma_raw(1);
+    } else {
 #pragma unroll
-    for (int k = -2; k <= 1; ++k) dma_group(k);
+        for (int k = -2; k <= 1; ++k) dma_group(k);
+    }
 
     // per lane and K-step: tap 4 ks + lg (taps past 48 read tap 48's pixels: their weights are zero), row offset kh,
     // column offset (kw & 1) plane + (kw >> 1) chunks
@@ -120,10 +166,21 @@ __global__ __launch_bounds__(64 * NWV, 1) void stem_r50_kernel(StemR50Args p) {
     };
 
     for (int m = 0; m <= PWD; ++m) {
-        if (wave < 4) wait_group<1>(m); else wait_group<0>(m);
-        lds_barrier();  // G(m) landed everywhere; conv rows 2m - 3 .. 2m - 1 complete; the slots written below were last
-                        // read in phase m - 1
-        dma_group(m + 2);  // (past the image: zero rows into free slots)
+        if (U8) {
+            if (wave < 2) wait_raw(m);
+        } else if (wave < 4) {
+            wait_group<1>(m);
+        } else {
+            wait_group<0>(m);
+        }
+        lds_barrier();  // G(m) landed everywhere (U8: raw G(m + 1)); conv rows 2m - 3 .. 2m - 1 complete; the slots
+                        // written below were last read in phase m - 1
+        if (U8) {
+            dma_raw(m + 2);  // into the slot of G(m), converted in phase m - 1
+            convert(m + 1);  // read by the next phase's conv
+        } else {
+            dma_group(m + 2);  // (past the image: zero rows into free slots)
+        }
 
         if (m < PWD) {
             const int y = 2 * m + sel;
@@ -205,13 +262,15 @@ bool stem_r50_supported(int H, int W, int Cin, int K, int Kpad, int Cout) {
 }
 
 hipError_t launch_stem_r50(const StemR50Args& a, hipStream_t s) {
-    if (a.B <= 0 || !a.x || !a.y || !a.w || !a.bias || a.Kpad < 32 * KS) return hipErrorInvalidValue;
+    if (a.B <= 0 || (!a.x && !a.u8) || !a.y || !a.w || !a.bias || a.Kpad < 32 * KS) return hipErrorInvalidValue;
     if ((size_t)a.B * IH * IH * 16 >= 0x80000000ull) return hipErrorInvalidValue;  // 31-bit buffer offsets
-    auto k = a.f16 ? stem_r50_kernel<true> : stem_r50_kernel<false>;
-    static bool attr[2] = {false, false};
-    if (!attr[a.f16 ? 1 : 0]) {
+    auto k = a.u8 ? (a.f16 ? stem_r50_kernel<true, true> : stem_r50_kernel<false, true>)
+                  : (a.f16 ? stem_r50_kernel<true, false> : stem_r50_kernel<false, false>);
+    static bool attr[4] = {false, false, false, false};
+    const int ai = (a.u8 ? 2 : 0) + (a.f16 ? 1 : 0);
+    if (!attr[ai]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, SR50_LDS);
-        attr[a.f16 ? 1 : 0] = true;
+        attr[ai] = true;
     }
     if (a.ev0)
         hipExtLaunchKernelGGL(k, dim3(a.B), dim3(64 * NWV), SR50_LDS, s, (hipEvent_t)a.ev0, (hipEvent_t)a.ev1, 0, a);

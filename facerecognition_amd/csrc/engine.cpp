@@ -2200,11 +2200,12 @@ static int run_stage(fr_handle* h, const Op& op, int B, int f16, const std::vect
         const DevConvW& cw = h->convw[cv.wi];
         StemR50Args a{};
         a.x = h->tensors[r.in].dev;
+        a.u8 = h->fwd_u8;  // the crops when the forward skipped the preparation op (forward, OP_PRE)
         a.y = h->tensors[r.out].dev;
         a.w = cw.w; a.bias = cw.bias; a.Kpad = cw.Kpad; a.B = B; a.f16 = f16 || h->tensors[r.in].f16;
         ProfScope ps(h, s);
         ps.flops = 2.0 * B * 3136.0 * 64.0 * 392.0;
-        ps.bytes = (double)B * (112.0 * 112 * 16 + 28.0 * 28 * 64 * 2);
+        ps.bytes = (double)B * (112.0 * 112 * (a.u8 ? 3.0 : 16.0) + 28.0 * 28 * 64 * 2);
         ps.start("stem r50");
         FR_HIP_CHECK(launch_stem_r50(a, s));
         return FR_OK;
@@ -2503,10 +2504,11 @@ int forward(fr_handle* h, const void* in, int in_fmt, int B, float* out, int fla
             case OP_PRE: {
                 h->fwd_u8 = nullptr;
                 if (in_fmt == FR_IN_U8_NHWC && oi + 1 < h->ops.size() && h->ops[oi + 1].kind == OP_STAGE &&
-                    h->stages[h->ops[oi + 1].stage].stem && !op_skipped(h->ops[oi + 1], stage_run) &&
+                    (h->stages[h->ops[oi + 1].stage].stem || h->stages[h->ops[oi + 1].stage].chain == 56) &&
+                    !op_skipped(h->ops[oi + 1], stage_run) &&
                     !(h->tuning && h->stage_mode == 1 && !h->keep_inter && !h->prof &&
                       stage_choice(h, h->ops[oi + 1].grp, B) < 0)) {
-                    h->fwd_u8 = (const uint8_t*)in;  // conv_stem160.hip prepares the crops itself (no prepared tensor)
+                    h->fwd_u8 = (const uint8_t*)in;  // conv_stem160 / conv_stem_r50 prepare the crops themselves
                     break;
                 }
                 ProfScope ps(h, s);

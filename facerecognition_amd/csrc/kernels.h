@@ -214,10 +214,11 @@ void bneck28_pack_block(const bf16_t* r1, int kp1, const bf16_t* r2, int kp2, co
                         bf16_t* out);
 hipError_t launch_bneck28(const Chain17Args& a, bool ds, hipStream_t s);
 // ResNet-50 stem (conv1 7x7/s2 3 -> 64 + ReLU + maxpool 3x3/s2) in one launch, one workgroup per image
-// (conv_stem_r50.hip): x = the prepared [B][112][112][8] input (launch_preprocess's stem format), y = the pooled
+// (conv_stem_r50.hip): x = the prepared [B][112][112][8] input (launch_preprocess's stem format) or u8, y = the pooled
 // [B][28][28][64], w / Kpad / bias = the conv's [Npad][Kpad] rows (stem hi/lo split) and folded bias
 struct StemR50Args {
     const bf16_t* x;
+    const uint8_t* u8;  // u8 crops [B][112][112][3] (non-null: prepared in-kernel, x unused)
     bf16_t* y;
     const bf16_t* w;
     const float* bias;

@@ -266,13 +266,18 @@ def test_bneck28_matches_member_convs(gpu, dtype, B):
 
 # ---- ResNet-50 stem (conv_stem_r50.hip: conv1 7x7/s2 + ReLU + maxpool 3x3/s2 in one launch, one workgroup per image;
 # reference: arcface_model.py:118-132, the torchvision resnet50 stem)
+@pytest.mark.parametrize("fmt", ["u8", "f32"])
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 @pytest.mark.parametrize("B", [1, 3, 9])
-def test_stem_r50_matches_member_ops(gpu, dtype, B):
+def test_stem_r50_matches_member_ops(gpu, dtype, B, fmt):
+    """u8 crops: the kernel prepares them itself (no preprocess launch); f32 (the reference transform's output in
+    NCHW): the kernel reads the prepared tensor."""
     from facerecognition_amd.model import FRModel
     from facerecognition_amd.synthetic import synthetic_crops
     m = FRModel.synthetic("resnet50_arcface", dtype=dtype)
-    x = torch.from_numpy(synthetic_crops(B, 112, seed=41))
+    u8 = synthetic_crops(B, 112, seed=41)
+    x = torch.from_numpy(u8) if fmt == "u8" else \
+        torch.from_numpy((u8.astype(np.float32) / 255 - 0.5) / 0.5).permute(0, 3, 1, 2).contiguous()
     m.set_option(N.FR_OPT_STAGE, 2)
     m.set_option(N.FR_OPT_FUSED_MASK, 64)
     assert " 64 392 392 1 " in _plan(m, B)
@@ -287,7 +292,7 @@ def test_stem_r50_matches_member_ops(gpu, dtype, B):
     assert np.array_equal(e_f, e_f2)
     rel = ((y_f - y_c).norm() / y_c.norm()).item()
     cos = np.sum(e_f * e_c, axis=1)
-    print(f"{dtype} B={B}: maxpool rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
+    print(f"{dtype} {fmt} B={B}: maxpool rel {rel:.2e}, max 1-cos {float((1 - cos).max()):.2e}")
     # one rounding to 16 bits (the conv output) in both paths; only the conv's f32 summation order differs
     assert rel < (2e-3 if dtype == "bf16" else 3e-4), f"stem: kernel vs member ops rel err {rel:.3e}"
     tol = 3e-4 if dtype == "bf16" else 2e-5
