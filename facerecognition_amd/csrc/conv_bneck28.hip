@@ -138,8 +138,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
     // 2 k + 1 at 32 positions (positions 28-31 repeat pixel 27), waves 0-3 one each
     constexpr int CIN = G::CIN;
     const uint64_t xp = (uint64_t)p.x;
-    const v4i32 xr = {(int)(uint32_t)xp, (int)((xp >> 32) & 0xffff), (int)min((size_t)0x7fffffff, (size_t)p.B * IW * IW * CIN * 2),
-                      0x00020000};
+    const v4i32 xr = {(int)(uint32_t)xp, (int)((xp >> 32) & 0xffff), (int)((size_t)p.B * IW * IW * CIN * 2), 0x00020000};
     auto piece_src = [&](int k) {
         if (DS) {
             const int pl = 2 * k + (lane >> 5), x = min(lane & 31, IW - 1);
@@ -308,6 +307,8 @@ void bneck28_pack_block(const bf16_t* r1, int kp1, const bf16_t* r2, int kp2, co
 // a.w / a.bias: this block's images and its [conv1 64 | conv2 64 | conv3 256] biases
 hipError_t launch_bneck28(const Chain17Args& a, bool ds, hipStream_t s) {
     if (a.B <= 0 || !a.x || !a.y || !a.w || !a.bias) return hipErrorInvalidValue;
+    if ((size_t)a.B * IW * IW * (ds ? Geo<true>::CIN : Geo<false>::CIN) * 2 >= 0x80000000ull)
+        return hipErrorInvalidValue;  // the x DMA's buffer offsets are 31-bit
     auto k = ds ? (a.f16 ? bneck28_kernel<true, true> : bneck28_kernel<false, true>)
                 : (a.f16 ? bneck28_kernel<true, false> : bneck28_kernel<false, false>);
     const int lds = ds ? Geo<true>::LDS : Geo<false>::LDS;
