@@ -86,6 +86,10 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
     return make_uint2(pack2_bf16(a, b), pack2_bf16(c, d));
 }
 
+// ReLU as one v_max_i32 on the bits (a negative float is a negative int; -0 becomes +0): fmaxf first canonicalizes
+// its operand in IEEE mode, two VALU per value
+__device__ __forceinline__ float relu(float v) { return __builtin_bit_cast(float, max(__builtin_bit_cast(int, v), 0)); }
+
 // Phase r waits for x row r + 2 (issued in phase r - 2, rows 0 / 1 before the loop).  VMEM ops per phase, in issue
 // order: D DMA instructions (the row r + 4; waves 0-5: two of the 14, 6-7: one), then S stores of row r - 2 when
 // r >= 2 (waves 0-5: two 16-B pieces per thread, 6-7: one).  Younger than row r + 2's DMA: phases -2 .. 2 -> the
@@ -245,17 +249,17 @@ __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
         if (pv) {
             if (C1)
                 *(uint2*)(smem + T1_OFF + (a & 3) * TROW + (2 * q + (lg >> 1)) * TPL + (px + 1) * 16 + (lg & 1) * 8) =
-                    pack4<F16>(fmaxf(a1[0], 0.f), fmaxf(a1[1], 0.f), fmaxf(a1[2], 0.f), fmaxf(a1[3], 0.f));
+                    pack4<F16>(relu(a1[0]), relu(a1[1]), relu(a1[2]), relu(a1[3]));
             if (C2)
                 *(uint2*)(smem + T2_OFF + (r & 1) * TROW + (2 * q + (lg >> 1)) * TPL + px * 16 + (lg & 1) * 8) =
-                    pack4<F16>(fmaxf(a2[0], 0.f), fmaxf(a2[1], 0.f), fmaxf(a2[2], 0.f), fmaxf(a2[3], 0.f));
+                    pack4<F16>(relu(a2[0]), relu(a2[1]), relu(a2[2]), relu(a2[3]));
             if (C3) {
                 char* const st = smem + Y_OFF + (c & 1) * YROW + px * 512;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const uint32_t ch = 16 * (4 * q + i) + 4 * lg;  // 4 channels: chunk ch / 8, half (ch & 4)
                     *(uint2*)(st + (((ch >> 3) ^ ysw) << 4) + (ch & 4) * 2) =
-                        pack4<F16>(fmaxf(a3[i][0], 0.f), fmaxf(a3[i][1], 0.f), fmaxf(a3[i][2], 0.f), fmaxf(a3[i][3], 0.f));
+                        pack4<F16>(relu(a3[i][0]), relu(a3[i][1]), relu(a3[i][2]), relu(a3[i][3]));
                 }
             }
         }
