@@ -125,6 +125,10 @@ struct Num<false> {  // bf16
     static __device__ __forceinline__ uint16_t cvt(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 };
 
+// ReLU as one v_max_i32 on the bits (a negative float is a negative int; -0 becomes +0).  fmaxf(v, 0.f) first
+// canonicalizes v in IEEE mode: two VALU per value in the fused kernels' epilogues
+__device__ __forceinline__ float relu_bits(float v) { return __builtin_bit_cast(float, max(__builtin_bit_cast(int, v), 0)); }
+
 __device__ __forceinline__ uint32_t pack2_f16(float a, float b) {
     a = fminf(fmaxf(a, -65504.f), 65504.f);  // saturate: an overflow must not become inf
     b = fminf(fmaxf(b, -65504.f), 65504.f);

@@ -1,5 +1,5 @@
 // ResNet-50 ArcFace layer1.1 and layer1.2 -- torchvision Bottlenecks at 28x28x256 (arcface_model.py:118-132; y =
-// relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1(x)))))))) + x), conv1 1x1 256 -> 64, conv2 3x3 64 -> 64, conv3 1x1
+// relu_bits(bn3(conv3(relu_bits(bn2(conv2(relu_bits(bn1(conv1(x)))))))) + x), conv1 1x1 256 -> 64, conv2 3x3 64 -> 64, conv3 1x1
 // 64 -> 256) -- one launch per block.  As per-conv launches each block is ~111 us at bs = 256
 // (profiles/r06_r50_layer_profile.txt: 31 + 35 + 47 us): conv1 reads and conv3 writes the 103 MB 256-channel tensors and
 // conv3 reads the residual again, and the 64-channel intermediates make two more HBM round trips.  Here one workgroup
@@ -85,10 +85,6 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
     if (F16) return make_uint2(pack2_f16(a, b), pack2_f16(c, d));
     return make_uint2(pack2_bf16(a, b), pack2_bf16(c, d));
 }
-
-// ReLU as one v_max_i32 on the bits (a negative float is a negative int; -0 becomes +0): fmaxf first canonicalizes
-// its operand in IEEE mode, two VALU per value
-__device__ __forceinline__ float relu(float v) { return __builtin_bit_cast(float, max(__builtin_bit_cast(int, v), 0)); }
 
 // Phase r waits for x row r + 2 (issued in phase r - 2, rows 0 / 1 before the loop).  VMEM ops per phase, in issue
 // order: D DMA instructions (the row r + 4; waves 0-5: two of the 14, 6-7: one), then S stores of row r - 2 when
@@ -249,17 +245,17 @@ __global__ __launch_bounds__(64 * NWV, 1) void bneck28_kernel(Chain17Args p) {
         if (pv) {
             if (C1)
                 *(uint2*)(smem + T1_OFF + (a & 3) * TROW + (2 * q + (lg >> 1)) * TPL + (px + 1) * 16 + (lg & 1) * 8) =
-                    pack4<F16>(relu(a1[0]), relu(a1[1]), relu(a1[2]), relu(a1[3]));
+                    pack4<F16>(relu_bits(a1[0]), relu_bits(a1[1]), relu_bits(a1[2]), relu_bits(a1[3]));
             if (C2)
                 *(uint2*)(smem + T2_OFF + (r & 1) * TROW + (2 * q + (lg >> 1)) * TPL + px * 16 + (lg & 1) * 8) =
-                    pack4<F16>(relu(a2[0]), relu(a2[1]), relu(a2[2]), relu(a2[3]));
+                    pack4<F16>(relu_bits(a2[0]), relu_bits(a2[1]), relu_bits(a2[2]), relu_bits(a2[3]));
             if (C3) {
                 char* const st = smem + Y_OFF + (c & 1) * YROW + px * 512;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const uint32_t ch = 16 * (4 * q + i) + 4 * lg;  // 4 channels: chunk ch / 8, half (ch & 4)
                     *(uint2*)(st + (((ch >> 3) ^ ysw) << 4) + (ch & 4) * 2) =
-                        pack4<F16>(relu(a3[i][0]), relu(a3[i][1]), relu(a3[i][2]), relu(a3[i][3]));
+                        pack4<F16>(relu_bits(a3[i][0]), relu_bits(a3[i][1]), relu_bits(a3[i][2]), relu_bits(a3[i][3]));
                 }
             }
         }

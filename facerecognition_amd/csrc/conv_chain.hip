@@ -184,8 +184,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain17_kernel(Chain17Args p) {
                           l15 * 16;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            *(uint2*)(dst + 256 * j) = pack4<F16>(fmaxf(acc[0][j][0], 0.f), fmaxf(acc[0][j][1], 0.f),
-                                                  fmaxf(acc[0][j][2], 0.f), fmaxf(acc[0][j][3], 0.f));
+            *(uint2*)(dst + 256 * j) = pack4<F16>(relu_bits(acc[0][j][0]), relu_bits(acc[0][j][1]),
+                                                  relu_bits(acc[0][j][2]), relu_bits(acc[0][j][3]));
         lds_barrier();
     };
 
@@ -232,8 +232,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain17_kernel(Chain17Args p) {
             char* const xd = smem + X_OFF + (2 * n + (lg >> 1)) * PLB + (lg & 1) * 8 + l15 * 16;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                *(uint2*)(xd + 256 * j) = pack4<F16>(fmaxf(acc[i][j][0], 0.f), fmaxf(acc[i][j][1], 0.f),
-                                                     fmaxf(acc[i][j][2], 0.f), fmaxf(acc[i][j][3], 0.f));
+                *(uint2*)(xd + 256 * j) = pack4<F16>(relu_bits(acc[i][j][0]), relu_bits(acc[i][j][1]),
+                                                     relu_bits(acc[i][j][2]), relu_bits(acc[i][j][3]));
         }
         lds_barrier();
     };

@@ -128,8 +128,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
                     const int px = 16 * (5 * pg + j) + l15;
                     if (px < NPX) {
                         const int a = dst_off + (padded ? pl * PPL + ppos(px) * 16 : pl * UPL + px * 16) + (lg & 1) * 8;
-                        *(uint2*)(smem + a) = pack4<F16>(fmaxf(acc[i][j][0], 0.f), fmaxf(acc[i][j][1], 0.f),
-                                                         fmaxf(acc[i][j][2], 0.f), fmaxf(acc[i][j][3], 0.f));
+                        *(uint2*)(smem + a) = pack4<F16>(relu_bits(acc[i][j][0]), relu_bits(acc[i][j][1]),
+                                                         relu_bits(acc[i][j][2]), relu_bits(acc[i][j][3]));
                     }
                 }
             }
@@ -219,8 +219,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
                     const int px = 16 * (5 * pg + j) + l15;
                     if (px < NPX) {
                         const int a = tsel == 2 ? B0_OFF + pl * UPL + px * 16 : (tsel == 0 ? T1_OFF : T2_OFF) + pl * PPL + ppos(px) * 16;
-                        *(uint2*)(smem + a + (lg & 1) * 8) = pack4<F16>(fmaxf(acc[i][j][0], 0.f), fmaxf(acc[i][j][1], 0.f),
-                                                                        fmaxf(acc[i][j][2], 0.f), fmaxf(acc[i][j][3], 0.f));
+                        *(uint2*)(smem + a + (lg & 1) * 8) = pack4<F16>(relu_bits(acc[i][j][0]), relu_bits(acc[i][j][1]),
+                                                                        relu_bits(acc[i][j][2]), relu_bits(acc[i][j][3]));
                     }
                 }
             }
@@ -294,8 +294,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void chain35_kernel(Chain35Args p) {
                     const int px = 16 * (5 * pg + j) + l15;
                     if (px < NPX) {
                         const size_t o = out_planar ? (size_t)((n >> 3) * NPX + px) * 8 + (n & 7) : (size_t)px * 256 + n;
-                        *(uint2*)(yout + img + o) = pack4<F16>(fmaxf(acc[i][j][0], 0.f), fmaxf(acc[i][j][1], 0.f),
-                                                               fmaxf(acc[i][j][2], 0.f), fmaxf(acc[i][j][3], 0.f));
+                        *(uint2*)(yout + img + o) = pack4<F16>(relu_bits(acc[i][j][0]), relu_bits(acc[i][j][1]),
+                                                               relu_bits(acc[i][j][2]), relu_bits(acc[i][j][3]));
                     }
                 }
             }

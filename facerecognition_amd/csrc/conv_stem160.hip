@@ -214,8 +214,8 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
 #pragma unroll
             for (int f = 0; f < 5; ++f)
                 if (16 * f + c15 < W1)
-                    *(uint2*)(dst + f * 256) = pack4<F16>(fmaxf(acc[0][f][0], 0.f), fmaxf(acc[0][f][1], 0.f),
-                                                          fmaxf(acc[0][f][2], 0.f), fmaxf(acc[0][f][3], 0.f));
+                    *(uint2*)(dst + f * 256) = pack4<F16>(relu_bits(acc[0][f][0]), relu_bits(acc[0][f][1]),
+                                                          relu_bits(acc[0][f][2]), relu_bits(acc[0][f][3]));
         }
         // ---- 2a: row i2 = 2s - 4 + hr from 1a rows i2 .. i2 + 2 (valid conv); 9 K-steps = taps x 32 channels
         {
@@ -243,8 +243,8 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
 #pragma unroll
                 for (int f = 0; f < 5; ++f)
                     if (16 * f + c15 < W2)
-                        *(uint2*)(dst + f * 256) = pack4<F16>(fmaxf(acc[0][f][0], 0.f), fmaxf(acc[0][f][1], 0.f),
-                                                              fmaxf(acc[0][f][2], 0.f), fmaxf(acc[0][f][3], 0.f));
+                        *(uint2*)(dst + f * 256) = pack4<F16>(relu_bits(acc[0][f][0]), relu_bits(acc[0][f][1]),
+                                                              relu_bits(acc[0][f][2]), relu_bits(acc[0][f][3]));
             }
         }
         // ---- 2b: row i3 = 2s - 7 + hr from 2a rows i3 - 1 .. i3 + 1 (padding rows: the zero row; padding
@@ -280,8 +280,8 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
                     for (int f = 0; f < 5; ++f)
                         if (16 * f + c15 < W2)
                             *(uint2*)(dst + (2 * (2 * nh + i) + (g >> 1)) * PL + f * 256) =
-                                pack4<F16>(fmaxf(acc[i][f][0], 0.f), fmaxf(acc[i][f][1], 0.f), fmaxf(acc[i][f][2], 0.f),
-                                           fmaxf(acc[i][f][3], 0.f));
+                                pack4<F16>(relu_bits(acc[i][f][0]), relu_bits(acc[i][f][1]), relu_bits(acc[i][f][2]),
+                                           relu_bits(acc[i][f][3]));
             }
         }
         // ---- 3b: row r3 = s - 6 of the pooled rows (1x1 64 -> 80), straight to global memory
@@ -312,8 +312,8 @@ __global__ __launch_bounds__(256, 1) void stem160_kernel(Stem160Args p) {
                             const int px = 16 * f + c15;
                             if (px < WP)
                                 *(uint2*)(yb + ((size_t)r3 * WP + px) * C3B + 16 * n4[i] + 4 * g) =
-                                    pack4<F16>(fmaxf(acc[i][f][0], 0.f), fmaxf(acc[i][f][1], 0.f), fmaxf(acc[i][f][2], 0.f),
-                                               fmaxf(acc[i][f][3], 0.f));
+                                    pack4<F16>(relu_bits(acc[i][f][0]), relu_bits(acc[i][f][1]), relu_bits(acc[i][f][2]),
+                                               relu_bits(acc[i][f][3]));
                         }
             }
         }
