@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void stem_r50_kernel(StemR50Args p) {
                     if (px < CWD) {
                         float v[8];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] > 0.f ? acc[i][j][e] : 0.f;
+                        for (int e = 0; e < 4; ++e) v[e] = relu_bits(acc[i][j][e]);  // +0 for v <= 0
                         const uint4 pk = T::pack8(v);
                         *(uint2*)(cr + px * 128 + (((n >> 3) ^ (px & 7)) << 4) + (n & 4) * 2) = make_uint2(pk.x, pk.y);
                     }
